@@ -1,0 +1,145 @@
+/*
+ * mtb.h — C ABI of the MI355X merge-tree batch replay engine ("mtb" = merge-tree batch).
+ *
+ * One batch holds many independent documents (SharedString / PermutationVector merge-trees).
+ * Each document is an *observer* merge-tree client: it receives the sequenced op stream of every
+ * other client and applies it exactly as the reference `Client.applyMsg` would
+ * (packages/dds/merge-tree/src/client.ts:858-887), then produces the same text
+ * (MergeTreeTextHelper.ts:20) and SnapshotV1 summary (client.ts:966-1005, snapshotV1.ts:122-312).
+ *
+ * Interfaces replaced (reference file:line -> entry point here):
+ *   Client ctor / startOrUpdateCollaboration   client.ts:107, :1133      -> mtb_batch_create, mtb_doc_init
+ *   Client.applyMsg(ISequencedDocumentMessage) client.ts:858              -> mtb_apply_msg_json (JSON) or
+ *                                                                           mtb_append_ops (pre-packed records)
+ *   (replay of the appended ops; synchronous in the reference)            -> mtb_replay
+ *   TestClient.getText / MergeTreeTextHelper   testClient.ts:185          -> mtb_get_text
+ *   Client.getLength / getCurrentSeq           client.ts:1129, :1122      -> mtb_get_length, mtb_get_seq
+ *   Client.summarize (SnapshotV1 branch)       client.ts:966-998          -> mtb_summarize_v1
+ *   (segment-level parity read-out)            mergeTreeNodeWalk.ts:170   -> mtb_dump_segments
+ *
+ * All calls return 0 on success or a negative MTB_E_* code; mtb_last_error() gives the message,
+ * which carries the reference assert code / error text where one exists (e.g. "0x038",
+ * "MergeTree insert failed").  A batch handle is not thread-safe; distinct handles are independent.
+ */
+#ifndef MTB_H
+#define MTB_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- op record (32 bytes). One record per merge-tree delta op; GROUP members are flattened into
+ * consecutive records sharing seq/ref_seq/msn; the last record of a message carries MTB_F_LAST. */
+enum {
+  MTB_OP_INSERT = 0,   /* ops.ts:58 INSERT   pos1 = pos, pos2 = text length (UTF-16 units) */
+  MTB_OP_REMOVE = 1,   /* ops.ts:59 REMOVE   [pos1, pos2) */
+  MTB_OP_ANNOTATE = 2, /* ops.ts:60 ANNOTATE [pos1, pos2), props = op-props id */
+  MTB_OP_NOOP = 3,     /* non-"op" message, or a member with no merge-tree effect */
+  MTB_OP_ACK = 4       /* op authored by the observer itself (client.ts:866 ack path): zamboni only */
+};
+enum {
+  MTB_F_LAST = 0x01,    /* run updateSeqNumbers(msn, seq) after this record (client.ts:874) */
+  MTB_F_MARKER = 0x02,  /* insert: Marker segment, pos2 = refType (0xFFFFFFFF = undefined) */
+  MTB_F_REWRITE = 0x04, /* annotate: combiningOp {name:"rewrite"} */
+  MTB_F_SEGOBJ = 0x08   /* insert: seg given as {text, props?} object (props id may be 0) */
+};
+typedef struct mtb_op {
+  uint8_t type;
+  uint8_t flags;
+  uint16_t client;   /* short client id (first-seen order, 0 = the observer) */
+  uint32_t seq;      /* sequenceNumber */
+  uint32_t ref_seq;  /* referenceSequenceNumber */
+  uint32_t msn;      /* minimumSequenceNumber */
+  uint32_t pos1;
+  uint32_t pos2;
+  uint32_t payload;  /* insert: offset (UTF-16 units) of the text in the payload passed with it */
+  uint32_t props;    /* insert/annotate: props id from mtb_intern_props (0 = none) */
+} mtb_op;
+
+typedef struct mtb_options {
+  int32_t new_length_calc; /* IMergeTreeOptions.mergeTreeUseNewLengthCalculations (mergeTree.ts:413) */
+  int32_t chunk_size;      /* IMergeTreeOptions.mergeTreeSnapshotChunkSize, 0 -> 10000 */
+  int32_t threads_per_doc; /* reserved (64) */
+  int32_t flags;           /* reserved */
+} mtb_options;
+
+typedef struct mtb_stats {
+  uint64_t ops_applied;     /* delta ops applied (each GROUP member counts once) */
+  uint64_t docs;            /* documents replayed */
+  uint64_t segments_final;  /* live segments after replay */
+  uint64_t text_units_final;/* visible UTF-16 units after replay */
+  uint64_t bytes_alg;       /* algorithmic bytes */
+  uint64_t checksum;        /* xor-fold of per-document state checksums */
+  uint64_t errors;          /* documents whose replay stopped on an error */
+  double kernel_ms;         /* device time of the replay kernel(s) (HIP events) */
+} mtb_stats;
+
+typedef struct mtb_blob {
+  const char* path;      /* "header", "body_0", ... */
+  const char* content;   /* UTF-8 blob contents (SummaryTreeBuilder.addBlob content) */
+  size_t content_len;
+} mtb_blob;
+typedef struct mtb_blob_list {
+  uint32_t count;
+  mtb_blob* blobs;
+  const char* summary_json; /* the ISummaryTreeWithStats object, JSON-serialized */
+  size_t summary_json_len;
+} mtb_blob_list;
+
+typedef struct mtb_batch mtb_batch;
+
+enum {
+  MTB_OK = 0,
+  MTB_E_ARG = -1,         /* bad argument */
+  MTB_E_NODEV = -2,       /* no usable GPU / HIP runtime (the engine never falls back to CPU) */
+  MTB_E_HIP = -3,         /* HIP runtime error */
+  MTB_E_ASSERT = -4,      /* reference assert (message holds the 0xNNN code) */
+  MTB_E_INSERT = -5,      /* UsageError("MergeTree insert failed") mergeTree.ts:1671 */
+  MTB_E_UNSUPPORTED = -6, /* input outside the engine's supported subset */
+  MTB_E_CAPACITY = -7,    /* a per-document arena overflowed */
+  MTB_E_PARSE = -8        /* malformed JSON message */
+};
+
+int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_mask, mtb_batch** out);
+void mtb_batch_destroy(mtb_batch* b);
+const char* mtb_last_error(mtb_batch* b);
+void mtb_free(void* p);
+
+/* Initial detached content (inserted locally before collaboration, like client.replay.spec.ts:27)
+ * and startOrUpdateCollaboration(observer_long_id, min_seq, cur_seq) (client.ts:1133). */
+int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_t n_units,
+                 const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq);
+
+/* Client.applyMsg(msg) with msg = JSON.stringify(ISequencedDocumentMessage).  Validates, interns the
+ * long client id and props, packs records and appends them to the document (no GPU work). */
+int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
+/* Pre-packed path: append records whose `payload` offsets index `payload` (UTF-16 units). */
+int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n,
+                   const uint16_t* payload, size_t payload_len);
+/* Register the long client id for the next short id of `doc` (used with mtb_append_ops). */
+int mtb_add_client(mtb_batch* b, uint32_t doc, const char* long_id);
+/* Intern a props object (JSON text); id 0 is reserved for "none". */
+int mtb_intern_props(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* id_out);
+
+/* Replay every pending op of every document on the GPU(s).  Blocking. */
+int mtb_replay(mtb_batch* b, mtb_stats* out);
+
+int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out);
+int mtb_get_length(mtb_batch* b, uint32_t doc, uint32_t* len_out);
+int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq);
+/* Canonical segment dump (JSON lines, engine-allocated; free with mtb_free). */
+int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len);
+/* Per-document state checksum (FNV-1a 64 over the canonical dump). */
+int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out);
+/* Client.summarize with newMergeTreeSnapshotFormat: if `msn`/`seq` >= 0 first runs
+ * updateSeqNumbers(msn, seq) (client.ts:979).  long_client_ids may be NULL (use registered ids). */
+int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,
+                     mtb_blob_list* out);
+void mtb_blob_list_free(mtb_blob_list* l);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

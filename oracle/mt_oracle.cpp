@@ -1,0 +1,1432 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — see mt_oracle.hpp for the contract.
+// Clean-room C++ restatement of the merge-tree remote-op (observer) path.  MT = packages/dds/merge-tree/src.
+#include "mt_oracle.hpp"
+
+#include <algorithm>
+#include <cassert>
+#include <functional>
+
+namespace orc {
+
+static constexpr int64_t MAX_SAFE = 9007199254740991LL;
+
+[[noreturn]] static void fail_assert(const char* code, const char* what) {
+  throw OracleError(-4, std::string(code) + " " + what);
+}
+[[noreturn]] static void fail_unsupported(const std::string& what) {
+  throw OracleError(-6, "unsupported: " + what);
+}
+
+// =====================================================================================
+// PartialSequenceLengthsSet  (MT/partialLengths.ts:19-95, MT/sortedSet.ts:45-71)
+// =====================================================================================
+std::pair<bool, size_t> PSLSet::find(int seq) const {
+  // SortedSet.findItemPosition -> lower_bound semantics
+  size_t lo = 0, hi = items.size();
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (items[mid].seq < seq) lo = mid + 1;
+    else hi = mid;
+  }
+  bool exists = lo < items.size() && items[lo].seq == seq;
+  return {exists, lo};
+}
+PSL* PSLSet::latestLeq(int seq) {
+  auto [exists, idx] = find(seq);
+  long i = exists ? (long)idx : (long)idx - 1;
+  return i >= 0 ? &items[i] : nullptr;
+}
+PSL* PSLSet::firstGte(int seq) {
+  auto [exists, idx] = find(seq);
+  (void)exists;
+  return idx < items.size() ? &items[idx] : nullptr;
+}
+static void combineOverlapClients(PSL& a, const PSL& b) {  // partialLengths.ts:1009-1027
+  if (a.overlap) {
+    if (b.overlap)
+      for (auto& kv : *b.overlap) (*a.overlap)[kv.first] += kv.second;
+  } else if (b.overlap) {
+    a.overlap = std::make_shared<std::map<int, int>>(*b.overlap);
+  }
+}
+void PSLSet::addOrUpdate(PSL item) {  // partialLengths.ts:24-47
+  PSL* prev = latestLeq(item.seq);
+  if (!prev || prev->seq != item.seq) item.len = (prev ? prev->len : 0) + item.seglen;
+  for (long i = (long)items.size() - 1; i >= 0; i--) {
+    if (items[i].seq <= item.seq) break;
+    items[i].len += item.seglen;
+  }
+  auto [exists, idx] = find(item.seq);
+  if (exists) {
+    PSL& cur = items[idx];
+    cur.seglen += item.seglen;
+    cur.len += item.seglen;
+    combineOverlapClients(cur, item);
+  } else {
+    items.insert(items.begin() + idx, std::move(item));
+  }
+}
+int PSLSet::copyDown(int minSeq) {  // partialLengths.ts:76-94
+  auto [exists, idx] = find(minSeq);
+  long mindex = exists ? (long)idx : (long)idx - 1;
+  int minLength = 0;
+  if (mindex >= 0) {
+    minLength = items[mindex].len;
+    size_t remaining = items.size() - mindex - 1;
+    for (size_t i = 0; i < remaining; i++) {
+      items[i] = items[i + mindex + 1];
+      items[i].len -= minLength;
+    }
+    items.resize(remaining);
+  }
+  return minLength;
+}
+
+// =====================================================================================
+// PartialSequenceLengths queries (partialLengths.ts:698-735, 809-819, 822-849)
+// =====================================================================================
+int PartialLengths::getPartialLength(int refSeq, int clientId) {
+  int pLen = minLength;
+  PSL* l = partialLengths.latestLeq(refSeq);
+  pLen += l ? l->len : 0;
+  auto it = clientSeqNumbers.find(clientId);
+  if (it != clientSeqNumbers.end() && !it->second.items.empty()) {
+    PSL& cliLatest = it->second.items.back();
+    if (cliLatest.seq > refSeq) {
+      pLen += cliLatest.len;
+      PSL* preceding = it->second.latestLeq(refSeq);
+      if (preceding) pLen -= preceding->len;
+    }
+  }
+  return pLen;
+}
+void PartialLengths::zamboni(const CollabWindow& w) {
+  minLength += partialLengths.copyDown(w.minSeq);
+  minSeq = w.minSeq;
+  for (auto& kv : clientSeqNumbers) kv.second.copyDown(w.minSeq);
+}
+void PartialLengths::addClientSeqNumber(int clientId, int seq, int seglen) {
+  PSL p;
+  p.seq = seq;
+  p.len = 0;
+  p.seglen = seglen;
+  clientSeqNumbers[clientId].addOrUpdate(p);
+}
+void PartialLengths::addClientSeqNumberFromPartial(const PSL& p) {
+  addClientSeqNumber(p.clientId, p.seq, p.seglen);
+  if (p.overlap)
+    for (auto& kv : *p.overlap)
+      if (p.clientId != kv.first) addClientSeqNumber(kv.first, p.seq, kv.second);
+}
+
+static void addSeq(PSLSet& set, int seq, int seqSeglen, int clientId) {  // partialLengths.ts:543-577
+  PSL* seqPartial = nullptr;
+  PSL* penult = nullptr;
+  PSL* p = set.latestLeq(seq);
+  if (p) {
+    if (p->seq == seq) {
+      seqPartial = p;
+      PSL* q = set.latestLeq(seq - 1);
+      if (q) penult = q;
+    } else {
+      penult = p;
+    }
+  }
+  int len = penult ? penult->len + seqSeglen : seqSeglen;
+  if (!seqPartial) {
+    PSL n;
+    n.clientId = clientId;
+    n.len = len;
+    n.seglen = seqSeglen;
+    n.seq = seq;
+    set.addOrUpdate(n);
+  } else {
+    seqPartial->seglen = seqSeglen;
+    seqPartial->len = len;
+  }
+}
+
+// =====================================================================================
+// MergeTree
+// =====================================================================================
+MergeTree::MergeTree(const Options& o) : options(o) {
+  root = makeBlock(0);
+  heap.push_back({nullptr, -2});  // LRUSegmentComparer.min (mergeTree.ts:112)
+}
+
+Block* MergeTree::makeBlock(int childCount) {
+  blockPool.emplace_back();
+  Block* b = &blockPool.back();
+  b->childCount = childCount;
+  return b;
+}
+
+// Heap (MT/collections/heap.ts:11-66) with compare = a.maxSeq - b.maxSeq
+void MergeTree::heapAdd(LRU x) {
+  heap.push_back(x);
+  size_t k = heap.size() - 1;
+  while (k > 1 && heap[k >> 1].maxSeq - heap[k].maxSeq > 0) {
+    std::swap(heap[k >> 1], heap[k]);
+    k >>= 1;
+  }
+}
+MergeTree::LRU MergeTree::heapGet() {
+  LRU x = heap[1];
+  size_t count = heap.size() - 1;
+  heap[1] = heap[count];
+  heap.pop_back();
+  count = heap.size() - 1;
+  size_t k = 1;
+  while ((k << 1) <= count) {
+    size_t j = k << 1;
+    if (j < count && heap[j].maxSeq - heap[j + 1].maxSeq > 0) j++;
+    if (heap[k].maxSeq - heap[j].maxSeq <= 0) break;
+    std::swap(heap[k], heap[j]);
+    k = j;
+  }
+  return x;
+}
+
+// localNetLength (mergeTree.ts:613-634), localSeq === undefined branch
+int MergeTree::localNetLength(const Seg* s) const {
+  if (s->removed) {
+    if (!options.newLengthCalc) {
+      int64_t norm = s->removedSeq == UnassignedSeq ? MAX_SAFE : s->removedSeq;
+      if (norm > window.minSeq) return 0;
+      return UNDEF_LEN;
+    }
+    return 0;
+  }
+  return s->cachedLength;
+}
+
+int MergeTree::bruteLength(Node* n, int refSeq, int clientId) {
+  if (n->leaf) {
+    int l = nodeLength(n, refSeq, clientId);
+    return l == UNDEF_LEN ? 0 : l;
+  }
+  Block* b = static_cast<Block*>(n);
+  int sum = 0;
+  for (int i = 0; i < b->childCount; i++) sum += bruteLength(b->children[i], refSeq, clientId);
+  return sum;
+}
+
+// nodeLength (mergeTree.ts:916-1004); returns UNDEF_LEN for `undefined`
+int MergeTree::nodeLength(Node* node, int refSeq, int clientId) {
+  if (!window.collaborating || window.clientId == clientId) {
+    if (node->leaf) return localNetLength(static_cast<Seg*>(node));
+    return node->cachedLength;
+  }
+  if (!node->leaf) {
+    Block* b = static_cast<Block*>(node);
+    int v = b->partial->getPartialLength(refSeq, clientId);
+    if (options.verify) {
+      int brute = 0;
+      for (int i = 0; i < b->childCount; i++) brute += bruteLength(b->children[i], refSeq, clientId);
+      if (brute != v)
+        throw OracleError(-4, "verify: partial length " + std::to_string(v) + " != leaf sum " + std::to_string(brute));
+    }
+    return v;
+  }
+  Seg* seg = static_cast<Seg*>(node);
+  if (options.newLengthCalc) {
+    int64_t seq = seg->seq == UnassignedSeq ? MAX_SAFE - 1 : seg->seq;
+    if (seg->removed) {
+      int64_t rs = seg->removedSeq == UnassignedSeq ? MAX_SAFE : seg->removedSeq;
+      if (rs <= window.minSeq) return UNDEF_LEN;
+      if (rs <= refSeq ||
+          std::find(seg->removedClientIds.begin(), seg->removedClientIds.end(), clientId) != seg->removedClientIds.end())
+        return 0;
+    }
+    return (seq <= refSeq || seg->clientId == clientId) ? seg->cachedLength : 0;
+  }
+  if (seg->removed && seg->removedSeq != UnassignedSeq && seg->removedSeq <= refSeq) return UNDEF_LEN;
+  if (seg->clientId == clientId || (seg->seq != UnassignedSeq && seg->seq <= refSeq)) {
+    if (seg->removed) {
+      return std::find(seg->removedClientIds.begin(), seg->removedClientIds.end(), clientId) != seg->removedClientIds.end()
+                 ? 0
+                 : seg->cachedLength;
+    }
+    return seg->cachedLength;
+  }
+  if (seg->removed && seg->removedSeq != UnassignedSeq) return UNDEF_LEN;
+  return 0;
+}
+
+int MergeTree::blockLength(Block* b, int refSeq, int clientId) {  // mergeTree.ts:884-888
+  return window.collaborating && clientId != window.clientId ? b->partial->getPartialLength(refSeq, clientId)
+                                                              : b->cachedLength;
+}
+
+// startCollaboration (mergeTree.ts:731-739)
+void MergeTree::startCollaboration(int localClientId, int minSeq, int currentSeq) {
+  window.clientId = localClientId;
+  window.minSeq = minSeq;
+  window.collaborating = true;
+  window.currentSeq = currentSeq;
+  heap.clear();
+  heap.push_back({nullptr, -2});
+  heapValid = true;
+  nodeUpdateLengthNewStructure(root, true);
+}
+
+// addToLRUSet (mergeTree.ts:741-751)
+void MergeTree::addToLRUSet(Seg* s, int seq) {
+  if (s->parent->needsScour != 1 && seq > window.currentSeq) {
+    s->parent->needsScour = 1;
+    heapAdd({s, seq});
+  }
+}
+
+// setMinSeq (mergeTree.ts:1025-1044)
+void MergeTree::setMinSeq(int minSeq) {
+  if (!(minSeq <= window.currentSeq)) fail_assert("0x04e", "Trying to set minSeq above currentSeq of collab window!");
+  if (!(window.minSeq <= minSeq)) fail_assert("0x04f", "minSeq of collab window > target minSeq!");
+  if (minSeq > window.minSeq) {
+    window.minSeq = minSeq;
+    zamboniSegments();
+  }
+}
+
+// breakTie (mergeTree.ts:1719-1738)
+bool MergeTree::breakTie(int pos, Node* node, int seq) {
+  if (node->leaf) {
+    if (pos == 0) {
+      int64_t newSeq = seq == UnassignedSeq ? MAX_SAFE : seq;
+      Seg* s = static_cast<Seg*>(node);
+      int64_t segSeq = s->seq == UnassignedSeq ? MAX_SAFE - 1 : s->seq;
+      return newSeq > segSeq;
+    }
+    return false;
+  }
+  return true;
+}
+
+// BaseSegment.splitAt + TextSegment.createSplitSegmentAt (mergeTreeNodes.ts:481-523, textSegment.ts:106-114)
+Seg* MergeTree::splitAt(Seg* s, int pos) {
+  if (pos <= 0 || s->isMarker) return nullptr;  // Marker.createSplitSegmentAt -> undefined
+  Seg* r = newSeg();
+  r->text = s->text.substr(pos);
+  s->text.resize(pos);
+  s->cachedLength = (int)s->text.size();
+  r->cachedLength = (int)r->text.size();
+  if (s->hasPropManager && s->props) {  // copyPropertiesTo
+    r->hasPropManager = true;
+    r->props = *s->props;
+  }
+  r->parent = s->parent;
+  r->removed = s->removed;
+  r->removedClientIds = s->removedClientIds;
+  r->removedSeq = s->removedSeq;
+  r->seq = s->seq;
+  r->clientId = s->clientId;
+  return r;
+}
+
+MergeTree::Changes MergeTree::leafAction(InsertCtx& ctx, Seg* segment, int pos) {
+  Changes c;
+  if (ctx.insertMode) {  // blockInsert.onLeaf (mergeTree.ts:1644-1654)
+    if (segment) {
+      c.replaceCurrent = ctx.candidate;
+      c.next = segment;
+    } else {
+      c.next = ctx.candidate;
+    }
+  } else {  // splitLeafSegment (mergeTree.ts:1686-1704)
+    if (!(pos > 0 && segment)) return c;
+    Seg* next = splitAt(segment, pos);
+    c.next = next;
+  }
+  return c;
+}
+
+// blockInsert.continueFrom: forwardExcursion(block) looking at the first following segment
+// (mergeTree.ts:1611-1615, mergeTreeNodeWalk.ts:121-138)
+bool MergeTree::continuePredicate(Block* node) {
+  // find first leaf after `node` in tree order
+  Node* cur = node;
+  while (cur->parent) {
+    Block* p = cur->parent;
+    for (int i = cur->index + 1; i < p->childCount; i++) {
+      Node* c = p->children[i];
+      while (c && !c->leaf) {
+        Block* cb = static_cast<Block*>(c);
+        c = cb->childCount > 0 ? cb->children[0] : nullptr;
+        if (!c) break;
+      }
+      if (c && c->leaf) return static_cast<Seg*>(c)->seq == UnassignedSeq;
+    }
+    cur = p;
+  }
+  return false;
+}
+
+// insertingWalk (mergeTree.ts:1740-1856)
+Block* MergeTree::insertingWalk(Block* block, int pos, int refSeq, int clientId, int seq, InsertCtx& ctx) {
+  int _pos = pos;
+  int childIndex;
+  Node* newNode = nullptr;
+  Block* fromSplit = nullptr;
+  for (childIndex = 0; childIndex < block->childCount; childIndex++) {
+    Node* child = block->children[childIndex];
+    int len = nodeLength(child, refSeq, clientId);
+    if (len == UNDEF_LEN) continue;
+    if (len < 0) fail_assert("0x4bc", "Length should not be negative");
+    if (_pos < len || (_pos == len && breakTie(_pos, child, seq))) {
+      if (!child->leaf) {
+        Block* splitNode = insertingWalk(static_cast<Block*>(child), _pos, refSeq, clientId, seq, ctx);
+        if (splitNode == nullptr) {
+          blockUpdateLength(block, seq, clientId);
+          return nullptr;
+        } else if (splitNode == UNFINISHED) {
+          _pos -= len;
+          continue;
+        } else {
+          newNode = splitNode;
+          fromSplit = splitNode;
+          childIndex++;
+        }
+      } else {
+        Seg* segment = static_cast<Seg*>(child);
+        Changes ch = leafAction(ctx, segment, _pos);
+        if (ch.replaceCurrent) block->assignChild(ch.replaceCurrent, childIndex);
+        if (ch.next) {
+          newNode = ch.next;
+          childIndex++;
+        } else {
+          return nullptr;
+        }
+      }
+      break;
+    } else {
+      _pos -= len;
+    }
+  }
+  if (!newNode) {
+    if (_pos == 0) {
+      if (seq != UnassignedSeq && ctx.insertMode && continuePredicate(block)) {
+        return UNFINISHED;
+      } else {
+        Changes ch = leafAction(ctx, nullptr, _pos);
+        newNode = ch.next;
+      }
+    }
+  }
+  if (newNode) {
+    if ((int)block->children.size() <= block->childCount) block->children.resize(block->childCount + 1, nullptr);
+    for (int i = block->childCount; i > childIndex; i--) {
+      block->children[i] = block->children[i - 1];
+      block->children[i]->index = i;
+    }
+    block->assignChild(newNode, childIndex);
+    block->childCount++;
+    (void)fromSplit;  // ordinals are not modelled (local references only)
+    if (block->childCount < MaxNodesInBlock) {
+      blockUpdateLength(block, seq, clientId);
+      return nullptr;
+    }
+    return split(block);
+  }
+  return nullptr;
+}
+
+// split (mergeTree.ts:1858-1871)
+Block* MergeTree::split(Block* node) {
+  const int half = MaxNodesInBlock / 2;
+  Block* nb = makeBlock(half);
+  node->childCount = half;
+  for (int i = 0; i < half; i++) {
+    nb->assignChild(node->children[half + i], i);
+    node->children[half + i] = nullptr;
+  }
+  nodeUpdateLengthNewStructure(node);
+  nodeUpdateLengthNewStructure(nb);
+  return nb;
+}
+
+// updateRoot (mergeTree.ts:1268-1277)
+void MergeTree::updateRoot(Block* splitNode) {
+  if (splitNode) {
+    Block* nr = makeBlock(2);
+    nr->assignChild(root, 0);
+    nr->assignChild(splitNode, 1);
+    root = nr;
+    nodeUpdateLengthNewStructure(root);
+  }
+}
+
+// ensureIntervalBoundary (mergeTree.ts:1706-1716)
+void MergeTree::ensureIntervalBoundary(int pos, int refSeq, int clientId) {
+  InsertCtx ctx;
+  ctx.insertMode = false;
+  Block* sn = insertingWalk(root, pos, refSeq, clientId, TreeMaintenanceSeq, ctx);
+  updateRoot(sn);
+}
+
+// blockInsert (mergeTree.ts:1594-1685), single segment
+void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg) {
+  if (seg->cachedLength > 0) {
+    seg->seq = seq;
+    seg->clientId = clientId;
+    InsertCtx ctx;
+    ctx.insertMode = true;
+    ctx.candidate = seg;
+    Block* sn = insertingWalk(root, pos, refSeq, clientId, seq, ctx);
+    if (seg->parent == nullptr) throw OracleError(-5, "MergeTree insert failed");
+    updateRoot(sn);
+    // saveIfLocal (mergeTree.ts:1617-1637)
+    if (window.collaborating) {
+      if (seg->seq == UnassignedSeq && clientId == window.clientId) {
+        fail_unsupported("local pending segment");
+      } else if (seg->seq > window.minSeq) {
+        addToLRUSet(seg, seg->seq);
+      }
+    }
+    counters.segsTouched += 1;
+  }
+}
+
+// insertSegments (mergeTree.ts:1397-1427)
+void MergeTree::insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
+  ensureIntervalBoundary(pos, refSeq, clientId);
+  blockInsert(pos, refSeq, clientId, seq, seg);
+  if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
+}
+
+// blockUpdate (mergeTree.ts:2392-2417): cachedLength = sum(nodeTotalLength ?? 0)
+void MergeTree::blockUpdate(Block* b) {
+  int len = 0;
+  for (int i = 0; i < b->childCount; i++) {
+    Node* c = b->children[i];
+    int l = c->leaf ? localNetLength(static_cast<Seg*>(c)) : c->cachedLength;
+    len += l == UNDEF_LEN ? 0 : l;
+  }
+  b->cachedLength = len;
+}
+
+// nodeUpdateLengthNewStructure (mergeTree.ts:2188-2194)
+void MergeTree::nodeUpdateLengthNewStructure(Block* b, bool recur) {
+  blockUpdate(b);
+  if (window.collaborating) b->partial = combine(b, recur);
+}
+
+// blockUpdateLength (mergeTree.ts:2436-2454)
+void MergeTree::blockUpdateLength(Block* b, int seq, int clientId) {
+  blockUpdate(b);
+  if (window.collaborating && seq != UnassignedSeq && seq != TreeMaintenanceSeq) {
+    if (b->partial && clientId != NonCollabClient) plUpdate(*b->partial, b, seq, clientId);
+    else b->partial = combine(b, false);
+  }
+}
+
+// blockUpdatePathLengths (mergeTree.ts:2419-2434)
+void MergeTree::blockUpdatePathLengths(Block* b, int seq, int clientId, bool newStructure) {
+  while (b) {
+    if (newStructure) nodeUpdateLengthNewStructure(b);
+    else blockUpdateLength(b, seq, clientId);
+    b = b->parent;
+  }
+}
+
+// ---------------------------------------------------------------- partial lengths construction
+void MergeTree::plInsertSegment(PartialLengths& pl, Seg* s, bool removal) {  // partialLengths.ts:444-541
+  int seq = s->seq;
+  int segLen = s->cachedLength;
+  int clientId = s->clientId;
+  const std::vector<int>* overlap = nullptr;
+  if (removal) {
+    seq = s->removedSeq;
+    segLen = -segLen;
+    clientId = s->removedClientIds[0];
+    if (s->removedClientIds.size() > 1) overlap = &s->removedClientIds;
+  }
+  PSL* firstGte = pl.partialLengths.firstGte(seq);
+  if (firstGte && firstGte->seq == seq) {
+    firstGte->seglen += segLen;
+    if (overlap) {  // accumulateRemoveClientOverlap (partialLengths.ts:405-425)
+      if (firstGte->overlap) {
+        for (int c : *overlap) (*firstGte->overlap)[c] += segLen;
+      } else {
+        firstGte->overlap = std::make_shared<std::map<int, int>>();
+        for (int c : *overlap) (*firstGte->overlap)[c] = segLen;
+      }
+    }
+  } else {
+    PSL e;
+    e.seq = seq;
+    e.clientId = clientId;
+    e.len = 0;
+    e.seglen = segLen;
+    if (overlap) {
+      e.overlap = std::make_shared<std::map<int, int>>();
+      for (int c : *overlap) (*e.overlap)[c] = segLen;  // getOverlapClients: put overwrites
+    }
+    pl.partialLengths.addOrUpdate(e);
+  }
+}
+
+std::unique_ptr<PartialLengths> MergeTree::fromLeaves(Block* b) {  // partialLengths.ts:344-403
+  auto pl = std::make_unique<PartialLengths>();
+  pl->minSeq = window.minSeq;
+  pl->segmentCount = b->childCount;
+  auto seqLTE = [&](int seq) { return seq != UnassignedSeq && seq <= window.minSeq; };
+  for (int i = 0; i < b->childCount; i++) {
+    Node* c = b->children[i];
+    if (!c->leaf) continue;
+    Seg* s = static_cast<Seg*>(c);
+    if (seqLTE(s->seq)) pl->minLength += s->cachedLength;
+    else plInsertSegment(*pl, s, false);
+    if (s->removed && seqLTE(s->removedSeq)) pl->minLength -= s->cachedLength;
+    else if (s->removed) plInsertSegment(*pl, s, true);
+  }
+  int prevLen = 0;
+  for (auto& p : pl->partialLengths.items) {
+    p.len = prevLen + p.seglen;
+    prevLen = p.len;
+    pl->addClientSeqNumberFromPartial(p);
+  }
+  return pl;
+}
+
+std::unique_ptr<PartialLengths> MergeTree::combine(Block* b, bool recur) {  // partialLengths.ts:256-338
+  auto leafPL = fromLeaves(b);
+  bool hasInternal = false;
+  std::vector<PartialLengths*> childPartials;
+  for (int i = 0; i < b->childCount; i++) {
+    Node* c = b->children[i];
+    if (!c->leaf) {
+      hasInternal = true;
+      Block* cb = static_cast<Block*>(c);
+      if (recur) cb->partial = combine(cb, true);
+      childPartials.push_back(cb->partial.get());
+    }
+  }
+  std::unique_ptr<PartialLengths> combined;
+  if (hasInternal) {
+    combined = std::make_unique<PartialLengths>();
+    combined->minSeq = window.minSeq;
+    if (!leafPL->partialLengths.items.empty()) childPartials.push_back(leafPL.get());
+    std::vector<const std::vector<PSL>*> lists;
+    for (auto* cp : childPartials) {
+      combined->segmentCount += cp->segmentCount;
+      combined->minLength += cp->minLength;
+      lists.push_back(&cp->partialLengths.items);
+    }
+    // mergePartialLengths + mergeSortedListsBySeq (partialLengths.ts:1013-1060)
+    std::vector<size_t> next(lists.size(), 0);
+    while (true) {
+      long best = -1;
+      for (size_t i = 0; i < lists.size(); i++) {
+        if (next[i] < lists[i]->size()) {
+          if (best < 0 || (*lists[i])[next[i]].seq < (*lists[best])[next[best]].seq) best = (long)i;
+        }
+      }
+      if (best < 0) break;
+      PSL item = (*lists[best])[next[best]++];
+      if (item.overlap) item.overlap = std::make_shared<std::map<int, int>>(*item.overlap);
+      combined->partialLengths.addOrUpdate(item);
+    }
+    for (auto& p : combined->partialLengths.items) combined->addClientSeqNumberFromPartial(p);
+  } else {
+    combined = std::move(leafPL);
+  }
+  combined->zamboni(window);
+  return combined;
+}
+
+void MergeTree::plUpdate(PartialLengths& pl, Block* node, int seq, int clientId) {  // partialLengths.ts:636-686
+  int seqSeglen = 0;
+  int segCount = 0;
+  for (int i = 0; i < node->childCount; i++) {
+    Node* c = node->children[i];
+    if (!c->leaf) {
+      Block* cb = static_cast<Block*>(c);
+      PSL* leq = cb->partial->partialLengths.latestLeq(seq);
+      if (leq && leq->seq == seq) seqSeglen += leq->seglen;
+      segCount += cb->partial->segmentCount;
+    } else {
+      Seg* s = static_cast<Seg*>(c);
+      if (s->seq == seq) {
+        if (!(s->removed && s->removedSeq == seq)) seqSeglen += s->cachedLength;
+      } else if (s->removed && s->removedSeq == seq) {
+        seqSeglen -= s->cachedLength;
+      }
+      segCount++;
+    }
+  }
+  pl.segmentCount = segCount;
+  addSeq(pl.partialLengths, seq, seqSeglen, clientId);
+  addSeq(pl.clientSeqNumbers[clientId], seq, seqSeglen, 0);
+  pl.zamboni(window);
+}
+
+// ---------------------------------------------------------------- nodeMap / depthFirstNodeWalk
+// nodeMap (mergeTree.ts:2531-2582) over depthFirstNodeWalk (mergeTreeNodeWalk.ts:35-115)
+template <class Leaf, class Post>
+void MergeTree::nodeMap(int refSeq, int clientId, Leaf&& leaf, Post&& post, int start, int end) {
+  int endPos = end;
+  if (endPos == start) return;
+  int pos = 0;
+  enum { CONTINUE = 0, EXIT = 1, SKIP = 2 };
+  auto down = [&](Node* node) -> int {
+    if (endPos <= pos) return EXIT;
+    int len = nodeLength(node, refSeq, clientId);
+    if (len == UNDEF_LEN || len == 0) return SKIP;
+    int nextPos = pos + len;
+    if (start >= nextPos) {
+      pos = nextPos;
+      return SKIP;
+    }
+    if (node->leaf) {
+      if (!leaf(static_cast<Seg*>(node), pos, start - pos, endPos - pos)) return EXIT;
+      pos = nextPos;
+    }
+    return CONTINUE;
+  };
+  Block* block = root;
+  int childCount = block->childCount;
+  Node* startNode = block->childCount > 0 ? block->children[0] : nullptr;
+  while (true) {
+    int blockResult = CONTINUE;
+    while (startNode && !startNode->leaf) {
+      block = static_cast<Block*>(startNode);
+      childCount = block->childCount;
+      blockResult = down(block);
+      startNode = blockResult == CONTINUE ? (childCount > 0 ? block->children[0] : nullptr) : nullptr;
+    }
+    bool exitFlag = blockResult == EXIT;
+    if (startNode) {
+      for (int i = startNode->index; i != -1 && i != childCount; i++) {
+        if (down(block->children[i]) == EXIT) {
+          exitFlag = true;
+          break;
+        }
+      }
+    }
+    int nextIndex = -1;
+    do {
+      if (blockResult == CONTINUE) post(block);
+      else blockResult = CONTINUE;
+      if (block->parent == nullptr) return;
+      startNode = block;
+      block = block->parent;
+      childCount = block->childCount;
+      nextIndex = startNode->index + 1;
+    } while (exitFlag || nextIndex == -1 || nextIndex == childCount);
+    startNode = block->children[nextIndex];
+  }
+}
+
+// markRangeRemoved (mergeTree.ts:1960-2052), remote (sequenced) ops only
+void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {
+  bool overwrite = false;
+  ensureIntervalBoundary(start, refSeq, clientId);
+  ensureIntervalBoundary(end, refSeq, clientId);
+  auto markRemoved = [&](Seg* s, int, int, int) -> bool {
+    if (s->removed) {
+      overwrite = true;
+      if (s->removedSeq == UnassignedSeq) fail_unsupported("local pending remove");
+      s->removedClientIds.push_back(clientId);
+    } else {
+      s->removed = true;
+      s->removedClientIds = {clientId};
+      s->removedSeq = seq;
+    }
+    counters.segsTouched += 1;
+    if (window.collaborating) {
+      if (s->removedSeq == UnassignedSeq && clientId == window.clientId) fail_unsupported("local pending remove");
+      addToLRUSet(s, seq);
+    }
+    return true;
+  };
+  auto post = [&](Block* b) {
+    if (overwrite) nodeUpdateLengthNewStructure(b);
+    else blockUpdateLength(b, seq, clientId);
+  };
+  nodeMap(refSeq, clientId, markRemoved, post, start, end);
+  if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
+}
+
+// PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) for a sequenced remote op or a
+// non-collaborating local op (no pending local state), combined with BaseSegment.addProperties.
+static void applyProps(Seg* s, const JObj& newProps, bool rewrite) {
+  s->hasPropManager = true;
+  if (!s->props) s->props = JObj();
+  JObj& old = *s->props;
+  if (rewrite) {
+    std::vector<u16str> keys;
+    for (auto& kv : old) keys.push_back(kv.first);
+    for (auto& k : keys) {
+      const JVal* nv = obj_get(newProps, k);
+      if (js_falsy(nv)) obj_del(old, k);
+    }
+  }
+  for (auto& kv : newProps) {
+    if (kv.second.t == JVal::Null) obj_del(old, kv.first);
+    else obj_set(old, kv.first, kv.second);
+  }
+}
+
+// annotateRange (mergeTree.ts:1895-1958)
+void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq) {
+  ensureIntervalBoundary(start, refSeq, clientId);
+  ensureIntervalBoundary(end, refSeq, clientId);
+  auto annotate = [&](Seg* s, int, int, int) -> bool {
+    applyProps(s, props, rewrite);
+    counters.segsTouched += 1;
+    if (window.collaborating) {
+      if (seq == UnassignedSeq) fail_unsupported("local pending annotate");
+      addToLRUSet(s, seq);
+    }
+    return true;
+  };
+  auto post = [&](Block*) {};
+  nodeMap(refSeq, clientId, annotate, post, start, end);
+  if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
+}
+
+// ---------------------------------------------------------------- zamboni (MT/zamboni.ts)
+static bool canAppend(const Seg* a, const Seg* b) {  // TextSegment.canAppend (textSegment.ts:71-78)
+  if (a->isMarker || b->isMarker) return false;
+  if (!a->text.empty() && a->text.back() == u'\n') return false;
+  return a->cachedLength <= TextSegmentGranularity || b->cachedLength <= TextSegmentGranularity;
+}
+static const JVal* propsAsVal(const Seg* s, JVal& holder) {
+  if (!s->props) return nullptr;
+  holder.t = JVal::Obj;
+  holder.obj = *s->props;
+  return &holder;
+}
+static bool matchSegProps(const Seg* a, const Seg* b) {
+  JVal ha, hb;
+  return match_properties(propsAsVal(a, ha), propsAsVal(b, hb));
+}
+
+void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {  // zamboni.ts:122-193
+  Seg* prev = nullptr;
+  for (int k = 0; k < node->childCount; k++) {
+    Node* c = node->children[k];
+    if (c->leaf) {
+      Seg* s = static_cast<Seg*>(c);
+      if (s->removed) {
+        if (s->removedSeq > window.minSeq) hold.push_back(s);
+        else s->parent = nullptr;  // unlink
+        prev = nullptr;
+      } else {
+        if (s->seq <= window.minSeq) {
+          int ln = localNetLength(s);
+          bool ok = prev && canAppend(prev, s) && matchSegProps(prev, s) && (ln == UNDEF_LEN ? 0 : ln) > 0;
+          if (ok) {
+            prev->text += s->text;  // TextSegment.append
+            prev->cachedLength += s->cachedLength;
+            s->parent = nullptr;
+          } else {
+            hold.push_back(s);
+            prev = (ln == UNDEF_LEN ? 0 : ln) > 0 ? s : nullptr;
+          }
+        } else {
+          hold.push_back(s);
+          prev = nullptr;
+        }
+      }
+    } else {
+      hold.push_back(c);
+      prev = nullptr;
+    }
+  }
+}
+
+void MergeTree::packParent(Block* parent) {  // zamboni.ts:63-120
+  std::vector<Node*> hold;
+  for (int i = 0; i < parent->childCount; i++) {
+    Block* cb = static_cast<Block*>(parent->children[i]);
+    scourNode(cb, hold);
+    cb->parent = nullptr;
+  }
+  if (!hold.empty()) {
+    int total = (int)hold.size();
+    int half = MaxNodesInBlock / 2;
+    int childCount = std::min(MaxNodesInBlock - 1, total / half);
+    if (childCount < 1) childCount = 1;
+    int base = total / childCount;
+    int rem = total % childCount;
+    std::vector<Block*> packed;
+    int packedCount = 0;
+    for (int ni = 0; ni < childCount; ni++) {
+      int n = base;
+      if (rem > 0) { n++; rem--; }
+      Block* pb = makeBlock(n);
+      if ((int)pb->children.size() < n) pb->children.resize(n, nullptr);
+      for (int j = 0; j < n; j++) pb->assignChild(hold[packedCount++], j);
+      pb->parent = parent;
+      packed.push_back(pb);
+      nodeUpdateLengthNewStructure(pb);
+    }
+    parent->children.assign(std::max(MaxNodesInBlock, childCount), nullptr);
+    for (int j = 0; j < childCount; j++) parent->assignChild(packed[j], j);
+    parent->childCount = childCount;
+  } else {
+    parent->children.assign(MaxNodesInBlock, nullptr);
+    parent->childCount = 0;
+  }
+  if (parent->childCount < MaxNodesInBlock / 2 && parent->parent) {
+    packParent(parent->parent);
+  } else {
+    blockUpdatePathLengths(parent, UnassignedSeq, -1, true);
+  }
+}
+
+void MergeTree::zamboniSegments() {  // zamboni.ts:19-60
+  if (!window.collaborating) return;
+  for (int i = 0; i < ZamboniSegmentsMax; i++) {
+    if (heap.size() <= 1) break;
+    LRU top = heap[1];
+    if (top.maxSeq > window.minSeq) break;
+    top = heapGet();
+    Seg* s = top.seg;
+    if (s->parent && s->parent->needsScour != 0) {
+      Block* block = s->parent;
+      std::vector<Node*> copy;
+      scourNode(block, copy);
+      block->needsScour = 0;
+      int newCount = (int)copy.size();
+      if (newCount < block->childCount) {
+        block->childCount = newCount;
+        block->children.assign(std::max(MaxNodesInBlock, newCount), nullptr);
+        for (int j = 0; j < newCount; j++) block->assignChild(copy[j], j);
+        if (block->childCount < MaxNodesInBlock / 2 && block->parent) {
+          packParent(block->parent);
+        } else {
+          blockUpdatePathLengths(block, UnassignedSeq, -1, true);
+        }
+      }
+    }
+  }
+}
+
+template <class F>
+void MergeTree::walkAllSegments(F&& f) {
+  std::function<void(Block*)> rec = [&](Block* b) {
+    for (int i = 0; i < b->childCount; i++) {
+      Node* c = b->children[i];
+      if (c->leaf) f(static_cast<Seg*>(c));
+      else rec(static_cast<Block*>(c));
+    }
+  };
+  rec(root);
+}
+
+// getText (MergeTreeTextHelper.ts:20-81) at (currentSeq, local client): visible text segments
+u16str MergeTree::getText() {
+  u16str out;
+  walkAllSegments([&](Seg* s) {
+    int l = nodeLength(s, window.currentSeq, window.clientId);
+    if (l != UNDEF_LEN && l > 0 && !s->isMarker) out += s->text;
+  });
+  return out;
+}
+
+// =====================================================================================
+// Doc (Client)
+// =====================================================================================
+int Doc::getOrAddShortClientId(const std::string& id) {  // client.ts:673-688
+  auto it = longToShort.find(id);
+  if (it != longToShort.end()) return it->second;
+  int s = (int)longIds.size();
+  longToShort[id] = s;
+  longIds.push_back(id);
+  return s;
+}
+std::string Doc::getLongClientId(int s) const {
+  return s >= 0 ? longIds.at(s) : std::string("original");
+}
+
+void Doc::startOrUpdateCollaboration(const std::string& id, int minSeq, int curSeq) {  // client.ts:1133-1146
+  if (!longClientId) {
+    longClientId = id;
+    int s = getOrAddShortClientId(id);
+    mt.startCollaboration(s, minSeq, curSeq);
+  } else {
+    int old = longToShort.at(*longClientId);
+    longClientId = id;
+    longToShort[id] = old;
+    longIds[old] = id;
+  }
+}
+
+void Doc::updateSeqNumbers(int min, int seq) {  // client.ts:877-887
+  if (!(mt.window.currentSeq <= seq)) fail_assert("0x038", "Incoming op sequence# < local collabWindow's currentSequence#");
+  mt.window.currentSeq = seq;
+  if (!(min <= seq)) fail_assert("0x039", "Incoming op sequence# < minSequence#");
+  mt.setMinSeq(min);
+}
+
+// Props of a segment spec: TextSegment.make(text, props) -> addProperties (textSegment.ts:35-40)
+JObj propsFromSpec(const JVal* spec) {
+  JObj o;
+  if (!spec || spec->t != JVal::Obj) return o;
+  for (auto& kv : spec->obj)
+    if (kv.second.t != JVal::Null) obj_set(o, kv.first, kv.second);
+  return o;
+}
+
+static Seg* makeSegFromSpec(MergeTree& mt, const JVal& spec) {  // testClient.ts:38-50 specToSegment
+  if (spec.t == JVal::Str) {
+    Seg* s = mt.newSeg();
+    s->text = spec.str;
+    s->cachedLength = (int)s->text.size();
+    return s;
+  }
+  if (spec.t == JVal::Obj) {
+    const JVal* text = obj_get(spec.obj, u"text");
+    const JVal* props = obj_get(spec.obj, u"props");
+    if (text) {
+      if (text->t != JVal::Str) fail_unsupported("non-string text segment");
+      Seg* s = mt.newSeg();
+      s->text = text->str;
+      s->cachedLength = (int)s->text.size();
+      if (props && !js_falsy(props)) {
+        s->hasPropManager = true;
+        s->props = propsFromSpec(props);
+      }
+      return s;
+    }
+    const JVal* marker = obj_get(spec.obj, u"marker");
+    if (marker) {
+      Seg* s = mt.newSeg();
+      s->isMarker = true;
+      s->cachedLength = 1;
+      const JVal* rt = marker->t == JVal::Obj ? obj_get(marker->obj, u"refType") : nullptr;
+      s->refType = (rt && rt->t == JVal::Num) ? (int)rt->num : -1;
+      if (props && !js_falsy(props)) {
+        s->hasPropManager = true;
+        s->props = propsFromSpec(props);
+      }
+      return s;
+    }
+  }
+  throw OracleError(-8, "Unrecognized IJSONSegment type");
+}
+
+static int getPos(const JVal& op, const char16_t* key, const char16_t* relKey) {
+  const JVal* p = obj_get(op.obj, key);
+  if (p && p->t == JVal::Num) return (int)p->num;
+  if (obj_get(op.obj, relKey)) fail_unsupported("relative positions");
+  fail_unsupported("missing position");
+}
+
+// applyRemoteOp (client.ts:802-829) for one decoded delta op
+void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
+  const JVal* type = obj_get(op.obj, u"type");
+  int t = type && type->t == JVal::Num ? (int)type->num : -1;
+  mt.counters.ops += (t >= 0 && t <= 2) ? 1 : 0;
+  switch (t) {
+    case 0: {  // applyInsertOp (client.ts:489-524)
+      int pos = getPos(op, u"pos1", u"relativePos1");
+      const JVal* spec = obj_get(op.obj, u"seg");
+      if (js_falsy(spec)) return;
+      Seg* s = makeSegFromSpec(mt, *spec);
+      mt.insertSegments(pos, s, refSeq, client, seq);
+      break;
+    }
+    case 1: {  // applyRemoveRangeOp (client.ts:430-455)
+      int a = getPos(op, u"pos1", u"relativePos1");
+      int b = getPos(op, u"pos2", u"relativePos2");
+      mt.markRangeRemoved(a, b, refSeq, client, seq);
+      break;
+    }
+    case 2: {  // applyAnnotateRangeOp (client.ts:457-487)
+      int a = getPos(op, u"pos1", u"relativePos1");
+      int b = getPos(op, u"pos2", u"relativePos2");
+      const JVal* props = obj_get(op.obj, u"props");
+      const JVal* comb = obj_get(op.obj, u"combiningOp");
+      bool rewrite = false;
+      if (comb && comb->t == JVal::Obj) {
+        const JVal* name = obj_get(comb->obj, u"name");
+        if (name && name->t == JVal::Str && name->str == u"rewrite") rewrite = true;
+        else fail_unsupported("combiningOp other than rewrite");
+      }
+      JObj p;
+      if (props && props->t == JVal::Obj) p = props->obj;
+      mt.annotateRange(a, b, p, rewrite, refSeq, client, seq);
+      break;
+    }
+    case 3: {  // GROUP (client.ts:816-824)
+      const JVal* ops = obj_get(op.obj, u"ops");
+      if (ops && ops->t == JVal::Arr)
+        for (auto& m : ops->arr) applyRemoteDelta(m, client, refSeq, seq);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+// applyMsg (client.ts:858-875)
+void Doc::applyMsg(const JVal& msg) {
+  if (msg.t != JVal::Obj) throw OracleError(-8, "message is not an object");
+  const JVal* cid = obj_get(msg.obj, u"clientId");
+  if (!cid || cid->t != JVal::Str) fail_unsupported("message without string clientId");
+  std::string longId = u16_to_utf8(cid->str);
+  int client = getOrAddShortClientId(longId);
+  auto num = [&](const char16_t* k) {
+    const JVal* v = obj_get(msg.obj, k);
+    if (!v || v->t != JVal::Num) throw OracleError(-8, "missing numeric field");
+    return (int)v->num;
+  };
+  int seq = num(u"sequenceNumber");
+  int refSeq = num(u"referenceSequenceNumber");
+  int msn = num(u"minimumSequenceNumber");
+  const JVal* type = obj_get(msg.obj, u"type");
+  if (type && type->t == JVal::Str && type->str == u"op") {
+    const JVal* contents = obj_get(msg.obj, u"contents");
+    if (!contents || contents->t != JVal::Obj) throw OracleError(-8, "op without contents");
+    if (longClientId && longId == *longClientId) {
+      // ackPendingSegment with no pending segment groups: one zamboni per member (mergeTree.ts:1283-1321)
+      const JVal* t = obj_get(contents->obj, u"type");
+      if (t && t->t == JVal::Num && (int)t->num == 3) {
+        const JVal* ops = obj_get(contents->obj, u"ops");
+        if (ops && ops->t == JVal::Arr)
+          for (size_t i = 0; i < ops->arr.size(); i++) mt.zamboniSegments();
+      } else {
+        mt.zamboniSegments();
+      }
+    } else {
+      applyRemoteDelta(*contents, client, refSeq, seq);
+    }
+  }
+  updateSeqNumbers(msn, seq);
+}
+
+void Doc::applyRecord(const Record& r, const uint16_t* text, const std::vector<std::string>& propsJson) {
+  auto propsOf = [&](uint32_t id) -> std::optional<JVal> {
+    if (id == 0) return std::nullopt;
+    if (id >= propsJson.size()) throw OracleError(-1, "bad props id");
+    return json_parse(propsJson[id]);
+  };
+  switch (r.type) {
+    case 0: {
+      mt.counters.ops++;
+      Seg* s = mt.newSeg();
+      if (r.flags & 0x02) {
+        s->isMarker = true;
+        s->cachedLength = 1;
+        s->refType = r.pos2 == 0xFFFFFFFFu ? -1 : (int)r.pos2;
+      } else {
+        s->text.assign(reinterpret_cast<const char16_t*>(text + r.payload), r.pos2);
+        s->cachedLength = (int)r.pos2;
+      }
+      auto p = propsOf(r.props);
+      if (p && !js_falsy(&*p)) {
+        s->hasPropManager = true;
+        s->props = propsFromSpec(&*p);
+      }
+      mt.insertSegments((int)r.pos1, s, (int)r.refSeq, r.client, (int)r.seq);
+      break;
+    }
+    case 1:
+      mt.counters.ops++;
+      mt.markRangeRemoved((int)r.pos1, (int)r.pos2, (int)r.refSeq, r.client, (int)r.seq);
+      break;
+    case 2: {
+      mt.counters.ops++;
+      auto p = propsOf(r.props);
+      JObj o;
+      if (p && p->t == JVal::Obj) o = p->obj;
+      mt.annotateRange((int)r.pos1, (int)r.pos2, o, (r.flags & 0x04) != 0, (int)r.refSeq, r.client, (int)r.seq);
+      break;
+    }
+    case 4:
+      mt.zamboniSegments();
+      break;
+    default:
+      break;
+  }
+  if (r.flags & 0x01) updateSeqNumbers((int)r.msn, (int)r.seq);
+}
+
+// ---------------------------------------------------------------- local (detached) edits
+void Doc::insertTextLocal(int pos, const u16str& text, const std::optional<JObj>& props) {
+  Seg* s = mt.newSeg();
+  s->text = text;
+  s->cachedLength = (int)text.size();
+  if (props) { s->hasPropManager = true; s->props = *props; }
+  int seq = mt.window.collaborating ? UnassignedSeq : UniversalSeq;
+  if (mt.window.collaborating) fail_unsupported("local edits while collaborating");
+  mt.insertSegments(pos, s, mt.window.currentSeq, mt.window.clientId, seq);
+}
+void Doc::insertMarkerLocal(int pos, int refType, const std::optional<JObj>& props) {
+  if (mt.window.collaborating) fail_unsupported("local edits while collaborating");
+  Seg* s = mt.newSeg();
+  s->isMarker = true;
+  s->refType = refType;
+  s->cachedLength = 1;
+  if (props) { s->hasPropManager = true; s->props = *props; }
+  mt.insertSegments(pos, s, mt.window.currentSeq, mt.window.clientId, UniversalSeq);
+}
+void Doc::annotateRangeLocal(int start, int end, const JObj& props) {
+  if (mt.window.collaborating) fail_unsupported("local edits while collaborating");
+  mt.annotateRange(start, end, props, false, mt.window.currentSeq, mt.window.clientId, UniversalSeq);
+}
+void Doc::removeRangeLocal(int start, int end) {
+  if (mt.window.collaborating) fail_unsupported("local edits while collaborating");
+  mt.markRangeRemoved(start, end, mt.window.currentSeq, mt.window.clientId, UniversalSeq);
+}
+
+// ---------------------------------------------------------------- SnapshotV1 (snapshotV1.ts)
+static JVal segJson(const Seg* s) {  // TextSegment.toJSONObject / Marker.toJSONObject
+  if (s->isMarker) {
+    JVal o;
+    o.t = JVal::Obj;
+    JVal m;
+    m.t = JVal::Obj;
+    if (s->refType >= 0) obj_set(m.obj, u"refType", JVal::number(s->refType));
+    o.obj.push_back({u"marker", m});
+    if (s->props) {
+      JVal p; p.t = JVal::Obj; p.obj = *s->props;
+      o.obj.push_back({u"props", p});
+    }
+    return o;
+  }
+  if (s->props) {
+    JVal o;
+    o.t = JVal::Obj;
+    o.obj.push_back({u"text", JVal::string(s->text)});
+    JVal p; p.t = JVal::Obj; p.obj = *s->props;
+    o.obj.push_back({u"props", p});
+    return o;
+  }
+  return JVal::string(s->text);
+}
+
+static int64_t utf8ByteLength(const std::string& utf8) {  // summaryUtils.ts:56-71 on the JS string
+  u16str s = utf8_to_u16(utf8);
+  int64_t n = (int64_t)s.size();
+  for (long i = (long)s.size() - 1; i >= 0; i--) {
+    uint32_t code = s[i];
+    if (code > 0x7f && code <= 0x7ff) n++;
+    else if (code > 0x7ff && code <= 0xffff) n += 2;
+    if (code >= 0xdc00 && code <= 0xdfff) i--;
+  }
+  return n;
+}
+
+std::vector<std::pair<std::string, std::string>> Doc::summarizeV1(std::string* summaryJson) {
+  MergeTree& t = mt;
+  const int minSeq = t.window.minSeq;
+  const int curSeq = t.window.currentSeq;
+  std::vector<JVal> segments;
+  std::vector<int> lengths;
+  auto normalize = [](Seg* s) {
+    if (s->props && s->props->empty()) {  // snapshotV1.ts:199-206 (mutates the live segment)
+      s->props.reset();
+      s->hasPropManager = false;
+    }
+  };
+  // prev: either a live segment or a coalesced clone (owned here)
+  std::optional<Seg> prevClone;
+  Seg* prev = nullptr;
+  auto pushSeg = [&](Seg* s) {
+    if (!s) return;
+    normalize(s);
+    segments.push_back(segJson(s));
+    lengths.push_back(s->cachedLength);
+  };
+  t.walkAllSegments([&](Seg* s) {  // extractSync (snapshotV1.ts:180-312)
+    if (s->seq == UnassignedSeq || (s->removed && s->removedSeq <= minSeq)) return;
+    if (s->seq <= minSeq && (!s->removed || s->removedSeq == UnassignedSeq)) {
+      if (!prev) {
+        prev = s;
+      } else if (canAppend(prev, s) && matchSegProps(prev, s)) {
+        Seg c = *prev;  // prev.clone(); prev.append(segment.clone())
+        if (c.props) c.hasPropManager = true;
+        c.text += s->text;
+        c.cachedLength += s->cachedLength;
+        c.parent = nullptr;
+        prevClone = std::move(c);
+        prev = &*prevClone;
+      } else {
+        pushSeg(prev);
+        prev = s;
+      }
+    } else {
+      pushSeg(prev);
+      prev = nullptr;
+      normalize(s);
+      JVal raw;
+      raw.t = JVal::Obj;
+      raw.obj.push_back({u"json", segJson(s)});
+      if (s->seq > minSeq) {
+        raw.obj.push_back({u"seq", JVal::number(s->seq)});
+        raw.obj.push_back({u"client", JVal::string(utf8_to_u16(getLongClientId(s->clientId)))});
+      }
+      if (s->removed) {
+        if (s->removedSeq == UnassignedSeq || s->removedSeq <= minSeq) fail_assert("0x065", "invalid removed seq");
+        raw.obj.push_back({u"removedSeq", JVal::number(s->removedSeq)});
+        raw.obj.push_back({u"removedClient", JVal::string(utf8_to_u16(getLongClientId(s->removedClientIds[0])))});
+        JVal ids;
+        ids.t = JVal::Arr;
+        for (int c : s->removedClientIds) ids.arr.push_back(JVal::string(utf8_to_u16(getLongClientId(c))));
+        raw.obj.push_back({u"removedClientIds", ids});
+      }
+      segments.push_back(raw);
+      lengths.push_back(s->cachedLength);
+    }
+  });
+  pushSeg(prev);
+
+  // emit (snapshotV1.ts:122-178)
+  struct Chunk { int segmentCount = 0, length = 0, startIndex = 0; };
+  std::vector<Chunk> chunks;
+  int totalSegmentCount = 0, totalLength = 0;
+  do {
+    Chunk c;
+    c.startIndex = totalSegmentCount;
+    while (c.length < t.options.chunkSize && c.startIndex + c.segmentCount < (int)segments.size()) {
+      c.length += lengths[c.startIndex + c.segmentCount];
+      c.segmentCount++;
+    }
+    chunks.push_back(c);
+    totalSegmentCount += c.segmentCount;
+    totalLength += c.length;
+  } while (totalSegmentCount < (int)segments.size());
+
+  auto chunkJson = [&](const Chunk& c, bool header) {
+    JVal o;
+    o.t = JVal::Obj;
+    o.obj.push_back({u"version", JVal::string(u"1")});
+    o.obj.push_back({u"segmentCount", JVal::number(c.segmentCount)});
+    o.obj.push_back({u"length", JVal::number(c.length)});
+    JVal segs;
+    segs.t = JVal::Arr;
+    for (int i = 0; i < c.segmentCount; i++) segs.arr.push_back(segments[c.startIndex + i]);
+    o.obj.push_back({u"segments", segs});
+    o.obj.push_back({u"startIndex", JVal::number(c.startIndex)});
+    if (header) {
+      JVal h;
+      h.t = JVal::Obj;
+      h.obj.push_back({u"minSequenceNumber", JVal::number(minSeq)});
+      h.obj.push_back({u"sequenceNumber", JVal::number(curSeq)});
+      JVal ids;
+      ids.t = JVal::Arr;
+      for (size_t i = 0; i < chunks.size(); i++) {
+        JVal id;
+        id.t = JVal::Obj;
+        std::string name = i == 0 ? "header" : "body_" + std::to_string(i - 1);
+        id.obj.push_back({u"id", JVal::string(utf8_to_u16(name))});
+        ids.arr.push_back(id);
+      }
+      h.obj.push_back({u"orderedChunkMetadata", ids});
+      h.obj.push_back({u"totalLength", JVal::number(totalLength)});
+      h.obj.push_back({u"totalSegmentCount", JVal::number(totalSegmentCount)});
+      o.obj.push_back({u"headerMetadata", h});
+    }
+    return json_stringify(o);
+  };
+  std::vector<std::pair<std::string, std::string>> blobs;
+  blobs.push_back({"header", chunkJson(chunks[0], true)});
+  for (size_t i = 1; i < chunks.size(); i++) blobs.push_back({"body_" + std::to_string(i - 1), chunkJson(chunks[i], false)});
+  if (summaryJson) {
+    // ISummaryTreeWithStats (summaryUtils.ts:138-198)
+    JVal tree;
+    tree.t = JVal::Obj;
+    int64_t total = 0;
+    for (auto& b : blobs) {
+      JVal blob;
+      blob.t = JVal::Obj;
+      blob.obj.push_back({u"type", JVal::number(2)});
+      blob.obj.push_back({u"content", JVal::string(utf8_to_u16(b.second))});
+      obj_set(tree.obj, utf8_to_u16(b.first), blob);
+      total += utf8ByteLength(b.second);
+    }
+    JVal summary;
+    summary.t = JVal::Obj;
+    summary.obj.push_back({u"type", JVal::number(1)});
+    summary.obj.push_back({u"tree", tree});
+    JVal stats;
+    stats.t = JVal::Obj;
+    stats.obj.push_back({u"treeNodeCount", JVal::number(1)});
+    stats.obj.push_back({u"blobNodeCount", JVal::number((double)blobs.size())});
+    stats.obj.push_back({u"handleNodeCount", JVal::number(0)});
+    stats.obj.push_back({u"totalBlobSize", JVal::number((double)total)});
+    stats.obj.push_back({u"unreferencedBlobSize", JVal::number(0)});
+    JVal all;
+    all.t = JVal::Obj;
+    all.obj.push_back({u"summary", summary});
+    all.obj.push_back({u"stats", stats});
+    *summaryJson = json_stringify(all);
+  }
+  return blobs;
+}
+
+// Canonical segment dump: header line then one JSON array per segment, in tree order:
+// [path, kind, text|refType, seq, client, removedSeq(-1 none), [removedClientIds], props|null]
+std::string Doc::dumpSegments() {
+  std::string out;
+  {
+    JVal h;
+    h.t = JVal::Obj;
+    h.obj.push_back({u"minSeq", JVal::number(mt.window.minSeq)});
+    h.obj.push_back({u"currentSeq", JVal::number(mt.window.currentSeq)});
+    h.obj.push_back({u"length", JVal::number(mt.length())});
+    out += json_stringify(h);
+    out.push_back('\n');
+  }
+  std::vector<int> path;
+  std::function<void(Block*)> rec = [&](Block* b) {
+    for (int i = 0; i < b->childCount; i++) {
+      path.push_back(i);
+      Node* c = b->children[i];
+      if (c->leaf) {
+        Seg* s = static_cast<Seg*>(c);
+        JVal row;
+        row.t = JVal::Arr;
+        JVal p;
+        p.t = JVal::Arr;
+        for (int x : path) p.arr.push_back(JVal::number(x));
+        row.arr.push_back(p);
+        if (s->isMarker) {
+          row.arr.push_back(JVal::string(u"M"));
+          row.arr.push_back(s->refType >= 0 ? JVal::number(s->refType) : JVal::null());
+        } else {
+          row.arr.push_back(JVal::string(u"T"));
+          row.arr.push_back(JVal::string(s->text));
+        }
+        row.arr.push_back(JVal::number(s->seq));
+        row.arr.push_back(JVal::number(s->clientId));
+        row.arr.push_back(JVal::number(s->removed ? s->removedSeq : -1));
+        JVal rc;
+        rc.t = JVal::Arr;
+        if (s->removed)
+          for (int c2 : s->removedClientIds) rc.arr.push_back(JVal::number(c2));
+        row.arr.push_back(rc);
+        if (s->props) {
+          JVal pr;
+          pr.t = JVal::Obj;
+          pr.obj = *s->props;
+          row.arr.push_back(pr);
+        } else {
+          row.arr.push_back(JVal::null());
+        }
+        out += json_stringify(row);
+        out.push_back('\n');
+      } else {
+        rec(static_cast<Block*>(c));
+      }
+      path.pop_back();
+    }
+  };
+  rec(mt.root);
+  return out;
+}
+
+uint64_t fnv1a64(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+}  // namespace orc

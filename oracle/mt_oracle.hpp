@@ -1,0 +1,236 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — CPU restatement of the reference merge-tree observer path.
+//
+// Parity pinning: tests/test_oracle_fixtures.py replays the reference's 30 committed conflict-farm
+// logs (packages/dds/merge-tree/src/test/results/*.json, 61,200 ops, text after every group) and
+// byte-compares the 6 committed SnapshotV1 summaries
+// (packages/dds/sequence/src/test/snapshots/v1/*.json).  Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg may load this code; the product engine never links it.
+//
+// Every function cites the reference file:line whose behaviour it restates
+// (MT = packages/dds/merge-tree/src).
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <memory>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "ojson.hpp"
+
+namespace orc {
+
+constexpr int MaxNodesInBlock = 8;         // MT/mergeTreeNodes.ts:330
+constexpr int UniversalSeq = 0;            // MT/constants.ts:11
+constexpr int UnassignedSeq = -1;          // MT/constants.ts:12
+constexpr int TreeMaintenanceSeq = -2;     // MT/constants.ts:13
+constexpr int LocalClientId = -1;          // MT/constants.ts:14
+constexpr int NonCollabClient = -2;        // MT/constants.ts:15
+constexpr int TextSegmentGranularity = 256;// MT/textSegment.ts:20
+constexpr int ZamboniSegmentsMax = 2;      // MT/zamboni.ts:14
+constexpr int UNDEF_LEN = -1;              // `undefined` result of nodeLength
+
+struct Block;
+
+struct Node {
+  bool leaf;
+  Block* parent = nullptr;
+  int index = 0;
+  int cachedLength = 0;
+  explicit Node(bool l) : leaf(l) {}
+};
+
+struct Seg : Node {
+  bool isMarker = false;
+  int refType = -1;                // -1 = undefined
+  u16str text;                     // TextSegment text (markers: empty)
+  int seq = UniversalSeq;          // BaseSegment.seq default (mergeTreeNodes.ts:368)
+  int clientId = LocalClientId;    // BaseSegment.clientId default
+  bool removed = false;
+  int removedSeq = 0;
+  std::vector<int> removedClientIds;
+  std::optional<JObj> props;       // properties (undefined when nullopt)
+  bool hasPropManager = false;     // propertyManager !== undefined
+  Seg() : Node(true) {}
+};
+
+// PartialSequenceLength entry (MT/partialLengths.ts:105-140)
+struct PSL {
+  int seq = 0, len = 0, seglen = 0, clientId = 0;
+  std::shared_ptr<std::map<int, int>> overlap;  // overlapRemoveClients: clientId -> seglen
+};
+
+// PartialSequenceLengthsSet (MT/partialLengths.ts:19-95 over SortedSet MT/sortedSet.ts)
+struct PSLSet {
+  std::vector<PSL> items;
+  std::pair<bool, size_t> find(int seq) const;
+  PSL* latestLeq(int seq);
+  PSL* firstGte(int seq);
+  void addOrUpdate(PSL item);
+  int copyDown(int minSeq);
+};
+
+struct CollabWindow {  // MT/mergeTreeNodes.ts:656-673
+  int clientId = LocalClientId;
+  bool collaborating = false;
+  int minSeq = 0;
+  int currentSeq = 0;
+};
+
+// PartialSequenceLengths (MT/partialLengths.ts:239-850), remote-perspective part only.
+struct PartialLengths {
+  int minSeq = 0;
+  int minLength = 0;
+  int segmentCount = 0;
+  PSLSet partialLengths;
+  std::map<int, PSLSet> clientSeqNumbers;
+  int getPartialLength(int refSeq, int clientId);
+  void zamboni(const CollabWindow& w);
+  void addClientSeqNumber(int clientId, int seq, int seglen);
+  void addClientSeqNumberFromPartial(const PSL& p);
+};
+
+struct Block : Node {
+  int childCount = 0;
+  std::vector<Node*> children;
+  int needsScour = -1;  // -1 undefined, 0 false, 1 true  (IMergeBlock.needsScour)
+  std::unique_ptr<PartialLengths> partial;
+  Block() : Node(false), children(MaxNodesInBlock, nullptr) {}
+  void assignChild(Node* c, int i) {
+    c->parent = this;
+    c->index = i;
+    if ((int)children.size() <= i) children.resize(i + 1, nullptr);
+    children[i] = c;
+  }
+};
+
+struct Options {
+  bool newLengthCalc = false;  // mergeTreeUseNewLengthCalculations
+  int chunkSize = 10000;       // SnapshotV1.chunkSize (snapshotV1.ts:37)
+  bool verify = false;         // cross-check partial lengths against a leaf sum (test-only)
+};
+
+struct OracleError : std::runtime_error {
+  int code;
+  OracleError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+struct Counters {
+  uint64_t ops = 0, segsTouched = 0;
+};
+
+class MergeTree {
+ public:
+  explicit MergeTree(const Options& o);
+  Options options;
+  CollabWindow window;
+  Block* root;
+  Counters counters;
+
+  // segment / block pools (pointers stay valid for the tree's lifetime)
+  std::deque<Seg> segPool;
+  std::deque<Block> blockPool;
+  Seg* newSeg() { segPool.emplace_back(); return &segPool.back(); }
+  Block* makeBlock(int childCount);
+
+  // LRU heap (MT/collections/heap.ts) of {segment, maxSeq}; index 0 is the {maxSeq:-2} sentinel.
+  struct LRU { Seg* seg; int maxSeq; };
+  std::vector<LRU> heap;
+  bool heapValid = false;
+  void heapAdd(LRU x);
+  LRU heapGet();
+
+  int localNetLength(const Seg* s) const;
+  int nodeLength(Node* n, int refSeq, int clientId);
+  int blockLength(Block* b, int refSeq, int clientId);
+  int getLength(int refSeq, int clientId) { return blockLength(root, refSeq, clientId); }
+  int length() const { return root->cachedLength; }
+
+  void startCollaboration(int localClientId, int minSeq, int currentSeq);
+  void setMinSeq(int minSeq);
+  void insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq);
+  void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
+  void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
+  void zamboniSegments();
+
+  // text / walks
+  u16str getText();
+  template <class F> void walkAllSegments(F&& f);
+
+  // structure maintenance (public for the snapshot code)
+  void nodeUpdateLengthNewStructure(Block* b, bool recur = false);
+  int bruteLength(Node* n, int refSeq, int clientId);
+
+ private:
+  struct Changes { Seg* replaceCurrent = nullptr; Node* next = nullptr; };
+  struct InsertCtx { bool insertMode = false; Seg* candidate = nullptr; };
+  Block* const UNFINISHED = reinterpret_cast<Block*>(1);
+
+  bool breakTie(int pos, Node* n, int seq);
+  Block* insertingWalk(Block* b, int pos, int refSeq, int clientId, int seq, InsertCtx& ctx);
+  Changes leafAction(InsertCtx& ctx, Seg* s, int pos);
+  Seg* splitAt(Seg* s, int pos);
+  void ensureIntervalBoundary(int pos, int refSeq, int clientId);
+  void blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg);
+  bool continuePredicate(Block* b);
+  Block* split(Block* b);
+  void updateRoot(Block* splitNode);
+  void blockUpdate(Block* b);
+  void blockUpdateLength(Block* b, int seq, int clientId);
+  void blockUpdatePathLengths(Block* b, int seq, int clientId, bool newStructure);
+  void addToLRUSet(Seg* s, int seq);
+  void scourNode(Block* node, std::vector<Node*>& hold);
+  void packParent(Block* parent);
+  template <class Leaf, class Post>
+  void nodeMap(int refSeq, int clientId, Leaf&& leaf, Post&& post, int start, int end);
+
+  // PartialSequenceLengths construction (partialLengths.ts:256-577, 636-686)
+  std::unique_ptr<PartialLengths> combine(Block* b, bool recur);
+  std::unique_ptr<PartialLengths> fromLeaves(Block* b);
+  void plInsertSegment(PartialLengths& pl, Seg* s, bool removal);
+  void plUpdate(PartialLengths& pl, Block* node, int seq, int clientId);
+};
+
+// -------------------------------------------------------------- client-level document
+class Doc {
+ public:
+  explicit Doc(const Options& o) : mt(o) {}
+  MergeTree mt;
+  std::vector<std::string> longIds;         // shortClientIdMap (client.ts:104)
+  std::map<std::string, int> longToShort;   // clientNameToIds
+  std::optional<std::string> longClientId;  // the observer's own long id
+
+  int getOrAddShortClientId(const std::string& id);
+  std::string getLongClientId(int shortId) const;
+  void startOrUpdateCollaboration(const std::string& id, int minSeq, int curSeq);
+  void updateSeqNumbers(int min, int seq);
+
+  // local, non-collaborating edits (detached documents; used for the V1 snapshot fixtures)
+  void insertTextLocal(int pos, const u16str& text, const std::optional<JObj>& props);
+  void insertMarkerLocal(int pos, int refType, const std::optional<JObj>& props);
+  void annotateRangeLocal(int start, int end, const JObj& props);
+  void removeRangeLocal(int start, int end);
+
+  // Client.applyMsg with a parsed ISequencedDocumentMessage
+  void applyMsg(const JVal& msg);
+  // remote delta op (already decoded)
+  void applyRemoteDelta(const JVal& op, int clientShort, int refSeq, int seq);
+  // binary record path (include/mtb.h mtb_op)
+  struct Record {
+    uint8_t type, flags;
+    uint16_t client;
+    uint32_t seq, refSeq, msn, pos1, pos2, payload, props;
+  };
+  void applyRecord(const Record& r, const uint16_t* text, const std::vector<std::string>& propsJson);
+
+  // SnapshotV1 (snapshotV1.ts:46-312) -> (blob path, content) list + ISummaryTreeWithStats JSON
+  std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);
+  // canonical segment dump used for engine parity (one JSON object per line)
+  std::string dumpSegments();
+};
+
+uint64_t fnv1a64(const std::string& s);
+JObj propsFromSpec(const JVal* spec);
+
+}  // namespace orc

@@ -1,0 +1,140 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY.  C entry points over the CPU restatement, loaded by tests/
+// through ctypes (tests/oracle.py) and by bench.py's cpu_baseline leg.  Never linked by the product.
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mt_oracle.hpp"
+
+using namespace orc;
+
+struct orc_doc {
+  Doc doc;
+  std::string err;
+  explicit orc_doc(const Options& o) : doc(o) {}
+};
+
+static char* dupstr(const std::string& s, size_t* len) {
+  char* p = (char*)malloc(s.size() + 1);
+  memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  if (len) *len = s.size();
+  return p;
+}
+
+template <class F>
+static int guard(orc_doc* d, F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const OracleError& e) {
+    d->err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    d->err = e.what();
+    return -8;
+  }
+}
+
+static std::optional<JObj> parseProps(const char* json) {
+  if (!json) return std::nullopt;
+  JVal v = json_parse(json, strlen(json));
+  if (v.t != JVal::Obj) return std::nullopt;
+  return propsFromSpec(&v);
+}
+
+extern "C" {
+
+orc_doc* orc_create(int new_length_calc, int chunk_size, int verify) {
+  Options o;
+  o.newLengthCalc = new_length_calc != 0;
+  if (chunk_size > 0) o.chunkSize = chunk_size;
+  o.verify = verify != 0;
+  return new orc_doc(o);
+}
+void orc_destroy(orc_doc* d) { delete d; }
+const char* orc_last_error(orc_doc* d) { return d->err.c_str(); }
+void orc_free(void* p) { free(p); }
+
+int orc_insert_text_local(orc_doc* d, int pos, const char* utf8, const char* props_json) {
+  return guard(d, [&] { d->doc.insertTextLocal(pos, utf8_to_u16(utf8, strlen(utf8)), parseProps(props_json)); });
+}
+int orc_insert_marker_local(orc_doc* d, int pos, int ref_type, const char* props_json) {
+  return guard(d, [&] { d->doc.insertMarkerLocal(pos, ref_type, parseProps(props_json)); });
+}
+int orc_annotate_local(orc_doc* d, int start, int end, const char* props_json) {
+  return guard(d, [&] {
+    JVal v = json_parse(props_json, strlen(props_json));
+    d->doc.annotateRangeLocal(start, end, v.t == JVal::Obj ? v.obj : JObj());
+  });
+}
+int orc_remove_local(orc_doc* d, int start, int end) {
+  return guard(d, [&] { d->doc.removeRangeLocal(start, end); });
+}
+int orc_start_collab(orc_doc* d, const char* long_id, int min_seq, int cur_seq) {
+  return guard(d, [&] { d->doc.startOrUpdateCollaboration(long_id, min_seq, cur_seq); });
+}
+int orc_apply_msg_json(orc_doc* d, const char* json, size_t len) {
+  return guard(d, [&] { d->doc.applyMsg(json_parse(json, len)); });
+}
+// Binary records (include/mtb.h layout). props_json: array of n_props NUL-terminated JSON strings.
+int orc_apply_records(orc_doc* d, const void* ops, uint32_t n, const uint16_t* text, const char* const* props_json,
+                      uint32_t n_props) {
+  return guard(d, [&] {
+    std::vector<std::string> props(n_props);
+    for (uint32_t i = 0; i < n_props; i++) props[i] = props_json[i] ? props_json[i] : "";
+    const Doc::Record* r = static_cast<const Doc::Record*>(ops);
+    for (uint32_t i = 0; i < n; i++) d->doc.applyRecord(r[i], text, props);
+  });
+}
+int orc_add_client(orc_doc* d, const char* long_id) {
+  return guard(d, [&] { d->doc.getOrAddShortClientId(long_id); });
+}
+int orc_update_seq(orc_doc* d, int min_seq, int seq) {
+  return guard(d, [&] { d->doc.updateSeqNumbers(min_seq, seq); });
+}
+// UTF-16 text (engine-allocated)
+int orc_get_text(orc_doc* d, uint16_t** out, size_t* n_units) {
+  return guard(d, [&] {
+    u16str t = d->doc.mt.getText();
+    uint16_t* p = (uint16_t*)malloc((t.size() + 1) * 2);
+    memcpy(p, t.data(), t.size() * 2);
+    *out = p;
+    *n_units = t.size();
+  });
+}
+int orc_get_length(orc_doc* d) { return d->doc.mt.length(); }
+int orc_get_remote_length(orc_doc* d, int ref_seq, int client) { return d->doc.mt.getLength(ref_seq, client); }
+int orc_current_seq(orc_doc* d) { return d->doc.mt.window.currentSeq; }
+int orc_min_seq(orc_doc* d) { return d->doc.mt.window.minSeq; }
+int orc_num_clients(orc_doc* d) { return (int)d->doc.longIds.size(); }
+const char* orc_client_long_id(orc_doc* d, int i) { return d->doc.longIds.at(i).c_str(); }
+uint64_t orc_ops_applied(orc_doc* d) { return d->doc.mt.counters.ops; }
+uint64_t orc_segs_touched(orc_doc* d) { return d->doc.mt.counters.segsTouched; }
+
+// Summary: returns a JSON object {"blobs":[[path, content],...], "summary": <ISummaryTreeWithStats>}
+int orc_summarize_v1(orc_doc* d, int msn, int seq, char** out, size_t* len) {
+  return guard(d, [&] {
+    if (msn >= 0 && seq >= 0) d->doc.updateSeqNumbers(msn, seq);
+    std::string summary;
+    auto blobs = d->doc.summarizeV1(&summary);
+    JVal arr;
+    arr.t = JVal::Arr;
+    for (auto& b : blobs) {
+      JVal pair;
+      pair.t = JVal::Arr;
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.first)));
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.second)));
+      arr.arr.push_back(pair);
+    }
+    std::string s = "{\"blobs\":" + json_stringify(arr) + ",\"summary\":" + summary + "}";
+    *out = dupstr(s, len);
+  });
+}
+int orc_dump_segments(orc_doc* d, char** out, size_t* len) {
+  return guard(d, [&] { *out = dupstr(d->doc.dumpSegments(), len); });
+}
+uint64_t orc_checksum(orc_doc* d) { return fnv1a64(d->doc.dumpSegments()); }
+
+}  // extern "C"

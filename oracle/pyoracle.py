@@ -1,0 +1,182 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (the CPU restatement).
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the parity checker.
+The product engine (fluidframework_amd) never imports this module.
+"""
+import ctypes
+import json
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle not built: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        vp, cp, i, sz = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_size_t
+        L.orc_create.restype = vp
+        L.orc_create.argtypes = [i, i, i]
+        L.orc_destroy.argtypes = [vp]
+        L.orc_last_error.restype = cp
+        L.orc_last_error.argtypes = [vp]
+        L.orc_free.argtypes = [vp]
+        L.orc_insert_text_local.argtypes = [vp, i, cp, cp]
+        L.orc_insert_marker_local.argtypes = [vp, i, i, cp]
+        L.orc_annotate_local.argtypes = [vp, i, i, cp]
+        L.orc_remove_local.argtypes = [vp, i, i]
+        L.orc_start_collab.argtypes = [vp, cp, i, i]
+        L.orc_apply_msg_json.argtypes = [vp, cp, sz]
+        L.orc_apply_records.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.POINTER(cp), ctypes.c_uint32]
+        L.orc_add_client.argtypes = [vp, cp]
+        L.orc_update_seq.argtypes = [vp, i, i]
+        L.orc_get_text.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
+        L.orc_get_length.argtypes = [vp]
+        L.orc_get_remote_length.argtypes = [vp, i, i]
+        L.orc_current_seq.argtypes = [vp]
+        L.orc_min_seq.argtypes = [vp]
+        L.orc_num_clients.argtypes = [vp]
+        L.orc_client_long_id.restype = cp
+        L.orc_client_long_id.argtypes = [vp, i]
+        L.orc_ops_applied.restype = ctypes.c_uint64
+        L.orc_ops_applied.argtypes = [vp]
+        L.orc_segs_touched.restype = ctypes.c_uint64
+        L.orc_segs_touched.argtypes = [vp]
+        L.orc_summarize_v1.argtypes = [vp, i, i, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
+        L.orc_dump_segments.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
+        L.orc_checksum.restype = ctypes.c_uint64
+        L.orc_checksum.argtypes = [vp]
+        _LIB = L
+    return _LIB
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class OracleDoc:
+    """One observer merge-tree client (Client/TestClient restated in C++)."""
+
+    def __init__(self, new_length_calc=False, chunk_size=0, verify=False):
+        self._L = lib()
+        self._h = self._L.orc_create(int(new_length_calc), int(chunk_size), int(verify))
+
+    def close(self):
+        if self._h:
+            self._L.orc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise OracleError(rc, self._L.orc_last_error(self._h).decode("utf-8", "replace"))
+
+    # --- detached local edits -------------------------------------------------------------
+    def insert_text_local(self, pos, text, props=None):
+        self._chk(self._L.orc_insert_text_local(self._h, pos, text.encode("utf-8", "surrogatepass"),
+                                                None if props is None else json.dumps(props).encode()))
+
+    def insert_marker_local(self, pos, ref_type, props=None):
+        self._chk(self._L.orc_insert_marker_local(self._h, pos, ref_type,
+                                                  None if props is None else json.dumps(props).encode()))
+
+    def annotate_local(self, start, end, props):
+        self._chk(self._L.orc_annotate_local(self._h, start, end, json.dumps(props).encode()))
+
+    def remove_local(self, start, end):
+        self._chk(self._L.orc_remove_local(self._h, start, end))
+
+    # --- collaboration ---------------------------------------------------------------------
+    def start_collab(self, long_id, min_seq=0, cur_seq=0):
+        self._chk(self._L.orc_start_collab(self._h, long_id.encode(), min_seq, cur_seq))
+
+    def apply_msg(self, msg):
+        s = msg if isinstance(msg, (bytes, bytearray)) else json.dumps(msg).encode()
+        self._chk(self._L.orc_apply_msg_json(self._h, s, len(s)))
+
+    def apply_records(self, ops_bytes, n, text_u16, props_json):
+        arr = (ctypes.c_char_p * max(1, len(props_json)))(*[p.encode() if p is not None else None for p in props_json])
+        tbuf = ctypes.create_string_buffer(bytes(text_u16), max(2, len(text_u16)))
+        obuf = ctypes.create_string_buffer(bytes(ops_bytes), max(1, len(ops_bytes)))
+        self._chk(self._L.orc_apply_records(self._h, obuf, n, tbuf, arr, len(props_json)))
+
+    def add_client(self, long_id):
+        self._chk(self._L.orc_add_client(self._h, long_id.encode()))
+
+    def update_seq(self, min_seq, seq):
+        self._chk(self._L.orc_update_seq(self._h, min_seq, seq))
+
+    # --- read-out --------------------------------------------------------------------------
+    def get_text(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_get_text(self._h, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            raw = ctypes.string_at(p, n.value * 2)
+        finally:
+            self._L.orc_free(p)
+        return raw.decode("utf-16-le", "surrogatepass")
+
+    def get_length(self):
+        return self._L.orc_get_length(self._h)
+
+    def remote_length(self, ref_seq, client):
+        return self._L.orc_get_remote_length(self._h, ref_seq, client)
+
+    @property
+    def current_seq(self):
+        return self._L.orc_current_seq(self._h)
+
+    @property
+    def min_seq(self):
+        return self._L.orc_min_seq(self._h)
+
+    def client_ids(self):
+        return [self._L.orc_client_long_id(self._h, i).decode() for i in range(self._L.orc_num_clients(self._h))]
+
+    def ops_applied(self):
+        return self._L.orc_ops_applied(self._h)
+
+    def segs_touched(self):
+        return self._L.orc_segs_touched(self._h)
+
+    def summarize_v1(self, msn=-1, seq=-1):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_summarize_v1(self._h, msn, seq, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            raw = ctypes.string_at(p, n.value)
+        finally:
+            self._L.orc_free(p)
+        return json.loads(raw.decode("utf-8"))
+
+    def dump_segments(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_dump_segments(self._h, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            raw = ctypes.string_at(p, n.value)
+        finally:
+            self._L.orc_free(p)
+        return raw.decode("utf-8")
+
+    def checksum(self):
+        return self._L.orc_checksum(self._h)
+
+
+def msg_from_compact(m):
+    """Expand a compact fixture row [clientId, seq, refSeq, msn, contents] to an ISequencedDocumentMessage."""
+    cid, seq, ref, msn, contents = m
+    return {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+            "minimumSequenceNumber": msn, "type": "op", "contents": contents}
