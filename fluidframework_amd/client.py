@@ -1,0 +1,213 @@
+"""Python mirror of the reference merge-tree `Client` / `TestClient` surface over the MI355X engine.
+
+Reference interface (packages/dds/merge-tree/src/client.ts:98): `startOrUpdateCollaboration` (:1133),
+`applyMsg` (:858), `getLength` (:1129), `getCurrentSeq` (:1122), `summarize` (:966); TestClient adds
+`getText` (test/testClient.ts:185) and `insertTextLocal` (detached initial content).
+
+Batched semantics: each `Client` is one document slot of a `MergeTreeBatch`.
+`applyMsg` only validates and packs the message; `flush()` -- or any read (`getText`, `getLength`,
+`summarize`) -- replays every pending op of every document of the batch on the GPU.  Per-op "delta"
+events are not emitted.  Only the observer (remote-op) path is supported; local ops after
+collaboration starts raise.
+"""
+import ctypes
+import json
+
+from . import _lib
+
+
+class MergeTreeError(RuntimeError):
+    """Error raised by the engine; `code` is the MTB_E_* value, `message` carries the reference's
+    assert code / error text where one exists (e.g. "0x038 ...", "MergeTree insert failed")."""
+
+    def __init__(self, code, message):
+        super().__init__(message)
+        self.code = code
+        self.name = _lib.ERRORS.get(code, str(code))
+
+
+class UsageError(MergeTreeError):
+    """container-utils UsageError equivalent (mergeTree.ts:1671 "MergeTree insert failed")."""
+
+
+def _check(L, h, rc):
+    if rc != 0:
+        msg = L.mtb_last_error(h).decode("utf-8", "replace")
+        if rc == -5:
+            raise UsageError(rc, msg)
+        raise MergeTreeError(rc, msg)
+
+
+class MergeTreeBatch:
+    """A batch of independent merge-tree documents replayed together on one MI355X."""
+
+    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0):
+        self._L = _lib.lib()
+        opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, 0)
+        h = ctypes.c_void_p()
+        rc = self._L.mtb_batch_create(ctypes.byref(opts), ndocs, 1 << device, ctypes.byref(h))
+        if rc != 0:
+            raise MergeTreeError(rc, "mtb_batch_create failed")
+        self._h = h
+        self.ndocs = ndocs
+        self._dirty = False
+        self._clients = [Client(self, i) for i in range(ndocs)]
+        self.last_stats = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mtb_batch_destroy(self._h)
+            self._h = None
+
+    def _chk(self, rc):
+        _check(self._L, self._h, rc)
+
+    def client(self, i):
+        return self._clients[i]
+
+    __getitem__ = client
+
+    def intern_props(self, props):
+        """Intern a props object (dict, or its JSON text) and return its id."""
+        if isinstance(props, str):
+            s = props.encode()
+        elif isinstance(props, (bytes, bytearray)):
+            s = bytes(props)
+        else:
+            s = json.dumps(props).encode()
+        out = ctypes.c_uint32()
+        self._chk(self._L.mtb_intern_props(self._h, s, len(s), ctypes.byref(out)))
+        return out.value
+
+    def append_records(self, doc, ops_bytes, n, payload_u16_bytes):
+        ob = ctypes.create_string_buffer(bytes(ops_bytes), max(1, len(ops_bytes)))
+        pb = ctypes.create_string_buffer(bytes(payload_u16_bytes), max(2, len(payload_u16_bytes)))
+        self._chk(self._L.mtb_append_ops(self._h, doc, ob, n, pb, len(payload_u16_bytes) // 2))
+        self._dirty = True
+
+    def add_client(self, doc, long_id):
+        self._chk(self._L.mtb_add_client(self._h, doc, long_id.encode()))
+
+    def init_doc(self, doc, initial_text, observer_long_id, min_seq=0, cur_seq=0):
+        raw = initial_text.encode("utf-16-le", "surrogatepass")
+        buf = ctypes.create_string_buffer(raw, max(2, len(raw)))
+        self._chk(self._L.mtb_doc_init(self._h, doc, buf, len(raw) // 2, observer_long_id.encode(), min_seq, cur_seq))
+
+    def replay(self):
+        """Replay every pending op of every document (blocking).  Returns the stats dict."""
+        st = _lib.MtbStats()
+        self._chk(self._L.mtb_replay(self._h, ctypes.byref(st)))
+        self._dirty = False
+        self.last_stats = {f: getattr(st, f) for f, _ in _lib.MtbStats._fields_}
+        return self.last_stats
+
+    flush = replay
+
+    def _ensure_flushed(self):
+        if self._dirty:
+            self.replay()
+
+    # --- per-document read-outs ---------------------------------------------------------------
+    def text(self, doc):
+        self._ensure_flushed()
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_get_text(self._h, doc, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(2, n.value * 2))
+        self._chk(self._L.mtb_get_text(self._h, doc, buf, n.value, ctypes.byref(n)))
+        return buf.raw[: n.value * 2].decode("utf-16-le", "surrogatepass")
+
+    def length(self, doc):
+        self._ensure_flushed()
+        out = ctypes.c_uint32()
+        self._chk(self._L.mtb_get_length(self._h, doc, ctypes.byref(out)))
+        return out.value
+
+    def seq(self, doc):
+        cur, mn = ctypes.c_uint32(), ctypes.c_uint32()
+        self._chk(self._L.mtb_get_seq(self._h, doc, ctypes.byref(cur), ctypes.byref(mn)))
+        return cur.value, mn.value
+
+    def dump_segments(self, doc):
+        self._ensure_flushed()
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._chk(self._L.mtb_dump_segments(self._h, doc, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return ctypes.string_at(p, n.value).decode("utf-8")
+        finally:
+            self._L.mtb_free(p)
+
+    def checksum(self, doc):
+        self._ensure_flushed()
+        out = ctypes.c_uint64()
+        self._chk(self._L.mtb_doc_checksum(self._h, doc, ctypes.byref(out)))
+        return out.value
+
+    def summarize_v1(self, doc, msn=-1, seq=-1):
+        """SnapshotV1 summary: returns (blobs [(path, content)], ISummaryTreeWithStats dict)."""
+        self._ensure_flushed()
+        lst = _lib.MtbBlobList()
+        self._chk(self._L.mtb_summarize_v1(self._h, doc, msn, seq, ctypes.byref(lst)))
+        try:
+            blobs = [(lst.blobs[i].path.decode(), ctypes.string_at(lst.blobs[i].content, lst.blobs[i].content_len).decode("utf-8"))
+                     for i in range(lst.count)]
+            summary = json.loads(ctypes.string_at(lst.summary_json, lst.summary_json_len).decode("utf-8"))
+        finally:
+            self._L.mtb_blob_list_free(ctypes.byref(lst))
+        return blobs, summary
+
+
+class Client:
+    """One document slot with the reference Client/TestClient call shapes."""
+
+    def __init__(self, batch, doc):
+        self._b = batch
+        self._doc = doc
+        self._initial = []
+        self.longClientId = None
+
+    # detached local edits before collaboration (client.replay.spec.ts:27 insertTextLocal)
+    def insertTextLocal(self, pos, text):
+        if self.longClientId is not None:
+            raise MergeTreeError(-6, "unsupported: local ops while collaborating (observer engine)")
+        cur = "".join(self._initial)
+        self._initial = [cur[:pos] + text + cur[pos:]]
+
+    def startOrUpdateCollaboration(self, longClientId, minSeq=0, currentSeq=0):
+        if self.longClientId is not None:
+            raise MergeTreeError(-6, "unsupported: re-keying the observer id")
+        self._b.init_doc(self._doc, "".join(self._initial), longClientId, minSeq, currentSeq)
+        self.longClientId = longClientId
+
+    def applyMsg(self, msg, local=False):
+        if local:
+            raise MergeTreeError(-6, "unsupported: local (ack) application on the observer engine")
+        s = msg if isinstance(msg, (bytes, bytearray)) else (msg.encode() if isinstance(msg, str) else json.dumps(msg).encode())
+        self._b._chk(self._b._L.mtb_apply_msg_json(self._b._h, self._doc, s, len(s)))
+        self._b._dirty = True
+
+    def getText(self):
+        return self._b.text(self._doc)
+
+    def getLength(self):
+        return self._b.length(self._doc)
+
+    def getCurrentSeq(self):
+        self._b._ensure_flushed()
+        return self._b.seq(self._doc)[0]
+
+    def getCollabWindow(self):
+        self._b._ensure_flushed()
+        cur, mn = self._b.seq(self._doc)
+        return {"clientId": 0, "collaborating": True, "minSeq": mn, "currentSeq": cur}
+
+    def summarize(self, minimumSequenceNumber=None, lastSequenceNumber=None):
+        """Client.summarize with newMergeTreeSnapshotFormat=true -> ISummaryTreeWithStats (dict)."""
+        msn = -1 if minimumSequenceNumber is None else minimumSequenceNumber
+        seq = -1 if lastSequenceNumber is None else lastSequenceNumber
+        return self._b.summarize_v1(self._doc, msn, seq)[1]

@@ -1,0 +1,1171 @@
+// Host side of the MI355X merge-tree batch replay engine: the C ABI declared in include/mtb.h.
+//
+//  * mtb_apply_msg_json packs an ISequencedDocumentMessage (client.ts:858) into 32-byte op records,
+//    interning long client ids (client.ts:673, first-seen order), property keys/values and props
+//    objects into batch-wide tables that the kernel reads.
+//  * mtb_replay sizes per-document HBM slices, uploads records / payload / tables, launches one
+//    64-lane wavefront per document (mtb_replay.hip) and reads back the document headers.
+//  * Read-outs (text, canonical segment dump, SnapshotV1 summary) download a document's slices and
+//    walk its tree on the host.  There is no CPU replay path: without a GPU every compute entry point
+//    fails with MTB_E_NODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mtb.h"
+#include "hjson.hpp"
+#include "mtb_device.h"
+
+// defined in mtb_replay.hip
+hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
+                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables);
+
+namespace {
+
+using hj::U16;
+
+struct MtbError {
+  int code;
+  std::string msg;
+};
+[[noreturn]] void raise(int code, const std::string& m) { throw MtbError{code, m}; }
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) raise(MTB_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ interning
+struct Interner {
+  std::vector<U16> keys;
+  std::map<U16, uint32_t> keyId;
+  std::vector<uint32_t> keyRank;
+  std::vector<uint8_t> keyKinds;  // bit0 primitive seen, bit1 object-like seen
+  std::vector<std::string> valJson;
+  std::unordered_map<std::string, uint32_t> valId;
+  std::vector<uint32_t> valClass;
+  std::vector<uint8_t> valFalsy;
+  std::unordered_map<std::string, uint32_t> classId;
+  std::vector<uint32_t> pool{0};   // offset 0 reserved
+  std::vector<uint32_t> pidx{0, 0};  // props id 0 = none
+  std::unordered_map<std::string, uint32_t> propsByJson;
+  bool dirty = true;
+
+  uint32_t key(const U16& k) {
+    auto it = keyId.find(k);
+    if (it != keyId.end()) return it->second;
+    uint32_t id = (uint32_t)keys.size();
+    keys.push_back(k);
+    keyId[k] = id;
+    uint32_t r;
+    keyRank.push_back(hj::array_index(k, &r) ? r : MTB_NONE);
+    keyKinds.push_back(0);
+    dirty = true;
+    return id;
+  }
+  // matchProperties equivalence class (properties.ts:71): arrays compare like objects with index keys
+  static void canon(std::string& o, const hj::Value& v) {
+    switch (v.kind) {
+      case hj::Value::kBool: o += v.b ? "b1" : "b0"; return;
+      case hj::Value::kNum: o += "n" + hj::number(v.n); return;
+      case hj::Value::kStr: o += "s"; hj::quote(o, v.s); return;
+      case hj::Value::kNull:
+      case hj::Value::kUndef:
+        raise(MTB_E_UNSUPPORTED, "unsupported: null nested inside a property value (matchProperties is not an equivalence there)");
+      case hj::Value::kArr:
+      case hj::Value::kObj: {
+        std::vector<std::pair<U16, const hj::Value*>> m;
+        if (v.kind == hj::Value::kArr) {
+          for (size_t i = 0; i < v.items.size(); i++) {
+            std::string s = std::to_string(i);
+            m.push_back({U16(s.begin(), s.end()), &v.items[i]});
+          }
+        } else {
+          for (auto& e : v.members) m.push_back({e.first, &e.second});
+        }
+        std::sort(m.begin(), m.end(), [](auto& a, auto& b) { return a.first < b.first; });
+        o += "{";
+        for (auto& e : m) {
+          hj::quote(o, e.first);
+          o += ":";
+          if (e.second->kind != hj::Value::kObj && e.second->kind != hj::Value::kArr &&
+              e.second->kind != hj::Value::kBool && e.second->kind != hj::Value::kNum &&
+              e.second->kind != hj::Value::kStr)
+            raise(MTB_E_UNSUPPORTED, "unsupported: null nested inside a property value");
+          canon(o, *e.second);
+          o += ",";
+        }
+        o += "}";
+        return;
+      }
+    }
+  }
+  uint32_t value(uint32_t k, const hj::Value& v) {
+    const bool objLike = v.kind == hj::Value::kObj || v.kind == hj::Value::kArr;
+    keyKinds[k] |= objLike ? 2 : 1;
+    if (keyKinds[k] == 3)
+      raise(MTB_E_UNSUPPORTED, "unsupported: property key holds both primitive and object values");
+    std::string js = hj::dump(v);
+    auto it = valId.find(js);
+    if (it != valId.end()) return it->second;
+    std::string c;
+    canon(c, v);
+    auto ci = classId.find(c);
+    uint32_t cls;
+    if (ci == classId.end()) {
+      cls = (uint32_t)classId.size();
+      classId[c] = cls;
+    } else {
+      cls = ci->second;
+    }
+    uint32_t id = (uint32_t)valJson.size();
+    valJson.push_back(js);
+    valId[js] = id;
+    valClass.push_back(cls);
+    valFalsy.push_back(v.truthy() ? 0 : 1);
+    dirty = true;
+    return id;
+  }
+  // props object -> id with (a) op-props list for annotate, (b) property set for insert specs.
+  uint32_t props(const hj::Value& obj) {
+    if (obj.kind != hj::Value::kObj) raise(MTB_E_PARSE, "props is not an object");
+    std::string js = hj::dump(obj);
+    auto it = propsByJson.find(js);
+    if (it != propsByJson.end()) return it->second;
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    for (auto& m : obj.members) {
+      const uint32_t k = key(m.first);
+      const uint32_t v = m.second.kind == hj::Value::kNull ? MTB_NONE : value(k, m.second);
+      kv.push_back({k, v});
+    }
+    const uint32_t opOff = (uint32_t)pool.size();
+    pool.push_back((uint32_t)kv.size());
+    for (auto& e : kv) { pool.push_back(e.first); pool.push_back(e.second); }
+    const uint32_t setOff = (uint32_t)pool.size();
+    uint32_t n = 0;
+    for (auto& e : kv) n += e.second != MTB_NONE;
+    pool.push_back(n);
+    for (auto& e : kv)
+      if (e.second != MTB_NONE) { pool.push_back(e.first); pool.push_back(e.second); }
+    const uint32_t id = (uint32_t)(pidx.size() / 2);
+    pidx.push_back(opOff);
+    pidx.push_back(setOff);
+    propsByJson[js] = id;
+    dirty = true;
+    return id;
+  }
+};
+
+// ------------------------------------------------------------------ host mirror of a document
+struct HostDoc {
+  std::vector<std::string> longIds;
+  std::unordered_map<std::string, uint16_t> shortOf;
+  std::string observer;
+  bool inited = false;
+  std::vector<uint16_t> initText;
+  uint32_t min0 = 0, cur0 = 0;
+  std::vector<mtb_op> pending;
+  std::vector<uint16_t> payload;  // payload of pending ops
+  int64_t lastSeq = 0;            // last appended message seq (host-side 0x038 check)
+  uint64_t totalOps = 0;          // all records ever appended (capacity sizing)
+  uint64_t totalPayload = 0;
+  // device mirror
+  DocState st{};
+  bool onDevice = false;
+  // read-back cache
+  bool cached = false;
+  std::vector<Seg> segs;
+  std::vector<Blk> blks;
+  std::vector<uint16_t> text;
+  std::vector<uint32_t> aux;
+
+  uint16_t client(const std::string& id) {
+    auto it = shortOf.find(id);
+    if (it != shortOf.end()) return it->second;
+    if (longIds.size() >= 0x7FFF) raise(MTB_E_UNSUPPORTED, "unsupported: more than 32767 clients in one document");
+    uint16_t s = (uint16_t)longIds.size();
+    shortOf[id] = s;
+    longIds.push_back(id);
+    return s;
+  }
+  std::string longId(int s) const { return s >= 0 && s < (int)longIds.size() ? longIds[s] : std::string("original"); }
+};
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void ensure(size_t want) {
+    if (want <= n) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    HIPCHK(hipMalloc((void**)&p, std::max<size_t>(want, 1) * sizeof(T)));
+    n = want;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct mtb_batch {
+  mtb_options opts{};
+  uint32_t ndocs = 0;
+  int device = 0;
+  std::vector<HostDoc> docs;
+  Interner in;
+  std::string err;
+  bool devInit = false;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf<DocState> dDocs;
+  DevBuf<mtb_op> dOps;
+  DevBuf<Seg> dSegs;
+  DevBuf<Blk> dBlks;
+  DevBuf<WEnt> dLists;
+  DevBuf<uint16_t> dText;
+  DevBuf<Lru> dHeap;
+  DevBuf<uint32_t> dAux, dFree;
+  DevBuf<uint32_t> dPool, dPidx, dValClass, dKeyRank;
+  DevBuf<uint8_t> dValFalsy;
+  std::vector<DocState> hst;
+  double lastKernelMs = 0;
+  ~mtb_batch() {
+    dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
+    dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
+    dKeyRank.release(); dValFalsy.release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+template <class F>
+int guarded(mtb_batch* b, F&& f) {
+  if (!b) return MTB_E_ARG;
+  try {
+    f();
+    return MTB_OK;
+  } catch (const MtbError& e) {
+    b->err = e.msg;
+    return e.code;
+  } catch (const hj::ParseError& e) {
+    b->err = std::string("JSON: ") + e.what();
+    return MTB_E_PARSE;
+  } catch (const std::exception& e) {
+    b->err = e.what();
+    return MTB_E_ARG;
+  }
+}
+
+HostDoc& docref(mtb_batch* b, uint32_t doc) {
+  if (doc >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
+  return b->docs[doc];
+}
+
+const hj::Value* member(const hj::Value& o, const char16_t* k) { return o.kind == hj::Value::kObj ? o.find(k) : nullptr; }
+
+uint32_t u32field(const hj::Value& o, const char16_t* k, const char* what) {
+  const hj::Value* v = member(o, k);
+  if (!v || v->kind != hj::Value::kNum || v->n < 0 || v->n > 4294967295.0 || v->n != std::floor(v->n))
+    raise(MTB_E_PARSE, std::string("missing or invalid ") + what);
+  return (uint32_t)v->n;
+}
+
+uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel) {
+  const hj::Value* v = member(op, k);
+  if (v && v->kind == hj::Value::kNum) return (uint32_t)v->n;
+  if (member(op, rel)) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions (marker-relative ops)");
+  raise(MTB_E_UNSUPPORTED, "unsupported: op without numeric position");
+}
+
+// One delta op -> record (client.ts:489-524 insert, :430 remove, :457 annotate)
+void pack_delta(mtb_batch* b, HostDoc& d, const hj::Value& op, mtb_op base, std::vector<mtb_op>& out) {
+  const hj::Value* t = member(op, u"type");
+  const int type = t && t->kind == hj::Value::kNum ? (int)t->n : -1;
+  mtb_op r = base;
+  if (type == 0) {
+    r.pos1 = position(op, u"pos1", u"relativePos1");
+    const hj::Value* seg = member(op, u"seg");
+    if (!seg || !seg->truthy()) {  // applyInsertOp: `if (op.seg)` -> no-op member
+      r.type = MTB_OP_NOOP;
+      out.push_back(r);
+      return;
+    }
+    r.type = MTB_OP_INSERT;
+    const U16* text = nullptr;
+    const hj::Value* props = nullptr;
+    if (seg->kind == hj::Value::kStr) {
+      text = &seg->s;
+    } else if (seg->kind == hj::Value::kObj && member(*seg, u"text")) {
+      const hj::Value* tv = member(*seg, u"text");
+      if (tv->kind != hj::Value::kStr) raise(MTB_E_UNSUPPORTED, "unsupported: non-string text segment");
+      text = &tv->s;
+      props = member(*seg, u"props");
+      r.flags |= MTB_F_SEGOBJ;
+    } else if (seg->kind == hj::Value::kObj && member(*seg, u"marker")) {
+      r.flags |= MTB_F_MARKER;
+      const hj::Value* mk = member(*seg, u"marker");
+      const hj::Value* rt = mk ? member(*mk, u"refType") : nullptr;
+      r.pos2 = (rt && rt->kind == hj::Value::kNum) ? (uint32_t)rt->n : 0xFFFFFFFFu;
+      props = member(*seg, u"props");
+    } else {
+      raise(MTB_E_PARSE, "Unrecognized IJSONSegment type");
+    }
+    if (text) {
+      r.pos2 = (uint32_t)text->size();
+      r.payload = (uint32_t)d.payload.size();
+      d.payload.insert(d.payload.end(), text->begin(), text->end());
+    }
+    if (props && props->truthy()) {
+      if (props->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: non-object segment props");
+      r.props = b->in.props(*props);
+    }
+    out.push_back(r);
+  } else if (type == 1 || type == 2) {
+    r.type = type == 1 ? MTB_OP_REMOVE : MTB_OP_ANNOTATE;
+    r.pos1 = position(op, u"pos1", u"relativePos1");
+    r.pos2 = position(op, u"pos2", u"relativePos2");
+    if (type == 2) {
+      const hj::Value* props = member(op, u"props");
+      hj::Value empty;
+      empty.kind = hj::Value::kObj;
+      r.props = b->in.props(props && props->kind == hj::Value::kObj ? *props : empty);
+      const hj::Value* comb = member(op, u"combiningOp");
+      if (comb && comb->kind == hj::Value::kObj) {
+        const hj::Value* name = member(*comb, u"name");
+        if (name && name->kind == hj::Value::kStr && name->s == u"rewrite") r.flags |= MTB_F_REWRITE;
+        else raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite");
+      }
+    }
+    out.push_back(r);
+  } else if (type == 3) {
+    const hj::Value* ops = member(op, u"ops");
+    if (ops && ops->kind == hj::Value::kArr)
+      for (auto& m : ops->items) pack_delta(b, d, m, base, out);
+  } else {
+    r.type = MTB_OP_NOOP;
+    out.push_back(r);
+  }
+}
+
+// ------------------------------------------------------------------ device management
+void ensure_stream(mtb_batch* b) {
+  if (b->stream) return;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) raise(MTB_E_NODEV, "no HIP device available (the engine has no CPU fallback)");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&b->ev0));
+  HIPCHK(hipEventCreate(&b->ev1));
+}
+
+// Per-document slice capacities from the record count (see DESIGN.md "HBM layout").  `n` is the
+// number of records the slices must hold (all records appended so far, times a growth margin).
+struct Caps {
+  uint32_t seg, blk, list, text, heap, aux;
+};
+Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
+  Caps c;
+  c.seg = (uint32_t)(2 * n + 64);
+  c.blk = (uint32_t)(n + 64);
+  c.list = (uint32_t)(40 * n + 4096);
+  c.text = (uint32_t)(5 * (payload + init) + 4096);
+  c.heap = (uint32_t)(3 * n + 64);
+  c.aux = (uint32_t)(24 * n + 1024);
+  return c;
+}
+bool fits(const DocState& s, const Caps& c) {
+  return s.seg_cap >= c.seg && s.blk_cap >= c.blk && s.list_cap >= c.list && s.text_cap >= c.text &&
+         s.heap_cap >= c.heap && s.aux_cap >= c.aux;
+}
+
+// (Re)lay out every document's slices so that each holds at least `want[i]`, copying live state.
+void layout(mtb_batch* b, const std::vector<Caps>& want) {
+  std::vector<DocState> ns = b->hst;
+  uint64_t seg = 0, blk = 0, lst = 0, txt = 0, hp = 0, ax = 0;
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    DocState& s = ns[i];
+    const Caps& c = want[i];
+    s.seg_cap = std::max(s.seg_cap, c.seg);
+    s.blk_cap = std::max(s.blk_cap, c.blk);
+    s.list_cap = std::max(s.list_cap, c.list);
+    s.text_cap = std::max(s.text_cap, c.text);
+    s.heap_cap = std::max(s.heap_cap, c.heap);
+    s.aux_cap = std::max(s.aux_cap, c.aux);
+    s.seg_base = seg; seg += s.seg_cap;
+    s.blk_base = blk; blk += s.blk_cap;
+    s.list_base = lst; lst += s.list_cap;
+    s.text_base = txt; txt += s.text_cap;
+    s.heap_base = hp; hp += s.heap_cap;
+    s.aux_base = ax; ax += s.aux_cap;
+    s.free_base = s.blk_base;
+  }
+  auto move = [&](auto& buf, uint64_t total, auto getBase, auto getUsed) {
+    using T = std::remove_pointer_t<decltype(buf.p)>;
+    T* np = nullptr;
+    HIPCHK(hipMalloc((void**)&np, std::max<uint64_t>(total, 1) * sizeof(T)));
+    if (buf.p) {
+      for (uint32_t i = 0; i < b->ndocs; i++) {
+        const uint64_t used = getUsed(b->hst[i]);
+        if (used)
+          HIPCHK(hipMemcpyAsync(np + getBase(ns[i]), buf.p + getBase(b->hst[i]), used * sizeof(T), hipMemcpyDeviceToDevice,
+                                b->stream));
+      }
+      HIPCHK(hipStreamSynchronize(b->stream));
+      (void)hipFree(buf.p);
+    }
+    buf.p = np;
+    buf.n = total;
+  };
+  move(b->dSegs, seg, [](const DocState& s) { return s.seg_base; }, [](const DocState& s) { return (uint64_t)s.seg_used; });
+  move(b->dBlks, blk, [](const DocState& s) { return s.blk_base; }, [](const DocState& s) { return (uint64_t)s.blk_used; });
+  move(b->dLists, lst, [](const DocState& s) { return s.list_base; }, [](const DocState& s) { return (uint64_t)s.list_used; });
+  move(b->dText, txt, [](const DocState& s) { return s.text_base; }, [](const DocState& s) { return (uint64_t)s.text_used; });
+  move(b->dHeap, hp, [](const DocState& s) { return s.heap_base; }, [](const DocState& s) { return (uint64_t)s.heap_cnt + 1; });
+  move(b->dAux, ax, [](const DocState& s) { return s.aux_base; }, [](const DocState& s) { return (uint64_t)s.aux_used; });
+  move(b->dFree, blk, [](const DocState& s) { return s.free_base; }, [](const DocState& s) { return (uint64_t)s.free_top; });
+  b->hst = ns;
+}
+
+void device_init(mtb_batch* b) {
+  ensure_stream(b);
+  b->hst.assign(b->ndocs, DocState{});
+  std::vector<Caps> want(b->ndocs);
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    want[i] = caps_for(d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()), d.initText.size());
+  }
+  layout(b, want);
+  // initial state: root block (+ the detached initial text segment), collaboration started
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    DocState& s = b->hst[i];
+    s.new_mode = b->opts.new_length_calc;
+    s.min_seq = (int32_t)d.min0;
+    s.cur_seq = (int32_t)d.cur0;
+    s.root = 0;
+    s.blk_used = 1;
+    s.aux_used = 1;
+    s.heap_cnt = 0;
+    s.list_used = 0;
+    Blk root{};
+    for (int k = 0; k < MTB_MAXCH; k++) root.child[k] = MTB_NONE;
+    root.parent = MTB_NONE;
+    root.scour = -1;
+    if (!d.initText.empty()) {
+      Seg sg{};
+      sg.len = (int32_t)d.initText.size();
+      sg.seq = 0;
+      sg.rseq = -1;
+      sg.text = 0;
+      sg.parent = 0;
+      sg.client = -1;  // LocalClientId: inserted before collaboration (client.replay.spec.ts:27)
+      sg.rc0 = -1;
+      root.child[0] = MTB_LEAF | 0;
+      root.count = 1;
+      root.len = sg.len;
+      s.seg_used = 1;
+      HIPCHK(hipMemcpyAsync(b->dSegs.p + s.seg_base, &sg, sizeof sg, hipMemcpyHostToDevice, b->stream));
+      HIPCHK(hipMemcpyAsync(b->dText.p + s.text_base, d.initText.data(), d.initText.size() * 2, hipMemcpyHostToDevice,
+                            b->stream));
+    }
+    s.text_used = (uint32_t)d.initText.size();
+    HIPCHK(hipMemcpyAsync(b->dBlks.p + s.blk_base, &root, sizeof root, hipMemcpyHostToDevice, b->stream));
+    d.onDevice = true;
+  }
+  HIPCHK(hipStreamSynchronize(b->stream));
+  b->dDocs.ensure(b->ndocs);
+  b->devInit = true;
+}
+
+void upload_tables(mtb_batch* b) {
+  Interner& in = b->in;
+  if (!in.dirty && b->dPool.p) return;
+  auto up = [&](auto& buf, const auto& vec) {
+    buf.ensure(vec.size() + 1);
+    if (!vec.empty())
+      HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice, b->stream));
+  };
+  up(b->dPool, in.pool);
+  up(b->dPidx, in.pidx);
+  up(b->dValClass, in.valClass);
+  up(b->dValFalsy, in.valFalsy);
+  up(b->dKeyRank, in.keyRank);
+  in.dirty = false;
+}
+
+void download_doc(mtb_batch* b, uint32_t i) {
+  HostDoc& d = b->docs[i];
+  if (d.cached) return;
+  if (!d.onDevice) raise(MTB_E_ARG, "document has not been replayed");
+  const DocState& s = b->hst[i];
+  d.segs.resize(s.seg_used);
+  d.blks.resize(s.blk_used);
+  d.text.resize(s.text_used);
+  d.aux.resize(s.aux_used);
+  if (s.seg_used) HIPCHK(hipMemcpyAsync(d.segs.data(), b->dSegs.p + s.seg_base, s.seg_used * sizeof(Seg), hipMemcpyDeviceToHost, b->stream));
+  if (s.blk_used) HIPCHK(hipMemcpyAsync(d.blks.data(), b->dBlks.p + s.blk_base, s.blk_used * sizeof(Blk), hipMemcpyDeviceToHost, b->stream));
+  if (s.text_used) HIPCHK(hipMemcpyAsync(d.text.data(), b->dText.p + s.text_base, s.text_used * 2, hipMemcpyDeviceToHost, b->stream));
+  if (s.aux_used) HIPCHK(hipMemcpyAsync(d.aux.data(), b->dAux.p + s.aux_base, s.aux_used * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  d.cached = true;
+}
+
+std::string derr_text(int e) {
+  switch (e) {
+    case DERR_INSERT: return "MergeTree insert failed";
+    case DERR_CAP_SEG: return "capacity: segment slice exhausted";
+    case DERR_CAP_BLK: return "capacity: block slice exhausted";
+    case DERR_CAP_LIST: return "capacity: window-list slice exhausted";
+    case DERR_CAP_TEXT: return "capacity: text arena exhausted";
+    case DERR_CAP_HEAP: return "capacity: LRU heap exhausted";
+    case DERR_CAP_AUX: return "capacity: aux arena exhausted";
+    case DERR_ASSERT_SEQ: return "0x038 Incoming op sequence# < local collabWindow's currentSequence#";
+    case DERR_ASSERT_MSN: return "0x04e/0x04f/0x039 minimum sequence number out of order";
+    case DERR_DEPTH: return "tree depth limit exceeded";
+    default: return "device error " + std::to_string(e);
+  }
+}
+int derr_code(int e) {
+  if (e == DERR_INSERT) return MTB_E_INSERT;
+  if (e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) return MTB_E_CAPACITY;
+  if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN) return MTB_E_ASSERT;
+  return MTB_E_UNSUPPORTED;
+}
+
+void replay(mtb_batch* b, mtb_stats* out) {
+  if (!b->devInit) device_init(b);
+  upload_tables(b);
+  // grow the slices of documents whose appended records no longer fit (2x headroom)
+  {
+    std::vector<Caps> want(b->ndocs);
+    bool grow = false;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      HostDoc& d = b->docs[i];
+      const DocState& s = b->hst[i];
+      Caps need = caps_for(d.totalOps, d.totalPayload + s.text_used, d.initText.size());
+      if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap) {
+        want[i] = caps_for(2 * d.totalOps, 2 * (d.totalPayload + s.text_used), d.initText.size());
+        grow = true;
+      } else {
+        want[i] = Caps{0, 0, 0, 0, 0, 0};
+      }
+    }
+    if (grow) layout(b, want);
+  }
+  // gather pending ops of every document into one buffer
+  uint64_t total = 0;
+  for (auto& d : b->docs) total += d.pending.size();
+  std::vector<mtb_op> ops;
+  ops.reserve(total);
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    DocState& s = b->hst[i];
+    if (s.err) continue;
+    // payload goes after the text already in the arena; rebase record offsets
+    const uint32_t base = s.text_used;
+    if (!d.payload.empty())
+      HIPCHK(hipMemcpyAsync(b->dText.p + s.text_base + base, d.payload.data(), d.payload.size() * 2, hipMemcpyHostToDevice,
+                            b->stream));
+    s.text_used += (uint32_t)d.payload.size();
+    s.op_base = ops.size();
+    s.n_ops = (uint32_t)d.pending.size();
+    s.op_next = 0;
+    for (mtb_op o : d.pending) {
+      if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_MARKER)) o.payload += base;
+      ops.push_back(o);
+    }
+  }
+  b->dOps.ensure(ops.size() + 1);
+  if (!ops.empty()) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.data(), ops.size() * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+  Tables t;
+  t.pool = b->dPool.p;
+  t.pidx = b->dPidx.p;
+  t.val_class = b->dValClass.p;
+  t.val_falsy = b->dValFalsy.p;
+  t.key_rank = b->dKeyRank.p;
+  HIPCHK(hipEventRecord(b->ev0, b->stream));
+  HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                           b->dHeap.p, b->dAux.p, b->dFree.p, t));
+  HIPCHK(hipEventRecord(b->ev1, b->stream));
+  HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->lastKernelMs = ms;
+  mtb_stats st{};
+  st.kernel_ms = ms;
+  int firstErr = 0;
+  uint32_t errDoc = 0;
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    DocState& s = b->hst[i];
+    d.pending.clear();
+    d.payload.clear();
+    d.cached = false;
+    st.docs++;
+    st.ops_applied += s.ops_applied;
+    st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
+    if (s.err) {
+      st.errors++;
+      if (!firstErr) { firstErr = s.err; errDoc = i; }
+    }
+  }
+  if (out) *out = st;
+  if (firstErr)
+    raise(derr_code(firstErr), "document " + std::to_string(errDoc) + " op " + std::to_string(b->hst[errDoc].err_op) + ": " +
+                                   derr_text(firstErr));
+}
+
+// ------------------------------------------------------------------ read-out helpers
+struct FlatSeg {
+  uint32_t id;
+  std::vector<int> path;
+};
+void flatten(const HostDoc& d, uint32_t root, std::vector<FlatSeg>& out, bool withPath) {
+  std::vector<int> path;
+  struct Fr { uint32_t b; int i; };
+  std::vector<Fr> st{{root, 0}};
+  while (!st.empty()) {
+    Fr& f = st.back();
+    const Blk& B = d.blks.at(f.b);
+    if (f.i >= B.count) {
+      st.pop_back();
+      if (!path.empty()) path.pop_back();
+      continue;
+    }
+    const int i = f.i++;
+    const uint32_t c = B.child[i];
+    if (c & MTB_LEAF) {
+      FlatSeg fs;
+      fs.id = c & ~MTB_LEAF;
+      if (withPath) {
+        fs.path = path;
+        fs.path.push_back(i);
+      }
+      out.push_back(std::move(fs));
+    } else {
+      path.push_back(i);
+      st.push_back({c, 0});
+    }
+  }
+}
+
+bool seg_removed(const Seg& s) { return s.rseq >= 0; }
+bool is_marker(const Seg& s) { return (s.text & MTB_MARKER) != 0; }
+
+struct PropView {
+  const uint32_t* p = nullptr;  // [n, (k, v)*n]
+  uint32_t n() const { return p ? p[0] : 0; }
+};
+PropView props_of(mtb_batch* b, const HostDoc& d, uint32_t h) {
+  PropView v;
+  if (!h) return v;
+  if (h & MTB_GPROPS) v.p = b->in.pool.data() + (h & ~MTB_GPROPS);
+  else v.p = d.aux.data() + h;
+  return v;
+}
+void props_json(mtb_batch* b, std::string& o, PropView v) {
+  o += '{';
+  for (uint32_t i = 0; i < v.n(); i++) {
+    if (i) o += ',';
+    hj::quote(o, b->in.keys[v.p[1 + 2 * i]]);
+    o += ':';
+    o += b->in.valJson[v.p[2 + 2 * i]];
+  }
+  o += '}';
+}
+bool props_match(mtb_batch* b, PropView a, PropView c) {
+  if (a.n() != c.n()) return false;
+  for (uint32_t i = 0; i < a.n(); i++) {
+    bool found = false;
+    for (uint32_t q = 0; q < c.n(); q++) {
+      if (c.p[1 + 2 * q] == a.p[1 + 2 * i]) {
+        found = true;
+        if (b->in.valClass[c.p[2 + 2 * q]] != b->in.valClass[a.p[2 + 2 * i]]) return false;
+      }
+    }
+    if (!found) return false;
+  }
+  return true;
+}
+
+void rc_list(const HostDoc& d, const Seg& s, std::vector<int>& out) {
+  out.clear();
+  if (!seg_removed(s)) return;
+  out.push_back(s.rc0);
+  if (s.rcx)
+    for (uint32_t i = 0; i < d.aux[s.rcx]; i++) out.push_back((int)d.aux[s.rcx + 1 + i]);
+}
+
+std::string dump_doc(mtb_batch* b, uint32_t i) {
+  download_doc(b, i);
+  const HostDoc& d = b->docs[i];
+  const DocState& s = b->hst[i];
+  std::string o = "{\"minSeq\":" + std::to_string(s.min_seq) + ",\"currentSeq\":" + std::to_string(s.cur_seq) +
+                  ",\"length\":" + std::to_string(d.blks[s.root].len) + "}\n";
+  std::vector<FlatSeg> fl;
+  flatten(d, s.root, fl, true);
+  std::vector<int> rc;
+  for (auto& f : fl) {
+    const Seg& g = d.segs[f.id];
+    o += "[[";
+    for (size_t k = 0; k < f.path.size(); k++) {
+      if (k) o += ',';
+      o += std::to_string(f.path[k]);
+    }
+    o += "],";
+    if (is_marker(g)) {
+      const uint32_t rt = g.text & ~MTB_MARKER;
+      o += "\"M\",";
+      o += rt == 0 ? "null" : std::to_string(rt - 1);
+    } else {
+      o += "\"T\",";
+      hj::quote(o, reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len);
+    }
+    o += ',' + std::to_string(g.seq) + ',' + std::to_string(g.client) + ',' + std::to_string(seg_removed(g) ? g.rseq : -1) + ",[";
+    rc_list(d, g, rc);
+    for (size_t k = 0; k < rc.size(); k++) {
+      if (k) o += ',';
+      o += std::to_string(rc[k]);
+    }
+    o += "],";
+    PropView pv = props_of(b, d, g.props);
+    if (g.props && pv.n() > 0) props_json(b, o, pv);
+    else o += "null";
+    o += "]\n";
+  }
+  return o;
+}
+
+uint64_t fnv(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+// utf8ByteLength (runtime-utils summaryUtils.ts:56-71) evaluated on the JS string of `utf8`
+uint64_t utf8_byte_length(const std::string& utf8) {
+  U16 s = hj::from_utf8(utf8);
+  int64_t n = (int64_t)s.size();
+  for (int64_t k = (int64_t)s.size() - 1; k >= 0; k--) {
+    const uint32_t c = s[(size_t)k];
+    if (c > 0x7f && c <= 0x7ff) n++;
+    else if (c > 0x7ff && c <= 0xffff) n += 2;
+    if (c >= 0xdc00 && c <= 0xdfff) k--;
+  }
+  return (uint64_t)n;
+}
+
+// SnapshotV1.extractSync + emit (snapshotV1.ts:122-312) over the downloaded document.
+void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
+  download_doc(b, i);
+  const HostDoc& d = b->docs[i];
+  const DocState& s = b->hst[i];
+  const int minSeq = s.min_seq, curSeq = s.cur_seq;
+  std::vector<FlatSeg> fl;
+  flatten(d, s.root, fl, false);
+  std::vector<std::string> segJson;
+  std::vector<int> segLen;
+  struct Prev {
+    bool live = false;
+    U16 text;
+    int len = 0;
+    bool marker = false;
+    uint32_t refType = 0;
+    uint32_t props = 0;
+  };
+  auto textOf = [&](const Seg& g) { return U16(reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len); };
+  auto json_of = [&](bool marker, uint32_t refType, const U16& text, uint32_t props) {
+    std::string o;
+    PropView pv = props_of(b, d, props);
+    const bool hasProps = props && pv.n() > 0;  // empty props normalized to undefined (snapshotV1.ts:199-206)
+    if (marker) {
+      o += "{\"marker\":{";
+      if (refType) o += "\"refType\":" + std::to_string(refType - 1);
+      o += "}";
+      if (hasProps) { o += ",\"props\":"; props_json(b, o, pv); }
+      o += "}";
+    } else if (hasProps) {
+      o += "{\"text\":";
+      hj::quote(o, text);
+      o += ",\"props\":";
+      props_json(b, o, pv);
+      o += "}";
+    } else {
+      hj::quote(o, text);
+    }
+    return o;
+  };
+  std::unique_ptr<Prev> prev;
+  auto pushPrev = [&]() {
+    if (!prev) return;
+    segJson.push_back(json_of(prev->marker, prev->refType, prev->text, prev->props));
+    segLen.push_back(prev->len);
+    prev.reset();
+  };
+  std::vector<int> rc;
+  for (auto& f : fl) {
+    const Seg& g = d.segs[f.id];
+    if (seg_removed(g) && g.rseq <= minSeq) continue;  // elided
+    if (g.seq <= minSeq && !seg_removed(g)) {
+      const bool marker = is_marker(g);
+      if (!prev) {
+        prev.reset(new Prev());
+        prev->live = true;
+        prev->marker = marker;
+        prev->refType = marker ? (g.text & ~MTB_MARKER) : 0;
+        if (!marker) prev->text = textOf(g);
+        prev->len = g.len;
+        prev->props = g.props;
+        continue;
+      }
+      // TextSegment.canAppend (textSegment.ts:71-78) + matchProperties
+      bool can = !prev->marker && !marker && !(prev->len > 0 && prev->text.back() == u'\n') &&
+                 (prev->len <= 256 || g.len <= 256) && props_match(b, props_of(b, d, prev->props), props_of(b, d, g.props));
+      if (can) {
+        prev->text += textOf(g);
+        prev->len += g.len;
+        prev->live = false;
+      } else {
+        pushPrev();
+        prev.reset(new Prev());
+        prev->live = true;
+        prev->marker = marker;
+        prev->refType = marker ? (g.text & ~MTB_MARKER) : 0;
+        if (!marker) prev->text = textOf(g);
+        prev->len = g.len;
+        prev->props = g.props;
+      }
+      continue;
+    }
+    pushPrev();
+    std::string o = "{\"json\":";
+    o += json_of(is_marker(g), is_marker(g) ? (g.text & ~MTB_MARKER) : 0, is_marker(g) ? U16() : textOf(g), g.props);
+    if (g.seq > minSeq) {
+      o += ",\"seq\":" + std::to_string(g.seq) + ",\"client\":";
+      hj::quote(o, hj::from_utf8(d.longId(g.client)));
+    }
+    if (seg_removed(g)) {
+      rc_list(d, g, rc);
+      o += ",\"removedSeq\":" + std::to_string(g.rseq) + ",\"removedClient\":";
+      hj::quote(o, hj::from_utf8(d.longId(rc[0])));
+      o += ",\"removedClientIds\":[";
+      for (size_t k = 0; k < rc.size(); k++) {
+        if (k) o += ',';
+        hj::quote(o, hj::from_utf8(d.longId(rc[k])));
+      }
+      o += "]";
+    }
+    o += "}";
+    segJson.push_back(o);
+    segLen.push_back(g.len);
+  }
+  pushPrev();
+  const int chunkSize = b->opts.chunk_size > 0 ? b->opts.chunk_size : 10000;
+  struct Chunk { int start = 0, count = 0, length = 0; };
+  std::vector<Chunk> chunks;
+  int totalCount = 0, totalLength = 0;
+  do {
+    Chunk c;
+    c.start = totalCount;
+    while (c.length < chunkSize && c.start + c.count < (int)segJson.size()) {
+      c.length += segLen[c.start + c.count];
+      c.count++;
+    }
+    chunks.push_back(c);
+    totalCount += c.count;
+    totalLength += c.length;
+  } while (totalCount < (int)segJson.size());
+  auto chunkText = [&](const Chunk& c, bool header) {
+    std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) + ",\"length\":" + std::to_string(c.length) +
+                    ",\"segments\":[";
+    for (int k = 0; k < c.count; k++) {
+      if (k) o += ',';
+      o += segJson[c.start + k];
+    }
+    o += "],\"startIndex\":" + std::to_string(c.start);
+    if (header) {
+      o += ",\"headerMetadata\":{\"minSequenceNumber\":" + std::to_string(minSeq) + ",\"sequenceNumber\":" + std::to_string(curSeq) +
+           ",\"orderedChunkMetadata\":[";
+      for (size_t k = 0; k < chunks.size(); k++) {
+        if (k) o += ',';
+        o += k == 0 ? std::string("{\"id\":\"header\"}") : "{\"id\":\"body_" + std::to_string(k - 1) + "\"}";
+      }
+      o += "],\"totalLength\":" + std::to_string(totalLength) + ",\"totalSegmentCount\":" + std::to_string(totalCount) + "}";
+    }
+    o += "}";
+    return o;
+  };
+  blobs.clear();
+  blobs.push_back({"header", chunkText(chunks[0], true)});
+  for (size_t k = 1; k < chunks.size(); k++) blobs.push_back({"body_" + std::to_string(k - 1), chunkText(chunks[k], false)});
+  // ISummaryTreeWithStats (runtime-utils summaryUtils.ts:138-198)
+  std::string tree = "{";
+  uint64_t totalBytes = 0;
+  for (size_t k = 0; k < blobs.size(); k++) {
+    if (k) tree += ',';
+    tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
+    hj::quote(tree, hj::from_utf8(blobs[k].second));
+    tree += "}";
+    totalBytes += utf8_byte_length(blobs[k].second);
+  }
+  tree += "}";
+  summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
+                std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
+                ",\"unreferencedBlobSize\":0}}";
+}
+
+char* dup(const std::string& s) {
+  char* p = (char*)malloc(s.size() + 1);
+  memcpy(p, s.data(), s.size());
+  p[s.size()] = 0;
+  return p;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_mask, mtb_batch** out) {
+  if (!out || ndocs == 0) return MTB_E_ARG;
+  auto* b = new mtb_batch();
+  if (opts) b->opts = *opts;
+  b->ndocs = ndocs;
+  b->docs.resize(ndocs);
+  b->device = 0;
+  for (int k = 0; k < 32; k++)
+    if (device_mask & (1u << k)) { b->device = k; break; }
+  *out = b;
+  return MTB_OK;
+}
+
+void mtb_batch_destroy(mtb_batch* b) { delete b; }
+const char* mtb_last_error(mtb_batch* b) { return b ? b->err.c_str() : "null batch"; }
+void mtb_free(void* p) { free(p); }
+
+int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_t n_units, const char* observer_long_id,
+                 uint32_t min_seq, uint32_t cur_seq) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
+    if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
+    d.initText.assign(initial_text, initial_text + n_units);
+    d.observer = observer_long_id;
+    d.client(d.observer);  // startOrUpdateCollaboration: observer gets short id 0 (client.ts:1133)
+    d.min0 = min_seq;
+    d.cur0 = cur_seq;
+    d.lastSeq = cur_seq;
+    d.inited = true;
+  });
+}
+
+int mtb_add_client(mtb_batch* b, uint32_t doc, const char* long_id) {
+  return guarded(b, [&] { docref(b, doc).client(long_id ? long_id : ""); });
+}
+
+int mtb_intern_props(mtb_batch* b, const char* json, size_t len, uint32_t* id_out) {
+  return guarded(b, [&] {
+    hj::Value v = hj::parse(json, len);
+    *id_out = b->in.props(v);
+  });
+}
+
+int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json, size_t len) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    hj::Value msg = hj::parse(json, len);
+    if (msg.kind != hj::Value::kObj) raise(MTB_E_PARSE, "message is not an object");
+    const hj::Value* cid = member(msg, u"clientId");
+    if (!cid || cid->kind != hj::Value::kStr) raise(MTB_E_UNSUPPORTED, "unsupported: message without a string clientId");
+    const std::string longId = hj::to_utf8(cid->s.data(), cid->s.size());
+    mtb_op base{};
+    base.client = d.client(longId);
+    base.seq = u32field(msg, u"sequenceNumber", "sequenceNumber");
+    base.ref_seq = u32field(msg, u"referenceSequenceNumber", "referenceSequenceNumber");
+    base.msn = u32field(msg, u"minimumSequenceNumber", "minimumSequenceNumber");
+    if ((int64_t)base.seq < d.lastSeq) raise(MTB_E_ASSERT, "0x038 Incoming op sequence# < local collabWindow's currentSequence#");
+    if (base.msn > base.seq) raise(MTB_E_ASSERT, "0x039 Incoming op sequence# < minSequence#");
+    std::vector<mtb_op> recs;
+    const size_t payloadBefore = d.payload.size();
+    const hj::Value* type = member(msg, u"type");
+    const bool isOp = type && type->kind == hj::Value::kStr && type->s == u"op";
+    const hj::Value* contents = member(msg, u"contents");
+    if (isOp) {
+      if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
+      if (longId == d.observer) {
+        // ack path with no pending local segments: one zamboni per member (client.ts:866, mergeTree.ts:1283)
+        const hj::Value* t = member(*contents, u"type");
+        size_t members = 1;
+        if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
+          const hj::Value* ops = member(*contents, u"ops");
+          members = ops && ops->kind == hj::Value::kArr ? ops->items.size() : 0;
+        }
+        for (size_t k = 0; k < members; k++) {
+          mtb_op r = base;
+          r.type = MTB_OP_ACK;
+          recs.push_back(r);
+        }
+      } else {
+        pack_delta(b, d, *contents, base, recs);
+      }
+    }
+    if (recs.empty()) {
+      mtb_op r = base;
+      r.type = MTB_OP_NOOP;
+      recs.push_back(r);
+    }
+    recs.back().flags |= MTB_F_LAST;
+    d.totalPayload += d.payload.size() - payloadBefore;
+    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
+    d.totalOps += recs.size();
+    d.lastSeq = base.seq;
+  });
+}
+
+int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, const uint16_t* payload, size_t payload_len) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    const uint32_t base = (uint32_t)d.payload.size();
+    d.payload.insert(d.payload.end(), payload, payload + payload_len);
+    d.totalPayload += payload_len;
+    for (uint32_t k = 0; k < n; k++) {
+      mtb_op o = ops[k];
+      if (o.type > MTB_OP_ACK) raise(MTB_E_ARG, "bad record type");
+      if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_MARKER)) {
+        if ((uint64_t)o.payload + o.pos2 > payload_len) raise(MTB_E_ARG, "record payload out of range");
+        o.payload += base;
+      }
+      if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_ANNOTATE) && o.props >= b->in.pidx.size() / 2)
+        raise(MTB_E_ARG, "record props id out of range");
+      if (o.client >= d.longIds.size() && o.type != MTB_OP_NOOP)
+        raise(MTB_E_ARG, "record client id not registered (mtb_add_client)");
+      d.pending.push_back(o);
+    }
+    d.totalOps += n;
+  });
+}
+
+int mtb_replay(mtb_batch* b, mtb_stats* out) {
+  return guarded(b, [&] { replay(b, out); });
+}
+
+int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out) {
+  return guarded(b, [&] {
+    download_doc(b, doc);
+    HostDoc& d = docref(b, doc);
+    std::vector<FlatSeg> fl;
+    flatten(d, b->hst[doc].root, fl, false);
+    size_t n = 0;
+    for (auto& f : fl) {
+      const Seg& g = d.segs[f.id];
+      if (seg_removed(g) || is_marker(g)) continue;  // MergeTreeTextHelper.gatherText on visible text segments
+      if (buf && n + (size_t)g.len <= cap) memcpy(buf + n, d.text.data() + g.text, (size_t)g.len * 2);
+      n += (size_t)g.len;
+    }
+    if (len_out) *len_out = n;
+    if (buf && n > cap) raise(MTB_E_ARG, "buffer too small");
+  });
+}
+
+int mtb_get_length(mtb_batch* b, uint32_t doc, uint32_t* len_out) {
+  return guarded(b, [&] {
+    docref(b, doc);
+    download_doc(b, doc);
+    *len_out = (uint32_t)b->docs[doc].blks[b->hst[doc].root].len;
+  });
+}
+
+int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (d.onDevice) {
+      if (cur_seq) *cur_seq = (uint32_t)b->hst[doc].cur_seq;
+      if (min_seq) *min_seq = (uint32_t)b->hst[doc].min_seq;
+    } else {
+      if (cur_seq) *cur_seq = d.cur0;
+      if (min_seq) *min_seq = d.min0;
+    }
+  });
+}
+
+int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len) {
+  return guarded(b, [&] {
+    docref(b, doc);
+    std::string s = dump_doc(b, doc);
+    *out = dup(s);
+    if (out_len) *out_len = s.size();
+  });
+}
+
+int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out) {
+  return guarded(b, [&] {
+    docref(b, doc);
+    *out = fnv(dump_doc(b, doc));
+  });
+}
+
+int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_blob_list* out) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (msn >= 0 && seq >= 0) {  // Client.summarize: updateSeqNumbers(deltaManager.MSN, lastSequenceNumber)
+      mtb_op r{};
+      r.type = MTB_OP_NOOP;
+      r.flags = MTB_F_LAST;
+      r.seq = (uint32_t)seq;
+      r.msn = (uint32_t)msn;
+      d.pending.push_back(r);
+      d.totalOps++;
+      replay(b, nullptr);
+    }
+    std::vector<std::pair<std::string, std::string>> blobs;
+    std::string summary;
+    summarize(b, doc, blobs, summary);
+    out->count = (uint32_t)blobs.size();
+    out->blobs = (mtb_blob*)calloc(blobs.size(), sizeof(mtb_blob));
+    for (size_t k = 0; k < blobs.size(); k++) {
+      out->blobs[k].path = dup(blobs[k].first);
+      out->blobs[k].content = dup(blobs[k].second);
+      out->blobs[k].content_len = blobs[k].second.size();
+    }
+    out->summary_json = dup(summary);
+    out->summary_json_len = summary.size();
+  });
+}
+
+void mtb_blob_list_free(mtb_blob_list* l) {
+  if (!l) return;
+  for (uint32_t k = 0; k < l->count; k++) {
+    free((void*)l->blobs[k].path);
+    free((void*)l->blobs[k].content);
+  }
+  free(l->blobs);
+  free((void*)l->summary_json);
+  l->blobs = nullptr;
+  l->summary_json = nullptr;
+  l->count = 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1205 @@
+// MI355X (gfx950) batched merge-tree replay kernel.
+//
+// One 64-lane wavefront owns one document and applies that document's sequenced ops in order,
+// exactly as the reference observer `Client.applyMsg` would (packages/dds/merge-tree/src/client.ts:858).
+// Control flow is wave-uniform (every lane walks the same tree path); the lanes parallelise the
+// per-op inner loops: the <=8 children of a block, the concatenated window lists of those children,
+// list/segment rebuilds and text copies.  There is no MFMA: nothing here is a dense contraction.
+//
+// Differences from the reference data structures (results are identical):
+//  * PartialSequenceLengths (partialLengths.ts:239) is replaced by one flat window list per block.
+//    A block's length in the (refSeq R, client C) perspective is
+//        cachedLength - sum_{e in list, e.seq > R} w(e)
+//    where w(e) = e.delta for MAIN entries of other clients and for OVERLAP entries of C.  This is the
+//    same quantity getPartialLength (partialLengths.ts:698) returns and the sum of the leaf
+//    visibilities (mergeTree.ts:916-1004) - the oracle verifies that identity on every query.
+//  * The recursive insertingWalk (mergeTree.ts:1740) runs iteratively with an explicit path.
+//  * Length/list bookkeeping is propagated incrementally along the recorded path instead of the
+//    reference's combine/update rebuilds; split/pack blocks rebuild their list from their children.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mtb.h"
+#include "mtb_device.h"
+
+namespace mtbk {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// single-wave workgroup: makes this wave's global stores visible to all of its lanes
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wscan_incl(int v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o, 64);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ int first_set(unsigned long long m) { return __ffsll((long long)m) - 1; }
+
+struct Scratch {  // LDS, one per wave
+  uint32_t path[MTB_MAXDEPTH];
+  uint32_t sb[MTB_MAXDEPTH];
+  int32_t sidx[MTB_MAXDEPTH];
+  int32_t scnt[MTB_MAXDEPTH];
+  int32_t acc[MTB_MAXDEPTH];
+  uint32_t cid[MTB_MAXDEPTH][MTB_MAXCH];
+  int32_t clen[MTB_MAXDEPTH][MTB_MAXCH];
+  uint32_t hold[64];
+  uint32_t pk[64];
+  uint32_t pv[64];
+};
+
+struct Eng {
+  DocState* ds;
+  Seg* seg;
+  Blk* blk;
+  WEnt* lst;
+  uint16_t* txt;
+  Lru* heap;
+  uint32_t* aux;
+  uint32_t* fre;
+  const mtb_op* ops;
+  Tables T;
+  Scratch* sh;
+  int lane;
+  // uniform document state (mirrors DocState)
+  int minSeq, curSeq;
+  uint32_t root;
+  bool newMode;
+  uint32_t seg_used, blk_used, free_top, list_used, text_used, heap_cnt, aux_used;
+  int err;
+  uint64_t n_mod, ops_applied, text_bytes;
+  // per-op memo for annotate
+  uint32_t memo_old, memo_new;
+
+  // ------------------------------------------------------------------ errors / allocation
+  __device__ void fail(int code) {
+    if (!err) err = code;
+  }
+  __device__ uint32_t alloc_seg() {
+    if (seg_used >= ds->seg_cap) { fail(DERR_CAP_SEG); return 0; }
+    return seg_used++;
+  }
+  __device__ uint32_t alloc_blk() {
+    uint32_t b;
+    if (free_top > 0) {
+      free_top--;
+      b = fre[free_top];
+    } else {
+      if (blk_used >= ds->blk_cap) { fail(DERR_CAP_BLK); return 0; }
+      b = blk_used++;
+    }
+    Blk& B = blk[b];
+    if (lane < MTB_MAXCH) B.child[lane] = MTB_NONE;
+    if (lane == 0) {
+      B.parent = MTB_NONE;
+      B.len = 0;
+      B.loff = 0;
+      B.lcnt = 0;
+      B.lcap = 0;
+      B.count = 0;
+      B.index = 0;
+      B.scour = -1;
+    }
+    wsync();
+    return b;
+  }
+  __device__ void free_blk(uint32_t b) {
+    if (lane == 0) fre[free_top] = b;
+    free_top++;
+  }
+  __device__ uint32_t alloc_aux(uint32_t n) {
+    if (aux_used + n > ds->aux_cap) { fail(DERR_CAP_AUX); return 1; }
+    uint32_t o = aux_used;
+    aux_used += n;
+    return o;
+  }
+
+  // ------------------------------------------------------------------ visibility
+  __device__ bool rc_has(const Seg& s, int C) const {
+    if (s.rc0 == C) return true;
+    if (s.rcx) {
+      uint32_t n = aux[s.rcx];
+      for (uint32_t i = 0; i < n; i++)
+        if ((int)aux[s.rcx + 1 + i] == C) return true;
+    }
+    return false;
+  }
+  // localNetLength (mergeTree.ts:613-634)
+  __device__ int local_len(const Seg& s) const {
+    if (s.rseq >= 0) {
+      if (!newMode) return s.rseq > minSeq ? 0 : MTB_UNDEF;
+      return 0;
+    }
+    return s.len;
+  }
+  // nodeLength for a leaf in a remote perspective (mergeTree.ts:935-1001)
+  __device__ int seg_vis(const Seg& s, int R, int C) const {
+    const bool removed = s.rseq >= 0;
+    if (newMode) {
+      if (removed) {
+        if (s.rseq <= minSeq) return MTB_UNDEF;
+        if (s.rseq <= R || rc_has(s, C)) return 0;
+      }
+      return (s.seq <= R || s.client == C) ? s.len : 0;
+    }
+    if (removed && s.rseq <= R) return MTB_UNDEF;
+    if (s.client == C || s.seq <= R) {
+      if (removed) return rc_has(s, C) ? 0 : s.len;
+      return s.len;
+    }
+    if (removed) return MTB_UNDEF;
+    return 0;
+  }
+
+  // Lengths of the children of block b in the (R, C) perspective (observer: cachedLength view).
+  // Lane j < count receives child id (cid), length (UNDEF allowed) and, for leaves, the seg seq.
+  __device__ int child_info(uint32_t b, int R, int C, bool observer, uint32_t& cid, int& clen, int& cseq) {
+    const Blk& B = blk[b];
+    const int count = B.count;
+    cid = MTB_NONE;
+    clen = 0;
+    cseq = 0;
+    uint32_t loff = 0, lcnt = 0;
+    if (lane < count) {
+      cid = B.child[lane];
+      if (cid & MTB_LEAF) {
+        const Seg s = seg[cid & ~MTB_LEAF];
+        clen = observer ? local_len(s) : seg_vis(s, R, C);
+        cseq = s.seq;
+      } else {
+        const Blk& cb = blk[cid];
+        clen = cb.len;
+        if (!observer) {
+          loff = cb.loff;
+          lcnt = cb.lcnt;
+        }
+      }
+    }
+    if (!observer) {
+      // concatenated scan of the children's window lists
+      const int incl = wscan_incl((int)lcnt);
+      const int excl = incl - (int)lcnt;
+      const int total = __shfl(incl, 63, 64);
+      if (total > 0) {
+        int pre[MTB_MAXCH], off[MTB_MAXCH];
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++) {
+          pre[k] = __shfl(excl, k, 64);
+          off[k] = __shfl((int)loff, k, 64);
+        }
+        int acc[MTB_MAXCH];
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++) acc[k] = 0;
+        for (int t = lane; t < total; t += 64) {
+          int j = 0;
+#pragma unroll
+          for (int k = 1; k < MTB_MAXCH; k++)
+            if (k < count && pre[k] <= t) j = k;
+          int base = 0;
+#pragma unroll
+          for (int k = 0; k < MTB_MAXCH; k++)
+            if (k == j) base = off[k] + (t - pre[k]);
+          const WEnt e = lst[base];
+          int w = 0;
+          if (e.seq > R) {
+            const int c = e.ck & 0xFFFF;
+            const int kind = e.ck >> 16;
+            if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) w = e.delta;
+          }
+#pragma unroll
+          for (int k = 0; k < MTB_MAXCH; k++)
+            if (k == j) acc[k] += w;
+        }
+        int mine = 0;
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++) {
+          const int s = wsum(acc[k]);
+          if (k == lane) mine = s;
+        }
+        if (lane < count && !(cid & MTB_LEAF)) clen -= mine;
+      }
+    }
+    return count;
+  }
+
+  // ------------------------------------------------------------------ window lists
+  // Allocate a list slice of `cap` entries.
+  __device__ uint32_t list_alloc(uint32_t cap) {
+    if (list_used + cap > ds->list_cap) { fail(DERR_CAP_LIST); return 0; }
+    uint32_t o = list_used;
+    list_used += cap;
+    return o;
+  }
+  // Append (seq, client, kind, delta) to the lists of `n` blocks in sh->path[0..n) (lane-parallel
+  // fast path, sequential re-allocation for full lists).
+  __device__ void list_append_path(int n, int seqv, int client, int kind, int delta) {
+    const int ck = (client & 0xFFFF) | (kind << 16);
+    bool need = false;
+    if (lane < n) {
+      const uint32_t b = sh->path[lane];
+      Blk& B = blk[b];
+      const uint32_t cnt = B.lcnt;
+      bool merged = false;
+      if (cnt > 0) {
+        WEnt& last = lst[B.loff + cnt - 1];
+        if (last.seq == seqv && last.ck == ck) {
+          last.delta += delta;
+          merged = true;
+        }
+      }
+      if (!merged) {
+        if (cnt < B.lcap) {
+          WEnt e;
+          e.seq = seqv;
+          e.ck = ck;
+          e.delta = delta;
+          e.pad = 0;
+          lst[B.loff + cnt] = e;
+          B.lcnt = cnt + 1;
+        } else {
+          need = true;
+        }
+      }
+    }
+    unsigned long long m = __ballot(need);
+    wsync();
+    while (m) {
+      const int i = first_set(m);
+      m &= m - 1;
+      const uint32_t b = sh->path[i];
+      list_grow(b, 1);
+      Blk& B = blk[b];
+      if (lane == 0) {
+        WEnt e;
+        e.seq = seqv;
+        e.ck = ck;
+        e.delta = delta;
+        e.pad = 0;
+        lst[B.loff + B.lcnt] = e;
+        B.lcnt = B.lcnt + 1;
+      }
+      wsync();
+    }
+  }
+  // Re-allocate block b's list with room for `extra` more entries, dropping entries <= minSeq.
+  __device__ void list_grow(uint32_t b, uint32_t extra) {
+    Blk& B = blk[b];
+    const uint32_t cnt = B.lcnt, off = B.loff;
+    // live entries
+    uint32_t live = 0;
+    for (uint32_t base = 0; base < cnt; base += 64) {
+      const uint32_t i = base + lane;
+      const bool keep = i < cnt && lst[off + i].seq > minSeq;
+      live += __popcll(__ballot(keep));
+    }
+    uint32_t cap = live + extra;
+    cap = cap < 8 ? 8 : cap * 2;
+    const uint32_t no = list_alloc(cap);
+    if (err) return;
+    uint32_t w = 0;
+    for (uint32_t base = 0; base < cnt; base += 64) {
+      const uint32_t i = base + lane;
+      WEnt e;
+      bool keep = false;
+      if (i < cnt) {
+        e = lst[off + i];
+        keep = e.seq > minSeq;
+      }
+      const unsigned long long m = __ballot(keep);
+      const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+      if (keep) lst[no + w + rank] = e;
+      w += __popcll(m);
+    }
+    if (lane == 0) {
+      B.loff = no;
+      B.lcnt = w;
+      B.lcap = cap;
+    }
+    wsync();
+  }
+  // Rebuild block b's window list from its children (after split / pack / root growth) and its
+  // cachedLength (blockUpdate, mergeTree.ts:2392).
+  __device__ void rebuild(uint32_t b) {
+    Blk& B = blk[b];
+    const int count = B.count;
+    // pass 1: count entries and observer length
+    int nent = 0, olen = 0;
+    uint32_t cid = MTB_NONE;
+    Seg s;
+    uint32_t coff = 0, ccnt = 0;
+    if (lane < count) {
+      cid = B.child[lane];
+      if (cid & MTB_LEAF) {
+        s = seg[cid & ~MTB_LEAF];
+        const int l = local_len(s);
+        olen = l == MTB_UNDEF ? 0 : l;
+        if (s.seq > minSeq) nent++;
+        if (s.rseq >= 0 && s.rseq > minSeq) {
+          nent++;
+          if (s.rcx) nent += (int)aux[s.rcx];
+        }
+      } else {
+        const Blk& cb = blk[cid];
+        olen = cb.len;
+        coff = cb.loff;
+        ccnt = cb.lcnt;
+      }
+    }
+    const int totalLen = wsum(olen);
+    // block children: count live entries of each child list
+    const int cincl = wscan_incl((int)ccnt);
+    const int cexcl = cincl - (int)ccnt;
+    const int ctotal = __shfl(cincl, 63, 64);
+    int live_from_children = 0;
+    // uniform helpers for the children lists
+    int pre[MTB_MAXCH], off[MTB_MAXCH];
+#pragma unroll
+    for (int k = 0; k < MTB_MAXCH; k++) {
+      pre[k] = __shfl(cexcl, k, 64);
+      off[k] = __shfl((int)coff, k, 64);
+    }
+    for (int base = 0; base < ctotal; base += 64) {
+      const int t = base + lane;
+      bool keep = false;
+      if (t < ctotal) {
+        int j = 0;
+#pragma unroll
+        for (int k = 1; k < MTB_MAXCH; k++)
+          if (k < count && pre[k] <= t) j = k;
+        int p = 0;
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++)
+          if (k == j) p = off[k] + (t - pre[k]);
+        keep = lst[p].seq > minSeq;
+      }
+      live_from_children += __popcll(__ballot(keep));
+    }
+    const int segEnt = wsum(nent);
+    const int total = segEnt + live_from_children;
+    uint32_t cap = (uint32_t)total;
+    cap = cap < 8 ? 8 : cap + cap / 2 + 4;
+    const uint32_t no = list_alloc(cap);
+    if (err) return;
+    // pass 2: write
+    const int sincl = wscan_incl(nent);
+    int w = sincl - nent;  // exclusive
+    if (lane < count && (cid & MTB_LEAF)) {
+      WEnt e;
+      e.pad = 0;
+      if (s.seq > minSeq) {
+        e.seq = s.seq;
+        e.ck = (s.client & 0xFFFF) | (WK_MAIN << 16);
+        e.delta = s.len;
+        lst[no + w++] = e;
+      }
+      if (s.rseq >= 0 && s.rseq > minSeq) {
+        e.seq = s.rseq;
+        e.ck = (s.rc0 & 0xFFFF) | (WK_MAIN << 16);
+        e.delta = -s.len;
+        lst[no + w++] = e;
+        if (s.rcx) {
+          const uint32_t n = aux[s.rcx];
+          for (uint32_t i = 0; i < n; i++) {
+            e.ck = ((int)aux[s.rcx + 1 + i] & 0xFFFF) | (WK_OVERLAP << 16);
+            e.delta = s.len;
+            lst[no + w++] = e;
+          }
+        }
+      }
+    }
+    uint32_t wpos = (uint32_t)segEnt;
+    for (int base = 0; base < ctotal; base += 64) {
+      const int t = base + lane;
+      bool keep = false;
+      WEnt e;
+      if (t < ctotal) {
+        int j = 0;
+#pragma unroll
+        for (int k = 1; k < MTB_MAXCH; k++)
+          if (k < count && pre[k] <= t) j = k;
+        int p = 0;
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++)
+          if (k == j) p = off[k] + (t - pre[k]);
+        e = lst[p];
+        keep = e.seq > minSeq;
+      }
+      const unsigned long long m = __ballot(keep);
+      const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+      if (keep) lst[no + wpos + rank] = e;
+      wpos += __popcll(m);
+    }
+    if (lane == 0) {
+      B.loff = no;
+      B.lcnt = (uint32_t)total;
+      B.lcap = cap;
+      B.len = totalLen;
+    }
+    wsync();
+  }
+
+  // ------------------------------------------------------------------ tree primitives
+  __device__ void set_parent(uint32_t node, uint32_t b, int idx) {
+    if (node & MTB_LEAF) {
+      seg[node & ~MTB_LEAF].parent = b;
+    } else {
+      blk[node].parent = b;
+      blk[node].index = (uint8_t)idx;
+    }
+  }
+  // Insert `node` at child index k of block b (insertingWalk shift, mergeTree.ts:1831-1837).
+  __device__ void insert_child(uint32_t b, int k, uint32_t node) {
+    Blk& B = blk[b];
+    const int count = B.count;
+    uint32_t c = MTB_NONE;
+    if (lane < count) c = B.child[lane];
+    wsync();
+    if (lane < count && lane >= k) {
+      B.child[lane + 1] = c;
+      set_parent(c, b, lane + 1);
+    }
+    if (lane == 0) {
+      B.child[k] = node;
+      set_parent(node, b, k);
+      B.count = (uint8_t)(count + 1);
+    }
+    wsync();
+  }
+  // split (mergeTree.ts:1858-1871): children 4..7 move to a new block.
+  __device__ uint32_t split_block(uint32_t b) {
+    const uint32_t nb = alloc_blk();
+    if (err) return 0;
+    Blk& B = blk[b];
+    Blk& N = blk[nb];
+    const int half = MTB_MAXCH / 2;
+    if (lane < half) {
+      const uint32_t c = B.child[half + lane];
+      N.child[lane] = c;
+      set_parent(c, nb, lane);
+      B.child[half + lane] = MTB_NONE;
+    }
+    if (lane == 0) {
+      B.count = (uint8_t)half;
+      N.count = (uint8_t)half;
+      N.parent = B.parent;
+    }
+    wsync();
+    rebuild(b);
+    rebuild(nb);
+    return nb;
+  }
+  // updateRoot (mergeTree.ts:1268-1277)
+  __device__ void grow_root(uint32_t left, uint32_t right) {
+    const uint32_t r = alloc_blk();
+    if (err) return;
+    Blk& R = blk[r];
+    if (lane == 0) {
+      R.child[0] = left;
+      R.child[1] = right;
+      R.count = 2;
+      blk[left].parent = r;
+      blk[left].index = 0;
+      blk[right].parent = r;
+      blk[right].index = 1;
+    }
+    wsync();
+    rebuild(r);
+    root = r;
+  }
+  // After inserting into block sh->path[d] (the leaf-level block), split every full block on the path.
+  __device__ void fix_overflow(int d) {
+    int level = d;
+    uint32_t cur = sh->path[level];
+    while (!err && blk[cur].count >= MTB_MAXCH) {
+      const uint32_t nb = split_block(cur);
+      if (err) return;
+      if (level == 0) {
+        grow_root(cur, nb);
+        return;
+      }
+      const uint32_t p = sh->path[level - 1];
+      insert_child(p, blk[cur].index + 1, nb);
+      cur = p;
+      level--;
+    }
+  }
+
+  // BaseSegment.splitAt (mergeTreeNodes.ts:481-510) + TextSegment.createSplitSegmentAt
+  __device__ uint32_t split_seg(uint32_t sid, int at) {
+    const uint32_t r = alloc_seg();
+    if (err) return 0;
+    Seg s = seg[sid];
+    Seg t = s;
+    t.len = s.len - at;
+    t.text = s.text + (uint32_t)at;
+    if (lane == 0) {
+      seg[r] = t;
+      seg[sid].len = at;
+    }
+    n_mod += 2;
+    wsync();
+    return r;
+  }
+
+  // ------------------------------------------------------------------ insertingWalk
+  // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
+  // mode 1: blockInsert of candidate `cand` (seq S).  Returns false if the candidate was not placed.
+  __device__ bool walk(int pos, int R, int C, int S, bool insertMode, uint32_t cand, int candLen) {
+    uint32_t b = root;
+    int p = pos;
+    int d = 0;
+    while (true) {
+      if (d >= MTB_MAXDEPTH) { fail(DERR_DEPTH); return false; }
+      sh->path[d] = b;
+      uint32_t cid;
+      int clen, cseq;
+      const int count = child_info(b, R, C, false, cid, clen, cseq);
+      const int def = (lane < count && clen > 0) ? clen : 0;
+      const int incl = wscan_incl(def);
+      const int pj = p - (incl - def);
+      const bool isBlk = lane < count && !(cid & MTB_LEAF);
+      const bool tie = isBlk || (insertMode && pj == 0 && S > cseq);
+      const bool qual = lane < count && clen != MTB_UNDEF && (pj < clen || (pj == clen && tie));
+      const unsigned long long m = __ballot(qual);
+      if (m) {
+        const int j = first_set(m);
+        const uint32_t cj = __shfl(cid, j, 64);
+        const int pjj = __shfl(pj, j, 64);
+        if (!(cj & MTB_LEAF)) {
+          b = cj;
+          p = pjj;
+          d++;
+          continue;
+        }
+        if (insertMode) {
+          insert_child(b, j, cand | MTB_LEAF);
+        } else {
+          if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
+          const uint32_t sid = cj & ~MTB_LEAF;
+          if (seg[sid].text & MTB_MARKER) return true;  // markers never split
+          const uint32_t r = split_seg(sid, pjj);
+          if (err) return false;
+          insert_child(b, j + 1, r | MTB_LEAF);
+          fix_overflow(d);
+          return true;
+        }
+      } else {
+        const int total = __shfl(incl, 63, 64);
+        if (p - total != 0 || !insertMode) return !insertMode;
+        insert_child(b, count, cand | MTB_LEAF);
+      }
+      // candidate inserted into block b at depth d: propagate its length and window entry
+      if (lane <= d) blk[sh->path[lane]].len += candLen;
+      wsync();
+      list_append_path(d + 1, S, C, WK_MAIN, candLen);
+      fix_overflow(d);
+      return true;
+    }
+  }
+
+  // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
+  __device__ void heap_add(uint32_t s, int maxSeq) {
+    if (heap_cnt + 1 >= ds->heap_cap) { fail(DERR_CAP_HEAP); return; }
+    uint32_t k = ++heap_cnt;
+    Lru x;
+    x.seg = s;
+    x.maxSeq = maxSeq;
+    while (k > 1) {
+      const Lru par = heap[k >> 1];
+      if (!(par.maxSeq - x.maxSeq > 0)) break;
+      if (lane == 0) heap[k] = par;
+      k >>= 1;
+    }
+    if (lane == 0) heap[k] = x;
+    wsync();
+  }
+  __device__ Lru heap_get() {
+    const Lru top = heap[1];
+    const Lru last = heap[heap_cnt];
+    heap_cnt--;
+    const uint32_t count = heap_cnt;
+    uint32_t k = 1;
+    // fixDown with the last element placed at the root
+    while ((k << 1) <= count) {
+      uint32_t j = k << 1;
+      Lru a = heap[j];
+      if (j < count) {
+        const Lru bb = heap[j + 1];
+        if (a.maxSeq - bb.maxSeq > 0) {
+          j++;
+          a = bb;
+        }
+      }
+      if (last.maxSeq - a.maxSeq <= 0) break;
+      if (lane == 0) heap[k] = a;
+      k = j;
+    }
+    if (count >= 1 && lane == 0) heap[k] = last;
+    wsync();
+    return top;
+  }
+  // addToLRUSet (mergeTree.ts:741-751)
+  __device__ void lru_add(uint32_t sid, int seqv) {
+    const uint32_t b = seg[sid].parent;
+    if (blk[b].scour != 1 && seqv > curSeq) {
+      if (lane == 0) blk[b].scour = 1;
+      wsync();
+      heap_add(sid, seqv);
+    }
+  }
+
+  // ------------------------------------------------------------------ properties
+  __device__ const uint32_t* props_ptr(uint32_t h) const {
+    return (h & MTB_GPROPS) ? (T.pool + (h & ~MTB_GPROPS)) : (aux + h);
+  }
+  // matchProperties (properties.ts:71-96) on interned property sets
+  __device__ bool props_match(uint32_t a, uint32_t b) const {
+    if (a == b) return true;
+    const uint32_t* pa = a ? props_ptr(a) : nullptr;
+    const uint32_t* pb = b ? props_ptr(b) : nullptr;
+    const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
+    if (na != nb) return false;
+    for (uint32_t i = 0; i < na; i++) {
+      const uint32_t k = pa[1 + 2 * i];
+      bool found = false;
+      for (uint32_t q = 0; q < nb; q++) {
+        if (pb[1 + 2 * q] == k) {
+          found = true;
+          if (T.val_class[pa[2 + 2 * i]] != T.val_class[pb[2 + 2 * q]]) return false;
+          break;
+        }
+      }
+      if (!found) return false;
+    }
+    return true;
+  }
+  // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157)
+  __device__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
+    if (old == memo_old && memo_new) return memo_new;
+    const uint32_t* op = T.pool + T.pidx[2 * opId];
+    const uint32_t nop = op[0];
+    uint32_t n = 0;
+    if (old) {
+      const uint32_t* po = props_ptr(old);
+      n = po[0];
+      if (n > 64) n = 64;
+      for (uint32_t i = lane; i < n; i += 64) {
+        sh->pk[i] = po[1 + 2 * i];
+        sh->pv[i] = po[2 + 2 * i];
+      }
+    }
+    wsync();
+    if (rewrite) {
+      // delete old keys whose new value is falsy/absent (the `!newProps[key]` test)
+      uint32_t w = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = sh->pk[i];
+        bool keep = false;
+        for (uint32_t q = 0; q < nop; q++) {
+          if (op[1 + 2 * q] == k) {
+            const uint32_t v = op[2 + 2 * q];
+            keep = v != MTB_NONE && !T.val_falsy[v];
+          }
+        }
+        if (keep) {
+          const uint32_t kk = sh->pk[i], vv = sh->pv[i];
+          wsync();
+          if (lane == 0) {
+            sh->pk[w] = kk;
+            sh->pv[w] = vv;
+          }
+          wsync();
+          w++;
+        }
+      }
+      n = w;
+    }
+    for (uint32_t q = 0; q < nop; q++) {
+      const uint32_t k = op[1 + 2 * q];
+      const uint32_t v = op[2 + 2 * q];
+      int at = -1;
+      for (uint32_t i = 0; i < n; i++)
+        if (sh->pk[i] == k) at = (int)i;
+      if (v == MTB_NONE) {
+        if (at >= 0) {
+          for (uint32_t i = (uint32_t)at; i + 1 < n; i++) {
+            const uint32_t kk = sh->pk[i + 1], vv = sh->pv[i + 1];
+            wsync();
+            if (lane == 0) {
+              sh->pk[i] = kk;
+              sh->pv[i] = vv;
+            }
+            wsync();
+          }
+          n--;
+        }
+      } else if (at >= 0) {
+        if (lane == 0) sh->pv[at] = v;
+        wsync();
+      } else if (n < 64) {
+        const uint32_t rank = T.key_rank[k];
+        uint32_t ins = n;
+        if (rank != MTB_NONE) {
+          ins = 0;
+          while (ins < n) {
+            const uint32_t r2 = T.key_rank[sh->pk[ins]];
+            if (r2 == MTB_NONE || r2 > rank) break;
+            ins++;
+          }
+        }
+        for (uint32_t i = n; i > ins; i--) {
+          const uint32_t kk = sh->pk[i - 1], vv = sh->pv[i - 1];
+          wsync();
+          if (lane == 0) {
+            sh->pk[i] = kk;
+            sh->pv[i] = vv;
+          }
+          wsync();
+        }
+        if (lane == 0) {
+          sh->pk[ins] = k;
+          sh->pv[ins] = v;
+        }
+        wsync();
+        n++;
+      }
+    }
+    const uint32_t h = alloc_aux(1 + 2 * n);
+    if (err) return 0;
+    if (lane == 0) aux[h] = n;
+    for (uint32_t i = lane; i < n; i += 64) {
+      aux[h + 1 + 2 * i] = sh->pk[i];
+      aux[h + 2 + 2 * i] = sh->pv[i];
+    }
+    wsync();
+    memo_old = old;
+    memo_new = h;
+    return h;
+  }
+
+  // ------------------------------------------------------------------ nodeMap (remove / annotate)
+  // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958)
+  __device__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
+    if (end == start) return;
+    int pos = 0;
+    int d = 0;
+    bool exiting = false;
+    auto enter = [&](uint32_t b) {
+      uint32_t cid;
+      int clen, cseq;
+      const int count = child_info(b, R, C, false, cid, clen, cseq);
+      if (lane < count) {
+        sh->cid[d][lane] = cid;
+        sh->clen[d][lane] = clen;
+      }
+      if (lane == 0) {
+        sh->sb[d] = b;
+        sh->sidx[d] = 0;
+        sh->scnt[d] = count;
+        sh->acc[d] = 0;
+      }
+      wsync();
+    };
+    enter(root);
+    while (!err) {
+      const int idx = sh->sidx[d];
+      if (exiting || idx >= sh->scnt[d]) {
+        // post-order: flush this block's accumulated observer-length delta
+        const int a = sh->acc[d];
+        if (a != 0) {
+          const uint32_t b = sh->sb[d];
+          if (lane == 0) {
+            blk[b].len += a;
+            sh->path[0] = b;
+          }
+          wsync();
+          list_append_path(1, S, C, WK_MAIN, a);
+          if (d > 0 && lane == 0) sh->acc[d - 1] += a;
+          wsync();
+        }
+        if (d == 0) break;
+        d--;
+        continue;
+      }
+      if (lane == 0) sh->sidx[d] = idx + 1;
+      wsync();
+      if (end <= pos) {
+        exiting = true;
+        continue;
+      }
+      const int len = sh->clen[d][idx];
+      if (len == MTB_UNDEF || len == 0) continue;
+      const int nextPos = pos + len;
+      if (start >= nextPos) {
+        pos = nextPos;
+        continue;
+      }
+      const uint32_t c = sh->cid[d][idx];
+      if (!(c & MTB_LEAF)) {
+        if (d + 1 >= MTB_MAXDEPTH) { fail(DERR_DEPTH); return; }
+        d++;
+        enter(c);
+        continue;
+      }
+      const uint32_t sid = c & ~MTB_LEAF;
+      Seg s = seg[sid];
+      n_mod += 1;
+      if (remove) {
+        if (s.rseq >= 0) {
+          // overlapping remove: append C to removedClientIds (copy-on-write list)
+          const uint32_t oldn = s.rcx ? aux[s.rcx] : 0;
+          const uint32_t h = alloc_aux(oldn + 2);
+          if (err) return;
+          for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[s.rcx + 1 + i];
+          if (lane == 0) {
+            aux[h] = oldn + 1;
+            aux[h + 1 + oldn] = (uint32_t)C;
+            seg[sid].rcx = h;
+          }
+          wsync();
+          // OVERLAP window entry on every ancestor (no observer-length change)
+          if (lane <= d) sh->path[lane] = sh->sb[lane];
+          wsync();
+          list_append_path(d + 1, s.rseq, C, WK_OVERLAP, s.len);
+        } else {
+          const int before = local_len(s);
+          if (lane == 0) {
+            seg[sid].rseq = S;
+            seg[sid].rc0 = (int16_t)C;
+            seg[sid].rcx = 0;
+          }
+          wsync();
+          Seg s2 = s;
+          s2.rseq = S;
+          const int after = local_len(s2);
+          const int dl = (after == MTB_UNDEF ? 0 : after) - (before == MTB_UNDEF ? 0 : before);
+          if (lane == 0) sh->acc[d] += dl;
+          wsync();
+        }
+      } else {
+        const uint32_t np = props_apply(s.props, opId, rewrite);
+        if (err) return;
+        if (lane == 0) seg[sid].props = np;
+        wsync();
+      }
+      lru_add(sid, S);
+      pos = nextPos;
+    }
+  }
+
+  // ------------------------------------------------------------------ zamboni (zamboni.ts)
+  __device__ bool can_append(const Seg& a, const Seg& b) const {  // TextSegment.canAppend
+    if ((a.text & MTB_MARKER) || (b.text & MTB_MARKER)) return false;
+    if (a.len > 0 && txt[a.text + a.len - 1] == (uint16_t)'\n') return false;
+    return a.len <= 256 || b.len <= 256;
+  }
+  __device__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
+    for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
+  }
+  // TextSegment.append (textSegment.ts:84-88): prev.text += s.text
+  __device__ void append_text(uint32_t prev, const Seg& s) {
+    Seg p = seg[prev];
+    if (p.text + (uint32_t)p.len == s.text) {
+      // contiguous in the arena: extend in place
+    } else if (p.text + (uint32_t)p.len == text_used) {
+      if (text_used + (uint32_t)s.len > ds->text_cap) { fail(DERR_CAP_TEXT); return; }
+      copy_text(text_used, s.text, (uint32_t)s.len);
+      text_used += (uint32_t)s.len;
+    } else {
+      const uint32_t need = (uint32_t)p.len + (uint32_t)s.len;
+      if (text_used + need > ds->text_cap) { fail(DERR_CAP_TEXT); return; }
+      copy_text(text_used, p.text, (uint32_t)p.len);
+      copy_text(text_used + (uint32_t)p.len, s.text, (uint32_t)s.len);
+      if (lane == 0) seg[prev].text = text_used;
+      text_used += need;
+    }
+    if (lane == 0) seg[prev].len = p.len + s.len;
+    wsync();
+  }
+  // scourNode (zamboni.ts:122-193): appends kept children of `node` to sh->hold[nh..]
+  __device__ int scour(uint32_t node, int nh) {
+    const Blk& B = blk[node];
+    const int count = B.count;
+    uint32_t prev = MTB_NONE;
+    for (int k = 0; k < count; k++) {
+      const uint32_t c = B.child[k];
+      if (c & MTB_LEAF) {
+        const uint32_t sid = c & ~MTB_LEAF;
+        const Seg s = seg[sid];
+        if (s.rseq >= 0) {
+          if (s.rseq > minSeq) {
+            if (lane == 0) sh->hold[nh] = c;
+            nh++;
+          } else {
+            if (lane == 0) seg[sid].parent = MTB_NONE;
+          }
+          prev = MTB_NONE;
+        } else if (s.seq <= minSeq) {
+          bool ok = false;
+          if (prev != MTB_NONE && s.len > 0) {
+            const Seg ps = seg[prev];
+            ok = can_append(ps, s) && props_match(ps.props, s.props);
+          }
+          if (ok) {
+            append_text(prev, s);
+            if (lane == 0) seg[sid].parent = MTB_NONE;
+          } else {
+            if (lane == 0) sh->hold[nh] = c;
+            nh++;
+            prev = s.len > 0 ? sid : MTB_NONE;
+          }
+        } else {
+          if (lane == 0) sh->hold[nh] = c;
+          nh++;
+          prev = MTB_NONE;
+        }
+      } else {
+        if (lane == 0) sh->hold[nh] = c;
+        nh++;
+        prev = MTB_NONE;
+      }
+      wsync();
+    }
+    return nh;
+  }
+  // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
+  __device__ void pack_parent(uint32_t parent) {
+    while (!err) {
+      Blk& P = blk[parent];
+      const int pc = P.count;
+      int nh = 0;
+      for (int i = 0; i < pc; i++) {
+        const uint32_t cb = P.child[i];
+        nh = scour(cb, nh);
+        free_blk(cb);
+      }
+      wsync();
+      int cc = 0;
+      if (nh > 0) {
+        cc = nh / (MTB_MAXCH / 2);
+        if (cc > MTB_MAXCH - 1) cc = MTB_MAXCH - 1;
+        if (cc < 1) cc = 1;
+        const int base = nh / cc;
+        int rem = nh % cc;
+        int taken = 0;
+        for (int q = 0; q < cc; q++) {
+          int n = base;
+          if (rem > 0) {
+            n++;
+            rem--;
+          }
+          const uint32_t nb = alloc_blk();
+          if (err) return;
+          Blk& N = blk[nb];
+          if (lane < n) {
+            const uint32_t c = sh->hold[taken + lane];
+            N.child[lane] = c;
+            set_parent(c, nb, lane);
+          }
+          if (lane == 0) {
+            N.count = (uint8_t)n;
+            N.parent = parent;
+            N.index = (uint8_t)q;
+            P.child[q] = nb;
+          }
+          wsync();
+          taken += n;
+          rebuild(nb);
+        }
+      }
+      if (lane < MTB_MAXCH && lane >= cc) P.child[lane] = MTB_NONE;
+      if (lane == 0) P.count = (uint8_t)cc;
+      wsync();
+      if (cc < MTB_MAXCH / 2 && P.parent != MTB_NONE) {
+        parent = P.parent;
+        continue;
+      }
+      break;
+    }
+  }
+  // zamboniSegments (zamboni.ts:19-60)
+  __device__ void zamboni() {
+    for (int i = 0; i < 2 && !err; i++) {
+      if (heap_cnt == 0) break;
+      const Lru top = heap[1];
+      if (top.maxSeq > minSeq) break;
+      heap_get();
+      const uint32_t b = seg[top.seg].parent;
+      if (b != MTB_NONE && blk[b].scour != 0) {
+        const int count = blk[b].count;
+        const int nh = scour(b, 0);
+        Blk& B = blk[b];
+        if (lane == 0) B.scour = 0;
+        wsync();
+        if (nh < count) {
+          if (lane < nh) {
+            const uint32_t c = sh->hold[lane];
+            B.child[lane] = c;
+            set_parent(c, b, lane);
+          }
+          if (lane < MTB_MAXCH && lane >= nh) B.child[lane] = MTB_NONE;
+          if (lane == 0) B.count = (uint8_t)nh;
+          wsync();
+          if (nh < MTB_MAXCH / 2 && B.parent != MTB_NONE) pack_parent(B.parent);
+        }
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ ops
+  __device__ void set_min_seq(int msn) {  // mergeTree.ts:1025-1044
+    if (!(msn <= curSeq) || !(minSeq <= msn)) { fail(DERR_ASSERT_MSN); return; }
+    if (msn > minSeq) {
+      minSeq = msn;
+      zamboni();
+    }
+  }
+  __device__ void apply(const mtb_op& o) {
+    memo_old = MTB_NONE;
+    memo_new = 0;
+    const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)o.client;
+    switch (o.type) {
+      case MTB_OP_INSERT: {
+        ops_applied++;
+        walk((int)o.pos1, R, C, -2, false, 0, 0);  // ensureIntervalBoundary
+        if (err) return;
+        const bool marker = (o.flags & MTB_F_MARKER) != 0;
+        const int len = marker ? 1 : (int)o.pos2;
+        if (len > 0) {
+          const uint32_t sid = alloc_seg();
+          if (err) return;
+          Seg s;
+          s.len = len;
+          s.seq = S;
+          s.rseq = -1;
+          s.props = o.props ? (MTB_GPROPS | T.pidx[2 * o.props + 1]) : 0;
+          s.text = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
+          s.parent = MTB_NONE;
+          s.rcx = 0;
+          s.client = (int16_t)C;
+          s.rc0 = -1;
+          if (lane == 0) seg[sid] = s;
+          wsync();
+          n_mod += 1;
+          text_bytes += marker ? 0 : 2ull * (uint64_t)len;
+          if (!walk((int)o.pos1, R, C, S, true, sid, len)) {
+            fail(DERR_INSERT);
+            return;
+          }
+          if (S > minSeq) lru_add(sid, S);  // saveIfLocal (mergeTree.ts:1617-1637)
+        }
+        zamboni();
+        break;
+      }
+      case MTB_OP_REMOVE:
+      case MTB_OP_ANNOTATE: {
+        ops_applied++;
+        walk((int)o.pos1, R, C, -2, false, 0, 0);
+        walk((int)o.pos2, R, C, -2, false, 0, 0);
+        if (err) return;
+        node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props,
+                 (o.flags & MTB_F_REWRITE) != 0);
+        zamboni();
+        break;
+      }
+      case MTB_OP_ACK:
+        zamboni();
+        break;
+      default:
+        break;
+    }
+    if (err) return;
+    if (o.flags & MTB_F_LAST) {  // updateSeqNumbers (client.ts:877-887)
+      if (!(curSeq <= S)) { fail(DERR_ASSERT_SEQ); return; }
+      curSeq = S;
+      if (!((int)o.msn <= S)) { fail(DERR_ASSERT_MSN); return; }
+      set_min_seq((int)o.msn);
+    }
+  }
+};
+
+}  // namespace mtbk
+
+using namespace mtbk;
+
+extern "C" __global__ void __launch_bounds__(64) mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs,
+                                                                   const mtb_op* ops, Seg* segs, Blk* blks, WEnt* lists,
+                                                                   uint16_t* text, Lru* heap, uint32_t* aux,
+                                                                   uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  const uint32_t doc = blockIdx.x;
+  if (doc >= ndocs) return;
+  DocState* ds = &docs[doc];
+  Eng e;
+  e.ds = ds;
+  e.seg = segs + ds->seg_base;
+  e.blk = blks + ds->blk_base;
+  e.lst = lists + ds->list_base;
+  e.txt = text + ds->text_base;
+  e.heap = heap + ds->heap_base;
+  e.aux = aux + ds->aux_base;
+  e.fre = freel + ds->free_base;
+  e.ops = ops + ds->op_base;
+  e.T = tables;
+  e.sh = &sh;
+  e.lane = lane_id();
+  e.minSeq = ds->min_seq;
+  e.curSeq = ds->cur_seq;
+  e.root = ds->root;
+  e.newMode = ds->new_mode != 0;
+  e.seg_used = ds->seg_used;
+  e.blk_used = ds->blk_used;
+  e.free_top = ds->free_top;
+  e.list_used = ds->list_used;
+  e.text_used = ds->text_used;
+  e.heap_cnt = ds->heap_cnt;
+  e.aux_used = ds->aux_used;
+  e.err = ds->err;
+  e.n_mod = ds->n_mod;
+  e.ops_applied = ds->ops_applied;
+  e.text_bytes = ds->text_bytes;
+  uint32_t k = ds->op_next;
+  const uint32_t n = ds->n_ops;
+  __syncthreads();
+  for (; k < n && !e.err; k++) {
+    const mtb_op o = e.ops[k];
+    e.apply(o);
+  }
+  __syncthreads();
+  if (e.lane == 0) {
+    ds->min_seq = e.minSeq;
+    ds->cur_seq = e.curSeq;
+    ds->root = e.root;
+    ds->seg_used = e.seg_used;
+    ds->blk_used = e.blk_used;
+    ds->free_top = e.free_top;
+    ds->list_used = e.list_used;
+    ds->text_used = e.text_used;
+    ds->heap_cnt = e.heap_cnt;
+    ds->aux_used = e.aux_used;
+    ds->n_mod = e.n_mod;
+    ds->ops_applied = e.ops_applied;
+    ds->text_bytes = e.text_bytes;
+    if (e.err && !ds->err) {
+      ds->err = e.err;
+      ds->err_op = k;
+    }
+    ds->op_next = e.err ? k : n;
+  }
+}
+
+hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
+                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segs, blks, lists, text, heap,
+                     aux, freel, tables);
+  return hipGetLastError();
+}

@@ -320,6 +320,7 @@ Seg* MergeTree::splitAt(Seg* s, int pos) {
   r->removedSeq = s->removedSeq;
   r->seq = s->seq;
   r->clientId = s->clientId;
+  counters.segsTouched += 2;  // split: left half modified + right half created
   return r;
 }
 
@@ -1099,10 +1100,19 @@ void Doc::applyMsg(const JVal& msg) {
 }
 
 void Doc::applyRecord(const Record& r, const uint16_t* text, const std::vector<std::string>& propsJson) {
-  auto propsOf = [&](uint32_t id) -> std::optional<JVal> {
-    if (id == 0) return std::nullopt;
-    if (id >= propsJson.size()) throw OracleError(-1, "bad props id");
-    return json_parse(propsJson[id]);
+  std::vector<std::optional<JVal>> parsed(propsJson.size());
+  if (r.props) {
+    if (r.props >= propsJson.size()) throw OracleError(-1, "bad props id");
+    parsed[r.props] = json_parse(propsJson[r.props]);
+  }
+  applyRecordParsed(r, text, parsed);
+}
+
+void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::vector<std::optional<JVal>>& props) {
+  auto propsOf = [&](uint32_t id) -> const JVal* {
+    if (id == 0) return nullptr;
+    if (id >= props.size() || !props[id]) throw OracleError(-1, "bad props id");
+    return &*props[id];
   };
   switch (r.type) {
     case 0: {
@@ -1116,10 +1126,10 @@ void Doc::applyRecord(const Record& r, const uint16_t* text, const std::vector<s
         s->text.assign(reinterpret_cast<const char16_t*>(text + r.payload), r.pos2);
         s->cachedLength = (int)r.pos2;
       }
-      auto p = propsOf(r.props);
-      if (p && !js_falsy(&*p)) {
+      const JVal* p = propsOf(r.props);
+      if (p && !js_falsy(p)) {
         s->hasPropManager = true;
-        s->props = propsFromSpec(&*p);
+        s->props = propsFromSpec(p);
       }
       mt.insertSegments((int)r.pos1, s, (int)r.refSeq, r.client, (int)r.seq);
       break;
@@ -1130,9 +1140,9 @@ void Doc::applyRecord(const Record& r, const uint16_t* text, const std::vector<s
       break;
     case 2: {
       mt.counters.ops++;
-      auto p = propsOf(r.props);
-      JObj o;
-      if (p && p->t == JVal::Obj) o = p->obj;
+      const JVal* p = propsOf(r.props);
+      static const JObj empty;
+      const JObj& o = (p && p->t == JVal::Obj) ? p->obj : empty;
       mt.annotateRange((int)r.pos1, (int)r.pos2, o, (r.flags & 0x04) != 0, (int)r.refSeq, r.client, (int)r.seq);
       break;
     }
@@ -1400,7 +1410,7 @@ std::string Doc::dumpSegments() {
         if (s->removed)
           for (int c2 : s->removedClientIds) rc.arr.push_back(JVal::number(c2));
         row.arr.push_back(rc);
-        if (s->props) {
+        if (s->props && !s->props->empty()) {  // {} and undefined are interchangeable (snapshotV1.ts:199)
           JVal pr;
           pr.t = JVal::Obj;
           pr.obj = *s->props;

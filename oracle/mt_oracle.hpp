@@ -223,6 +223,7 @@ class Doc {
     uint32_t seq, refSeq, msn, pos1, pos2, payload, props;
   };
   void applyRecord(const Record& r, const uint16_t* text, const std::vector<std::string>& propsJson);
+  void applyRecordParsed(const Record& r, const uint16_t* text, const std::vector<std::optional<JVal>>& props);
 
   // SnapshotV1 (snapshotV1.ts:46-312) -> (blob path, content) list + ISummaryTreeWithStats JSON
   std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);

@@ -1,0 +1,105 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY: ctypes binding of the synthetic op-log generator (oracle/loggen.cpp).
+
+The generator drives the oracle as the observer so that every generated op is valid in its author's
+(refSeq, client) perspective; the oracle's final state is the expected result.
+"""
+import ctypes
+import os
+
+from pyoracle import lib as _oracle_lib
+
+
+class LoggenCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("n_clients", ctypes.c_int32), ("n_ops", ctypes.c_int32),
+                ("lag", ctypes.c_int32), ("initial_len", ctypes.c_int32), ("pct_insert", ctypes.c_int32),
+                ("pct_remove", ctypes.c_int32), ("pct_group", ctypes.c_int32),
+                ("new_length_calc", ctypes.c_int32), ("min_length", ctypes.c_int32),
+                ("annotate_keys", ctypes.c_int32)]
+
+
+class LoggenDoc(ctypes.Structure):
+    _fields_ = [("ops", ctypes.c_void_p), ("n_ops", ctypes.c_uint32), ("n_msgs", ctypes.c_uint32),
+                ("text", ctypes.c_void_p), ("n_text", ctypes.c_uint32), ("initial_len", ctypes.c_uint32),
+                ("client_writer", ctypes.c_uint16 * 256), ("n_short", ctypes.c_uint32),
+                ("checksum", ctypes.c_uint64), ("ops_applied", ctypes.c_uint64),
+                ("segs_touched", ctypes.c_uint64), ("final_len", ctypes.c_uint32),
+                ("final_segments", ctypes.c_uint32), ("error", ctypes.c_int32)]
+
+
+def _lib():
+    L = _oracle_lib()
+    if not getattr(L, "_loggen_ready", False):
+        L.loggen_generate.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.POINTER(LoggenDoc)]
+        L.loggen_generate_batch.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_int, ctypes.POINTER(LoggenDoc)]
+        L.loggen_free.argtypes = [ctypes.POINTER(LoggenDoc)]
+        L.loggen_props_count.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.loggen_props_json.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.loggen_cpu_replay.restype = ctypes.c_double
+        L.loggen_cpu_replay.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.POINTER(LoggenDoc), ctypes.c_uint32,
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int32)]
+        L._loggen_ready = True
+    return L
+
+
+def make_cfg(seed=1, n_clients=8, n_ops=1000, lag=128, initial_len=64, pct_insert=50, pct_remove=30,
+             pct_group=5, new_length_calc=False, min_length=1, annotate_keys=1):
+    return LoggenCfg(seed, n_clients, n_ops, lag, initial_len, pct_insert, pct_remove, pct_group,
+                     int(new_length_calc), min_length, annotate_keys)
+
+
+class LogBatch:
+    """Generated logs for docs [begin, end) (owned C buffers, freed on close)."""
+
+    def __init__(self, cfg, begin, end, threads=None):
+        self.cfg = cfg
+        self.n = end - begin
+        self.docs = (LoggenDoc * self.n)()
+        L = _lib()
+        threads = threads or min(16, os.cpu_count() or 1)
+        rc = L.loggen_generate_batch(ctypes.byref(cfg), begin, end, threads, self.docs)
+        if rc != 0:
+            raise RuntimeError(f"loggen failed rc={rc}")
+
+    def props_json(self):
+        L = _lib()
+        n = L.loggen_props_count(self.cfg.n_clients, self.cfg.annotate_keys)
+        out = []
+        buf = ctypes.create_string_buffer(256)
+        for i in range(n):
+            k = L.loggen_props_json(self.cfg.n_clients, self.cfg.annotate_keys, i, buf, 256)
+            out.append(buf.value.decode() if k > 0 else None)
+        return out
+
+    def doc_ops_bytes(self, i):
+        d = self.docs[i]
+        return ctypes.string_at(d.ops, d.n_ops * 32)
+
+    def doc_text_bytes(self, i):
+        d = self.docs[i]
+        return ctypes.string_at(d.text, d.n_text * 2)
+
+    def client_ids(self, i):
+        d = self.docs[i]
+        return ["obs"] + [f"c{d.client_writer[s]}" for s in range(1, d.n_short)]
+
+    def cpu_replay(self, n=None, threads=1):
+        L = _lib()
+        ck = ctypes.c_uint64()
+        err = ctypes.c_int32()
+        n = self.n if n is None else n
+        secs = L.loggen_cpu_replay(ctypes.byref(self.cfg), self.docs, n, threads, ctypes.byref(ck), ctypes.byref(err))
+        return secs, ck.value, err.value
+
+    def close(self):
+        if self.docs is not None:
+            L = _lib()
+            for i in range(self.n):
+                L.loggen_free(ctypes.byref(self.docs[i]))
+            self.docs = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
