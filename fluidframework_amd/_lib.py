@@ -20,7 +20,7 @@ ERRORS = {0: "MTB_OK", -1: "MTB_E_ARG", -2: "MTB_E_NODEV", -3: "MTB_E_HIP", -4: 
 EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free", "mtb_doc_init",
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
-           "mtb_summarize_v1", "mtb_blob_list_free"]
+           "mtb_summarize_v1", "mtb_blob_list_free", "mtb_rewind", "mtb_replay_resident"]
 
 
 class MtbOptions(ctypes.Structure):
@@ -52,6 +52,13 @@ def lib():
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build the HIP engine with `python -m fluidframework_amd.build`")
+    # PyTorch-ROCm bundles its own libamdhip64.so.7.  Load it first so this process has exactly one HIP
+    # runtime (the engine's DT_NEEDED soname then resolves to the already-loaded copy); loading the
+    # system runtime first makes torch report "No HIP GPUs are available".
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
     L.mtb_batch_create.argtypes = [ctypes.POINTER(MtbOptions), u32, u32, ctypes.POINTER(vp)]
@@ -72,5 +79,7 @@ def lib():
     L.mtb_doc_checksum.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_uint64)]
     L.mtb_summarize_v1.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MtbBlobList)]
     L.mtb_blob_list_free.argtypes = [ctypes.POINTER(MtbBlobList)]
+    L.mtb_rewind.argtypes = [vp]
+    L.mtb_replay_resident.argtypes = [vp, ctypes.POINTER(MtbStats)]
     _LIB = L
     return L

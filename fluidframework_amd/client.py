@@ -109,6 +109,17 @@ class MergeTreeBatch:
 
     flush = replay
 
+    def rewind(self):
+        """Restore every document to its state before its first replay (records stay in HBM)."""
+        self._chk(self._L.mtb_rewind(self._h))
+
+    def replay_resident(self):
+        """Replay the HBM-resident records again (after rewind); returns the stats dict."""
+        st = _lib.MtbStats()
+        self._chk(self._L.mtb_replay_resident(self._h, ctypes.byref(st)))
+        self.last_stats = {f: getattr(st, f) for f, _ in _lib.MtbStats._fields_}
+        return self.last_stats
+
     def _ensure_flushed(self):
         if self._dirty:
             self.replay()

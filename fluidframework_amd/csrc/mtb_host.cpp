@@ -24,6 +24,8 @@
 #include "mtb_device.h"
 
 // defined in mtb_replay.hip
+hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, Seg* segs,
+                             const Seg* pseg, Blk* blks, const Blk* pblk);
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
                              WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables);
 
@@ -242,10 +244,16 @@ struct mtb_batch {
   DevBuf<uint8_t> dValFalsy;
   std::vector<DocState> hst;
   double lastKernelMs = 0;
+  // rewind support: state right after the first upload of every document's records
+  bool haveRewind = false;
+  std::vector<DocState> hPristine;
+  DevBuf<DocState> dPristine;
+  DevBuf<Seg> dPSeg;
+  DevBuf<Blk> dPBlk;
   ~mtb_batch() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
-    dKeyRank.release(); dValFalsy.release();
+    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
@@ -396,6 +404,7 @@ bool fits(const DocState& s, const Caps& c) {
 
 // (Re)lay out every document's slices so that each holds at least `want[i]`, copying live state.
 void layout(mtb_batch* b, const std::vector<Caps>& want) {
+  b->haveRewind = false;  // slice bases move: the pristine snapshot is no longer valid
   std::vector<DocState> ns = b->hst;
   uint64_t seg = 0, blk = 0, lst = 0, txt = 0, hp = 0, ax = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
@@ -548,6 +557,21 @@ int derr_code(int e) {
   return MTB_E_UNSUPPORTED;
 }
 
+// Snapshot the freshly initialised documents (before their first replay) for mtb_rewind.
+void capture_pristine(mtb_batch* b) {
+  b->hPristine = b->hst;
+  b->dPristine.ensure(b->ndocs);
+  b->dPSeg.ensure(b->ndocs);
+  b->dPBlk.ensure(b->ndocs);
+  HIPCHK(hipMemcpyAsync(b->dPristine.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    const DocState& s = b->hst[i];
+    HIPCHK(hipMemcpyAsync(b->dPBlk.p + i, b->dBlks.p + s.blk_base, sizeof(Blk), hipMemcpyDeviceToDevice, b->stream));
+    HIPCHK(hipMemcpyAsync(b->dPSeg.p + i, b->dSegs.p + s.seg_base, sizeof(Seg), hipMemcpyDeviceToDevice, b->stream));
+  }
+  b->haveRewind = true;
+}
+
 void replay(mtb_batch* b, mtb_stats* out) {
   if (!b->devInit) device_init(b);
   upload_tables(b);
@@ -594,6 +618,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
   b->dOps.ensure(ops.size() + 1);
   if (!ops.empty()) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.data(), ops.size() * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+  if (!b->haveRewind) capture_pristine(b);
   Tables t;
   t.pool = b->dPool.p;
   t.pidx = b->dPidx.p;
@@ -1070,6 +1095,50 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
 
 int mtb_replay(mtb_batch* b, mtb_stats* out) {
   return guarded(b, [&] { replay(b, out); });
+}
+
+int mtb_rewind(mtb_batch* b) {
+  return guarded(b, [&] {
+    if (!b->haveRewind) raise(MTB_E_ARG, "nothing to rewind: replay the batch first");
+    for (auto& d : b->docs)
+      if (!d.pending.empty()) raise(MTB_E_ARG, "rewind with pending (unreplayed) ops");
+    HIPCHK(mtb_launch_rewind(b->stream, b->ndocs, b->dDocs.p, b->dPristine.p, b->dSegs.p, b->dPSeg.p, b->dBlks.p, b->dPBlk.p));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    b->hst = b->hPristine;
+    for (auto& d : b->docs) d.cached = false;
+  });
+}
+
+// Replay the records already resident on the device (after mtb_rewind); no host->device traffic.
+int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
+  return guarded(b, [&] {
+    if (!b->haveRewind) raise(MTB_E_ARG, "no resident records");
+    Tables t;
+    t.pool = b->dPool.p;
+    t.pidx = b->dPidx.p;
+    t.val_class = b->dValClass.p;
+    t.val_falsy = b->dValFalsy.p;
+    t.key_rank = b->dKeyRank.p;
+    HIPCHK(hipEventRecord(b->ev0, b->stream));
+    HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t));
+    HIPCHK(hipEventRecord(b->ev1, b->stream));
+    HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    mtb_stats st{};
+    st.kernel_ms = ms;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      const DocState& s = b->hst[i];
+      b->docs[i].cached = false;
+      st.docs++;
+      st.ops_applied += s.ops_applied;
+      st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
+      if (s.err) st.errors++;
+    }
+    if (out) *out = st;
+  });
 }
 
 int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out) {

@@ -1203,3 +1203,25 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
                      aux, freel, tables);
   return hipGetLastError();
 }
+
+// Rewind every document to its post-init state (benchmark / re-replay utility): restores the
+// DocState header, the root block and the initial segment; ops and payload stay resident.
+extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, Seg* segs,
+                                             const Seg* pseg, Blk* blks, const Blk* pblk) {
+  // one 64-lane wave per document: lanes copy the 256-byte header, the root block and the initial segment
+  const uint32_t i = blockIdx.x;
+  const int l = threadIdx.x;
+  if (i >= ndocs) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(pristine + i);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(docs + i);
+  dst[l] = src[l];
+  const uint64_t bb = pristine[i].blk_base, sb = pristine[i].seg_base;
+  if (l < 16) reinterpret_cast<uint32_t*>(blks + bb)[l] = reinterpret_cast<const uint32_t*>(pblk + i)[l];
+  if (pristine[i].seg_used && l < 8) reinterpret_cast<uint32_t*>(segs + sb)[l] = reinterpret_cast<const uint32_t*>(pseg + i)[l];
+}
+
+hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, Seg* segs,
+                             const Seg* pseg, Blk* blks, const Blk* pblk) {
+  hipLaunchKernelGGL(mtb_rewind_kernel, dim3(ndocs), dim3(64), 0, stream, docs, pristine, ndocs, segs, pseg, blks, pblk);
+  return hipGetLastError();
+}

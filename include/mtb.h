@@ -139,6 +139,12 @@ int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,
                      mtb_blob_list* out);
 void mtb_blob_list_free(mtb_blob_list* l);
 
+/* ---- benchmark / re-replay utilities (no reference counterpart) ----
+ * mtb_rewind restores every document to its state before its first replay while keeping the op
+ * records resident in HBM; mtb_replay_resident then replays them again without host traffic. */
+int mtb_rewind(mtb_batch* b);
+int mtb_replay_resident(mtb_batch* b, mtb_stats* out);
+
 #ifdef __cplusplus
 }
 #endif

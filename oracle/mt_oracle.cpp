@@ -89,12 +89,13 @@ int PartialLengths::getPartialLength(int refSeq, int clientId) {
   int pLen = minLength;
   PSL* l = partialLengths.latestLeq(refSeq);
   pLen += l ? l->len : 0;
-  auto it = clientSeqNumbers.find(clientId);
-  if (it != clientSeqNumbers.end() && !it->second.items.empty()) {
-    PSL& cliLatest = it->second.items.back();
+  const size_t k = (size_t)(clientId + 2);
+  if (k < clientSeqNumbers.size() && !clientSeqNumbers[k].items.empty()) {
+    PSLSet& cs = clientSeqNumbers[k];
+    PSL& cliLatest = cs.items.back();
     if (cliLatest.seq > refSeq) {
       pLen += cliLatest.len;
-      PSL* preceding = it->second.latestLeq(refSeq);
+      PSL* preceding = cs.latestLeq(refSeq);
       if (preceding) pLen -= preceding->len;
     }
   }
@@ -103,14 +104,14 @@ int PartialLengths::getPartialLength(int refSeq, int clientId) {
 void PartialLengths::zamboni(const CollabWindow& w) {
   minLength += partialLengths.copyDown(w.minSeq);
   minSeq = w.minSeq;
-  for (auto& kv : clientSeqNumbers) kv.second.copyDown(w.minSeq);
+  for (auto& cs : clientSeqNumbers) cs.copyDown(w.minSeq);
 }
 void PartialLengths::addClientSeqNumber(int clientId, int seq, int seglen) {
   PSL p;
   p.seq = seq;
   p.len = 0;
   p.seglen = seglen;
-  clientSeqNumbers[clientId].addOrUpdate(p);
+  cli(clientId).addOrUpdate(p);
 }
 void PartialLengths::addClientSeqNumberFromPartial(const PSL& p) {
   addClientSeqNumber(p.clientId, p.seq, p.seglen);
@@ -657,7 +658,7 @@ void MergeTree::plUpdate(PartialLengths& pl, Block* node, int seq, int clientId)
   }
   pl.segmentCount = segCount;
   addSeq(pl.partialLengths, seq, seqSeglen, clientId);
-  addSeq(pl.clientSeqNumbers[clientId], seq, seqSeglen, 0);
+  addSeq(pl.cli(clientId), seq, seqSeglen, 0);
   pl.zamboni(window);
 }
 
@@ -792,15 +793,23 @@ static bool canAppend(const Seg* a, const Seg* b) {  // TextSegment.canAppend (t
   if (!a->text.empty() && a->text.back() == u'\n') return false;
   return a->cachedLength <= TextSegmentGranularity || b->cachedLength <= TextSegmentGranularity;
 }
-static const JVal* propsAsVal(const Seg* s, JVal& holder) {
-  if (!s->props) return nullptr;
-  holder.t = JVal::Obj;
-  holder.obj = *s->props;
-  return &holder;
-}
+// matchProperties(a.properties, b.properties) (properties.ts:71-96) on two property maps
 static bool matchSegProps(const Seg* a, const Seg* b) {
-  JVal ha, hb;
-  return match_properties(propsAsVal(a, ha), propsAsVal(b, hb));
+  const JObj* pa = a->props ? &*a->props : nullptr;
+  const JObj* pb = b->props ? &*b->props : nullptr;
+  const size_t na = pa ? pa->size() : 0, nb = pb ? pb->size() : 0;
+  if (na != nb) return false;
+  for (size_t i = 0; i < na; i++) {
+    const JVal* bv = obj_get(*pb, (*pa)[i].first);
+    if (!bv || bv->t == JVal::Undef) return false;
+    const JVal* av = &(*pa)[i].second;
+    if (bv->t == JVal::Obj || bv->t == JVal::Arr || bv->t == JVal::Null) {
+      if (!match_properties(av, bv)) return false;
+    } else if (!js_strict_equal(bv, av)) {
+      return false;
+    }
+  }
+  return true;
 }
 
 void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {  // zamboni.ts:122-193

@@ -84,7 +84,13 @@ struct PartialLengths {
   int minLength = 0;
   int segmentCount = 0;
   PSLSet partialLengths;
-  std::map<int, PSLSet> clientSeqNumbers;
+  // clientSeqNumbers[clientId] (partialLengths.ts:585), indexed by clientId + 2 (ids >= NonCollabClient)
+  std::vector<PSLSet> clientSeqNumbers;
+  PSLSet& cli(int clientId) {
+    size_t k = (size_t)(clientId + 2);
+    if (k >= clientSeqNumbers.size()) clientSeqNumbers.resize(k + 1);
+    return clientSeqNumbers[k];
+  }
   int getPartialLength(int refSeq, int clientId);
   void zamboni(const CollabWindow& w);
   void addClientSeqNumber(int clientId, int seq, int seglen);
