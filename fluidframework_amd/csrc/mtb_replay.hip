@@ -24,9 +24,14 @@
 
 namespace mtbk {
 
+#define MTB_LDS_HEAP 256
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-// single-wave workgroup: makes this wave's global stores visible to all of its lanes
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// Cross-lane hand-off inside the single wave that owns a document.  A wavefront's vector-memory and
+// LDS instructions are performed in program order for the whole wave, so a wavefront-scope fence
+// (no instruction; it only stops the compiler from moving memory operations across it) is enough
+// to make one lane's store visible to another lane's later load of the same document state.
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 __device__ __forceinline__ int wsum(int v) {
 #pragma unroll
@@ -55,6 +60,8 @@ struct Scratch {  // LDS, one per wave
   uint32_t hold[64];
   uint32_t pk[64];
   uint32_t pv[64];
+  int32_t pp[MTB_MAXDEPTH];   // remaining position at each level of the last walk
+  Lru heap[MTB_LDS_HEAP];     // LRU heap while it fits (index 0 unused)
 };
 
 struct Eng {
@@ -79,16 +86,19 @@ struct Eng {
   uint64_t n_mod, ops_applied, text_bytes;
   // per-op memo for annotate
   uint32_t memo_old, memo_new;
+  bool heap_lds;       // LRU heap lives in LDS (spills to the global slice when it outgrows it)
+  int walk_depth;      // depth of the leaf-level block reached by the last walk (-1: none)
+  bool struct_changed; // a block split / root growth happened since the last walk started
 
   // ------------------------------------------------------------------ errors / allocation
-  __device__ void fail(int code) {
+  __device__ __forceinline__ void fail(int code) {
     if (!err) err = code;
   }
-  __device__ uint32_t alloc_seg() {
+  __device__ __forceinline__ uint32_t alloc_seg() {
     if (seg_used >= ds->seg_cap) { fail(DERR_CAP_SEG); return 0; }
     return seg_used++;
   }
-  __device__ uint32_t alloc_blk() {
+  __device__ __forceinline__ uint32_t alloc_blk() {
     uint32_t b;
     if (free_top > 0) {
       free_top--;
@@ -112,11 +122,11 @@ struct Eng {
     wsync();
     return b;
   }
-  __device__ void free_blk(uint32_t b) {
-    if (lane == 0) fre[free_top] = b;
+  __device__ __forceinline__ void free_blk(uint32_t b) {
+    fre[free_top] = b;
     free_top++;
   }
-  __device__ uint32_t alloc_aux(uint32_t n) {
+  __device__ __forceinline__ uint32_t alloc_aux(uint32_t n) {
     if (aux_used + n > ds->aux_cap) { fail(DERR_CAP_AUX); return 1; }
     uint32_t o = aux_used;
     aux_used += n;
@@ -124,7 +134,7 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ visibility
-  __device__ bool rc_has(const Seg& s, int C) const {
+  __device__ __forceinline__ bool rc_has(const Seg& s, int C) const {
     if (s.rc0 == C) return true;
     if (s.rcx) {
       uint32_t n = aux[s.rcx];
@@ -134,7 +144,7 @@ struct Eng {
     return false;
   }
   // localNetLength (mergeTree.ts:613-634)
-  __device__ int local_len(const Seg& s) const {
+  __device__ __forceinline__ int local_len(const Seg& s) const {
     if (s.rseq >= 0) {
       if (!newMode) return s.rseq > minSeq ? 0 : MTB_UNDEF;
       return 0;
@@ -142,7 +152,7 @@ struct Eng {
     return s.len;
   }
   // nodeLength for a leaf in a remote perspective (mergeTree.ts:935-1001)
-  __device__ int seg_vis(const Seg& s, int R, int C) const {
+  __device__ __forceinline__ int seg_vis(const Seg& s, int R, int C) const {
     const bool removed = s.rseq >= 0;
     if (newMode) {
       if (removed) {
@@ -162,7 +172,7 @@ struct Eng {
 
   // Lengths of the children of block b in the (R, C) perspective (observer: cachedLength view).
   // Lane j < count receives child id (cid), length (UNDEF allowed) and, for leaves, the seg seq.
-  __device__ int child_info(uint32_t b, int R, int C, bool observer, uint32_t& cid, int& clen, int& cseq) {
+  __device__ __forceinline__ int child_info(uint32_t b, int R, int C, bool observer, uint32_t& cid, int& clen, int& cseq) {
     const Blk& B = blk[b];
     const int count = B.count;
     cid = MTB_NONE;
@@ -233,7 +243,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ window lists
   // Allocate a list slice of `cap` entries.
-  __device__ uint32_t list_alloc(uint32_t cap) {
+  __device__ __forceinline__ uint32_t list_alloc(uint32_t cap) {
     if (list_used + cap > ds->list_cap) { fail(DERR_CAP_LIST); return 0; }
     uint32_t o = list_used;
     list_used += cap;
@@ -241,7 +251,7 @@ struct Eng {
   }
   // Append (seq, client, kind, delta) to the lists of `n` blocks in sh->path[0..n) (lane-parallel
   // fast path, sequential re-allocation for full lists).
-  __device__ void list_append_path(int n, int seqv, int client, int kind, int delta) {
+  __device__ __forceinline__ void list_append_path(int n, int seqv, int client, int kind, int delta) {
     const int ck = (client & 0xFFFF) | (kind << 16);
     bool need = false;
     if (lane < n) {
@@ -291,7 +301,7 @@ struct Eng {
     }
   }
   // Re-allocate block b's list with room for `extra` more entries, dropping entries <= minSeq.
-  __device__ void list_grow(uint32_t b, uint32_t extra) {
+  __device__ __forceinline__ void list_grow(uint32_t b, uint32_t extra) {
     Blk& B = blk[b];
     const uint32_t cnt = B.lcnt, off = B.loff;
     // live entries
@@ -328,7 +338,7 @@ struct Eng {
   }
   // Rebuild block b's window list from its children (after split / pack / root growth) and its
   // cachedLength (blockUpdate, mergeTree.ts:2392).
-  __device__ void rebuild(uint32_t b) {
+  __device__ __forceinline__ void rebuild(uint32_t b) {
     Blk& B = blk[b];
     const int count = B.count;
     // pass 1: count entries and observer length
@@ -448,7 +458,7 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ tree primitives
-  __device__ void set_parent(uint32_t node, uint32_t b, int idx) {
+  __device__ __forceinline__ void set_parent(uint32_t node, uint32_t b, int idx) {
     if (node & MTB_LEAF) {
       seg[node & ~MTB_LEAF].parent = b;
     } else {
@@ -457,7 +467,7 @@ struct Eng {
     }
   }
   // Insert `node` at child index k of block b (insertingWalk shift, mergeTree.ts:1831-1837).
-  __device__ void insert_child(uint32_t b, int k, uint32_t node) {
+  __device__ __forceinline__ void insert_child(uint32_t b, int k, uint32_t node) {
     Blk& B = blk[b];
     const int count = B.count;
     uint32_t c = MTB_NONE;
@@ -475,7 +485,8 @@ struct Eng {
     wsync();
   }
   // split (mergeTree.ts:1858-1871): children 4..7 move to a new block.
-  __device__ uint32_t split_block(uint32_t b) {
+  __device__ __forceinline__ uint32_t split_block(uint32_t b) {
+    struct_changed = true;
     const uint32_t nb = alloc_blk();
     if (err) return 0;
     Blk& B = blk[b];
@@ -498,7 +509,7 @@ struct Eng {
     return nb;
   }
   // updateRoot (mergeTree.ts:1268-1277)
-  __device__ void grow_root(uint32_t left, uint32_t right) {
+  __device__ __forceinline__ void grow_root(uint32_t left, uint32_t right) {
     const uint32_t r = alloc_blk();
     if (err) return;
     Blk& R = blk[r];
@@ -516,7 +527,7 @@ struct Eng {
     root = r;
   }
   // After inserting into block sh->path[d] (the leaf-level block), split every full block on the path.
-  __device__ void fix_overflow(int d) {
+  __device__ __forceinline__ void fix_overflow(int d) {
     int level = d;
     uint32_t cur = sh->path[level];
     while (!err && blk[cur].count >= MTB_MAXCH) {
@@ -534,7 +545,7 @@ struct Eng {
   }
 
   // BaseSegment.splitAt (mergeTreeNodes.ts:481-510) + TextSegment.createSplitSegmentAt
-  __device__ uint32_t split_seg(uint32_t sid, int at) {
+  __device__ __forceinline__ uint32_t split_seg(uint32_t sid, int at) {
     const uint32_t r = alloc_seg();
     if (err) return 0;
     Seg s = seg[sid];
@@ -553,13 +564,25 @@ struct Eng {
   // ------------------------------------------------------------------ insertingWalk
   // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
   // mode 1: blockInsert of candidate `cand` (seq S).  Returns false if the candidate was not placed.
-  __device__ bool walk(int pos, int R, int C, int S, bool insertMode, uint32_t cand, int candLen) {
+  // `resume`: start at the leaf-level block reached by the previous walk (same (R, C) and position,
+  // no block split since): internal-level decisions of both walks are identical (blocks tie-break
+  // the same way in both modes and a segment split changes no block length).
+  __device__ __forceinline__ bool walk(int pos, int R, int C, int S, bool insertMode, uint32_t cand, int candLen,
+                                       bool resume = false) {
     uint32_t b = root;
     int p = pos;
     int d = 0;
+    if (resume && walk_depth >= 0 && !struct_changed) {
+      d = walk_depth;
+      b = sh->path[d];
+      p = sh->pp[d];
+    }
+    walk_depth = -1;
+    struct_changed = false;
     while (true) {
       if (d >= MTB_MAXDEPTH) { fail(DERR_DEPTH); return false; }
       sh->path[d] = b;
+      sh->pp[d] = p;
       uint32_t cid;
       int clen, cseq;
       const int count = child_info(b, R, C, false, cid, clen, cseq);
@@ -580,6 +603,7 @@ struct Eng {
           d++;
           continue;
         }
+        walk_depth = d;
         if (insertMode) {
           insert_child(b, j, cand | MTB_LEAF);
         } else {
@@ -594,6 +618,7 @@ struct Eng {
         }
       } else {
         const int total = __shfl(incl, 63, 64);
+        if (p - total == 0) walk_depth = d;
         if (p - total != 0 || !insertMode) return !insertMode;
         insert_child(b, count, cand | MTB_LEAF);
       }
@@ -607,62 +632,69 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
-  __device__ void heap_add(uint32_t s, int maxSeq) {
+  __device__ __forceinline__ Lru hget(uint32_t k) const { return heap_lds ? sh->heap[k] : heap[k]; }
+  __device__ __forceinline__ void hset(uint32_t k, Lru v) {
+    if (heap_lds) sh->heap[k] = v;
+    else heap[k] = v;
+  }
+  __device__ __forceinline__ void heap_spill() {  // LDS -> global slice
+    for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) heap[i] = sh->heap[i];
+    heap_lds = false;
+    wsync();
+  }
+  __device__ __forceinline__ void heap_add(uint32_t s, int maxSeq) {
     if (heap_cnt + 1 >= ds->heap_cap) { fail(DERR_CAP_HEAP); return; }
+    if (heap_lds && heap_cnt + 1 >= MTB_LDS_HEAP) heap_spill();
     uint32_t k = ++heap_cnt;
     Lru x;
     x.seg = s;
     x.maxSeq = maxSeq;
     while (k > 1) {
-      const Lru par = heap[k >> 1];
+      const Lru par = hget(k >> 1);
       if (!(par.maxSeq - x.maxSeq > 0)) break;
-      if (lane == 0) heap[k] = par;
+      hset(k, par);
       k >>= 1;
     }
-    if (lane == 0) heap[k] = x;
-    wsync();
+    hset(k, x);
   }
-  __device__ Lru heap_get() {
-    const Lru top = heap[1];
-    const Lru last = heap[heap_cnt];
+  __device__ __forceinline__ Lru heap_get() {
+    const Lru top = hget(1);
+    const Lru last = hget(heap_cnt);
     heap_cnt--;
     const uint32_t count = heap_cnt;
     uint32_t k = 1;
     // fixDown with the last element placed at the root
     while ((k << 1) <= count) {
       uint32_t j = k << 1;
-      Lru a = heap[j];
+      Lru a = hget(j);
       if (j < count) {
-        const Lru bb = heap[j + 1];
+        const Lru bb = hget(j + 1);
         if (a.maxSeq - bb.maxSeq > 0) {
           j++;
           a = bb;
         }
       }
       if (last.maxSeq - a.maxSeq <= 0) break;
-      if (lane == 0) heap[k] = a;
+      hset(k, a);
       k = j;
     }
-    if (count >= 1 && lane == 0) heap[k] = last;
-    wsync();
+    if (count >= 1) hset(k, last);
     return top;
   }
-  // addToLRUSet (mergeTree.ts:741-751)
-  __device__ void lru_add(uint32_t sid, int seqv) {
-    const uint32_t b = seg[sid].parent;
-    if (blk[b].scour != 1 && seqv > curSeq) {
-      if (lane == 0) blk[b].scour = 1;
-      wsync();
+  // addToLRUSet (mergeTree.ts:741-751); `b` is the segment's current parent block
+  __device__ __forceinline__ void lru_add(uint32_t sid, uint32_t b, int seqv) {
+    if (seqv > curSeq && blk[b].scour != 1) {
+      blk[b].scour = 1;
       heap_add(sid, seqv);
     }
   }
 
   // ------------------------------------------------------------------ properties
-  __device__ const uint32_t* props_ptr(uint32_t h) const {
+  __device__ __forceinline__ const uint32_t* props_ptr(uint32_t h) const {
     return (h & MTB_GPROPS) ? (T.pool + (h & ~MTB_GPROPS)) : (aux + h);
   }
   // matchProperties (properties.ts:71-96) on interned property sets
-  __device__ bool props_match(uint32_t a, uint32_t b) const {
+  __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
     if (a == b) return true;
     const uint32_t* pa = a ? props_ptr(a) : nullptr;
     const uint32_t* pb = b ? props_ptr(b) : nullptr;
@@ -683,7 +715,7 @@ struct Eng {
     return true;
   }
   // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157)
-  __device__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
+  __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
     if (old == memo_old && memo_new) return memo_new;
     const uint32_t* op = T.pool + T.pidx[2 * opId];
     const uint32_t nop = op[0];
@@ -788,7 +820,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ nodeMap (remove / annotate)
   // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958)
-  __device__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
+  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
     if (end == start) return;
     int pos = 0;
     int d = 0;
@@ -891,22 +923,22 @@ struct Eng {
         if (lane == 0) seg[sid].props = np;
         wsync();
       }
-      lru_add(sid, S);
+      lru_add(sid, sh->sb[d], S);
       pos = nextPos;
     }
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
-  __device__ bool can_append(const Seg& a, const Seg& b) const {  // TextSegment.canAppend
+  __device__ __forceinline__ bool can_append(const Seg& a, const Seg& b) const {  // TextSegment.canAppend
     if ((a.text & MTB_MARKER) || (b.text & MTB_MARKER)) return false;
     if (a.len > 0 && txt[a.text + a.len - 1] == (uint16_t)'\n') return false;
     return a.len <= 256 || b.len <= 256;
   }
-  __device__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
+  __device__ __forceinline__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
     for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
   }
   // TextSegment.append (textSegment.ts:84-88): prev.text += s.text
-  __device__ void append_text(uint32_t prev, const Seg& s) {
+  __device__ __forceinline__ void append_text(uint32_t prev, const Seg& s) {
     Seg p = seg[prev];
     if (p.text + (uint32_t)p.len == s.text) {
       // contiguous in the arena: extend in place
@@ -926,7 +958,7 @@ struct Eng {
     wsync();
   }
   // scourNode (zamboni.ts:122-193): appends kept children of `node` to sh->hold[nh..]
-  __device__ int scour(uint32_t node, int nh) {
+  __device__ __forceinline__ int scour(uint32_t node, int nh) {
     const Blk& B = blk[node];
     const int count = B.count;
     uint32_t prev = MTB_NONE;
@@ -972,7 +1004,7 @@ struct Eng {
     return nh;
   }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
-  __device__ void pack_parent(uint32_t parent) {
+  __device__ __forceinline__ void pack_parent(uint32_t parent) {
     while (!err) {
       Blk& P = blk[parent];
       const int pc = P.count;
@@ -1027,10 +1059,10 @@ struct Eng {
     }
   }
   // zamboniSegments (zamboni.ts:19-60)
-  __device__ void zamboni() {
+  __device__ __forceinline__ void zamboni() {
     for (int i = 0; i < 2 && !err; i++) {
       if (heap_cnt == 0) break;
-      const Lru top = heap[1];
+      const Lru top = hget(1);
       if (top.maxSeq > minSeq) break;
       heap_get();
       const uint32_t b = seg[top.seg].parent;
@@ -1056,14 +1088,14 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ ops
-  __device__ void set_min_seq(int msn) {  // mergeTree.ts:1025-1044
+  __device__ __forceinline__ void set_min_seq(int msn) {  // mergeTree.ts:1025-1044
     if (!(msn <= curSeq) || !(minSeq <= msn)) { fail(DERR_ASSERT_MSN); return; }
     if (msn > minSeq) {
       minSeq = msn;
       zamboni();
     }
   }
-  __device__ void apply(const mtb_op& o) {
+  __device__ __forceinline__ void apply(const mtb_op& o) {
     memo_old = MTB_NONE;
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)o.client;
@@ -1091,11 +1123,11 @@ struct Eng {
           wsync();
           n_mod += 1;
           text_bytes += marker ? 0 : 2ull * (uint64_t)len;
-          if (!walk((int)o.pos1, R, C, S, true, sid, len)) {
+          if (!walk((int)o.pos1, R, C, S, true, sid, len, true)) {
             fail(DERR_INSERT);
             return;
           }
-          if (S > minSeq) lru_add(sid, S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (S > minSeq) lru_add(sid, seg[sid].parent, S);  // saveIfLocal (mergeTree.ts:1617-1637)
         }
         zamboni();
         break;
@@ -1169,11 +1201,23 @@ extern "C" __global__ void __launch_bounds__(64) mtb_replay_kernel(DocState* __r
   e.text_bytes = ds->text_bytes;
   uint32_t k = ds->op_next;
   const uint32_t n = ds->n_ops;
+  e.walk_depth = -1;
+  e.struct_changed = false;
+  // bring the LRU heap into LDS when it fits
+  e.heap_lds = e.heap_cnt + 1 < MTB_LDS_HEAP;
+  if (e.heap_lds)
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) sh.heap[i] = e.heap[i];
   __syncthreads();
-  for (; k < n && !e.err; k++) {
-    const mtb_op o = e.ops[k];
-    e.apply(o);
+  if (k < n) {
+    mtb_op cur = e.ops[k];
+    for (; k < n && !e.err; k++) {
+      const mtb_op nxt = e.ops[k + 1 < n ? k + 1 : k];  // prefetch the next record
+      e.apply(cur);
+      cur = nxt;
+    }
   }
+  if (e.heap_lds)
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) e.heap[i] = sh.heap[i];
   __syncthreads();
   if (e.lane == 0) {
     ds->min_seq = e.minSeq;

@@ -165,6 +165,7 @@ Block* MergeTree::makeBlock(int childCount) {
 // Heap (MT/collections/heap.ts:11-66) with compare = a.maxSeq - b.maxSeq
 void MergeTree::heapAdd(LRU x) {
   heap.push_back(x);
+  if (heap.size() - 1 > counters.maxHeap) counters.maxHeap = heap.size() - 1;
   size_t k = heap.size() - 1;
   while (k > 1 && heap[k >> 1].maxSeq - heap[k].maxSeq > 0) {
     std::swap(heap[k >> 1], heap[k]);

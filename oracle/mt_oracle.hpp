@@ -123,7 +123,7 @@ struct OracleError : std::runtime_error {
 };
 
 struct Counters {
-  uint64_t ops = 0, segsTouched = 0;
+  uint64_t ops = 0, segsTouched = 0, maxHeap = 0, maxDepth = 0;
 };
 
 class MergeTree {
