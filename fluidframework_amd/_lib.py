@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmtb.so")
+LIB_PATH = os.environ.get("MTB_LIB") or os.path.join(HERE, "libmtb.so")  # MTB_LIB: alternate build (tuning)
 
 MTB_OP_INSERT, MTB_OP_REMOVE, MTB_OP_ANNOTATE, MTB_OP_NOOP, MTB_OP_ACK = 0, 1, 2, 3, 4
 MTB_F_LAST, MTB_F_MARKER, MTB_F_REWRITE, MTB_F_SEGOBJ = 0x01, 0x02, 0x04, 0x08

@@ -18,14 +18,17 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force=False, arch="gfx950"):
-    if not force and not needs_build():
+def build(force=False, arch="gfx950", out=OUT, defines=()):
+    if not force and out == OUT and not needs_build():
         return OUT
     cmd = ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", OUT] + SRCS
+           "-Wno-unused-result"] + [f"-D{d}" for d in defines] + ["-o", out] + SRCS
     subprocess.check_call(cmd)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
+    if "--variants" in sys.argv:  # occupancy variants for tuning runs (MTB_LIB=...)
+        for w in (2, 3, 4):
+            print(build(force=True, out=os.path.join(HERE, f"libmtb_w{w}.so"), defines=[f"MTB_WAVES_PER_SIMD={w}"]))
     print(build(force="--force" in sys.argv))

@@ -44,7 +44,8 @@ struct Blk {          // 64 bytes
   uint8_t index;      // index in parent
   int8_t scour;       // needsScour: -1 undefined, 0 false, 1 true
   uint8_t pad0;
-  uint32_t pad1[2];
+  int32_t lseq;       // key (seq, ck) of the list's last entry, so appends can merge without a
+  int32_t lck;        //   dependent load of the entry (lseq = INT32_MIN: unknown, never merge)
 };
 
 // Window-list entry.  For a query (R, C):  length(block) = len - sum(w(e) for e.seq > R), where

@@ -4,7 +4,7 @@
 // exactly as the reference observer `Client.applyMsg` would (packages/dds/merge-tree/src/client.ts:858).
 // Control flow is wave-uniform (every lane walks the same tree path); the lanes parallelise the
 // per-op inner loops: the <=8 children of a block, the concatenated window lists of those children,
-// list/segment rebuilds and text copies.  There is no MFMA: nothing here is a dense contraction.
+// scour decisions, list/segment rebuilds and text copies.  No MFMA: nothing here is a contraction.
 //
 // Differences from the reference data structures (results are identical):
 //  * PartialSequenceLengths (partialLengths.ts:239) is replaced by one flat window list per block.
@@ -13,9 +13,11 @@
 //    where w(e) = e.delta for MAIN entries of other clients and for OVERLAP entries of C.  This is the
 //    same quantity getPartialLength (partialLengths.ts:698) returns and the sum of the leaf
 //    visibilities (mergeTree.ts:916-1004) - the oracle verifies that identity on every query.
-//  * The recursive insertingWalk (mergeTree.ts:1740) runs iteratively with an explicit path.
+//  * The recursive insertingWalk (mergeTree.ts:1740) runs iteratively with an explicit path; all walks
+//    of one op share an LDS cache of the children lengths (they use the same (R, C)).
 //  * Length/list bookkeeping is propagated incrementally along the recorded path instead of the
 //    reference's combine/update rebuilds; split/pack blocks rebuild their list from their children.
+//  * The zamboni LRU heap (collections/heap.ts) lives in LDS while it fits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,6 +27,7 @@
 namespace mtbk {
 
 #define MTB_LDS_HEAP 256
+#define MTB_NOKEY ((int32_t)0x80000000)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Cross-lane hand-off inside the single wave that owns a document.  A wavefront's vector-memory and
@@ -50,18 +53,24 @@ __device__ __forceinline__ int wscan_incl(int v) {
 __device__ __forceinline__ int first_set(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
 struct Scratch {  // LDS, one per wave
-  uint32_t path[MTB_MAXDEPTH];
-  uint32_t sb[MTB_MAXDEPTH];
-  int32_t sidx[MTB_MAXDEPTH];
-  int32_t scnt[MTB_MAXDEPTH];
-  int32_t acc[MTB_MAXDEPTH];
+  // per-op child-info cache, one slot per tree depth (all walks of one op share (R, C))
+  uint32_t cb[MTB_MAXDEPTH];                 // block cached in the slot (MTB_NONE: empty)
+  int32_t ccount[MTB_MAXDEPTH];
+  int32_t cscour[MTB_MAXDEPTH];
   uint32_t cid[MTB_MAXDEPTH][MTB_MAXCH];
   int32_t clen[MTB_MAXDEPTH][MTB_MAXCH];
+  int32_t cseq[MTB_MAXDEPTH][MTB_MAXCH];
+  int32_t corr[MTB_MAXCH];                   // list-scan accumulators
+  // walk / nodeMap stacks
+  uint32_t path[MTB_MAXDEPTH];
+  int32_t pp[MTB_MAXDEPTH];                  // remaining position at each level of the last walk
+  int32_t sidx[MTB_MAXDEPTH];
+  int32_t acc[MTB_MAXDEPTH];
+  // scour / pack / props scratch
   uint32_t hold[64];
   uint32_t pk[64];
   uint32_t pv[64];
-  int32_t pp[MTB_MAXDEPTH];   // remaining position at each level of the last walk
-  Lru heap[MTB_LDS_HEAP];     // LRU heap while it fits (index 0 unused)
+  Lru heap[MTB_LDS_HEAP];                    // LRU heap while it fits (index 0 unused)
 };
 
 struct Eng {
@@ -84,11 +93,10 @@ struct Eng {
   uint32_t seg_used, blk_used, free_top, list_used, text_used, heap_cnt, aux_used;
   int err;
   uint64_t n_mod, ops_applied, text_bytes;
-  // per-op memo for annotate
-  uint32_t memo_old, memo_new;
-  bool heap_lds;       // LRU heap lives in LDS (spills to the global slice when it outgrows it)
-  int walk_depth;      // depth of the leaf-level block reached by the last walk (-1: none)
-  bool struct_changed; // a block split / root growth happened since the last walk started
+  uint32_t memo_old, memo_new;  // per-op annotate memo (old props -> new props)
+  bool heap_lds;                // LRU heap lives in LDS (spills to the global slice when it outgrows it)
+  int walk_depth;               // depth of the leaf-level block reached by the last walk (-1: none)
+  bool struct_changed;          // a block split / root growth happened since the last walk started
 
   // ------------------------------------------------------------------ errors / allocation
   __device__ __forceinline__ void fail(int code) {
@@ -109,16 +117,16 @@ struct Eng {
     }
     Blk& B = blk[b];
     if (lane < MTB_MAXCH) B.child[lane] = MTB_NONE;
-    if (lane == 0) {
-      B.parent = MTB_NONE;
-      B.len = 0;
-      B.loff = 0;
-      B.lcnt = 0;
-      B.lcap = 0;
-      B.count = 0;
-      B.index = 0;
-      B.scour = -1;
-    }
+    B.parent = MTB_NONE;
+    B.len = 0;
+    B.loff = 0;
+    B.lcnt = 0;
+    B.lcap = 0;
+    B.count = 0;
+    B.index = 0;
+    B.scour = -1;
+    B.lseq = MTB_NOKEY;
+    B.lck = 0;
     wsync();
     return b;
   }
@@ -131,6 +139,10 @@ struct Eng {
     uint32_t o = aux_used;
     aux_used += n;
     return o;
+  }
+  __device__ __forceinline__ void cache_clear() {
+    if (lane < MTB_MAXDEPTH) sh->cb[lane] = MTB_NONE;
+    wsync();
   }
 
   // ------------------------------------------------------------------ visibility
@@ -170,11 +182,20 @@ struct Eng {
     return 0;
   }
 
-  // Lengths of the children of block b in the (R, C) perspective (observer: cachedLength view).
-  // Lane j < count receives child id (cid), length (UNDEF allowed) and, for leaves, the seg seq.
-  __device__ __forceinline__ int child_info(uint32_t b, int R, int C, bool observer, uint32_t& cid, int& clen, int& cseq) {
+  // Children of block b (tree depth d) in the (R, C) perspective: lane j < count receives the child id,
+  // its length (UNDEF allowed) and, for leaves, the segment's seq.  Results are cached in LDS slot d for
+  // the rest of the op.
+  __device__ __forceinline__ int child_info(uint32_t b, int d, int R, int C, uint32_t& cid, int& clen, int& cseq) {
+    if (sh->cb[d] == b) {
+      const int count = sh->ccount[d];
+      cid = lane < count ? sh->cid[d][lane] : MTB_NONE;
+      clen = lane < count ? sh->clen[d][lane] : 0;
+      cseq = lane < count ? sh->cseq[d][lane] : 0;
+      return count;
+    }
     const Blk& B = blk[b];
     const int count = B.count;
+    const int scour = B.scour;
     cid = MTB_NONE;
     clen = 0;
     cseq = 0;
@@ -183,101 +204,92 @@ struct Eng {
       cid = B.child[lane];
       if (cid & MTB_LEAF) {
         const Seg s = seg[cid & ~MTB_LEAF];
-        clen = observer ? local_len(s) : seg_vis(s, R, C);
+        clen = seg_vis(s, R, C);
         cseq = s.seq;
       } else {
         const Blk& cb = blk[cid];
         clen = cb.len;
-        if (!observer) {
-          loff = cb.loff;
-          lcnt = cb.lcnt;
-        }
+        loff = cb.loff;
+        lcnt = cb.lcnt;
       }
     }
-    if (!observer) {
-      // concatenated scan of the children's window lists
-      const int incl = wscan_incl((int)lcnt);
+    // concatenated scan of the children's window lists, accumulated per child in LDS
+    const int incl = wscan_incl((int)lcnt);
+    const int total = __shfl(incl, 63, 64);
+    if (total > 0) {
       const int excl = incl - (int)lcnt;
-      const int total = __shfl(incl, 63, 64);
-      if (total > 0) {
-        int pre[MTB_MAXCH], off[MTB_MAXCH];
+      if (lane < MTB_MAXCH) sh->corr[lane] = 0;
+      int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++) {
-          pre[k] = __shfl(excl, k, 64);
-          off[k] = __shfl((int)loff, k, 64);
-        }
-        int acc[MTB_MAXCH];
-#pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++) acc[k] = 0;
-        for (int t = lane; t < total; t += 64) {
-          int j = 0;
-#pragma unroll
-          for (int k = 1; k < MTB_MAXCH; k++)
-            if (k < count && pre[k] <= t) j = k;
-          int base = 0;
-#pragma unroll
-          for (int k = 0; k < MTB_MAXCH; k++)
-            if (k == j) base = off[k] + (t - pre[k]);
-          const WEnt e = lst[base];
-          int w = 0;
-          if (e.seq > R) {
-            const int c = e.ck & 0xFFFF;
-            const int kind = e.ck >> 16;
-            if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) w = e.delta;
-          }
-#pragma unroll
-          for (int k = 0; k < MTB_MAXCH; k++)
-            if (k == j) acc[k] += w;
-        }
-        int mine = 0;
-#pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++) {
-          const int s = wsum(acc[k]);
-          if (k == lane) mine = s;
-        }
-        if (lane < count && !(cid & MTB_LEAF)) clen -= mine;
+      for (int k = 0; k < MTB_MAXCH; k++) {
+        pre[k] = __shfl(excl, k, 64);
+        off[k] = __shfl((int)loff, k, 64);
       }
+      wsync();
+      for (int t = lane; t < total; t += 64) {
+        int j = 0;
+#pragma unroll
+        for (int k = 1; k < MTB_MAXCH; k++)
+          if (k < count && pre[k] <= t) j = k;
+        int base = 0;
+#pragma unroll
+        for (int k = 0; k < MTB_MAXCH; k++)
+          if (k == j) base = off[k] + (t - pre[k]);
+        const WEnt e = lst[base];
+        if (e.seq > R) {
+          const int c = e.ck & 0xFFFF;
+          const int kind = e.ck >> 16;
+          if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[j], e.delta);
+        }
+      }
+      wsync();
+      if (lane < count && !(cid & MTB_LEAF)) clen -= sh->corr[lane];
     }
+    if (lane < count) {
+      sh->cid[d][lane] = cid;
+      sh->clen[d][lane] = clen;
+      sh->cseq[d][lane] = cseq;
+    }
+    sh->ccount[d] = count;
+    sh->cscour[d] = scour;
+    sh->cb[d] = b;
+    wsync();
     return count;
   }
 
   // ------------------------------------------------------------------ window lists
-  // Allocate a list slice of `cap` entries.
   __device__ __forceinline__ uint32_t list_alloc(uint32_t cap) {
     if (list_used + cap > ds->list_cap) { fail(DERR_CAP_LIST); return 0; }
     uint32_t o = list_used;
     list_used += cap;
     return o;
   }
-  // Append (seq, client, kind, delta) to the lists of `n` blocks in sh->path[0..n) (lane-parallel
-  // fast path, sequential re-allocation for full lists).
-  __device__ __forceinline__ void list_append_path(int n, int seqv, int client, int kind, int delta) {
+  // Add `dlen` to the cachedLength of the `n` blocks sh->path[0..n) and append (seq, client, kind,
+  // delta) to their window lists.  One lane per block; blocks whose list is full are re-allocated
+  // afterwards, one at a time.
+  __device__ __forceinline__ void path_update(int n, int dlen, int seqv, int client, int kind, int delta) {
     const int ck = (client & 0xFFFF) | (kind << 16);
     bool need = false;
     if (lane < n) {
       const uint32_t b = sh->path[lane];
       Blk& B = blk[b];
-      const uint32_t cnt = B.lcnt;
-      bool merged = false;
-      if (cnt > 0) {
-        WEnt& last = lst[B.loff + cnt - 1];
-        if (last.seq == seqv && last.ck == ck) {
-          last.delta += delta;
-          merged = true;
-        }
-      }
-      if (!merged) {
-        if (cnt < B.lcap) {
-          WEnt e;
-          e.seq = seqv;
-          e.ck = ck;
-          e.delta = delta;
-          e.pad = 0;
-          lst[B.loff + cnt] = e;
-          B.lcnt = cnt + 1;
-        } else {
-          need = true;
-        }
+      const uint32_t cnt = B.lcnt, cap = B.lcap, off = B.loff;
+      const int ls = B.lseq, lk = B.lck;
+      if (dlen) B.len = B.len + dlen;
+      if (cnt > 0 && ls == seqv && lk == ck) {
+        lst[off + cnt - 1].delta += delta;  // same (seq, client, kind) as the last entry (GROUP members)
+      } else if (cnt < cap) {
+        WEnt e;
+        e.seq = seqv;
+        e.ck = ck;
+        e.delta = delta;
+        e.pad = 0;
+        lst[off + cnt] = e;
+        B.lcnt = cnt + 1;
+        B.lseq = seqv;
+        B.lck = ck;
+      } else {
+        need = true;
       }
     }
     unsigned long long m = __ballot(need);
@@ -287,16 +299,18 @@ struct Eng {
       m &= m - 1;
       const uint32_t b = sh->path[i];
       list_grow(b, 1);
+      if (err) return;
       Blk& B = blk[b];
-      if (lane == 0) {
-        WEnt e;
-        e.seq = seqv;
-        e.ck = ck;
-        e.delta = delta;
-        e.pad = 0;
-        lst[B.loff + B.lcnt] = e;
-        B.lcnt = B.lcnt + 1;
-      }
+      WEnt e;
+      e.seq = seqv;
+      e.ck = ck;
+      e.delta = delta;
+      e.pad = 0;
+      const uint32_t cnt = B.lcnt;
+      lst[B.loff + cnt] = e;
+      B.lcnt = cnt + 1;
+      B.lseq = seqv;
+      B.lck = ck;
       wsync();
     }
   }
@@ -304,7 +318,6 @@ struct Eng {
   __device__ __forceinline__ void list_grow(uint32_t b, uint32_t extra) {
     Blk& B = blk[b];
     const uint32_t cnt = B.lcnt, off = B.loff;
-    // live entries
     uint32_t live = 0;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
@@ -329,11 +342,10 @@ struct Eng {
       if (keep) lst[no + w + rank] = e;
       w += __popcll(m);
     }
-    if (lane == 0) {
-      B.loff = no;
-      B.lcnt = w;
-      B.lcap = cap;
-    }
+    B.loff = no;
+    B.lcnt = w;
+    B.lcap = cap;
+    B.lseq = MTB_NOKEY;
     wsync();
   }
   // Rebuild block b's window list from its children (after split / pack / root growth) and its
@@ -341,7 +353,6 @@ struct Eng {
   __device__ __forceinline__ void rebuild(uint32_t b) {
     Blk& B = blk[b];
     const int count = B.count;
-    // pass 1: count entries and observer length
     int nent = 0, olen = 0;
     uint32_t cid = MTB_NONE;
     Seg s;
@@ -365,18 +376,16 @@ struct Eng {
       }
     }
     const int totalLen = wsum(olen);
-    // block children: count live entries of each child list
     const int cincl = wscan_incl((int)ccnt);
     const int cexcl = cincl - (int)ccnt;
     const int ctotal = __shfl(cincl, 63, 64);
-    int live_from_children = 0;
-    // uniform helpers for the children lists
     int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
     for (int k = 0; k < MTB_MAXCH; k++) {
       pre[k] = __shfl(cexcl, k, 64);
       off[k] = __shfl((int)coff, k, 64);
     }
+    int live_from_children = 0;
     for (int base = 0; base < ctotal; base += 64) {
       const int t = base + lane;
       bool keep = false;
@@ -399,9 +408,8 @@ struct Eng {
     cap = cap < 8 ? 8 : cap + cap / 2 + 4;
     const uint32_t no = list_alloc(cap);
     if (err) return;
-    // pass 2: write
     const int sincl = wscan_incl(nent);
-    int w = sincl - nent;  // exclusive
+    int w = sincl - nent;
     if (lane < count && (cid & MTB_LEAF)) {
       WEnt e;
       e.pad = 0;
@@ -448,12 +456,11 @@ struct Eng {
       if (keep) lst[no + wpos + rank] = e;
       wpos += __popcll(m);
     }
-    if (lane == 0) {
-      B.loff = no;
-      B.lcnt = (uint32_t)total;
-      B.lcap = cap;
-      B.len = totalLen;
-    }
+    B.loff = no;
+    B.lcnt = (uint32_t)total;
+    B.lcap = cap;
+    B.len = totalLen;
+    B.lseq = MTB_NOKEY;
     wsync();
   }
 
@@ -466,22 +473,28 @@ struct Eng {
       blk[node].index = (uint8_t)idx;
     }
   }
-  // Insert `node` at child index k of block b (insertingWalk shift, mergeTree.ts:1831-1837).
-  __device__ __forceinline__ void insert_child(uint32_t b, int k, uint32_t node) {
+  // Insert `node` at child index k of block b (insertingWalk shift, mergeTree.ts:1831-1837).  `d` is the
+  // depth of b in the current walk (its cache slot holds the children), or -1.
+  __device__ __forceinline__ void insert_child(uint32_t b, int k, uint32_t node, int d) {
     Blk& B = blk[b];
-    const int count = B.count;
+    int count;
     uint32_t c = MTB_NONE;
-    if (lane < count) c = B.child[lane];
+    if (d >= 0 && sh->cb[d] == b) {
+      count = sh->ccount[d];
+      if (lane < count) c = sh->cid[d][lane];
+      sh->cb[d] = MTB_NONE;  // children change
+    } else {
+      count = B.count;
+      if (lane < count) c = B.child[lane];
+    }
     wsync();
     if (lane < count && lane >= k) {
       B.child[lane + 1] = c;
-      set_parent(c, b, lane + 1);
+      if (!(c & MTB_LEAF)) blk[c].index = (uint8_t)(lane + 1);
     }
-    if (lane == 0) {
-      B.child[k] = node;
-      set_parent(node, b, k);
-      B.count = (uint8_t)(count + 1);
-    }
+    B.child[k] = node;
+    set_parent(node, b, k);
+    B.count = (uint8_t)(count + 1);
     wsync();
   }
   // split (mergeTree.ts:1858-1871): children 4..7 move to a new block.
@@ -498,11 +511,9 @@ struct Eng {
       set_parent(c, nb, lane);
       B.child[half + lane] = MTB_NONE;
     }
-    if (lane == 0) {
-      B.count = (uint8_t)half;
-      N.count = (uint8_t)half;
-      N.parent = B.parent;
-    }
+    B.count = (uint8_t)half;
+    N.count = (uint8_t)half;
+    N.parent = B.parent;
     wsync();
     rebuild(b);
     rebuild(nb);
@@ -513,15 +524,13 @@ struct Eng {
     const uint32_t r = alloc_blk();
     if (err) return;
     Blk& R = blk[r];
-    if (lane == 0) {
-      R.child[0] = left;
-      R.child[1] = right;
-      R.count = 2;
-      blk[left].parent = r;
-      blk[left].index = 0;
-      blk[right].parent = r;
-      blk[right].index = 1;
-    }
+    R.child[0] = left;
+    R.child[1] = right;
+    R.count = 2;
+    blk[left].parent = r;
+    blk[left].index = 0;
+    blk[right].parent = r;
+    blk[right].index = 1;
     wsync();
     rebuild(r);
     root = r;
@@ -535,27 +544,25 @@ struct Eng {
       if (err) return;
       if (level == 0) {
         grow_root(cur, nb);
-        return;
+        break;
       }
       const uint32_t p = sh->path[level - 1];
-      insert_child(p, blk[cur].index + 1, nb);
+      insert_child(p, blk[cur].index + 1, nb, -1);
       cur = p;
       level--;
     }
+    if (struct_changed) cache_clear();
   }
 
   // BaseSegment.splitAt (mergeTreeNodes.ts:481-510) + TextSegment.createSplitSegmentAt
   __device__ __forceinline__ uint32_t split_seg(uint32_t sid, int at) {
     const uint32_t r = alloc_seg();
     if (err) return 0;
-    Seg s = seg[sid];
-    Seg t = s;
-    t.len = s.len - at;
-    t.text = s.text + (uint32_t)at;
-    if (lane == 0) {
-      seg[r] = t;
-      seg[sid].len = at;
-    }
+    Seg t = seg[sid];
+    t.len -= at;
+    t.text += (uint32_t)at;
+    seg[r] = t;
+    seg[sid].len = at;
     n_mod += 2;
     wsync();
     return r;
@@ -564,9 +571,9 @@ struct Eng {
   // ------------------------------------------------------------------ insertingWalk
   // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
   // mode 1: blockInsert of candidate `cand` (seq S).  Returns false if the candidate was not placed.
-  // `resume`: start at the leaf-level block reached by the previous walk (same (R, C) and position,
-  // no block split since): internal-level decisions of both walks are identical (blocks tie-break
-  // the same way in both modes and a segment split changes no block length).
+  // `resume`: start at the leaf-level block reached by the previous walk (same (R, C) and position, no
+  // block split since): internal-level decisions of both walks are identical (blocks tie-break the same
+  // way in both modes and a segment split changes no block length).
   __device__ __forceinline__ bool walk(int pos, int R, int C, int S, bool insertMode, uint32_t cand, int candLen,
                                        bool resume = false) {
     uint32_t b = root;
@@ -585,7 +592,7 @@ struct Eng {
       sh->pp[d] = p;
       uint32_t cid;
       int clen, cseq;
-      const int count = child_info(b, R, C, false, cid, clen, cseq);
+      const int count = child_info(b, d, R, C, cid, clen, cseq);
       const int def = (lane < count && clen > 0) ? clen : 0;
       const int incl = wscan_incl(def);
       const int pj = p - (incl - def);
@@ -605,14 +612,14 @@ struct Eng {
         }
         walk_depth = d;
         if (insertMode) {
-          insert_child(b, j, cand | MTB_LEAF);
+          insert_child(b, j, cand | MTB_LEAF, d);
         } else {
           if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
           const uint32_t sid = cj & ~MTB_LEAF;
           if (seg[sid].text & MTB_MARKER) return true;  // markers never split
           const uint32_t r = split_seg(sid, pjj);
           if (err) return false;
-          insert_child(b, j + 1, r | MTB_LEAF);
+          insert_child(b, j + 1, r | MTB_LEAF, d);
           fix_overflow(d);
           return true;
         }
@@ -620,12 +627,11 @@ struct Eng {
         const int total = __shfl(incl, 63, 64);
         if (p - total == 0) walk_depth = d;
         if (p - total != 0 || !insertMode) return !insertMode;
-        insert_child(b, count, cand | MTB_LEAF);
+        insert_child(b, count, cand | MTB_LEAF, d);
       }
       // candidate inserted into block b at depth d: propagate its length and window entry
-      if (lane <= d) blk[sh->path[lane]].len += candLen;
-      wsync();
-      list_append_path(d + 1, S, C, WK_MAIN, candLen);
+      cache_clear();
+      path_update(d + 1, candLen, S, C, WK_MAIN, candLen);
       fix_overflow(d);
       return true;
     }
@@ -681,12 +687,14 @@ struct Eng {
     if (count >= 1) hset(k, last);
     return top;
   }
-  // addToLRUSet (mergeTree.ts:741-751); `b` is the segment's current parent block
-  __device__ __forceinline__ void lru_add(uint32_t sid, uint32_t b, int seqv) {
-    if (seqv > curSeq && blk[b].scour != 1) {
+  // addToLRUSet (mergeTree.ts:741-751); `b` is the segment's parent block, `scour` its needsScour
+  __device__ __forceinline__ bool lru_add(uint32_t sid, uint32_t b, int scour, int seqv) {
+    if (seqv > curSeq && scour != 1) {
       blk[b].scour = 1;
       heap_add(sid, seqv);
+      return true;
     }
+    return false;
   }
 
   // ------------------------------------------------------------------ properties
@@ -714,7 +722,8 @@ struct Eng {
     }
     return true;
   }
-  // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157)
+  // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157).
+  // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
   __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
     if (old == memo_old && memo_new) return memo_new;
     const uint32_t* op = T.pool + T.pidx[2 * opId];
@@ -734,7 +743,7 @@ struct Eng {
       // delete old keys whose new value is falsy/absent (the `!newProps[key]` test)
       uint32_t w = 0;
       for (uint32_t i = 0; i < n; i++) {
-        const uint32_t k = sh->pk[i];
+        const uint32_t k = sh->pk[i], v0 = sh->pv[i];
         bool keep = false;
         for (uint32_t q = 0; q < nop; q++) {
           if (op[1 + 2 * q] == k) {
@@ -743,12 +752,9 @@ struct Eng {
           }
         }
         if (keep) {
-          const uint32_t kk = sh->pk[i], vv = sh->pv[i];
           wsync();
-          if (lane == 0) {
-            sh->pk[w] = kk;
-            sh->pv[w] = vv;
-          }
+          sh->pk[w] = k;
+          sh->pv[w] = v0;
           wsync();
           w++;
         }
@@ -766,16 +772,14 @@ struct Eng {
           for (uint32_t i = (uint32_t)at; i + 1 < n; i++) {
             const uint32_t kk = sh->pk[i + 1], vv = sh->pv[i + 1];
             wsync();
-            if (lane == 0) {
-              sh->pk[i] = kk;
-              sh->pv[i] = vv;
-            }
+            sh->pk[i] = kk;
+            sh->pv[i] = vv;
             wsync();
           }
           n--;
         }
       } else if (at >= 0) {
-        if (lane == 0) sh->pv[at] = v;
+        sh->pv[at] = v;
         wsync();
       } else if (n < 64) {
         const uint32_t rank = T.key_rank[k];
@@ -791,23 +795,19 @@ struct Eng {
         for (uint32_t i = n; i > ins; i--) {
           const uint32_t kk = sh->pk[i - 1], vv = sh->pv[i - 1];
           wsync();
-          if (lane == 0) {
-            sh->pk[i] = kk;
-            sh->pv[i] = vv;
-          }
+          sh->pk[i] = kk;
+          sh->pv[i] = vv;
           wsync();
         }
-        if (lane == 0) {
-          sh->pk[ins] = k;
-          sh->pv[ins] = v;
-        }
+        sh->pk[ins] = k;
+        sh->pv[ins] = v;
         wsync();
         n++;
       }
     }
     const uint32_t h = alloc_aux(1 + 2 * n);
     if (err) return 0;
-    if (lane == 0) aux[h] = n;
+    aux[h] = n;
     for (uint32_t i = lane; i < n; i += 64) {
       aux[h + 1 + 2 * i] = sh->pk[i];
       aux[h + 2 + 2 * i] = sh->pv[i];
@@ -819,8 +819,11 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ nodeMap (remove / annotate)
-  // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958)
-  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
+  // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958).
+  // Emulates depthFirstNodeWalk (mergeTreeNodeWalk.ts:35) with an explicit stack; block post-actions
+  // (blockUpdateLength) become one flush of the accumulated observer-length delta per block.
+  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId,
+                                           bool rewrite) {
     if (end == start) return;
     int pos = 0;
     int d = 0;
@@ -828,41 +831,33 @@ struct Eng {
     auto enter = [&](uint32_t b) {
       uint32_t cid;
       int clen, cseq;
-      const int count = child_info(b, R, C, false, cid, clen, cseq);
-      if (lane < count) {
-        sh->cid[d][lane] = cid;
-        sh->clen[d][lane] = clen;
-      }
-      if (lane == 0) {
-        sh->sb[d] = b;
-        sh->sidx[d] = 0;
-        sh->scnt[d] = count;
-        sh->acc[d] = 0;
-      }
+      child_info(b, d, R, C, cid, clen, cseq);
+      sh->path[d] = b;
+      sh->sidx[d] = 0;
+      sh->acc[d] = 0;
       wsync();
     };
     enter(root);
     while (!err) {
       const int idx = sh->sidx[d];
-      if (exiting || idx >= sh->scnt[d]) {
+      if (exiting || idx >= sh->ccount[d]) {
         // post-order: flush this block's accumulated observer-length delta
         const int a = sh->acc[d];
         if (a != 0) {
-          const uint32_t b = sh->sb[d];
-          if (lane == 0) {
-            blk[b].len += a;
-            sh->path[0] = b;
-          }
+          const uint32_t b = sh->path[d];
+          const uint32_t keep = sh->path[0];
+          sh->path[0] = b;
           wsync();
-          list_append_path(1, S, C, WK_MAIN, a);
-          if (d > 0 && lane == 0) sh->acc[d - 1] += a;
+          path_update(1, a, S, C, WK_MAIN, a);
+          sh->path[0] = keep;
+          if (d > 0) sh->acc[d - 1] += a;
           wsync();
         }
         if (d == 0) break;
         d--;
         continue;
       }
-      if (lane == 0) sh->sidx[d] = idx + 1;
+      sh->sidx[d] = idx + 1;
       wsync();
       if (end <= pos) {
         exiting = true;
@@ -883,125 +878,176 @@ struct Eng {
         continue;
       }
       const uint32_t sid = c & ~MTB_LEAF;
-      Seg s = seg[sid];
+      const Seg s = seg[sid];
       n_mod += 1;
       if (remove) {
         if (s.rseq >= 0) {
-          // overlapping remove: append C to removedClientIds (copy-on-write list)
+          // overlapping remove: append C to removedClientIds (copy-on-write list) and add an OVERLAP
+          // window entry on every ancestor (no observer-length change)
           const uint32_t oldn = s.rcx ? aux[s.rcx] : 0;
           const uint32_t h = alloc_aux(oldn + 2);
           if (err) return;
           for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[s.rcx + 1 + i];
-          if (lane == 0) {
-            aux[h] = oldn + 1;
-            aux[h + 1 + oldn] = (uint32_t)C;
-            seg[sid].rcx = h;
-          }
+          aux[h] = oldn + 1;
+          aux[h + 1 + oldn] = (uint32_t)C;
+          seg[sid].rcx = h;
           wsync();
-          // OVERLAP window entry on every ancestor (no observer-length change)
-          if (lane <= d) sh->path[lane] = sh->sb[lane];
-          wsync();
-          list_append_path(d + 1, s.rseq, C, WK_OVERLAP, s.len);
+          path_update(d + 1, 0, s.rseq, C, WK_OVERLAP, s.len);
         } else {
           const int before = local_len(s);
-          if (lane == 0) {
-            seg[sid].rseq = S;
-            seg[sid].rc0 = (int16_t)C;
-            seg[sid].rcx = 0;
-          }
-          wsync();
+          seg[sid].rseq = S;
+          seg[sid].rc0 = (int16_t)C;
+          seg[sid].rcx = 0;
           Seg s2 = s;
           s2.rseq = S;
           const int after = local_len(s2);
           const int dl = (after == MTB_UNDEF ? 0 : after) - (before == MTB_UNDEF ? 0 : before);
-          if (lane == 0) sh->acc[d] += dl;
+          sh->acc[d] += dl;
           wsync();
         }
       } else {
         const uint32_t np = props_apply(s.props, opId, rewrite);
         if (err) return;
-        if (lane == 0) seg[sid].props = np;
-        wsync();
+        seg[sid].props = np;
       }
-      lru_add(sid, sh->sb[d], S);
+      if (lru_add(sid, sh->path[d], sh->cscour[d], S)) sh->cscour[d] = 1;
+      wsync();
       pos = nextPos;
     }
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
-  __device__ __forceinline__ bool can_append(const Seg& a, const Seg& b) const {  // TextSegment.canAppend
-    if ((a.text & MTB_MARKER) || (b.text & MTB_MARKER)) return false;
-    if (a.len > 0 && txt[a.text + a.len - 1] == (uint16_t)'\n') return false;
-    return a.len <= 256 || b.len <= 256;
-  }
   __device__ __forceinline__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
     for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
   }
-  // TextSegment.append (textSegment.ts:84-88): prev.text += s.text
-  __device__ __forceinline__ void append_text(uint32_t prev, const Seg& s) {
-    Seg p = seg[prev];
-    if (p.text + (uint32_t)p.len == s.text) {
-      // contiguous in the arena: extend in place
-    } else if (p.text + (uint32_t)p.len == text_used) {
-      if (text_used + (uint32_t)s.len > ds->text_cap) { fail(DERR_CAP_TEXT); return; }
-      copy_text(text_used, s.text, (uint32_t)s.len);
-      text_used += (uint32_t)s.len;
-    } else {
-      const uint32_t need = (uint32_t)p.len + (uint32_t)s.len;
-      if (text_used + need > ds->text_cap) { fail(DERR_CAP_TEXT); return; }
-      copy_text(text_used, p.text, (uint32_t)p.len);
-      copy_text(text_used + (uint32_t)p.len, s.text, (uint32_t)s.len);
-      if (lane == 0) seg[prev].text = text_used;
-      text_used += need;
-    }
-    if (lane == 0) seg[prev].len = p.len + s.len;
-    wsync();
-  }
-  // scourNode (zamboni.ts:122-193): appends kept children of `node` to sh->hold[nh..]
+  // scourNode (zamboni.ts:122-193) for block `node`: kept children are appended to sh->hold[nh..].
+  // Every child record (and the last UTF-16 unit of every text) is fetched at once, lane-parallel;
+  // the sequential keep/drop/append decisions then run on registers (shuffles), and the text of each
+  // run of appended segments is written with one parallel copy (TextSegment.append, textSegment.ts:84).
   __device__ __forceinline__ int scour(uint32_t node, int nh) {
     const Blk& B = blk[node];
     const int count = B.count;
-    uint32_t prev = MTB_NONE;
-    for (int k = 0; k < count; k++) {
-      const uint32_t c = B.child[k];
+    uint32_t c = MTB_NONE;
+    Seg s;
+    s.len = 0;
+    s.seq = 0;
+    s.rseq = -1;
+    s.props = 0;
+    s.text = 0;
+    uint16_t last = 0;
+    int kind = 0;  // 0 hold+reset, 1 drop (tombstone below MSN), 2 acked text/marker (may append)
+    if (lane < count) {
+      c = B.child[lane];
       if (c & MTB_LEAF) {
-        const uint32_t sid = c & ~MTB_LEAF;
-        const Seg s = seg[sid];
-        if (s.rseq >= 0) {
-          if (s.rseq > minSeq) {
-            if (lane == 0) sh->hold[nh] = c;
-            nh++;
-          } else {
-            if (lane == 0) seg[sid].parent = MTB_NONE;
-          }
-          prev = MTB_NONE;
-        } else if (s.seq <= minSeq) {
-          bool ok = false;
-          if (prev != MTB_NONE && s.len > 0) {
-            const Seg ps = seg[prev];
-            ok = can_append(ps, s) && props_match(ps.props, s.props);
-          }
-          if (ok) {
-            append_text(prev, s);
-            if (lane == 0) seg[sid].parent = MTB_NONE;
-          } else {
-            if (lane == 0) sh->hold[nh] = c;
-            nh++;
-            prev = s.len > 0 ? sid : MTB_NONE;
-          }
+        s = seg[c & ~MTB_LEAF];
+        if (s.rseq >= 0) kind = s.rseq > minSeq ? 0 : 1;
+        else if (s.seq <= minSeq) kind = 2;
+        if (kind == 2 && !(s.text & MTB_MARKER) && s.len > 0) last = txt[s.text + s.len - 1];
+      }
+    }
+    // sequential decisions (uniform), values pulled from lane k by shuffles
+    int prev = -1;            // lane index of the current append target
+    int prevLen = 0;          // its (growing) length
+    uint16_t prevLast = 0;    // its (growing) last unit
+    bool prevMarker = false;
+    uint32_t prevProps = 0;
+    int target = -1;          // per lane: lane it was appended into (-1 kept / dropped)
+    int newLen = 0;           // per lane: final length if it is an append target
+    for (int k = 0; k < count; k++) {
+      const int kk = __shfl(kind, k, 64);
+      const int klen = __shfl(s.len, k, 64);
+      const uint32_t ktext = __shfl(s.text, k, 64);
+      const uint32_t kprops = __shfl(s.props, k, 64);
+      const uint16_t klast = (uint16_t)__shfl((int)last, k, 64);
+      if (kk == 1) {
+        prev = -1;
+        continue;
+      }
+      if (kk == 2) {
+        const bool kmarker = (ktext & MTB_MARKER) != 0;
+        bool ok = false;
+        if (prev >= 0 && klen > 0 && !prevMarker && !kmarker && prevLast != (uint16_t)'\n' &&
+            (prevLen <= 256 || klen <= 256))
+          ok = props_match(prevProps, kprops);
+        if (ok) {
+          if (lane == k) target = prev;
+          prevLen += klen;
+          prevLast = klast;
+          if (lane == prev) newLen = prevLen;
         } else {
-          if (lane == 0) sh->hold[nh] = c;
-          nh++;
-          prev = MTB_NONE;
+          prev = klen > 0 ? k : -1;
+          prevLen = klen;
+          prevLast = klast;
+          prevMarker = kmarker;
+          prevProps = kprops;
+          if (lane == k) newLen = klen;
         }
-      } else {
-        if (lane == 0) sh->hold[nh] = c;
-        nh++;
-        prev = MTB_NONE;
+        continue;
+      }
+      prev = -1;
+    }
+    // targets that received appends: build their new text
+    const bool isTarget = lane < count && kind == 2 && target < 0 && newLen != s.len;
+    unsigned long long tm = __ballot(isTarget);
+    while (tm) {
+      const int t = first_set(tm);
+      tm &= tm - 1;
+      // members of the run: t and every lane whose target is t, in order
+      const unsigned long long run = __ballot(lane == t || target == t);
+      const uint32_t ttext = __shfl(s.text, t, 64);
+      const int tlen = __shfl(s.len, t, 64);
+      const int total = __shfl(newLen, t, 64);
+      // contiguous in the arena already?
+      bool contiguous = true;
+      {
+        uint32_t expect = ttext + (uint32_t)tlen;
+        unsigned long long r = run & ~(1ull << t);
+        while (r) {
+          const int q = first_set(r);
+          r &= r - 1;
+          const uint32_t qt = __shfl(s.text, q, 64);
+          const int ql = __shfl(s.len, q, 64);
+          if (qt != expect) contiguous = false;
+          expect = qt + (uint32_t)ql;
+        }
+      }
+      uint32_t dst = ttext;
+      if (!contiguous) {
+        const bool atEnd = ttext + (uint32_t)tlen == text_used;
+        const uint32_t need = atEnd ? (uint32_t)(total - tlen) : (uint32_t)total;
+        if (text_used + need > ds->text_cap) { fail(DERR_CAP_TEXT); return nh; }
+        uint32_t w = text_used;
+        if (!atEnd) {
+          copy_text(w, ttext, (uint32_t)tlen);
+          dst = w;
+          w += (uint32_t)tlen;
+        } else {
+          w = ttext + (uint32_t)tlen;
+        }
+        unsigned long long r = run & ~(1ull << t);
+        while (r) {
+          const int q = first_set(r);
+          r &= r - 1;
+          const uint32_t qt = __shfl(s.text, q, 64);
+          const int ql = __shfl(s.len, q, 64);
+          copy_text(w, qt, (uint32_t)ql);
+          w += (uint32_t)ql;
+        }
+        text_used += need;
+      }
+      if (lane == t) {
+        seg[c & ~MTB_LEAF].text = dst;
+        seg[c & ~MTB_LEAF].len = total;
       }
       wsync();
     }
-    return nh;
+    // unlink dropped / appended segments, compact the kept ones into hold[]
+    const bool keep = lane < count && kind != 1 && target < 0;
+    if (lane < count && !keep) seg[c & ~MTB_LEAF].parent = MTB_NONE;
+    const unsigned long long km = __ballot(keep);
+    if (keep) sh->hold[nh + __popcll(km & ((1ull << lane) - 1))] = c;
+    wsync();
+    return nh + __popcll(km);
   }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
   __device__ __forceinline__ void pack_parent(uint32_t parent) {
@@ -1037,19 +1083,17 @@ struct Eng {
             N.child[lane] = c;
             set_parent(c, nb, lane);
           }
-          if (lane == 0) {
-            N.count = (uint8_t)n;
-            N.parent = parent;
-            N.index = (uint8_t)q;
-            P.child[q] = nb;
-          }
+          N.count = (uint8_t)n;
+          N.parent = parent;
+          N.index = (uint8_t)q;
+          P.child[q] = nb;
           wsync();
           taken += n;
           rebuild(nb);
         }
       }
       if (lane < MTB_MAXCH && lane >= cc) P.child[lane] = MTB_NONE;
-      if (lane == 0) P.count = (uint8_t)cc;
+      P.count = (uint8_t)cc;
       wsync();
       if (cc < MTB_MAXCH / 2 && P.parent != MTB_NONE) {
         parent = P.parent;
@@ -1070,19 +1114,19 @@ struct Eng {
         const int count = blk[b].count;
         const int nh = scour(b, 0);
         Blk& B = blk[b];
-        if (lane == 0) B.scour = 0;
-        wsync();
+        B.scour = 0;
         if (nh < count) {
           if (lane < nh) {
             const uint32_t c = sh->hold[lane];
             B.child[lane] = c;
-            set_parent(c, b, lane);
+            if (!(c & MTB_LEAF)) blk[c].index = (uint8_t)lane;
           }
           if (lane < MTB_MAXCH && lane >= nh) B.child[lane] = MTB_NONE;
-          if (lane == 0) B.count = (uint8_t)nh;
+          B.count = (uint8_t)nh;
           wsync();
           if (nh < MTB_MAXCH / 2 && B.parent != MTB_NONE) pack_parent(B.parent);
         }
+        wsync();
       }
     }
   }
@@ -1102,6 +1146,7 @@ struct Eng {
     switch (o.type) {
       case MTB_OP_INSERT: {
         ops_applied++;
+        cache_clear();
         walk((int)o.pos1, R, C, -2, false, 0, 0);  // ensureIntervalBoundary
         if (err) return;
         const bool marker = (o.flags & MTB_F_MARKER) != 0;
@@ -1119,7 +1164,7 @@ struct Eng {
           s.rcx = 0;
           s.client = (int16_t)C;
           s.rc0 = -1;
-          if (lane == 0) seg[sid] = s;
+          seg[sid] = s;
           wsync();
           n_mod += 1;
           text_bytes += marker ? 0 : 2ull * (uint64_t)len;
@@ -1127,7 +1172,10 @@ struct Eng {
             fail(DERR_INSERT);
             return;
           }
-          if (S > minSeq) lru_add(sid, seg[sid].parent, S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (S > minSeq) {  // saveIfLocal (mergeTree.ts:1617-1637)
+            const uint32_t pb = seg[sid].parent;
+            lru_add(sid, pb, blk[pb].scour, S);
+          }
         }
         zamboni();
         break;
@@ -1135,11 +1183,11 @@ struct Eng {
       case MTB_OP_REMOVE:
       case MTB_OP_ANNOTATE: {
         ops_applied++;
+        cache_clear();
         walk((int)o.pos1, R, C, -2, false, 0, 0);
         walk((int)o.pos2, R, C, -2, false, 0, 0);
         if (err) return;
-        node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props,
-                 (o.flags & MTB_F_REWRITE) != 0);
+        node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
         zamboni();
         break;
       }
@@ -1163,7 +1211,10 @@ struct Eng {
 
 using namespace mtbk;
 
-extern "C" __global__ void __launch_bounds__(64) mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs,
+#ifndef MTB_WAVES_PER_SIMD
+#define MTB_WAVES_PER_SIMD 3
+#endif
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD) mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs,
                                                                    const mtb_op* ops, Seg* segs, Blk* blks, WEnt* lists,
                                                                    uint16_t* text, Lru* heap, uint32_t* aux,
                                                                    uint32_t* freel, Tables tables) {
