@@ -20,7 +20,8 @@ ERRORS = {0: "MTB_OK", -1: "MTB_E_ARG", -2: "MTB_E_NODEV", -3: "MTB_E_HIP", -4: 
 EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free", "mtb_doc_init",
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
-           "mtb_summarize_v1", "mtb_blob_list_free", "mtb_rewind", "mtb_replay_resident"]
+           "mtb_summarize_v1", "mtb_blob_list_free", "mtb_rewind", "mtb_replay_resident",
+           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id"]
 
 
 class MtbOptions(ctypes.Structure):
@@ -55,10 +56,13 @@ def lib():
     # PyTorch-ROCm bundles its own libamdhip64.so.7.  Load it first so this process has exactly one HIP
     # runtime (the engine's DT_NEEDED soname then resolves to the already-loaded copy); loading the
     # system runtime first makes torch report "No HIP GPUs are available".
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # MTB_NO_TORCH=1 keeps torch out of the process (e.g. under rocprofv3 --pmc, whose tool library
+    # binds to the system HSA runtime).
+    if os.environ.get("MTB_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t
     L.mtb_batch_create.argtypes = [ctypes.POINTER(MtbOptions), u32, u32, ctypes.POINTER(vp)]
@@ -81,5 +85,8 @@ def lib():
     L.mtb_blob_list_free.argtypes = [ctypes.POINTER(MtbBlobList)]
     L.mtb_rewind.argtypes = [vp]
     L.mtb_replay_resident.argtypes = [vp, ctypes.POINTER(MtbStats)]
+    L.mtb_export_pending.argtypes = [vp, u32, vp, u32, ctypes.POINTER(u32), vp, sz, ctypes.POINTER(sz)]
+    L.mtb_props_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.mtb_client_long_id.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     _LIB = L
     return L

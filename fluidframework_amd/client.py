@@ -124,6 +124,30 @@ class MergeTreeBatch:
         if self._dirty:
             self.replay()
 
+    # --- host-side inspection (no GPU) --------------------------------------------------------
+    def export_pending(self, doc):
+        """(records bytes, n, payload u16 bytes) packed for `doc` and not yet replayed."""
+        n, pl = ctypes.c_uint32(), ctypes.c_size_t()
+        self._chk(self._L.mtb_export_pending(self._h, doc, None, 0, ctypes.byref(n), None, 0, ctypes.byref(pl)))
+        ob = ctypes.create_string_buffer(max(1, n.value * 32))
+        pb = ctypes.create_string_buffer(max(2, pl.value * 2))
+        self._chk(self._L.mtb_export_pending(self._h, doc, ob, n.value, ctypes.byref(n), pb, pl.value, ctypes.byref(pl)))
+        return ob.raw[: n.value * 32], n.value, pb.raw[: pl.value * 2]
+
+    def props_json(self, pid):
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_props_json(self._h, pid, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self._L.mtb_props_json(self._h, pid, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
+
+    def client_long_id(self, doc, short_id):
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_client_long_id(self._h, doc, short_id, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self._L.mtb_client_long_id(self._h, doc, short_id, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
+
     # --- per-document read-outs ---------------------------------------------------------------
     def text(self, doc):
         self._ensure_flushed()

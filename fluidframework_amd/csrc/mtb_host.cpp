@@ -24,6 +24,10 @@
 #include "mtb_device.h"
 
 // defined in mtb_replay.hip
+hipError_t mtb_launch_move_words(hipStream_t stream, const uint32_t* src, const uint64_t* src_off, uint32_t* dst,
+                                 const uint64_t* dst_off, const uint32_t* len, uint32_t n);
+hipError_t mtb_launch_move_u16(hipStream_t stream, const uint16_t* src, const uint64_t* src_off, uint16_t* dst,
+                               const uint64_t* dst_off, const uint32_t* len, uint32_t n);
 hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, Seg* segs,
                              const Seg* pseg, Blk* blks, const Blk* pblk);
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
@@ -250,10 +254,15 @@ struct mtb_batch {
   DevBuf<DocState> dPristine;
   DevBuf<Seg> dPSeg;
   DevBuf<Blk> dPBlk;
+  // batched moves: chunk tables and host->device staging
+  DevBuf<uint64_t> dMvSrc, dMvDst;
+  DevBuf<uint32_t> dMvLen, dStageW;
+  DevBuf<uint16_t> dStageH;
   ~mtb_batch() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
     dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release();
+    dMvSrc.release(); dMvDst.release(); dMvLen.release(); dStageW.release(); dStageH.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (stream) (void)hipStreamDestroy(stream);
@@ -382,6 +391,53 @@ void ensure_stream(mtb_batch* b) {
   HIPCHK(hipEventCreate(&b->ev1));
 }
 
+// A list of (src offset, dst offset, length) chunks moved by one kernel launch.
+struct Chunks {
+  std::vector<uint64_t> src, dst;
+  std::vector<uint32_t> len;
+  void add(uint64_t s, uint64_t d, uint64_t n) {
+    if (!n) return;
+    src.push_back(s);
+    dst.push_back(d);
+    len.push_back((uint32_t)n);
+  }
+};
+void upload_chunks(mtb_batch* b, const Chunks& c) {
+  b->dMvSrc.ensure(c.src.size());
+  b->dMvDst.ensure(c.dst.size());
+  b->dMvLen.ensure(c.len.size());
+  HIPCHK(hipMemcpyAsync(b->dMvSrc.p, c.src.data(), c.src.size() * 8, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(b->dMvDst.p, c.dst.data(), c.dst.size() * 8, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(b->dMvLen.p, c.len.data(), c.len.size() * 4, hipMemcpyHostToDevice, b->stream));
+}
+// device words -> device words
+void move_words(mtb_batch* b, const void* src, void* dst, const Chunks& c) {
+  if (c.len.empty()) return;
+  upload_chunks(b, c);
+  HIPCHK(mtb_launch_move_words(b->stream, (const uint32_t*)src, b->dMvSrc.p, (uint32_t*)dst, b->dMvDst.p, b->dMvLen.p,
+                               (uint32_t)c.len.size()));
+  HIPCHK(hipStreamSynchronize(b->stream));
+}
+void move_u16(mtb_batch* b, const uint16_t* src, uint16_t* dst, const Chunks& c) {
+  if (c.len.empty()) return;
+  upload_chunks(b, c);
+  HIPCHK(mtb_launch_move_u16(b->stream, src, b->dMvSrc.p, dst, b->dMvDst.p, b->dMvLen.p, (uint32_t)c.len.size()));
+  HIPCHK(hipStreamSynchronize(b->stream));
+}
+// host words -> device (via one staging upload)
+void scatter_words(mtb_batch* b, const std::vector<uint32_t>& host, void* dst, const Chunks& c) {
+  if (c.len.empty()) return;
+  b->dStageW.ensure(host.size());
+  HIPCHK(hipMemcpyAsync(b->dStageW.p, host.data(), host.size() * 4, hipMemcpyHostToDevice, b->stream));
+  move_words(b, b->dStageW.p, dst, c);
+}
+void scatter_u16(mtb_batch* b, const std::vector<uint16_t>& host, uint16_t* dst, const Chunks& c) {
+  if (c.len.empty()) return;
+  b->dStageH.ensure(host.size());
+  HIPCHK(hipMemcpyAsync(b->dStageH.p, host.data(), host.size() * 2, hipMemcpyHostToDevice, b->stream));
+  move_u16(b, b->dStageH.p, dst, c);
+}
+
 // Per-document slice capacities from the record count (see DESIGN.md "HBM layout").  `n` is the
 // number of records the slices must hold (all records appended so far, times a growth margin).
 struct Caps {
@@ -424,27 +480,37 @@ void layout(mtb_batch* b, const std::vector<Caps>& want) {
     s.aux_base = ax; ax += s.aux_cap;
     s.free_base = s.blk_base;
   }
+  // allocate the new pools and move every document's live prefix with one kernel per pool
   auto move = [&](auto& buf, uint64_t total, auto getBase, auto getUsed) {
     using T = std::remove_pointer_t<decltype(buf.p)>;
     T* np = nullptr;
     HIPCHK(hipMalloc((void**)&np, std::max<uint64_t>(total, 1) * sizeof(T)));
     if (buf.p) {
-      for (uint32_t i = 0; i < b->ndocs; i++) {
-        const uint64_t used = getUsed(b->hst[i]);
-        if (used)
-          HIPCHK(hipMemcpyAsync(np + getBase(ns[i]), buf.p + getBase(b->hst[i]), used * sizeof(T), hipMemcpyDeviceToDevice,
-                                b->stream));
-      }
-      HIPCHK(hipStreamSynchronize(b->stream));
+      Chunks c;
+      const uint64_t w = sizeof(T) / 4;  // words per element (u16 handled separately)
+      for (uint32_t i = 0; i < b->ndocs; i++) c.add(getBase(b->hst[i]) * w, getBase(ns[i]) * w, getUsed(b->hst[i]) * w);
+      move_words(b, buf.p, np, c);
       (void)hipFree(buf.p);
     }
     buf.p = np;
     buf.n = total;
   };
+  auto move_text = [&](uint64_t total) {
+    uint16_t* np = nullptr;
+    HIPCHK(hipMalloc((void**)&np, std::max<uint64_t>(total, 1) * 2));
+    if (b->dText.p) {
+      Chunks c;
+      for (uint32_t i = 0; i < b->ndocs; i++) c.add(b->hst[i].text_base, ns[i].text_base, b->hst[i].text_used);
+      move_u16(b, b->dText.p, np, c);
+      (void)hipFree(b->dText.p);
+    }
+    b->dText.p = np;
+    b->dText.n = total;
+  };
   move(b->dSegs, seg, [](const DocState& s) { return s.seg_base; }, [](const DocState& s) { return (uint64_t)s.seg_used; });
   move(b->dBlks, blk, [](const DocState& s) { return s.blk_base; }, [](const DocState& s) { return (uint64_t)s.blk_used; });
   move(b->dLists, lst, [](const DocState& s) { return s.list_base; }, [](const DocState& s) { return (uint64_t)s.list_used; });
-  move(b->dText, txt, [](const DocState& s) { return s.text_base; }, [](const DocState& s) { return (uint64_t)s.text_used; });
+  move_text(txt);
   move(b->dHeap, hp, [](const DocState& s) { return s.heap_base; }, [](const DocState& s) { return (uint64_t)s.heap_cnt + 1; });
   move(b->dAux, ax, [](const DocState& s) { return s.aux_base; }, [](const DocState& s) { return (uint64_t)s.aux_used; });
   move(b->dFree, blk, [](const DocState& s) { return s.free_base; }, [](const DocState& s) { return (uint64_t)s.free_top; });
@@ -461,6 +527,9 @@ void device_init(mtb_batch* b) {
   }
   layout(b, want);
   // initial state: root block (+ the detached initial text segment), collaboration started
+  std::vector<uint32_t> recs;
+  std::vector<uint16_t> texts;
+  Chunks segc, blkc, txtc;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
@@ -476,6 +545,7 @@ void device_init(mtb_batch* b) {
     for (int k = 0; k < MTB_MAXCH; k++) root.child[k] = MTB_NONE;
     root.parent = MTB_NONE;
     root.scour = -1;
+    root.lseq = (int32_t)0x80000000;
     if (!d.initText.empty()) {
       Seg sg{};
       sg.len = (int32_t)d.initText.size();
@@ -489,15 +559,21 @@ void device_init(mtb_batch* b) {
       root.count = 1;
       root.len = sg.len;
       s.seg_used = 1;
-      HIPCHK(hipMemcpyAsync(b->dSegs.p + s.seg_base, &sg, sizeof sg, hipMemcpyHostToDevice, b->stream));
-      HIPCHK(hipMemcpyAsync(b->dText.p + s.text_base, d.initText.data(), d.initText.size() * 2, hipMemcpyHostToDevice,
-                            b->stream));
+      segc.add(recs.size(), s.seg_base * (sizeof(Seg) / 4), sizeof(Seg) / 4);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(&sg);
+      recs.insert(recs.end(), w, w + sizeof(Seg) / 4);
+      txtc.add(texts.size(), s.text_base, d.initText.size());
+      texts.insert(texts.end(), d.initText.begin(), d.initText.end());
     }
     s.text_used = (uint32_t)d.initText.size();
-    HIPCHK(hipMemcpyAsync(b->dBlks.p + s.blk_base, &root, sizeof root, hipMemcpyHostToDevice, b->stream));
+    blkc.add(recs.size(), s.blk_base * (sizeof(Blk) / 4), sizeof(Blk) / 4);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&root);
+    recs.insert(recs.end(), w, w + sizeof(Blk) / 4);
     d.onDevice = true;
   }
-  HIPCHK(hipStreamSynchronize(b->stream));
+  scatter_words(b, recs, b->dSegs.p, segc);
+  scatter_words(b, recs, b->dBlks.p, blkc);
+  scatter_u16(b, texts, b->dText.p, txtc);
   b->dDocs.ensure(b->ndocs);
   b->devInit = true;
 }
@@ -564,11 +640,14 @@ void capture_pristine(mtb_batch* b) {
   b->dPSeg.ensure(b->ndocs);
   b->dPBlk.ensure(b->ndocs);
   HIPCHK(hipMemcpyAsync(b->dPristine.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+  Chunks bc, sc;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     const DocState& s = b->hst[i];
-    HIPCHK(hipMemcpyAsync(b->dPBlk.p + i, b->dBlks.p + s.blk_base, sizeof(Blk), hipMemcpyDeviceToDevice, b->stream));
-    HIPCHK(hipMemcpyAsync(b->dPSeg.p + i, b->dSegs.p + s.seg_base, sizeof(Seg), hipMemcpyDeviceToDevice, b->stream));
+    bc.add(s.blk_base * (sizeof(Blk) / 4), (uint64_t)i * (sizeof(Blk) / 4), sizeof(Blk) / 4);
+    sc.add(s.seg_base * (sizeof(Seg) / 4), (uint64_t)i * (sizeof(Seg) / 4), sizeof(Seg) / 4);
   }
+  move_words(b, b->dBlks.p, b->dPBlk.p, bc);
+  move_words(b, b->dSegs.p, b->dPSeg.p, sc);
   b->haveRewind = true;
 }
 
@@ -593,19 +672,24 @@ void replay(mtb_batch* b, mtb_stats* out) {
     if (grow) layout(b, want);
   }
   // gather pending ops of every document into one buffer
-  uint64_t total = 0;
-  for (auto& d : b->docs) total += d.pending.size();
+  uint64_t total = 0, totalPay = 0;
+  for (auto& d : b->docs) {
+    total += d.pending.size();
+    totalPay += d.payload.size();
+  }
   std::vector<mtb_op> ops;
   ops.reserve(total);
+  std::vector<uint16_t> pay;
+  pay.reserve(totalPay);
+  Chunks payc;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
     if (s.err) continue;
     // payload goes after the text already in the arena; rebase record offsets
     const uint32_t base = s.text_used;
-    if (!d.payload.empty())
-      HIPCHK(hipMemcpyAsync(b->dText.p + s.text_base + base, d.payload.data(), d.payload.size() * 2, hipMemcpyHostToDevice,
-                            b->stream));
+    payc.add(pay.size(), s.text_base + base, d.payload.size());
+    pay.insert(pay.end(), d.payload.begin(), d.payload.end());
     s.text_used += (uint32_t)d.payload.size();
     s.op_base = ops.size();
     s.n_ops = (uint32_t)d.pending.size();
@@ -615,6 +699,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
       ops.push_back(o);
     }
   }
+  scatter_u16(b, pay, b->dText.p, payc);
   b->dOps.ensure(ops.size() + 1);
   if (!ops.empty()) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.data(), ops.size() * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
@@ -1221,6 +1306,52 @@ int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_b
     }
     out->summary_json = dup(summary);
     out->summary_json_len = summary.size();
+  });
+}
+
+int mtb_export_pending(mtb_batch* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out, uint16_t* payload,
+                       size_t pcap, size_t* plen_out) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (n_out) *n_out = (uint32_t)d.pending.size();
+    if (plen_out) *plen_out = d.payload.size();
+    if (ops) {
+      if (cap < d.pending.size()) raise(MTB_E_ARG, "record buffer too small");
+      memcpy(ops, d.pending.data(), d.pending.size() * sizeof(mtb_op));
+    }
+    if (payload) {
+      if (pcap < d.payload.size()) raise(MTB_E_ARG, "payload buffer too small");
+      memcpy(payload, d.payload.data(), d.payload.size() * 2);
+    }
+  });
+}
+
+int mtb_props_json(mtb_batch* b, uint32_t id, char* buf, size_t cap, size_t* len_out) {
+  return guarded(b, [&] {
+    for (auto& kv : b->in.propsByJson) {
+      if (kv.second == id) {
+        if (len_out) *len_out = kv.first.size();
+        if (buf) {
+          if (cap < kv.first.size() + 1) raise(MTB_E_ARG, "buffer too small");
+          memcpy(buf, kv.first.c_str(), kv.first.size() + 1);
+        }
+        return;
+      }
+    }
+    raise(MTB_E_ARG, "unknown props id");
+  });
+}
+
+int mtb_client_long_id(mtb_batch* b, uint32_t doc, uint32_t short_id, char* buf, size_t cap, size_t* len_out) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (short_id >= d.longIds.size()) raise(MTB_E_ARG, "unknown short client id");
+    const std::string& s = d.longIds[short_id];
+    if (len_out) *len_out = s.size();
+    if (buf) {
+      if (cap < s.size() + 1) raise(MTB_E_ARG, "buffer too small");
+      memcpy(buf, s.c_str(), s.size() + 1);
+    }
   });
 }
 

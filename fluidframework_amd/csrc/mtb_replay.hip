@@ -1320,3 +1320,36 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
   hipLaunchKernelGGL(mtb_rewind_kernel, dim3(ndocs), dim3(64), 0, stream, docs, pristine, ndocs, segs, pseg, blks, pblk);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------- batched host<->slice moves
+// One launch moves every document's piece instead of one hipMemcpy per document.
+// Chunk i: `len[i]` 32-bit words from src + src_off[i] to dst + dst_off[i]; one wave per chunk.
+extern "C" __global__ void mtb_move_words_kernel(const uint32_t* src, const uint64_t* src_off, uint32_t* dst,
+                                                 const uint64_t* dst_off, const uint32_t* len, uint32_t n) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  const uint32_t* s = src + src_off[i];
+  uint32_t* d = dst + dst_off[i];
+  for (uint32_t k = threadIdx.x; k < len[i]; k += blockDim.x) d[k] = s[k];
+}
+extern "C" __global__ void mtb_move_u16_kernel(const uint16_t* src, const uint64_t* src_off, uint16_t* dst,
+                                               const uint64_t* dst_off, const uint32_t* len, uint32_t n) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  const uint16_t* s = src + src_off[i];
+  uint16_t* d = dst + dst_off[i];
+  for (uint32_t k = threadIdx.x; k < len[i]; k += blockDim.x) d[k] = s[k];
+}
+
+hipError_t mtb_launch_move_words(hipStream_t stream, const uint32_t* src, const uint64_t* src_off, uint32_t* dst,
+                                 const uint64_t* dst_off, const uint32_t* len, uint32_t n) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(mtb_move_words_kernel, dim3(n), dim3(64), 0, stream, src, src_off, dst, dst_off, len, n);
+  return hipGetLastError();
+}
+hipError_t mtb_launch_move_u16(hipStream_t stream, const uint16_t* src, const uint64_t* src_off, uint16_t* dst,
+                               const uint64_t* dst_off, const uint32_t* len, uint32_t n) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(mtb_move_u16_kernel, dim3(n), dim3(64), 0, stream, src, src_off, dst, dst_off, len, n);
+  return hipGetLastError();
+}

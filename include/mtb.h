@@ -145,6 +145,14 @@ void mtb_blob_list_free(mtb_blob_list* l);
 int mtb_rewind(mtb_batch* b);
 int mtb_replay_resident(mtb_batch* b, mtb_stats* out);
 
+/* ---- host-side inspection (tests): the records/payload packed for `doc` and not yet replayed, the
+ * JSON of an interned props id, and the long id of a short client id (Client.getLongClientId,
+ * client.ts:682).  None of these touch the GPU. */
+int mtb_export_pending(mtb_batch* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out,
+                       uint16_t* payload, size_t pcap, size_t* plen_out);
+int mtb_props_json(mtb_batch* b, uint32_t id, char* buf, size_t cap, size_t* len_out);
+int mtb_client_long_id(mtb_batch* b, uint32_t doc, uint32_t short_id, char* buf, size_t cap, size_t* len_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,110 @@
+"""Host-side checks of the engine library (no GPU needed).
+
+* libmtb.so loads and exports every entry point declared in include/mtb.h.
+* Without a GPU the engine fails loudly (MTB_E_NODEV) instead of computing on the CPU.
+* The host packer (mtb_apply_msg_json: ISequencedDocumentMessage -> 32-byte records, client-id and
+  props interning) is checked by replaying its records through the oracle's record path and comparing
+  with the reference's golden texts.
+"""
+import os
+import re
+
+import pytest
+
+from helpers import ROOT, msg_from_compact, replay_fixtures
+
+
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "mtb.h")).read()
+    return sorted(set(re.findall(r"\b(mtb_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    from fluidframework_amd import _lib
+    L = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(syms) == set(_lib.EXPORTS)
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    B = MergeTreeBatch(1)
+    B[0].startOrUpdateCollaboration("A")
+    B[0].applyMsg({"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                   "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": 0, "seg": "x"}})
+    with pytest.raises(MergeTreeError) as ei:
+        B.flush()
+    assert ei.value.code == -2  # MTB_E_NODEV
+
+
+def test_unsupported_inputs_are_rejected_at_pack_time():
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    B = MergeTreeBatch(1)
+    B[0].startOrUpdateCollaboration("A")
+    base = {"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0, "type": "op"}
+    with pytest.raises(MergeTreeError, match="relative positions"):
+        B[0].applyMsg(dict(base, contents={"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
+    with pytest.raises(MergeTreeError, match="combiningOp"):
+        B[0].applyMsg(dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
+                                           "combiningOp": {"name": "incr"}}))
+    with pytest.raises(MergeTreeError, match="0x038"):
+        B[0].applyMsg(dict(base, sequenceNumber=5, contents={"type": 0, "pos1": 0, "seg": "x"}))
+        B[0].applyMsg(dict(base, sequenceNumber=4, contents={"type": 0, "pos1": 0, "seg": "y"}))
+
+
+@pytest.mark.parametrize("idx", [0, 5, 13, 21, 29])
+def test_packed_records_replay_to_golden_text(idx):
+    """Pack a reference log with the product packer; the oracle's record path reproduces the golden text."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    name, d = replay_fixtures()[idx]
+    B = MergeTreeBatch(1)
+    B[0].insertTextLocal(0, d["initialText"])
+    B[0].startOrUpdateCollaboration("A")
+    for g in d["groups"]:
+        for m in g["msgs"]:
+            B[0].applyMsg(msg_from_compact(m))
+    ops, n, payload = B.export_pending(0)
+    assert n == sum(len(g["msgs"]) for g in d["groups"])  # fixture logs have no GROUP ops
+    # props table: ids in first-interned order
+    props = [None]
+    k = 1
+    while True:
+        try:
+            props.append(B.props_json(k))
+        except Exception:
+            break
+        k += 1
+    o = OracleDoc()
+    o.insert_text_local(0, d["initialText"])
+    o.start_collab("A")
+    longs = [B.client_long_id(0, i) for i in range(1, 64) if _has_client(B, i)]
+    for lid in longs:
+        o.add_client(lid)
+    o.apply_records(ops, n, payload, props)
+    assert o.get_text() == d["groups"][-1]["resultText"], name
+
+
+def _has_client(B, i):
+    try:
+        B.client_long_id(0, i)
+        return True
+    except Exception:
+        return False
+
+
+def test_props_interning_js_key_order():
+    """Object key order follows V8: array-index keys ascending first, then insertion order."""
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1)
+    pid = B.intern_props('{"b":1,"2":2,"a":3,"1":4}')
+    assert B.props_json(pid) == '{"1":4,"2":2,"b":1,"a":3}'
+    # duplicate keys: last value wins, first position kept (JSON.parse)
+    pid2 = B.intern_props('{"x":1,"y":2,"x":3}')
+    assert B.props_json(pid2) == '{"x":3,"y":2}'

@@ -1,0 +1,145 @@
+"""CPU oracle vs the reference's own golden data (no GPU).
+
+* 30 committed conflict-farm replay logs (packages/dds/merge-tree/src/test/results, replayed by
+  client.replay.spec.ts:16-72): the text after each of the 1,920 groups.
+* the same logs with the partial-length verifier on: every remote-perspective block length returned by
+  the PartialSequenceLengths restatement equals the sum of its leaves' visibilities (the identity the
+  GPU's window lists rely on).
+* the 6 committed SnapshotV1 summaries (packages/dds/sequence/src/test/snapshots/v1), byte-exact, from
+  the generateSharedStrings.ts:47-146 recipes.
+* known-answer tests restated from client.applyMsg.spec.ts on the observer path.
+"""
+import pytest
+from pyoracle import OracleDoc
+
+from helpers import msg_from_compact, replay_fixtures, snapshot_fixture
+
+FIXTURES = replay_fixtures()
+
+
+@pytest.mark.parametrize("name,d", FIXTURES, ids=[n for n, _ in FIXTURES])
+def test_replay_log_text_after_every_group(name, d):
+    o = OracleDoc()
+    o.insert_text_local(0, d["initialText"])
+    o.start_collab("A")
+    for gi, g in enumerate(d["groups"]):
+        for m in g["msgs"]:
+            o.apply_msg(msg_from_compact(m))
+        assert o.get_text() == g["resultText"], f"{name}: group {gi}"
+
+
+@pytest.mark.parametrize("idx", [0, 7, 15, 22, 29])
+def test_partial_lengths_equal_leaf_sums(idx):
+    name, d = FIXTURES[idx]
+    o = OracleDoc(verify=True)
+    o.insert_text_local(0, d["initialText"])
+    o.start_collab("A")
+    for g in d["groups"]:
+        for m in g["msgs"]:
+            o.apply_msg(msg_from_compact(m))
+    assert o.get_text() == d["groups"][-1]["resultText"]
+
+
+SIZE_OF_FIRST_CHUNK = 10000  # SnapshotLegacy.sizeOfFirstChunk
+
+
+def _build_detached(name):
+    """generateSharedStrings.ts:47-146 on a detached (non-collaborating) string."""
+    d = OracleDoc()
+    t = "text"
+    if name in ("headerOnly", "withIntervals"):
+        for i in range(int(SIZE_OF_FIRST_CHUNK / len(t) / 2)):
+            d.insert_text_local(0, f"{t}{i}")
+    elif name == "headerAndBody":
+        for i in range(int(SIZE_OF_FIRST_CHUNK / len(t) * 2)):
+            d.insert_text_local(0, f"{t}{i}")
+    elif name == "largeBody":
+        for i in range(SIZE_OF_FIRST_CHUNK):
+            d.insert_text_local(0, f"{t}-{i}")
+    elif name == "withMarkers":
+        for i in range(int(SIZE_OF_FIRST_CHUNK / len(t) * 2)):
+            d.insert_text_local(0, f"{t}{i}")
+        i = 0
+        while i < d.get_length():
+            d.insert_marker_local(i, 1, {"ItemType": "Paragraph", "Properties": {"Bold": False},
+                                         "markerId": f"marker{i}", "referenceTileLabels": ["Eop"]})
+            i += 70
+    elif name == "withAnnotations":
+        for i in range(int(SIZE_OF_FIRST_CHUNK / len(t) * 2)):
+            d.insert_text_local(0, f"{t}{i}")
+        i = 0
+        while i < d.get_length():
+            d.annotate_local(i, i + 10, {"bold": True})
+            i += 70
+    return d
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations",
+                                  "withIntervals"])
+def test_snapshot_v1_fixture_bytes(name):
+    expected = [b for b in snapshot_fixture(name)]
+    got = _build_detached(name).summarize_v1(0, 0)
+    assert [list(b) for b in got["blobs"]] == expected
+    stats = got["summary"]["stats"]
+    assert stats["blobNodeCount"] == len(expected)
+    assert stats["treeNodeCount"] == 1
+
+
+def _msg(client, seq, ref, contents, msn=0):
+    return {"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+            "minimumSequenceNumber": msn, "type": "op", "contents": contents}
+
+
+def _initial(state, new_mode=False):
+    """createClientsAtInitialState (testClientLogger.ts:51): '-' become detached tombstones."""
+    o = OracleDoc(new_length_calc=new_mode)
+    o.insert_text_local(0, state)
+    while "-" in o.get_text():
+        i = o.get_text().index("-")
+        o.remove_local(i, i + 1)
+    o.start_collab("A")
+    return o
+
+
+def test_kat_conflicting_inserts_at_deleted_segment_position():
+    # client.applyMsg.spec.ts:440-462 -> "ab"
+    o = _initial("a----bcd-ef")
+    o.apply_msg(_msg("B", 1, 0, {"type": 0, "pos1": 4, "seg": "B"}))
+    o.apply_msg(_msg("C", 2, 0, {"type": 0, "pos1": 4, "seg": "CC"}))
+    o.apply_msg(_msg("C", 3, 0, {"type": 1, "pos1": 2, "pos2": 8}))
+    o.apply_msg(_msg("B", 4, 2, {"type": 1, "pos1": 5, "pos2": 8}))
+    assert o.get_text() == "ab"
+
+
+def test_kat_9703_new_length_calculations():
+    # client.applyMsg.spec.ts:464-493 (mergeTreeUseNewLengthCalculations: true) -> "ayzXd"
+    o = _initial("abcd", new_mode=True)
+    o.apply_msg(_msg("B", 1, 0, {"type": 1, "pos1": 1, "pos2": 3}))
+    o.apply_msg(_msg("B", 2, 1, {"type": 0, "pos1": 1, "seg": "yz"}))
+    o.apply_msg(_msg("C", 3, 0, {"type": 0, "pos1": 2, "seg": "X"}))
+    assert o.get_text() == "ayzXd"
+
+
+def test_kat_remote_remove_before_conflicting_insert():
+    # client.applyMsg.spec.ts:415-438 -> "CB"
+    o = _initial("Z")
+    o.apply_msg(_msg("B", 1, 0, {"type": 1, "pos1": 0, "pos2": 1}))
+    o.apply_msg(_msg("B", 2, 0, {"type": 0, "pos1": 0, "seg": "B"}))
+    o.apply_msg(_msg("C", 3, 1, {"type": 0, "pos1": 0, "seg": "C"}))
+    assert o.get_text() == "CB"
+
+
+def test_assert_codes():
+    o = _initial("abc")
+    o.apply_msg(_msg("B", 5, 0, {"type": 0, "pos1": 0, "seg": "x"}))
+    with pytest.raises(Exception, match="0x038"):
+        o.apply_msg(_msg("B", 4, 0, {"type": 0, "pos1": 0, "seg": "y"}))
+
+
+def test_group_op_members_share_seq():
+    o = _initial("hello")
+    o.apply_msg(_msg("B", 1, 0, {"type": 3, "ops": [{"type": 0, "pos1": 5, "seg": " world"},
+                                                     {"type": 2, "pos1": 0, "pos2": 5, "props": {"bold": True}}]}))
+    assert o.get_text() == "hello world"
+    dump = o.dump_segments().splitlines()
+    assert any('"bold":true' in line for line in dump)
