@@ -1,4 +1,9 @@
-"""Build the engine's shared library in-tree (hipcc, gfx950).  `python -m fluidframework_amd.build`."""
+"""Build the engine in-tree: `python -m fluidframework_amd.build`.
+
+* fluidframework_amd/libmtb.so          HIP engine (hipcc, gfx950) exporting the C ABI of include/mtb.h
+* fluidframework_amd/js/mtb_napi.node   Node N-API addon over that C ABI (gcc + node's headers), used by
+                                        the JS drop-in package fluidframework_amd/js (index.js)
+"""
 import os
 import subprocess
 import sys
@@ -7,15 +12,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, "csrc", "mtb_replay.hip"), os.path.join(HERE, "csrc", "mtb_host.cpp")]
 OUT = os.path.join(HERE, "libmtb.so")
+NAPI_SRC = os.path.join(HERE, "js", "src", "mtb_napi.c")
+NAPI_OUT = os.path.join(HERE, "js", "mtb_napi.node")
+NODE_INCLUDE = "/usr/include/node"
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(p) > t for p in deps)
 
 
 def needs_build():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
     deps = SRCS + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))] + \
         [os.path.join(ROOT, "include", "mtb.h")]
-    return any(os.path.getmtime(p) > t for p in deps)
+    return _stale(OUT, deps)
 
 
 def build(force=False, arch="gfx950", out=OUT, defines=()):
@@ -27,8 +39,22 @@ def build(force=False, arch="gfx950", out=OUT, defines=()):
     return out
 
 
+def build_napi(force=False):
+    """The N-API addon links libmtb.so (rpath $ORIGIN/..); node resolves the napi_* symbols at load."""
+    if not os.path.exists(os.path.join(NODE_INCLUDE, "node_api.h")):
+        print("build_napi: node headers not found, JS addon not built", file=sys.stderr)
+        return None
+    if not force and not _stale(NAPI_OUT, [NAPI_SRC, OUT, os.path.join(ROOT, "include", "mtb.h")]):
+        return NAPI_OUT
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-DNODE_GYP_MODULE_NAME=mtb_napi",
+           f"-I{NODE_INCLUDE}", NAPI_SRC, f"-L{HERE}", "-lmtb", "-Wl,-rpath,$ORIGIN/..", "-o", NAPI_OUT]
+    subprocess.check_call(cmd)
+    return NAPI_OUT
+
+
 if __name__ == "__main__":
     if "--variants" in sys.argv:  # occupancy variants for tuning runs (MTB_LIB=...)
-        for w in (2, 3, 4):
+        for w in (3, 4, 5):
             print(build(force=True, out=os.path.join(HERE, f"libmtb_w{w}.so"), defines=[f"MTB_WAVES_PER_SIMD={w}"]))
     print(build(force="--force" in sys.argv))
+    print(build_napi(force="--force" in sys.argv))

@@ -36,19 +36,27 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // to make one lane's store visible to another lane's later load of the same document state.
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-__device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Cross-lane primitives.  Every scan / sum in this kernel runs over the <=8 children of one block,
+// i.e. lanes 0..7 of DPP row 0, so it is three DPP row_shr steps (plain VALU, no LDS round trip);
+// values are read from a uniform lane with v_readlane (SGPR result) instead of ds_bpermute.
+template <int CTRL>
+__device__ __forceinline__ int dpp_shr_t(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);  // bound_ctrl: out-of-row source -> 0
+}
+// inclusive scan over lanes 0..7 (lanes >= count must hold 0)
+__device__ __forceinline__ int cscan8(int v) {
+  v += dpp_shr_t<0x111>(v);  // row_shr:1
+  v += dpp_shr_t<0x112>(v);  // row_shr:2
+  v += dpp_shr_t<0x114>(v);  // row_shr:4
   return v;
 }
-__device__ __forceinline__ int wscan_incl(int v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int t = __shfl_up(v, o, 64);
-    if (l >= o) v += t;
-  }
-  return v;
+__device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ uint32_t rlu(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+// sum over lanes 0..7
+__device__ __forceinline__ int csum8(int v) { return rl(cscan8(v), 7); }
+// number of set bits of m below this lane
+__device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ __forceinline__ int first_set(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
@@ -214,16 +222,16 @@ struct Eng {
       }
     }
     // concatenated scan of the children's window lists, accumulated per child in LDS
-    const int incl = wscan_incl((int)lcnt);
-    const int total = __shfl(incl, 63, 64);
+    const int incl = cscan8((int)lcnt);
+    const int total = rl(incl, 7);
     if (total > 0) {
       const int excl = incl - (int)lcnt;
       if (lane < MTB_MAXCH) sh->corr[lane] = 0;
       int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
       for (int k = 0; k < MTB_MAXCH; k++) {
-        pre[k] = __shfl(excl, k, 64);
-        off[k] = __shfl((int)loff, k, 64);
+        pre[k] = rl(excl, k);
+        off[k] = rl((int)loff, k);
       }
       wsync();
       for (int t = lane; t < total; t += 64) {
@@ -338,7 +346,7 @@ struct Eng {
         keep = e.seq > minSeq;
       }
       const unsigned long long m = __ballot(keep);
-      const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+      const uint32_t rank = rank_below(m);
       if (keep) lst[no + w + rank] = e;
       w += __popcll(m);
     }
@@ -375,15 +383,15 @@ struct Eng {
         ccnt = cb.lcnt;
       }
     }
-    const int totalLen = wsum(olen);
-    const int cincl = wscan_incl((int)ccnt);
+    const int totalLen = csum8(olen);
+    const int cincl = cscan8((int)ccnt);
     const int cexcl = cincl - (int)ccnt;
-    const int ctotal = __shfl(cincl, 63, 64);
+    const int ctotal = rl(cincl, 7);
     int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
     for (int k = 0; k < MTB_MAXCH; k++) {
-      pre[k] = __shfl(cexcl, k, 64);
-      off[k] = __shfl((int)coff, k, 64);
+      pre[k] = rl(cexcl, k);
+      off[k] = rl((int)coff, k);
     }
     int live_from_children = 0;
     for (int base = 0; base < ctotal; base += 64) {
@@ -402,13 +410,13 @@ struct Eng {
       }
       live_from_children += __popcll(__ballot(keep));
     }
-    const int segEnt = wsum(nent);
+    const int segEnt = csum8(nent);
     const int total = segEnt + live_from_children;
     uint32_t cap = (uint32_t)total;
     cap = cap < 8 ? 8 : cap + cap / 2 + 4;
     const uint32_t no = list_alloc(cap);
     if (err) return;
-    const int sincl = wscan_incl(nent);
+    const int sincl = cscan8(nent);
     int w = sincl - nent;
     if (lane < count && (cid & MTB_LEAF)) {
       WEnt e;
@@ -452,7 +460,7 @@ struct Eng {
         keep = e.seq > minSeq;
       }
       const unsigned long long m = __ballot(keep);
-      const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+      const uint32_t rank = rank_below(m);
       if (keep) lst[no + wpos + rank] = e;
       wpos += __popcll(m);
     }
@@ -594,7 +602,7 @@ struct Eng {
       int clen, cseq;
       const int count = child_info(b, d, R, C, cid, clen, cseq);
       const int def = (lane < count && clen > 0) ? clen : 0;
-      const int incl = wscan_incl(def);
+      const int incl = cscan8(def);
       const int pj = p - (incl - def);
       const bool isBlk = lane < count && !(cid & MTB_LEAF);
       const bool tie = isBlk || (insertMode && pj == 0 && S > cseq);
@@ -602,8 +610,8 @@ struct Eng {
       const unsigned long long m = __ballot(qual);
       if (m) {
         const int j = first_set(m);
-        const uint32_t cj = __shfl(cid, j, 64);
-        const int pjj = __shfl(pj, j, 64);
+        const uint32_t cj = rlu(cid, j);
+        const int pjj = rl(pj, j);
         if (!(cj & MTB_LEAF)) {
           b = cj;
           p = pjj;
@@ -624,7 +632,7 @@ struct Eng {
           return true;
         }
       } else {
-        const int total = __shfl(incl, 63, 64);
+        const int total = rl(incl, 7);
         if (p - total == 0) walk_depth = d;
         if (p - total != 0 || !insertMode) return !insertMode;
         insert_child(b, count, cand | MTB_LEAF, d);
@@ -954,11 +962,11 @@ struct Eng {
     int target = -1;          // per lane: lane it was appended into (-1 kept / dropped)
     int newLen = 0;           // per lane: final length if it is an append target
     for (int k = 0; k < count; k++) {
-      const int kk = __shfl(kind, k, 64);
-      const int klen = __shfl(s.len, k, 64);
-      const uint32_t ktext = __shfl(s.text, k, 64);
-      const uint32_t kprops = __shfl(s.props, k, 64);
-      const uint16_t klast = (uint16_t)__shfl((int)last, k, 64);
+      const int kk = rl(kind, k);
+      const int klen = rl(s.len, k);
+      const uint32_t ktext = rlu(s.text, k);
+      const uint32_t kprops = rlu(s.props, k);
+      const uint16_t klast = (uint16_t)rl((int)last, k);
       if (kk == 1) {
         prev = -1;
         continue;
@@ -994,9 +1002,9 @@ struct Eng {
       tm &= tm - 1;
       // members of the run: t and every lane whose target is t, in order
       const unsigned long long run = __ballot(lane == t || target == t);
-      const uint32_t ttext = __shfl(s.text, t, 64);
-      const int tlen = __shfl(s.len, t, 64);
-      const int total = __shfl(newLen, t, 64);
+      const uint32_t ttext = rlu(s.text, t);
+      const int tlen = rl(s.len, t);
+      const int total = rl(newLen, t);
       // contiguous in the arena already?
       bool contiguous = true;
       {
@@ -1005,8 +1013,8 @@ struct Eng {
         while (r) {
           const int q = first_set(r);
           r &= r - 1;
-          const uint32_t qt = __shfl(s.text, q, 64);
-          const int ql = __shfl(s.len, q, 64);
+          const uint32_t qt = rlu(s.text, q);
+          const int ql = rl(s.len, q);
           if (qt != expect) contiguous = false;
           expect = qt + (uint32_t)ql;
         }
@@ -1028,8 +1036,8 @@ struct Eng {
         while (r) {
           const int q = first_set(r);
           r &= r - 1;
-          const uint32_t qt = __shfl(s.text, q, 64);
-          const int ql = __shfl(s.len, q, 64);
+          const uint32_t qt = rlu(s.text, q);
+          const int ql = rl(s.len, q);
           copy_text(w, qt, (uint32_t)ql);
           w += (uint32_t)ql;
         }
@@ -1045,7 +1053,7 @@ struct Eng {
     const bool keep = lane < count && kind != 1 && target < 0;
     if (lane < count && !keep) seg[c & ~MTB_LEAF].parent = MTB_NONE;
     const unsigned long long km = __ballot(keep);
-    if (keep) sh->hold[nh + __popcll(km & ((1ull << lane) - 1))] = c;
+    if (keep) sh->hold[nh + rank_below(km)] = c;
     wsync();
     return nh + __popcll(km);
   }

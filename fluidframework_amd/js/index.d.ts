@@ -1,0 +1,52 @@
+// Type declarations for @fluid-mi355x/merge-tree-batch (see index.js).
+export interface ReplayStats {
+  opsApplied: number;
+  docs: number;
+  segmentsFinal: number;
+  textUnitsFinal: number;
+  bytesAlg: number;
+  errors: number;
+  kernelMs: number;
+  checksum: string;
+}
+export interface BatchOptions {
+  mergeTreeUseNewLengthCalculations?: boolean;
+  mergeTreeSnapshotChunkSize?: number;
+  device?: number;
+}
+export interface ISequencedDocumentMessage {
+  clientId: string | null;
+  sequenceNumber: number;
+  referenceSequenceNumber: number;
+  minimumSequenceNumber: number;
+  type: string;
+  contents: unknown;
+}
+export declare class MergeTreeBatch {
+  constructor(ndocs: number, options?: BatchOptions);
+  readonly ndocs: number;
+  lastStats: ReplayStats | undefined;
+  client(i: number): Client;
+  flush(): ReplayStats;
+  flushAsync(): Promise<ReplayStats>;
+  internProps(props: object | string): number;
+  appendOps(doc: number, records: Uint8Array, payload: Uint16Array): void;
+  addClient(doc: number, longId: string): void;
+  dumpSegments(doc: number): string;
+  checksum(doc: number): string;
+  summarizeV1(doc: number, msn?: number, seq?: number): { blobs: [string, string][]; summary: unknown };
+  rewind(): void;
+  replayResident(): ReplayStats;
+}
+export declare class Client {
+  insertTextLocal(pos: number, text: string): void;
+  startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
+  applyMsg(msg: ISequencedDocumentMessage | string, local?: boolean): void;
+  getText(start?: number, end?: number): string;
+  getLength(): number;
+  getCurrentSeq(): number;
+  getCollabWindow(): { clientId: number; collaborating: boolean; minSeq: number; currentSeq: number };
+  getLongClientId(shortClientId: number): string;
+  summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }): unknown;
+}
+export declare const TestClient: typeof Client;

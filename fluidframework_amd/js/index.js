@@ -1,0 +1,199 @@
+"use strict";
+/*
+ * @fluid-mi355x/merge-tree-batch — drop-in for the observer (remote-op) path of the reference
+ * merge-tree `Client` (packages/dds/merge-tree/src/client.ts:98) and its test harness `TestClient`
+ * (packages/dds/merge-tree/src/test/testClient.ts:54), backed by the MI355X replay engine.
+ *
+ * Each Client is one document slot of a MergeTreeBatch.  applyMsg(msg) validates and packs the
+ * ISequencedDocumentMessage (no GPU work); flush() -- or any read (getText, getLength, summarize,
+ * getCurrentSeq) -- replays every pending op of every document of the batch in one GPU launch.
+ * Per-op "delta"/"maintenance" events are not emitted in batched mode.  Local edits are accepted
+ * only before startOrUpdateCollaboration (detached initial content, client.replay.spec.ts:27).
+ *
+ * Errors keep the reference's messages: a failed insert throws an Error named "UsageError" with
+ * message "MergeTree insert failed" (mergeTree.ts:1671); out-of-order sequence numbers throw with
+ * the reference assert code ("0x038 ...", client.ts:880).  There is no CPU fallback: without a GPU,
+ * flush() throws with code -2 (MTB_E_NODEV).
+ */
+const path = require("path");
+
+const native = require(path.join(__dirname, "mtb_napi.node"));
+
+const ERR_UNSUPPORTED = -6;
+
+function unsupported(what) {
+  const e = new Error(`unsupported: ${what}`);
+  e.code = ERR_UNSUPPORTED;
+  e.name = "MergeTreeBatchError";
+  return e;
+}
+
+class MergeTreeBatch {
+  /**
+   * @param {number} ndocs documents in the batch
+   * @param {object} [options] IMergeTreeOptions subset: mergeTreeUseNewLengthCalculations
+   *   (mergeTree.ts:413), mergeTreeSnapshotChunkSize (snapshotV1.ts:37); plus `device` (GPU index)
+   */
+  constructor(ndocs, options = {}) {
+    this.ndocs = ndocs;
+    this.handle = native.create(ndocs, options.mergeTreeUseNewLengthCalculations ? 1 : 0,
+      options.mergeTreeSnapshotChunkSize || 0, options.device || 0);
+    this.dirty = false;
+    this.busy = false;
+    this.lastStats = undefined;
+    this.clients = [];
+    for (let i = 0; i < ndocs; i++) this.clients.push(new Client(this, i));
+  }
+
+  client(i) { return this.clients[i]; }
+
+  checkIdle() {
+    if (this.busy) throw new Error("MergeTreeBatch: an asynchronous flush is in progress");
+  }
+
+  /** Replay every pending op of every document (blocking).  Returns the replay statistics. */
+  flush() {
+    this.checkIdle();
+    this.lastStats = native.replay(this.handle);
+    this.dirty = false;
+    return this.lastStats;
+  }
+
+  /** flush() on the libuv thread pool; the batch must not be touched until the promise settles. */
+  flushAsync() {
+    this.checkIdle();
+    this.busy = true;
+    return native.replayAsync(this.handle).then((st) => {
+      this.busy = false;
+      this.dirty = false;
+      this.lastStats = st;
+      return st;
+    }, (e) => {
+      this.busy = false;
+      throw e;
+    });
+  }
+
+  ensureFlushed() {
+    this.checkIdle();
+    if (this.dirty) this.flush();
+  }
+
+  internProps(props) {
+    return native.internProps(this.handle, typeof props === "string" ? props : JSON.stringify(props));
+  }
+
+  /** Pre-packed records (32-byte mtb_op each, include/mtb.h) and their UTF-16 payload. */
+  appendOps(doc, records, payload) {
+    this.checkIdle();
+    native.appendOps(this.handle, doc, records, payload);
+    this.dirty = true;
+  }
+
+  addClient(doc, longId) { native.addClient(this.handle, doc, longId); }
+
+  /** Canonical segment dump (parity read-out; one JSON line per segment). */
+  dumpSegments(doc) {
+    this.ensureFlushed();
+    return native.dumpSegments(this.handle, doc);
+  }
+
+  checksum(doc) {
+    this.ensureFlushed();
+    return native.checksum(this.handle, doc);
+  }
+
+  /** SnapshotV1 blobs [[path, content], ...] and the ISummaryTreeWithStats object. */
+  summarizeV1(doc, msn = -1, seq = -1) {
+    this.ensureFlushed();
+    const r = native.summarizeV1(this.handle, doc, msn, seq);
+    return { blobs: r.blobs, summary: JSON.parse(r.summary) };
+  }
+
+  /** Benchmark utilities: restore every document to its pre-replay state / replay resident records. */
+  rewind() { native.rewind(this.handle); }
+
+  replayResident() { return native.replayResident(this.handle); }
+}
+
+/** One document slot with the reference Client / TestClient call shapes (observer path). */
+class Client {
+  constructor(batch, doc) {
+    this.batch = batch;
+    this.doc = doc;
+    this.initial = "";
+    this.longClientId = undefined;
+  }
+
+  // ---- detached content (before collaboration) ------------------------------------------------
+  /** TestClient.insertTextLocal (testClient.ts:195) before startOrUpdateCollaboration. */
+  insertTextLocal(pos, text) {
+    if (this.longClientId !== undefined) throw unsupported("local ops while collaborating (observer engine)");
+    this.initial = this.initial.slice(0, pos) + text + this.initial.slice(pos);
+  }
+
+  /** Client.startOrUpdateCollaboration (client.ts:1133). */
+  startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
+    if (this.longClientId !== undefined) throw unsupported("re-keying the observer id");
+    native.docInit(this.batch.handle, this.doc, this.initial, longClientId, minSeq, currentSeq);
+    this.longClientId = longClientId;
+  }
+
+  // ---- op application ---------------------------------------------------------------------------
+  /** Client.applyMsg (client.ts:858): `msg` is an ISequencedDocumentMessage (object or JSON text). */
+  applyMsg(msg, local = false) {
+    if (local) throw unsupported("local (ack) application on the observer engine");
+    this.batch.checkIdle();
+    native.applyMsg(this.batch.handle, this.doc, typeof msg === "string" ? msg : JSON.stringify(msg));
+    this.batch.dirty = true;
+  }
+
+  /** Client.updateSeqNumbers is folded into applyMsg (client.ts:874); summarize takes (msn, seq). */
+
+  // ---- reads (flush first) ----------------------------------------------------------------------
+  /** TestClient.getText (testClient.ts:185). */
+  getText(start, end) {
+    this.batch.ensureFlushed();
+    const t = native.getText(this.batch.handle, this.doc);
+    return start === undefined && end === undefined ? t : t.substring(start || 0, end === undefined ? t.length : end);
+  }
+
+  /** Client.getLength (client.ts:1129). */
+  getLength() {
+    this.batch.ensureFlushed();
+    return native.getLength(this.batch.handle, this.doc);
+  }
+
+  /** Client.getCurrentSeq (client.ts:1122). */
+  getCurrentSeq() {
+    this.batch.ensureFlushed();
+    return native.getSeq(this.batch.handle, this.doc)[0];
+  }
+
+  /** Client.getCollabWindow (client.ts:348), observer view. */
+  getCollabWindow() {
+    this.batch.ensureFlushed();
+    const [currentSeq, minSeq] = native.getSeq(this.batch.handle, this.doc);
+    return { clientId: 0, collaborating: true, minSeq, currentSeq };
+  }
+
+  /** Client.getLongClientId (client.ts:682). */
+  getLongClientId(shortClientId) { return native.clientLongId(this.batch.handle, this.doc, shortClientId); }
+
+  /**
+   * Client.summarize (client.ts:966) with newMergeTreeSnapshotFormat: the SnapshotV1 summary tree.
+   * `runtime.deltaManager.{minimumSequenceNumber,lastSequenceNumber}` (client.ts:979) are passed
+   * through when given.
+   */
+  summarize(runtime) {
+    const dm = runtime && runtime.deltaManager;
+    const msn = dm && dm.minimumSequenceNumber !== undefined ? dm.minimumSequenceNumber : -1;
+    const seq = dm && dm.lastSequenceNumber !== undefined ? dm.lastSequenceNumber : -1;
+    return this.batch.summarizeV1(this.doc, msn, seq).summary;
+  }
+}
+
+/** TestClient alias: the same observer slot plus getText (testClient.ts:54). */
+const TestClient = Client;
+
+module.exports = { MergeTreeBatch, Client, TestClient, native };

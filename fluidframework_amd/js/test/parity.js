@@ -1,0 +1,95 @@
+"use strict";
+/*
+ * Parity test of the JS drop-in package, written like the reference's client.replay.spec.ts:16-72:
+ * every committed conflict-farm replay log (tests/golden/replay, from
+ * packages/dds/merge-tree/src/test/results) is applied message by message through
+ * Client.applyMsg on an observer that started from `initialText`, and getText() must equal the
+ * log's resultText after every group.  All 30 logs are documents of one batch (one GPU launch per
+ * group).
+ *
+ *   node test/parity.js          GPU run (expects an MI355X)
+ *   node test/parity.js --cpu    no GPU: package/addon load, message packing, loud NODEV failure
+ */
+const assert = require("assert");
+const fs = require("fs");
+const path = require("path");
+const zlib = require("zlib");
+
+const { MergeTreeBatch, native } = require("..");
+
+const GOLDEN = path.join(__dirname, "..", "..", "..", "tests", "golden", "replay");
+
+function loadFixtures() {
+  return fs.readdirSync(GOLDEN).filter((f) => f.endsWith(".json.gz")).sort().map((f) => ({
+    name: f.replace(".json.gz", ""),
+    log: JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(GOLDEN, f))).toString("utf8")),
+  }));
+}
+
+function toMsg(m) {
+  const [clientId, sequenceNumber, referenceSequenceNumber, minimumSequenceNumber, contents] = m;
+  return { clientId, sequenceNumber, referenceSequenceNumber, minimumSequenceNumber, type: "op", contents };
+}
+
+function cpuChecks() {
+  const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
+    "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
+    "clientLongId"];
+  for (const n of names) assert.strictEqual(typeof native[n], "function", n);
+  const fx = loadFixtures();
+  assert.strictEqual(fx.length, 30);
+  const batch = new MergeTreeBatch(fx.length);
+  fx.forEach(({ log }, i) => {
+    const c = batch.client(i);
+    c.insertTextLocal(0, log.initialText);
+    c.startOrUpdateCollaboration("A");
+    for (const g of log.groups) for (const m of g.msgs) c.applyMsg(toMsg(m));
+  });
+  // reference error text survives the boundary (client.ts:880 assert 0x038)
+  const b2 = new MergeTreeBatch(1);
+  b2.client(0).startOrUpdateCollaboration("A");
+  b2.client(0).applyMsg(toMsg(["B", 5, 0, 0, { type: 0, pos1: 0, seg: "x" }]));
+  assert.throws(() => b2.client(0).applyMsg(toMsg(["B", 4, 0, 0, { type: 0, pos1: 0, seg: "y" }])), /0x038/);
+  // no CPU fallback
+  assert.throws(() => batch.flush(), (e) => e.code === -2);
+  console.log("js cpu checks ok: 30 logs packed, flush fails with MTB_E_NODEV");
+}
+
+async function gpuChecks() {
+  const fx = loadFixtures();
+  const batch = new MergeTreeBatch(fx.length);
+  fx.forEach(({ log }, i) => {
+    const c = batch.client(i);
+    c.insertTextLocal(0, log.initialText);
+    c.startOrUpdateCollaboration("A");
+  });
+  const ngroups = fx[0].log.groups.length;
+  let checked = 0;
+  const bad = [];
+  for (let g = 0; g < ngroups; g++) {
+    fx.forEach(({ log }, i) => { for (const m of log.groups[g].msgs) batch.client(i).applyMsg(toMsg(m)); });
+    if (g % 2) await batch.flushAsync(); else batch.flush();
+    fx.forEach(({ name, log }, i) => {
+      checked++;
+      if (batch.client(i).getText() !== log.groups[g].resultText) bad.push(`${name}#${g}`);
+    });
+  }
+  assert.deepStrictEqual(bad, [], `mismatching checkpoints: ${bad.slice(0, 5)}`);
+  // summary read-out and collab window through the drop-in surface
+  const c0 = batch.client(0);
+  const s = c0.summarize();
+  assert.strictEqual(s.summary.type, 1);
+  assert.ok(s.summary.tree.header);
+  assert.strictEqual(c0.getLength(), c0.getText().length);
+  assert.strictEqual(c0.getCurrentSeq(), fx[0].log.groups[ngroups - 1].msgs.slice(-1)[0][1]);
+  console.log(`js gpu parity ok: ${checked} text checkpoints over ${fx.length} reference logs`);
+}
+
+if (process.argv.includes("--cpu")) {
+  cpuChecks();
+} else {
+  gpuChecks().catch((e) => {
+    console.error(e);
+    process.exit(1);
+  });
+}

@@ -1,0 +1,40 @@
+"""The JS drop-in package (fluidframework_amd/js: index.js over the N-API addon mtb_napi.node).
+
+CPU: the addon loads, exposes one function per C-ABI entry point, packs all 30 reference replay logs
+through Client.applyMsg, keeps the reference's assert text (0x038) and fails loudly without a GPU.
+GPU: node replays the 30 reference logs (client.replay.spec.ts style) and checks the text after every
+group, through both flush() and the thread-pool flushAsync().
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JS = os.path.join(ROOT, "fluidframework_amd", "js")
+ADDON = os.path.join(JS, "mtb_napi.node")
+
+needs_node = pytest.mark.skipif(shutil.which("node") is None or not os.path.exists(ADDON),
+                                reason="node or the built addon is not available")
+
+
+def _node(*args, timeout=240):
+    r = subprocess.run(["node", os.path.join(JS, "test", "parity.js"), *args], capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@needs_node
+def test_js_package_cpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present (the CPU check expects MTB_E_NODEV)")
+    assert "js cpu checks ok" in _node("--cpu")
+
+
+@needs_node
+@pytest.mark.gpu
+def test_js_package_replays_reference_logs_on_gpu():
+    assert "js gpu parity ok" in _node()
