@@ -2,9 +2,11 @@
 //
 // Every document owns disjoint slices of a few batch-wide pools in HBM (structure of arrays per
 // node type, array of structures per node so one wave-instruction fetches a whole record):
-//   segs   : Seg  (32 B)  leaf segments           (reference: BaseSegment, mergeTreeNodes.ts:367)
-//   blks   : Blk  (64 B)  internal blocks          (reference: MergeBlock, mergeTreeNodes.ts:332)
-//   lists  : WEnt (16 B)  per-block window lists   (replaces PartialSequenceLengths, partialLengths.ts:239)
+//   segs   : u32          parent block of each segment (the LRU heap refers to segments)
+//   blks   : FBlk (320 B) tree nodes with their children's hot fields inline
+//                         (reference: MergeBlock mergeTreeNodes.ts:332 + BaseSegment :367)
+//   lists  : WEnt (16 B)  per-block slot-tagged window lists (replace PartialSequenceLengths,
+//                         partialLengths.ts:239)
 //   text   : u16          per-document UTF-16 text arena (insert payloads + zamboni appends)
 //   heap   : Lru  (8 B)   zamboni LRU heap         (reference: Heap<LRUSegment>, collections/heap.ts)
 //   aux    : u32          property sets and overlapping-remove client lists
@@ -21,7 +23,39 @@
 #define MTB_MARKER 0x80000000u  // Seg.text flag: marker, low bits = refType + 1 (0 = undefined)
 #define MTB_GPROPS 0x80000000u  // props handle flag: batch-global table (else per-doc aux arena)
 
-struct Seg {          // 32 bytes
+// ---- device records -------------------------------------------------------------------------
+// A tree node ("fat block", 320 B).  Besides its children's ids it holds the hot fields of every
+// child, so one coalesced 320-byte fetch gives everything a walk needs at that level:
+//   segment child : raw length, seq, removedSeq, client | rc0 << 16, overlap-remover list, props, text
+//   block child   : the child's cachedLength (observer view) and the child's window-list metadata
+// A block's window list holds the remote-length corrections of its BLOCK children, each entry tagged
+// with the child's slot, so a block whose children are segments has no list at all; the list metadata
+// of a block lives in its parent's slot (the root's in its own header), which lets a walk issue the
+// fetch of a block and of its list together.
+#define F_ID 0
+#define F_LEN 1     // segment: cachedLength (UTF-16 units, markers 1) | block: cachedLength (observer)
+#define F_SEQ 2     // segment: seq                                     | block: list offset
+#define F_RSEQ 3    // segment: removedSeq (-1 = not removed)           | block: list count
+#define F_CLI 4     // segment: client & 0xFFFF | removedClientIds[0] << 16 | block: list capacity
+#define F_RCX 5     // segment: aux offset of [n, c1..cn] overlapping removers | block: seq of the last entry
+#define F_PROPS 6   // segment: property-set handle (0 = none)         | block: key of the last entry
+#define F_TEXT 7    // segment: text arena offset or MTB_MARKER | (refType + 1) | block: 0
+struct FBlk {
+  uint32_t f[8][MTB_MAXCH];  // [field][slot]
+  uint32_t count;            // childCount
+  uint32_t parent;           // MTB_NONE for the root
+  uint32_t index;            // index in parent
+  int32_t scour;             // needsScour: -1 undefined, 0 false, 1 true
+  int32_t len;               // cachedLength (observer view, mergeTree.ts:2392 blockUpdate)
+  uint32_t loff, lcnt, lcap; // root only: its window-list metadata
+  int32_t lseq, lck;
+  uint32_t pad[6];
+};
+static_assert(sizeof(FBlk) == 320, "FBlk is fetched as 80 dwords");
+#define FB_HDR 64            // dword index of `count`
+
+// ---- host-side views (read-out; rebuilt from the device records by download_doc) ---------------
+struct Seg {          // reference: BaseSegment (mergeTreeNodes.ts:367)
   int32_t len;        // cachedLength (UTF-16 units; markers 1)
   int32_t seq;        // insert seq (0 = universal)
   int32_t rseq;       // removedSeq, -1 = not removed
@@ -33,31 +67,27 @@ struct Seg {          // 32 bytes
   int16_t rc0;        // first remover (removedClientIds[0])
 };
 
-struct Blk {          // 64 bytes
+struct Blk {          // reference: MergeBlock (mergeTreeNodes.ts:332)
   uint32_t child[MTB_MAXCH];  // MTB_LEAF | seg id, or block id
   uint32_t parent;
-  int32_t len;        // cachedLength: observer-view length (mergeTree.ts:2392 blockUpdate)
-  uint32_t loff;      // window list: offset / count / capacity in the doc's list slice
-  uint32_t lcnt;
-  uint32_t lcap;
-  uint8_t count;      // childCount
-  uint8_t index;      // index in parent
-  int8_t scour;       // needsScour: -1 undefined, 0 false, 1 true
-  uint8_t pad0;
-  int32_t lseq;       // key (seq, ck) of the list's last entry, so appends can merge without a
-  int32_t lck;        //   dependent load of the entry (lseq = INT32_MIN: unknown, never merge)
+  int32_t len;
+  uint8_t count;
+  uint8_t index;
+  int8_t scour;
 };
 
-// Window-list entry.  For a query (R, C):  length(block) = len - sum(w(e) for e.seq > R), where
-// w = delta if (kind == MAIN && client != C) or (kind == OVERLAP && client == C), else 0.
+// Window-list entry of block B, for B's child in slot `slot`.  For a query (R, C):
+//   length(child) = child cachedLength - sum(w(e) for e in B's list, e.slot == slot, e.seq > R)
+// with w = delta if (kind == MAIN && client != C) or (kind == OVERLAP && client == C), else 0.
 struct WEnt {
   int32_t seq;
-  int32_t ck;         // client | (kind << 16)
+  int32_t ck;         // client & 0xFFFF | kind << 16 | slot << 20
   int32_t delta;
   int32_t pad;
 };
 #define WK_MAIN 0
 #define WK_OVERLAP 1
+#define WE_KEY(client, kind, slot) (((client) & 0xFFFF) | ((kind) << 16) | ((slot) << 20))
 
 struct Lru {
   uint32_t seg;
@@ -82,8 +112,11 @@ struct DocState {     // 256 bytes
   uint64_t ops_applied;
   uint64_t n_mod;       // segment records created or modified (SURVEY 8(d) n_mod)
   uint64_t text_bytes;  // UTF-16 payload bytes of applied inserts
-  uint32_t pad[10];
+  uint64_t prof[7];     // MTB_PROFILE builds: s_memtime cycles per replay phase (see mtb_replay.hip)
+  uint32_t flags;       // DSF_* (host-computed document properties)
+  uint32_t cnt[5];      // MTB_PROFILE builds: event counters
 };
+static_assert(sizeof(DocState) == 256, "DocState is copied as 64 dwords (mtb_rewind_kernel)");
 
 // Batch-global interned tables (read-only on the device).
 struct Tables {
@@ -106,3 +139,6 @@ struct Tables {
 #define DERR_ASSERT_SEQ 8  // 0x038
 #define DERR_ASSERT_MSN 9  // 0x039 / 0x04e / 0x04f
 #define DERR_DEPTH 10
+#define DERR_SHAPE 11      // a block mixing segment and block children (never produced by the reference)
+
+#define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -28,10 +30,11 @@ hipError_t mtb_launch_move_words(hipStream_t stream, const uint32_t* src, const 
                                  const uint64_t* dst_off, const uint32_t* len, uint32_t n);
 hipError_t mtb_launch_move_u16(hipStream_t stream, const uint16_t* src, const uint64_t* src_off, uint16_t* dst,
                                const uint64_t* dst_off, const uint32_t* len, uint32_t n);
-hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, Seg* segs,
-                             const Seg* pseg, Blk* blks, const Blk* pblk);
-hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
-                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables);
+hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, uint32_t* segp,
+                             const uint32_t* psegp, FBlk* blks, const FBlk* pblk);
+hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                             FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                             Tables tables);
 
 namespace {
 
@@ -238,8 +241,8 @@ struct mtb_batch {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevBuf<DocState> dDocs;
   DevBuf<mtb_op> dOps;
-  DevBuf<Seg> dSegs;
-  DevBuf<Blk> dBlks;
+  DevBuf<uint32_t> dSegs;  // parent block of each segment
+  DevBuf<FBlk> dBlks;
   DevBuf<WEnt> dLists;
   DevBuf<uint16_t> dText;
   DevBuf<Lru> dHeap;
@@ -252,8 +255,8 @@ struct mtb_batch {
   bool haveRewind = false;
   std::vector<DocState> hPristine;
   DevBuf<DocState> dPristine;
-  DevBuf<Seg> dPSeg;
-  DevBuf<Blk> dPBlk;
+  DevBuf<uint32_t> dPSeg;
+  DevBuf<FBlk> dPBlk;
   // batched moves: chunk tables and host->device staging
   DevBuf<uint64_t> dMvSrc, dMvDst;
   DevBuf<uint32_t> dMvLen, dStageW;
@@ -444,13 +447,16 @@ struct Caps {
   uint32_t seg, blk, list, text, heap, aux;
 };
 Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
+  // Measured maxima: bench documents (10k records) 15.7k segments, 738 blocks, 3.8k list entries,
+  // 10.2k aux words; reference replay logs (2k records) 11.8k list entries, 21k aux words.  Segments can
+  // never exceed 2 per record (+ the initial one); the other slices keep several-fold headroom.
   Caps c;
   c.seg = (uint32_t)(2 * n + 64);
-  c.blk = (uint32_t)(n + 64);
-  c.list = (uint32_t)(40 * n + 4096);
+  c.blk = (uint32_t)(n / 2 + 256);
+  c.list = (uint32_t)(8 * n + 8192);
   c.text = (uint32_t)(5 * (payload + init) + 4096);
-  c.heap = (uint32_t)(3 * n + 64);
-  c.aux = (uint32_t)(24 * n + 1024);
+  c.heap = (uint32_t)(n + 256);
+  c.aux = (uint32_t)(16 * n + 4096);
   return c;
 }
 bool fits(const DocState& s, const Caps& c) {
@@ -512,7 +518,7 @@ void layout(mtb_batch* b, const std::vector<Caps>& want) {
   move(b->dLists, lst, [](const DocState& s) { return s.list_base; }, [](const DocState& s) { return (uint64_t)s.list_used; });
   move_text(txt);
   move(b->dHeap, hp, [](const DocState& s) { return s.heap_base; }, [](const DocState& s) { return (uint64_t)s.heap_cnt + 1; });
-  move(b->dAux, ax, [](const DocState& s) { return s.aux_base; }, [](const DocState& s) { return (uint64_t)s.aux_used; });
+  move(b->dAux, ax + 8, [](const DocState& s) { return s.aux_base; }, [](const DocState& s) { return (uint64_t)s.aux_used; });
   move(b->dFree, blk, [](const DocState& s) { return s.free_base; }, [](const DocState& s) { return (uint64_t)s.free_top; });
   b->hst = ns;
 }
@@ -541,34 +547,31 @@ void device_init(mtb_batch* b) {
     s.aux_used = 1;
     s.heap_cnt = 0;
     s.list_used = 0;
-    Blk root{};
-    for (int k = 0; k < MTB_MAXCH; k++) root.child[k] = MTB_NONE;
+    FBlk root{};
+    for (int k = 0; k < MTB_MAXCH; k++) root.f[F_ID][k] = MTB_NONE;
     root.parent = MTB_NONE;
     root.scour = -1;
     root.lseq = (int32_t)0x80000000;
     if (!d.initText.empty()) {
-      Seg sg{};
-      sg.len = (int32_t)d.initText.size();
-      sg.seq = 0;
-      sg.rseq = -1;
-      sg.text = 0;
-      sg.parent = 0;
-      sg.client = -1;  // LocalClientId: inserted before collaboration (client.replay.spec.ts:27)
-      sg.rc0 = -1;
-      root.child[0] = MTB_LEAF | 0;
+      // the detached initial text: one segment, LocalClientId, seq 0 (client.replay.spec.ts:27)
+      root.f[F_ID][0] = MTB_LEAF | 0;
+      root.f[F_LEN][0] = (uint32_t)d.initText.size();
+      root.f[F_SEQ][0] = 0;
+      root.f[F_RSEQ][0] = (uint32_t)-1;
+      root.f[F_CLI][0] = 0xFFFFu | 0xFFFF0000u;  // client -1, no remover
+      root.f[F_TEXT][0] = 0;
       root.count = 1;
-      root.len = sg.len;
+      root.len = (int32_t)d.initText.size();
       s.seg_used = 1;
-      segc.add(recs.size(), s.seg_base * (sizeof(Seg) / 4), sizeof(Seg) / 4);
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(&sg);
-      recs.insert(recs.end(), w, w + sizeof(Seg) / 4);
+      segc.add(recs.size(), s.seg_base, 1);
+      recs.push_back(0);  // parent: root block 0
       txtc.add(texts.size(), s.text_base, d.initText.size());
       texts.insert(texts.end(), d.initText.begin(), d.initText.end());
     }
     s.text_used = (uint32_t)d.initText.size();
-    blkc.add(recs.size(), s.blk_base * (sizeof(Blk) / 4), sizeof(Blk) / 4);
+    blkc.add(recs.size(), s.blk_base * (sizeof(FBlk) / 4), sizeof(FBlk) / 4);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&root);
-    recs.insert(recs.end(), w, w + sizeof(Blk) / 4);
+    recs.insert(recs.end(), w, w + sizeof(FBlk) / 4);
     d.onDevice = true;
   }
   scatter_words(b, recs, b->dSegs.p, segc);
@@ -582,7 +585,7 @@ void upload_tables(mtb_batch* b) {
   Interner& in = b->in;
   if (!in.dirty && b->dPool.p) return;
   auto up = [&](auto& buf, const auto& vec) {
-    buf.ensure(vec.size() + 1);
+    buf.ensure(vec.size() + 8);  // tail padding: the kernel reads property sets 5 words at a time
     if (!vec.empty())
       HIPCHK(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice, b->stream));
   };
@@ -599,15 +602,45 @@ void download_doc(mtb_batch* b, uint32_t i) {
   if (d.cached) return;
   if (!d.onDevice) raise(MTB_E_ARG, "document has not been replayed");
   const DocState& s = b->hst[i];
-  d.segs.resize(s.seg_used);
-  d.blks.resize(s.blk_used);
+  std::vector<FBlk> fb(s.blk_used);
+  std::vector<uint32_t> segp(s.seg_used);
   d.text.resize(s.text_used);
   d.aux.resize(s.aux_used);
-  if (s.seg_used) HIPCHK(hipMemcpyAsync(d.segs.data(), b->dSegs.p + s.seg_base, s.seg_used * sizeof(Seg), hipMemcpyDeviceToHost, b->stream));
-  if (s.blk_used) HIPCHK(hipMemcpyAsync(d.blks.data(), b->dBlks.p + s.blk_base, s.blk_used * sizeof(Blk), hipMemcpyDeviceToHost, b->stream));
+  if (s.seg_used) HIPCHK(hipMemcpyAsync(segp.data(), b->dSegs.p + s.seg_base, s.seg_used * 4, hipMemcpyDeviceToHost, b->stream));
+  if (s.blk_used) HIPCHK(hipMemcpyAsync(fb.data(), b->dBlks.p + s.blk_base, s.blk_used * sizeof(FBlk), hipMemcpyDeviceToHost, b->stream));
   if (s.text_used) HIPCHK(hipMemcpyAsync(d.text.data(), b->dText.p + s.text_base, s.text_used * 2, hipMemcpyDeviceToHost, b->stream));
   if (s.aux_used) HIPCHK(hipMemcpyAsync(d.aux.data(), b->dAux.p + s.aux_base, s.aux_used * 4, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
+  // host views: blocks from the records, segments from their parent's slot (hot fields live inline)
+  d.blks.assign(s.blk_used, Blk{});
+  d.segs.assign(s.seg_used, Seg{});
+  for (uint32_t k = 0; k < s.seg_used; k++) d.segs[k].parent = MTB_NONE;
+  for (uint32_t bi = 0; bi < s.blk_used; bi++) {
+    const FBlk& F = fb[bi];
+    Blk& B = d.blks[bi];
+    B.count = (uint8_t)std::min<uint32_t>(F.count, MTB_MAXCH);
+    B.parent = F.parent;
+    B.len = F.len;
+    B.index = (uint8_t)F.index;
+    B.scour = (int8_t)F.scour;
+    for (int k = 0; k < MTB_MAXCH; k++) B.child[k] = k < B.count ? F.f[F_ID][k] : MTB_NONE;
+    for (int k = 0; k < B.count; k++) {
+      const uint32_t c = F.f[F_ID][k];
+      if (!(c & MTB_LEAF)) continue;
+      const uint32_t sid = c & ~MTB_LEAF;
+      if (sid >= s.seg_used || segp[sid] != bi) continue;  // stale slot of a freed block
+      Seg& g = d.segs[sid];
+      g.len = (int32_t)F.f[F_LEN][k];
+      g.seq = (int32_t)F.f[F_SEQ][k];
+      g.rseq = (int32_t)F.f[F_RSEQ][k];
+      g.props = F.f[F_PROPS][k];
+      g.text = F.f[F_TEXT][k];
+      g.parent = bi;
+      g.rcx = F.f[F_RCX][k];
+      g.client = (int16_t)(F.f[F_CLI][k] & 0xFFFF);
+      g.rc0 = (int16_t)(F.f[F_CLI][k] >> 16);
+    }
+  }
   d.cached = true;
 }
 
@@ -643,8 +676,8 @@ void capture_pristine(mtb_batch* b) {
   Chunks bc, sc;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     const DocState& s = b->hst[i];
-    bc.add(s.blk_base * (sizeof(Blk) / 4), (uint64_t)i * (sizeof(Blk) / 4), sizeof(Blk) / 4);
-    sc.add(s.seg_base * (sizeof(Seg) / 4), (uint64_t)i * (sizeof(Seg) / 4), sizeof(Seg) / 4);
+    bc.add((s.blk_base + s.root) * (sizeof(FBlk) / 4), (uint64_t)i * (sizeof(FBlk) / 4), sizeof(FBlk) / 4);
+    sc.add(s.seg_base, (uint64_t)i, 1);
   }
   move_words(b, b->dBlks.p, b->dPBlk.p, bc);
   move_words(b, b->dSegs.p, b->dPSeg.p, sc);
@@ -691,6 +724,11 @@ void replay(mtb_batch* b, mtb_stats* out) {
     payc.add(pay.size(), s.text_base + base, d.payload.size());
     pay.insert(pay.end(), d.payload.begin(), d.payload.end());
     s.text_used += (uint32_t)d.payload.size();
+    if (!(s.flags & DSF_NEWLINE)) {
+      bool nl = std::find(d.payload.begin(), d.payload.end(), (uint16_t)'\n') != d.payload.end();
+      if (!nl) nl = std::find(d.initText.begin(), d.initText.end(), (uint16_t)'\n') != d.initText.end();
+      if (nl) s.flags |= DSF_NEWLINE;
+    }
     s.op_base = ops.size();
     s.n_ops = (uint32_t)d.pending.size();
     s.op_next = 0;
@@ -736,6 +774,28 @@ void replay(mtb_batch* b, mtb_stats* out) {
       st.errors++;
       if (!firstErr) { firstErr = s.err; errDoc = i; }
     }
+  }
+  if (getenv("MTB_PROFILE_OUT")) {  // MTB_PROFILE builds: per-phase device cycles and events per op, summed over documents
+    double p[7] = {0, 0, 0, 0, 0, 0, 0}, c[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      for (int k = 0; k < 7; k++) p[k] += (double)b->hst[i].prof[k];
+      for (int k = 0; k < 5; k++) c[k] += b->hst[i].cnt[k];
+    }
+    const double n = (double)std::max<uint64_t>(1, st.ops_applied);
+    fprintf(stderr, "mtb_profile cycles/op: boundary %.0f insert %.0f nodemap %.0f zamboni %.0f total %.0f | view %.0f scour %.0f (ops %llu)\n",
+            p[0] / n, p[1] / n, p[2] / n, p[3] / n, p[4] / n, p[5] / n, p[6] / n, (unsigned long long)st.ops_applied);
+    fprintf(stderr, "mtb_profile events/op: scour %.3f pack %.3f rebuild %.3f view %.3f entries %.2f\n", c[0] / n, c[1] / n,
+            c[2] / n, c[3] / n, c[4] / n);
+    uint64_t mx[7] = {0, 0, 0, 0, 0, 0, 0}, mxo = 0;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      const DocState& q = b->hst[i];
+      const uint64_t v[7] = {q.seg_used, q.blk_used, q.list_used, q.text_used, q.heap_cnt, q.aux_used, q.n_ops};
+      for (int k = 0; k < 7; k++) mx[k] = std::max(mx[k], v[k]);
+      mxo = std::max<uint64_t>(mxo, q.ops_applied);
+    }
+    fprintf(stderr, "mtb_profile max usage: seg %llu blk %llu list %llu text %llu heap %llu aux %llu (records %llu, ops %llu)\n",
+            (unsigned long long)mx[0], (unsigned long long)mx[1], (unsigned long long)mx[2], (unsigned long long)mx[3],
+            (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mxo);
   }
   if (out) *out = st;
   if (firstErr)

@@ -3,20 +3,29 @@
 // One 64-lane wavefront owns one document and applies that document's sequenced ops in order,
 // exactly as the reference observer `Client.applyMsg` would (packages/dds/merge-tree/src/client.ts:858).
 // Control flow is wave-uniform (every lane walks the same tree path); the lanes parallelise the
-// per-op inner loops: the <=8 children of a block, the concatenated window lists of those children,
-// scour decisions, list/segment rebuilds and text copies.  No MFMA: nothing here is a contraction.
+// per-op inner loops: the <=8 children of a block, the block's window list, the segments of a
+// leaf-level block touched by a remove / annotate, scour decisions, list rebuilds and text copies.
+// No MFMA: nothing here is a contraction.
 //
-// Differences from the reference data structures (results are identical):
-//  * PartialSequenceLengths (partialLengths.ts:239) is replaced by one flat window list per block.
-//    A block's length in the (refSeq R, client C) perspective is
-//        cachedLength - sum_{e in list, e.seq > R} w(e)
-//    where w(e) = e.delta for MAIN entries of other clients and for OVERLAP entries of C.  This is the
-//    same quantity getPartialLength (partialLengths.ts:698) returns and the sum of the leaf
-//    visibilities (mergeTree.ts:916-1004) - the oracle verifies that identity on every query.
-//  * The recursive insertingWalk (mergeTree.ts:1740) runs iteratively with an explicit path; all walks
-//    of one op share an LDS cache of the children lengths (they use the same (R, C)).
-//  * Length/list bookkeeping is propagated incrementally along the recorded path instead of the
-//    reference's combine/update rebuilds; split/pack blocks rebuild their list from their children.
+// Data structures (mtb_device.h) and how they differ from the reference (results are identical):
+//  * A tree node is one 320-byte record holding its children's hot fields inline (segment: length,
+//    seq, removal info, props, text; block: cachedLength and the child's window-list metadata), so a
+//    walk fetches one record per level and never touches a separate segment record.
+//  * PartialSequenceLengths (partialLengths.ts:239) is replaced by slot-tagged window lists: block B's
+//    list holds, for each of B's block children, the (seq, client, kind, delta) changes below it.  The
+//    length of B's child k in the (refSeq R, client C) perspective is
+//        childLen[k] - sum_{e in list(B), e.slot == k, e.seq > R} w(e)
+//    with w(e) = e.delta for MAIN entries of other clients and for OVERLAP entries of C -- the quantity
+//    getPartialLength (partialLengths.ts:698) returns, equal to the sum of the leaf visibilities
+//    (mergeTree.ts:916-1004); the oracle verifies that identity on every query.  Blocks whose
+//    children are segments need no list: their children's visibility is computed directly.  A block's
+//    list metadata lives in its parent's slot, so a block and its list are fetched together.
+//  * The recursive insertingWalk (mergeTree.ts:1740) and depthFirstNodeWalk (mergeTreeNodeWalk.ts:35)
+//    run iteratively; every block an op visits is cached in LDS per tree depth ("view") together with
+//    its children's lengths in the op's (R, C) perspective, and all walks of one op share the cache.
+//  * Length/list bookkeeping is applied incrementally along the cached path instead of the
+//    reference's combine/update rebuilds; split, root growth and packParent rebuild the lists of the
+//    blocks whose children changed.
 //  * The zamboni LRU heap (collections/heap.ts) lives in LDS while it fits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,8 +35,27 @@
 
 namespace mtbk {
 
-#define MTB_LDS_HEAP 256
+// MTB_PROFILE builds accumulate s_memtime cycles per replay phase and event counts into DocState
+// (diagnostic only; `MTB_PROFILE_OUT=1` prints them per op).
+#ifdef MTB_PROFILE
+#define PROF_T() ((uint64_t)__builtin_amdgcn_s_memtime())
+#define PROF_ADD(i, t0) (prof[i] += PROF_T() - (t0))
+#define PROF_CNT(i, n) ((i) < NCN ? (void)(evc[(i) < NCN ? (i) : 0] += (n)) : (void)0)
+#else
+#define PROF_T() ((uint64_t)0)
+#define PROF_ADD(i, t0) ((void)(t0))
+#define PROF_CNT(i, n) ((void)0)
+#endif
+enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL = 4, PH_VIEW = 5, PH_SCOUR = 6, NPH = 7 };
+enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, NCN = 5, CN_SPLIT = 99, CN_GROW = 99, CN_ZRECORD = 99 };
+
+#define MTB_LDS_HEAP 128
+#define MTB_VDEPTH 12  // depth of the LDS path cache; 4^12 segments per document is far beyond any input
 #define MTB_NOKEY ((int32_t)0x80000000)
+// Window lists are allocated in power-of-two capacities (8 << class) from the document's list slice;
+// released lists go to a per-class free stack whose heads live in the slice's first 16 words.
+#define MTB_LCLASSES 16
+#define MTB_LIST_RESERVED 4  // WEnt entries (16 words) reserved for the heads
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Cross-lane hand-off inside the single wave that owns a document.  A wavefront's vector-memory and
@@ -52,7 +80,6 @@ __device__ __forceinline__ int cscan8(int v) {
 }
 __device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 __device__ __forceinline__ uint32_t rlu(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
-// sum over lanes 0..7
 __device__ __forceinline__ int csum8(int v) { return rl(cscan8(v), 7); }
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
@@ -60,51 +87,95 @@ __device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
 }
 __device__ __forceinline__ int first_set(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
-struct Scratch {  // LDS, one per wave
-  // per-op child-info cache, one slot per tree depth (all walks of one op share (R, C))
-  uint32_t cb[MTB_MAXDEPTH];                 // block cached in the slot (MTB_NONE: empty)
-  int32_t ccount[MTB_MAXDEPTH];
-  int32_t cscour[MTB_MAXDEPTH];
-  uint32_t cid[MTB_MAXDEPTH][MTB_MAXCH];
-  int32_t clen[MTB_MAXDEPTH][MTB_MAXCH];
-  int32_t cseq[MTB_MAXDEPTH][MTB_MAXCH];
-  int32_t corr[MTB_MAXCH];                   // list-scan accumulators
-  // walk / nodeMap stacks
-  uint32_t path[MTB_MAXDEPTH];
-  int32_t pp[MTB_MAXDEPTH];                  // remaining position at each level of the last walk
-  int32_t sidx[MTB_MAXDEPTH];
-  int32_t acc[MTB_MAXDEPTH];
-  // scour / pack / props scratch
-  uint32_t hold[64];
-  uint32_t pk[64];
-  uint32_t pv[64];
-  Lru heap[MTB_LDS_HEAP];                    // LRU heap while it fits (index 0 unused)
+__device__ __forceinline__ int cli_client(uint32_t cli) { return (int)(int16_t)(cli & 0xFFFF); }
+__device__ __forceinline__ int cli_rc0(uint32_t cli) { return (int)(int16_t)(cli >> 16); }
+
+// One block cached per tree depth: its record and its children's lengths in the op's (R, C) view.
+struct View {
+  uint32_t b;       // block id (MTB_NONE: empty)
+  int32_t count;
+  int32_t scour;
+  int32_t len;
+  uint32_t parent;
+  int32_t rlv;      // rl[] valid
+  int32_t pad[2];
+  uint32_t f[8][MTB_MAXCH];
+  int32_t rl[MTB_MAXCH];
 };
+// A block record staged for zamboni / rebuild.
+struct Rec {
+  uint32_t f[8][MTB_MAXCH];
+  int32_t count;
+  uint32_t parent;
+  uint32_t index;
+  int32_t scour;
+};
+
+struct Scratch {  // LDS, one per wave
+  View v[MTB_VDEPTH];
+  uint32_t path[MTB_VDEPTH];   // block at each depth of the current walk
+  int32_t slot[MTB_VDEPTH];    // child slot taken at each depth
+  int32_t pp[MTB_VDEPTH];      // remaining position at each depth of the last walk
+  int32_t sidx[MTB_VDEPTH];    // node_map cursor
+  int32_t acc[MTB_VDEPTH];     // node_map accumulated observer-length delta
+  uint32_t rmeta[4];           // root window-list metadata (loff, lcnt, lcap)
+  uint32_t lfree[MTB_LCLASSES];  // free window lists per capacity class (8 << c entries)
+  int32_t corr[MTB_MAXCH];
+  uint32_t nseg[8];            // staged fields of a child being inserted
+  uint32_t sp[8];              // split_block results: cachedLength and list metadata of both halves
+  int32_t ins[4];              // the segment placed by the last insert walk: block, slot, depth, needsScour
+  uint32_t memo[2];            // per-op annotate memo: old props -> new props
+  Tables tab;                  // batch-wide property tables
+  Lru* gheap;                  // the document's global LRU heap slice
+  uint32_t* gfree;             // free-block stack
+  uint16_t* gtext;             // UTF-16 text arena
+  Rec zr;                      // zamboni / pack / rebuild record
+  Rec pr[MTB_MAXCH];           // scour inputs: the block(s) being scoured (packParent: all siblings)
+  uint32_t hold[8][64];        // scour / pack: kept children, [field][i]
+  uint32_t pk[64];             // props edit scratch
+  uint32_t pv[64];
+  Lru heap[MTB_LDS_HEAP];      // LRU heap while it fits (index 0 unused)
+};
+
+// cold uniform state kept in LDS (frees scalar registers on the hot path)
+#define sp_lenL sh->sp[0]
+#define sp_lenR sh->sp[1]
+#define sp_loffL sh->sp[2]
+#define sp_lcntL sh->sp[3]
+#define sp_lcapL sh->sp[4]
+#define sp_loffR sh->sp[5]
+#define sp_lcntR sh->sp[6]
+#define sp_lcapR sh->sp[7]
+#define ins_blk sh->ins[0]
+#define ins_slot sh->ins[1]
+#define ins_depth sh->ins[2]
+#define ins_scour sh->ins[3]
+#define memo_old sh->memo[0]
+#define memo_new sh->memo[1]
 
 struct Eng {
   DocState* ds;
-  Seg* seg;
-  Blk* blk;
+  uint32_t* segp;  // parent block of each segment
+  FBlk* blk;
   WEnt* lst;
-  uint16_t* txt;
-  Lru* heap;
   uint32_t* aux;
-  uint32_t* fre;
-  const mtb_op* ops;
-  Tables T;
   Scratch* sh;
   int lane;
   // uniform document state (mirrors DocState)
   int minSeq, curSeq;
   uint32_t root;
   bool newMode;
+  bool hasNL;
   uint32_t seg_used, blk_used, free_top, list_used, text_used, heap_cnt, aux_used;
   int err;
-  uint64_t n_mod, ops_applied, text_bytes;
-  uint32_t memo_old, memo_new;  // per-op annotate memo (old props -> new props)
+  uint32_t n_mod, ops_applied, text_bytes;  // this launch's counts (added to DocState at the end)
   bool heap_lds;                // LRU heap lives in LDS (spills to the global slice when it outgrows it)
   int walk_depth;               // depth of the leaf-level block reached by the last walk (-1: none)
   bool struct_changed;          // a block split / root growth happened since the last walk started
+  bool sp_internal;
+  int pending_fix;              // depth of a block that reached MaxNodesInBlock children (-1: none)
+  uint64_t prof[NPH];
+  uint32_t evc[NCN];
 
   // ------------------------------------------------------------------ errors / allocation
   __device__ __forceinline__ void fail(int code) {
@@ -114,32 +185,30 @@ struct Eng {
     if (seg_used >= ds->seg_cap) { fail(DERR_CAP_SEG); return 0; }
     return seg_used++;
   }
+  __device__ __forceinline__ uint32_t* bw(uint32_t b) const { return reinterpret_cast<uint32_t*>(&blk[b]); }
   __device__ __forceinline__ uint32_t alloc_blk() {
     uint32_t b;
     if (free_top > 0) {
       free_top--;
-      b = fre[free_top];
+      b = sh->gfree[free_top];
     } else {
       if (blk_used >= ds->blk_cap) { fail(DERR_CAP_BLK); return 0; }
       b = blk_used++;
     }
-    Blk& B = blk[b];
-    if (lane < MTB_MAXCH) B.child[lane] = MTB_NONE;
-    B.parent = MTB_NONE;
-    B.len = 0;
-    B.loff = 0;
-    B.lcnt = 0;
-    B.lcap = 0;
-    B.count = 0;
-    B.index = 0;
-    B.scour = -1;
-    B.lseq = MTB_NOKEY;
-    B.lck = 0;
+    uint32_t* w = bw(b);
+    w[lane] = lane < MTB_MAXCH ? MTB_NONE : 0u;
+    if (lane < 16) {
+      uint32_t h = 0;
+      if (lane == 1) h = MTB_NONE;             // parent
+      if (lane == 3) h = (uint32_t)-1;         // needsScour: undefined
+      if (lane == 8) h = (uint32_t)MTB_NOKEY;  // lseq
+      w[FB_HDR + lane] = h;
+    }
     wsync();
     return b;
   }
   __device__ __forceinline__ void free_blk(uint32_t b) {
-    fre[free_top] = b;
+    sh->gfree[free_top] = b;
     free_top++;
   }
   __device__ __forceinline__ uint32_t alloc_aux(uint32_t n) {
@@ -148,194 +217,220 @@ struct Eng {
     aux_used += n;
     return o;
   }
-  __device__ __forceinline__ void cache_clear() {
-    if (lane < MTB_MAXDEPTH) sh->cb[lane] = MTB_NONE;
+  __device__ __forceinline__ void view_clear() {
+    if (lane < MTB_VDEPTH) sh->v[lane].b = MTB_NONE;
     wsync();
   }
 
   // ------------------------------------------------------------------ visibility
-  __device__ __forceinline__ bool rc_has(const Seg& s, int C) const {
-    if (s.rc0 == C) return true;
-    if (s.rcx) {
-      uint32_t n = aux[s.rcx];
+  __device__ __forceinline__ bool rc_has(int rc0, uint32_t rcx, int C) const {
+    if (rc0 == C) return true;
+    if (rcx) {
+      const uint32_t n = aux[rcx];
       for (uint32_t i = 0; i < n; i++)
-        if ((int)aux[s.rcx + 1 + i] == C) return true;
+        if ((int)aux[rcx + 1 + i] == C) return true;
     }
     return false;
   }
   // localNetLength (mergeTree.ts:613-634)
-  __device__ __forceinline__ int local_len(const Seg& s) const {
-    if (s.rseq >= 0) {
-      if (!newMode) return s.rseq > minSeq ? 0 : MTB_UNDEF;
+  __device__ __forceinline__ int local_len(int len, int rseq) const {
+    if (rseq >= 0) {
+      if (!newMode) return rseq > minSeq ? 0 : MTB_UNDEF;
       return 0;
     }
-    return s.len;
+    return len;
   }
   // nodeLength for a leaf in a remote perspective (mergeTree.ts:935-1001)
-  __device__ __forceinline__ int seg_vis(const Seg& s, int R, int C) const {
-    const bool removed = s.rseq >= 0;
+  __device__ __forceinline__ int seg_vis(int len, int seq, int rseq, uint32_t cli, uint32_t rcx, int R, int C) const {
+    const bool removed = rseq >= 0;
+    const int client = cli_client(cli);
     if (newMode) {
       if (removed) {
-        if (s.rseq <= minSeq) return MTB_UNDEF;
-        if (s.rseq <= R || rc_has(s, C)) return 0;
+        if (rseq <= minSeq) return MTB_UNDEF;
+        if (rseq <= R || rc_has(cli_rc0(cli), rcx, C)) return 0;
       }
-      return (s.seq <= R || s.client == C) ? s.len : 0;
+      return (seq <= R || client == C) ? len : 0;
     }
-    if (removed && s.rseq <= R) return MTB_UNDEF;
-    if (s.client == C || s.seq <= R) {
-      if (removed) return rc_has(s, C) ? 0 : s.len;
-      return s.len;
+    if (removed && rseq <= R) return MTB_UNDEF;
+    if (client == C || seq <= R) {
+      if (removed) return rc_has(cli_rc0(cli), rcx, C) ? 0 : len;
+      return len;
     }
     if (removed) return MTB_UNDEF;
     return 0;
   }
+  // observer-view length contribution of a child (blockUpdate: cachedLength = sum localNetLength ?? 0)
+  __device__ __forceinline__ int child_olen(uint32_t id, int len, int rseq) const {
+    if (!(id & MTB_LEAF)) return len;
+    const int l = local_len(len, rseq);
+    return l == MTB_UNDEF ? 0 : l;
+  }
 
-  // Children of block b (tree depth d) in the (R, C) perspective: lane j < count receives the child id,
-  // its length (UNDEF allowed) and, for leaves, the segment's seq.  Results are cached in LDS slot d for
-  // the rest of the op.
-  __device__ __forceinline__ int child_info(uint32_t b, int d, int R, int C, uint32_t& cid, int& clen, int& cseq) {
-    if (sh->cb[d] == b) {
-      const int count = sh->ccount[d];
-      cid = lane < count ? sh->cid[d][lane] : MTB_NONE;
-      clen = lane < count ? sh->clen[d][lane] : 0;
-      cseq = lane < count ? sh->cseq[d][lane] : 0;
-      return count;
+  // ------------------------------------------------------------------ views
+  // Window-list metadata of the block at depth d of the current path (root: rmeta).
+  __device__ __forceinline__ void meta_of(int d, uint32_t& loff, uint32_t& lcnt, uint32_t& lcap) const {
+    if (d == 0) {
+      loff = sh->rmeta[0];
+      lcnt = sh->rmeta[1];
+      lcap = sh->rmeta[2];
+    } else {
+      const View& P = sh->v[d - 1];
+      const int k = sh->slot[d - 1];
+      loff = P.f[F_SEQ][k];
+      lcnt = P.f[F_RSEQ][k];
+      lcap = P.f[F_CLI][k];
     }
-    const Blk& B = blk[b];
-    const int count = B.count;
-    const int scour = B.scour;
-    cid = MTB_NONE;
-    clen = 0;
-    cseq = 0;
-    uint32_t loff = 0, lcnt = 0;
-    if (lane < count) {
-      cid = B.child[lane];
-      if (cid & MTB_LEAF) {
-        const Seg s = seg[cid & ~MTB_LEAF];
-        clen = seg_vis(s, R, C);
-        cseq = s.seq;
-      } else {
-        const Blk& cb = blk[cid];
-        clen = cb.len;
-        loff = cb.loff;
-        lcnt = cb.lcnt;
+  }
+  // Fetch block b (depth d of the current path) together with its window list, and compute its
+  // children's lengths in the (R, C) view.  Returns the child count.
+  __device__ __forceinline__ int load_view(int d, uint32_t b, int R, int C) {
+    View& V = sh->v[d];
+    if (V.b == b && V.rlv) return V.count;
+    if (V.b == b) {  // record still valid (e.g. after a segment split): recompute lengths from LDS
+      const int count = V.count;
+      bool segs = true;
+      if (lane < count) segs = (V.f[F_ID][lane] & MTB_LEAF) != 0;
+      if (__ballot(!segs) == 0) {
+        if (lane < count)
+          V.rl[lane] = seg_vis((int)V.f[F_LEN][lane], (int)V.f[F_SEQ][lane], (int)V.f[F_RSEQ][lane], V.f[F_CLI][lane],
+                               V.f[F_RCX][lane], R, C);
+        if (lane == 0) V.rlv = 1;
+        wsync();
+        return count;
       }
     }
-    // concatenated scan of the children's window lists, accumulated per child in LDS
-    const int incl = cscan8((int)lcnt);
-    const int total = rl(incl, 7);
-    if (total > 0) {
-      const int excl = incl - (int)lcnt;
-      if (lane < MTB_MAXCH) sh->corr[lane] = 0;
-      int pre[MTB_MAXCH], off[MTB_MAXCH];
-#pragma unroll
-      for (int k = 0; k < MTB_MAXCH; k++) {
-        pre[k] = rl(excl, k);
-        off[k] = rl((int)loff, k);
-      }
-      wsync();
-      for (int t = lane; t < total; t += 64) {
-        int j = 0;
-#pragma unroll
-        for (int k = 1; k < MTB_MAXCH; k++)
-          if (k < count && pre[k] <= t) j = k;
-        int base = 0;
-#pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++)
-          if (k == j) base = off[k] + (t - pre[k]);
-        const WEnt e = lst[base];
+    PROF_CNT(CN_VIEW, 1);
+    const uint64_t tv0 = PROF_T();
+    uint32_t loff, lcnt, lcap0;
+    meta_of(d, loff, lcnt, lcap0);
+    const uint32_t* src = bw(b);
+    const uint32_t w = src[lane];
+    const uint32_t h = lane < 5 ? src[FB_HDR + lane] : 0u;
+    WEnt e0;
+    e0.seq = MTB_NOKEY;
+    e0.ck = 0;
+    e0.delta = 0;
+    if ((uint32_t)lane < lcnt) e0 = lst[loff + lane];
+    if (lane < MTB_MAXCH) sh->corr[lane] = 0;
+    (&V.f[0][0])[lane] = w;
+    const int count = rl((int)h, 0);
+    const uint32_t hpar = rlu(h, 1);
+    const int hsc = rl((int)h, 3), hlen = rl((int)h, 4);
+    wsync();
+    PROF_CNT(CN_ENTRIES, lcnt);
+    // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength)
+    if ((uint32_t)lane < lcnt && e0.seq > R) {
+      const int c = e0.ck & 0xFFFF, kind = (e0.ck >> 16) & 0xF;
+      if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[(e0.ck >> 20) & 7], e0.delta);
+    }
+    for (uint32_t base = 64; base < lcnt; base += 64) {
+      if (base + lane < lcnt) {
+        const WEnt e = lst[loff + base + lane];
         if (e.seq > R) {
-          const int c = e.ck & 0xFFFF;
-          const int kind = e.ck >> 16;
-          if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[j], e.delta);
+          const int c = e.ck & 0xFFFF, kind = (e.ck >> 16) & 0xF;
+          if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
         }
       }
-      wsync();
-      if (lane < count && !(cid & MTB_LEAF)) clen -= sh->corr[lane];
     }
-    if (lane < count) {
-      sh->cid[d][lane] = cid;
-      sh->clen[d][lane] = clen;
-      sh->cseq[d][lane] = cseq;
-    }
-    sh->ccount[d] = count;
-    sh->cscour[d] = scour;
-    sh->cb[d] = b;
     wsync();
+    if (lane < count) {
+      const uint32_t id = V.f[F_ID][lane];
+      int r;
+      if (id & MTB_LEAF)
+        r = seg_vis((int)V.f[F_LEN][lane], (int)V.f[F_SEQ][lane], (int)V.f[F_RSEQ][lane], V.f[F_CLI][lane], V.f[F_RCX][lane], R, C);
+      else
+        r = (int)V.f[F_LEN][lane] - sh->corr[lane];
+      V.rl[lane] = r;
+    }
+    if (lane == 0) {
+      V.b = b;
+      V.count = count;
+      V.parent = hpar;
+      V.scour = hsc;
+      V.len = hlen;
+      V.rlv = 1;
+    }
+    wsync();
+    PROF_ADD(PH_VIEW, tv0);
     return count;
   }
 
   // ------------------------------------------------------------------ window lists
-  __device__ __forceinline__ uint32_t list_alloc(uint32_t cap) {
-    if (list_used + cap > ds->list_cap) { fail(DERR_CAP_LIST); return 0; }
-    uint32_t o = list_used;
+  __device__ __forceinline__ static uint32_t list_class_cap(uint32_t want) {
+    uint32_t c = 8;
+    while (c < want) c <<= 1;
+    return c;
+  }
+  __device__ __forceinline__ static int list_class(uint32_t cap) { return 28 - __builtin_clz(cap); }  // 8 -> 0
+  // A list with room for `want` entries; `cap` receives its (power-of-two) capacity.
+  __device__ __forceinline__ uint32_t list_alloc(uint32_t want, uint32_t& cap) {
+    cap = list_class_cap(want);
+    const int c = list_class(cap);
+    if (c < MTB_LCLASSES) {
+      const uint32_t head = sh->lfree[c];
+      if (head != MTB_NONE) {
+        const uint32_t next = reinterpret_cast<const uint32_t*>(&lst[head])[0];
+        wsync();
+        if (lane == 0) sh->lfree[c] = next;
+        wsync();
+        return head;
+      }
+    }
+    if (list_used + cap > ds->list_cap) {
+      fail(DERR_CAP_LIST);
+      return 0;
+    }
+    const uint32_t o = list_used;
     list_used += cap;
     return o;
   }
-  // Add `dlen` to the cachedLength of the `n` blocks sh->path[0..n) and append (seq, client, kind,
-  // delta) to their window lists.  One lane per block; blocks whose list is full are re-allocated
-  // afterwards, one at a time.
-  __device__ __forceinline__ void path_update(int n, int dlen, int seqv, int client, int kind, int delta) {
-    const int ck = (client & 0xFFFF) | (kind << 16);
-    bool need = false;
-    if (lane < n) {
-      const uint32_t b = sh->path[lane];
-      Blk& B = blk[b];
-      const uint32_t cnt = B.lcnt, cap = B.lcap, off = B.loff;
-      const int ls = B.lseq, lk = B.lck;
-      if (dlen) B.len = B.len + dlen;
-      if (cnt > 0 && ls == seqv && lk == ck) {
-        lst[off + cnt - 1].delta += delta;  // same (seq, client, kind) as the last entry (GROUP members)
-      } else if (cnt < cap) {
-        WEnt e;
-        e.seq = seqv;
-        e.ck = ck;
-        e.delta = delta;
-        e.pad = 0;
-        lst[off + cnt] = e;
-        B.lcnt = cnt + 1;
-        B.lseq = seqv;
-        B.lck = ck;
-      } else {
-        need = true;
-      }
+  __device__ __forceinline__ void list_free(uint32_t off, uint32_t cap) {
+    if (cap < 8 || (cap & (cap - 1))) return;
+    const int c = list_class(cap);
+    if (c >= MTB_LCLASSES) return;
+    if (lane == 0) {
+      reinterpret_cast<uint32_t*>(&lst[off])[0] = sh->lfree[c];
+      sh->lfree[c] = off;
     }
-    unsigned long long m = __ballot(need);
     wsync();
-    while (m) {
-      const int i = first_set(m);
-      m &= m - 1;
-      const uint32_t b = sh->path[i];
-      list_grow(b, 1);
-      if (err) return;
-      Blk& B = blk[b];
-      WEnt e;
-      e.seq = seqv;
-      e.ck = ck;
-      e.delta = delta;
-      e.pad = 0;
-      const uint32_t cnt = B.lcnt;
-      lst[B.loff + cnt] = e;
-      B.lcnt = cnt + 1;
-      B.lseq = seqv;
-      B.lck = ck;
-      wsync();
+  }
+
+  // Store the window-list metadata of the path block at depth d (its parent's slot, or the root
+  // header).  Called by one lane.
+  __device__ __forceinline__ void set_meta(int d, uint32_t loff, uint32_t lcnt, uint32_t lcap) {
+    if (d == 0) {
+      sh->rmeta[0] = loff;
+      sh->rmeta[1] = lcnt;
+      sh->rmeta[2] = lcap;
+      FBlk& B = blk[sh->path[0]];
+      B.loff = loff;
+      B.lcnt = lcnt;
+      B.lcap = lcap;
+    } else {
+      View& P = sh->v[d - 1];
+      const int k = sh->slot[d - 1];
+      P.f[F_SEQ][k] = loff;
+      P.f[F_RSEQ][k] = lcnt;
+      P.f[F_CLI][k] = lcap;
+      FBlk& B = blk[sh->path[d - 1]];
+      B.f[F_SEQ][k] = loff;
+      B.f[F_RSEQ][k] = lcnt;
+      B.f[F_CLI][k] = lcap;
     }
   }
-  // Re-allocate block b's list with room for `extra` more entries, dropping entries <= minSeq.
-  __device__ __forceinline__ void list_grow(uint32_t b, uint32_t extra) {
-    Blk& B = blk[b];
-    const uint32_t cnt = B.lcnt, off = B.loff;
-    uint32_t live = 0;
+  // Copy `cnt` entries at `off` into a fresh list with room for `extra` more, dropping entries at or
+  // below minSeq.  Returns the new offset; `live` receives the kept count and `cap` the capacity.
+  __device__ __forceinline__ uint32_t list_regrow(uint32_t off, uint32_t cnt, uint32_t ocap, uint32_t extra, uint32_t& live,
+                                                   uint32_t& cap) {
+    PROF_CNT(CN_GROW, 1);
+    uint32_t n = 0;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
       const bool keep = i < cnt && lst[off + i].seq > minSeq;
-      live += __popcll(__ballot(keep));
+      n += __popcll(__ballot(keep));
     }
-    uint32_t cap = live + extra;
-    cap = cap < 8 ? 8 : cap * 2;
-    const uint32_t no = list_alloc(cap);
-    if (err) return;
+    const uint32_t no = list_alloc(2 * (n + extra), cap);
+    if (err) return 0;
     uint32_t w = 0;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
@@ -346,244 +441,440 @@ struct Eng {
         keep = e.seq > minSeq;
       }
       const unsigned long long m = __ballot(keep);
-      const uint32_t rank = rank_below(m);
-      if (keep) lst[no + w + rank] = e;
+      if (keep) lst[no + w + rank_below(m)] = e;
       w += __popcll(m);
     }
-    B.loff = no;
-    B.lcnt = w;
-    B.lcap = cap;
-    B.lseq = MTB_NOKEY;
+    live = w;
     wsync();
+    list_free(off, ocap);
+    return no;
   }
-  // Rebuild block b's window list from its children (after split / pack / root growth) and its
-  // cachedLength (blockUpdate, mergeTree.ts:2392).
-  __device__ __forceinline__ void rebuild(uint32_t b) {
-    Blk& B = blk[b];
-    const int count = B.count;
-    int nent = 0, olen = 0;
-    uint32_t cid = MTB_NONE;
-    Seg s;
-    uint32_t coff = 0, ccnt = 0;
-    if (lane < count) {
-      cid = B.child[lane];
-      if (cid & MTB_LEAF) {
-        s = seg[cid & ~MTB_LEAF];
-        const int l = local_len(s);
-        olen = l == MTB_UNDEF ? 0 : l;
-        if (s.seq > minSeq) nent++;
-        if (s.rseq >= 0 && s.rseq > minSeq) {
-          nent++;
-          if (s.rcx) nent += (int)aux[s.rcx];
+  // Append (seqv, client, kind, delta) to the lists of the path blocks at depths [lo, hi), each entry
+  // tagged with the slot the path takes at that depth.  One lane per depth; full lists are
+  // re-allocated afterwards, one at a time.
+  __device__ __forceinline__ void append_levels(int lo, int hi, int seqv, int client, int kind, int delta) {
+    if (hi <= lo) return;
+    bool need = false;
+    const int i = lane;
+    if (i >= lo && i < hi) {
+      uint32_t loff, lcnt, lcap;
+      if (i == 0) {
+        loff = sh->rmeta[0];
+        lcnt = sh->rmeta[1];
+        lcap = sh->rmeta[2];
+      } else {
+        const View& P = sh->v[i - 1];
+        const int k = sh->slot[i - 1];
+        loff = P.f[F_SEQ][k];
+        lcnt = P.f[F_RSEQ][k];
+        lcap = P.f[F_CLI][k];
+      }
+      if (lcnt < lcap) {
+        WEnt e;
+        e.seq = seqv;
+        e.ck = WE_KEY(client, kind, sh->slot[i]);
+        e.delta = delta;
+        e.pad = 0;
+        lst[loff + lcnt] = e;
+        if (i == 0) {
+          sh->rmeta[1] = lcnt + 1;
+          blk[sh->path[0]].lcnt = lcnt + 1;
+        } else {
+          const int k = sh->slot[i - 1];
+          sh->v[i - 1].f[F_RSEQ][k] = lcnt + 1;
+          blk[sh->path[i - 1]].f[F_RSEQ][k] = lcnt + 1;
         }
       } else {
-        const Blk& cb = blk[cid];
-        olen = cb.len;
-        coff = cb.loff;
-        ccnt = cb.lcnt;
+        need = true;
       }
     }
-    const int totalLen = csum8(olen);
-    const int cincl = cscan8((int)ccnt);
-    const int cexcl = cincl - (int)ccnt;
-    const int ctotal = rl(cincl, 7);
-    int pre[MTB_MAXCH], off[MTB_MAXCH];
-#pragma unroll
-    for (int k = 0; k < MTB_MAXCH; k++) {
-      pre[k] = rl(cexcl, k);
-      off[k] = rl((int)coff, k);
-    }
-    int live_from_children = 0;
-    for (int base = 0; base < ctotal; base += 64) {
-      const int t = base + lane;
-      bool keep = false;
-      if (t < ctotal) {
-        int j = 0;
-#pragma unroll
-        for (int k = 1; k < MTB_MAXCH; k++)
-          if (k < count && pre[k] <= t) j = k;
-        int p = 0;
-#pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++)
-          if (k == j) p = off[k] + (t - pre[k]);
-        keep = lst[p].seq > minSeq;
+    unsigned long long m = __ballot(need);
+    wsync();
+    while (m) {
+      const int d = first_set(m);
+      m &= m - 1;
+      uint32_t loff, lcnt, lcap;
+      meta_of(d, loff, lcnt, lcap);
+      uint32_t live, cap;
+      const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
+      if (err) return;
+      if (lane == 0) {
+        WEnt e;
+        e.seq = seqv;
+        e.ck = WE_KEY(client, kind, sh->slot[d]);
+        e.delta = delta;
+        e.pad = 0;
+        lst[no + live] = e;
+        set_meta(d, no, live + 1, cap);
       }
-      live_from_children += __popcll(__ballot(keep));
+      wsync();
     }
-    const int segEnt = csum8(nent);
-    const int total = segEnt + live_from_children;
-    uint32_t cap = (uint32_t)total;
-    cap = cap < 8 ? 8 : cap + cap / 2 + 4;
-    const uint32_t no = list_alloc(cap);
-    if (err) return;
-    const int sincl = cscan8(nent);
-    int w = sincl - nent;
-    if (lane < count && (cid & MTB_LEAF)) {
-      WEnt e;
-      e.pad = 0;
-      if (s.seq > minSeq) {
-        e.seq = s.seq;
-        e.ck = (s.client & 0xFFFF) | (WK_MAIN << 16);
-        e.delta = s.len;
-        lst[no + w++] = e;
-      }
-      if (s.rseq >= 0 && s.rseq > minSeq) {
-        e.seq = s.rseq;
-        e.ck = (s.rc0 & 0xFFFF) | (WK_MAIN << 16);
-        e.delta = -s.len;
-        lst[no + w++] = e;
-        if (s.rcx) {
-          const uint32_t n = aux[s.rcx];
-          for (uint32_t i = 0; i < n; i++) {
-            e.ck = ((int)aux[s.rcx + 1 + i] & 0xFFFF) | (WK_OVERLAP << 16);
-            e.delta = s.len;
-            lst[no + w++] = e;
+  }
+  // Observer-length bookkeeping along the path: the path slot's childLen at depths [lo, hi) and the
+  // block's own cachedLength at depths [lo, hdr_hi].
+  __device__ __forceinline__ void add_len_levels(int lo, int hi, int hdr_hi, int dlen) {
+    if (!dlen) return;
+    const int i = lane;
+    if (i >= lo && i < hi) {
+      const int k = sh->slot[i];
+      const int v = (int)sh->v[i].f[F_LEN][k] + dlen;
+      sh->v[i].f[F_LEN][k] = (uint32_t)v;
+      blk[sh->path[i]].f[F_LEN][k] = (uint32_t)v;
+    }
+    if (i >= lo && i <= hdr_hi) {
+      const int v = sh->v[i].len + dlen;
+      sh->v[i].len = v;
+      blk[sh->path[i]].len = v;
+    }
+    wsync();
+  }
+  // Rebuild block P's window list from its children (after split / packParent / root growth): for
+  // each block child k, the entries of k's own list plus entries derived from k's segment children
+  // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
+  // where P's metadata lives.
+  __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
+                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
+    PROF_CNT(CN_REBUILD, 1);
+    Rec& Z = sh->zr;
+    const uint32_t* src = bw(P);
+    const uint32_t w = src[lane];
+    const int count = (int)src[FB_HDR];
+    (&Z.f[0][0])[lane] = w;
+    wsync();
+    // lane (k, s): segment child s of block child k
+    const int k = lane >> 3, s = lane & 7;
+    uint32_t ck = MTB_NONE;
+    if (k < count) ck = Z.f[F_ID][k];
+    const bool kblk = k < count && !(ck & MTB_LEAF);
+    int ne = 0, nov = 0;
+    int slen = 0, sseq = 0, srseq = -1;
+    uint32_t scli = 0, srcx = 0;
+    if (kblk) {
+      const uint32_t* c = bw(ck);
+      const int ccount = (int)c[FB_HDR];
+      if (s < ccount) {
+        const uint32_t sid = c[F_ID * 8 + s];
+        if (sid & MTB_LEAF) {
+          slen = (int)c[F_LEN * 8 + s];
+          sseq = (int)c[F_SEQ * 8 + s];
+          srseq = (int)c[F_RSEQ * 8 + s];
+          scli = c[F_CLI * 8 + s];
+          srcx = c[F_RCX * 8 + s];
+          if (sseq > minSeq) ne++;
+          if (srseq >= 0 && srseq > minSeq) {
+            ne++;
+            if (srcx) nov = (int)aux[srcx];
           }
         }
       }
     }
-    uint32_t wpos = (uint32_t)segEnt;
-    for (int base = 0; base < ctotal; base += 64) {
+    // the block children's own lists (metadata in P's slots), concatenated
+    uint32_t lc = 0, lo = 0;
+    if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
+      lo = Z.f[F_SEQ][lane];
+      lc = Z.f[F_RSEQ][lane];
+    }
+    const int lincl = cscan8((int)lc);
+    const int ltotal = rl(lincl, 7);
+    const int lexcl = lincl - (int)lc;
+    int pre[MTB_MAXCH], off[MTB_MAXCH];
+#pragma unroll
+    for (int q = 0; q < MTB_MAXCH; q++) {
+      pre[q] = rl(lexcl, q);
+      off[q] = rl((int)lo, q);
+    }
+    const unsigned long long b1 = __ballot(ne >= 1), b2 = __ballot(ne >= 2);
+    const int nder = __popcll(b1) + __popcll(b2);
+    int novt = 0;
+    if (__ballot(nov > 0)) {
+      novt = nov;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) novt += __shfl_xor(novt, o, 64);
+    }
+    const uint32_t total = (uint32_t)(nder + novt + ltotal);
+    uint32_t cap;
+    const uint32_t no = list_alloc(total + total / 2 + 4, cap);
+    if (err) return;
+    // derived entries: insert (seq, client, +len), removal (removedSeq, rc0, -len)
+    uint32_t wp = rank_below(b1) + rank_below(b2);
+    if (ne) {
+      WEnt e;
+      e.pad = 0;
+      if (sseq > minSeq) {
+        e.seq = sseq;
+        e.ck = WE_KEY(cli_client(scli), WK_MAIN, k);
+        e.delta = slen;
+        lst[no + wp++] = e;
+      }
+      if (srseq >= 0 && srseq > minSeq) {
+        e.seq = srseq;
+        e.ck = WE_KEY(cli_rc0(scli), WK_MAIN, k);
+        e.delta = -slen;
+        lst[no + wp++] = e;
+      }
+    }
+    uint32_t wpos = (uint32_t)nder;
+    // overlapping removers (rare): (removedSeq, c, OVERLAP, +len), lane by lane
+    unsigned long long om = __ballot(nov > 0);
+    while (om) {
+      const int t = first_set(om);
+      om &= om - 1;
+      const uint32_t rcx = rlu(srcx, t);
+      const int n = rl(nov, t);
+      const int rseq = rl(srseq, t), len = rl(slen, t), kk = t >> 3;
+      for (int i = lane; i < n; i += 64) {
+        WEnt e;
+        e.seq = rseq;
+        e.ck = WE_KEY((int)aux[rcx + 1 + i], WK_OVERLAP, kk);
+        e.delta = len;
+        e.pad = 0;
+        lst[no + wpos + i] = e;
+      }
+      wpos += (uint32_t)n;
+    }
+    // children's lists, retagged with the child's slot, entries above minSeq only
+    for (int base = 0; base < ltotal; base += 64) {
       const int t = base + lane;
       bool keep = false;
       WEnt e;
-      if (t < ctotal) {
+      if (t < ltotal) {
         int j = 0;
 #pragma unroll
-        for (int k = 1; k < MTB_MAXCH; k++)
-          if (k < count && pre[k] <= t) j = k;
+        for (int q = 1; q < MTB_MAXCH; q++)
+          if (q < count && pre[q] <= t) j = q;
         int p = 0;
 #pragma unroll
-        for (int k = 0; k < MTB_MAXCH; k++)
-          if (k == j) p = off[k] + (t - pre[k]);
+        for (int q = 0; q < MTB_MAXCH; q++)
+          if (q == j) p = off[q] + (t - pre[q]);
         e = lst[p];
         keep = e.seq > minSeq;
+        e.ck = (e.ck & 0xFFFFF) | (j << 20);
       }
       const unsigned long long m = __ballot(keep);
-      const uint32_t rank = rank_below(m);
-      if (keep) lst[no + wpos + rank] = e;
+      if (keep) lst[no + wpos + rank_below(m)] = e;
       wpos += __popcll(m);
     }
-    B.loff = no;
-    B.lcnt = (uint32_t)total;
-    B.lcap = cap;
-    B.len = totalLen;
-    B.lseq = MTB_NOKEY;
     wsync();
+    list_free(old_loff, old_lcap);
+    loff_out = no;
+    lcnt_out = wpos;
+    lcap_out = cap;
   }
 
   // ------------------------------------------------------------------ tree primitives
   __device__ __forceinline__ void set_parent(uint32_t node, uint32_t b, int idx) {
     if (node & MTB_LEAF) {
-      seg[node & ~MTB_LEAF].parent = b;
+      segp[node & ~MTB_LEAF] = b;
     } else {
       blk[node].parent = b;
-      blk[node].index = (uint8_t)idx;
+      blk[node].index = (uint32_t)idx;
     }
   }
-  // Insert `node` at child index k of block b (insertingWalk shift, mergeTree.ts:1831-1837).  `d` is the
-  // depth of b in the current walk (its cache slot holds the children), or -1.
-  __device__ __forceinline__ void insert_child(uint32_t b, int k, uint32_t node, int d) {
-    Blk& B = blk[b];
-    int count;
-    uint32_t c = MTB_NONE;
-    if (d >= 0 && sh->cb[d] == b) {
-      count = sh->ccount[d];
-      if (lane < count) c = sh->cid[d][lane];
-      sh->cb[d] = MTB_NONE;  // children change
-    } else {
-      count = B.count;
-      if (lane < count) c = B.child[lane];
+  // Insert a child with fields sh->nseg[] at slot k of the block cached at depth d
+  // (insertingWalk shift, mergeTree.ts:1831-1837).  Updates the record, the view and the parents.
+  __device__ __forceinline__ void insert_slot(int d, int k) {
+    View& V = sh->v[d];
+    const uint32_t b = V.b;
+    const int count = V.count;
+    const int fld = lane >> 3, s = lane & 7;
+    uint32_t nv = (&V.f[0][0])[lane];
+    if (s == k) nv = sh->nseg[fld];
+    else if (s > k && s <= count) nv = V.f[fld][s - 1];
+    wsync();
+    if (s <= count) {
+      (&V.f[0][0])[lane] = nv;
+      bw(b)[lane] = nv;
     }
     wsync();
-    if (lane < count && lane >= k) {
-      B.child[lane + 1] = c;
-      if (!(c & MTB_LEAF)) blk[c].index = (uint8_t)(lane + 1);
+    // parents / indices of the new child and of the shifted block children
+    if (lane < MTB_MAXCH && lane >= k && lane <= count) {
+      const uint32_t c = V.f[F_ID][lane];
+      if (lane == k || !(c & MTB_LEAF)) set_parent(c, b, lane);
     }
-    B.child[k] = node;
-    set_parent(node, b, k);
-    B.count = (uint8_t)(count + 1);
+    if (lane == 0) {
+      V.count = count + 1;
+      V.rlv = 0;
+      blk[b].count = (uint32_t)(count + 1);
+    }
     wsync();
   }
-  // split (mergeTree.ts:1858-1871): children 4..7 move to a new block.
-  __device__ __forceinline__ uint32_t split_block(uint32_t b) {
+  // split (mergeTree.ts:1858-1871): children 4..7 of the block at depth `level` move to a new block.
+  // The halves' cachedLength and list metadata are left in sp_* for the caller, which links them in.
+  __device__ __forceinline__ uint32_t split_block(int level) {
+    PROF_CNT(CN_SPLIT, 1);
     struct_changed = true;
     const uint32_t nb = alloc_blk();
     if (err) return 0;
-    Blk& B = blk[b];
-    Blk& N = blk[nb];
+    View& V = sh->v[level];
+    const uint32_t b = V.b;
     const int half = MTB_MAXCH / 2;
-    if (lane < half) {
-      const uint32_t c = B.child[half + lane];
-      N.child[lane] = c;
-      set_parent(c, nb, lane);
-      B.child[half + lane] = MTB_NONE;
+    const int fld = lane >> 3, s = lane & 7;
+    const uint32_t val = (&V.f[0][0])[lane];
+    if (s >= half) {
+      bw(nb)[fld * 8 + s - half] = val;
+      bw(b)[lane] = fld == F_ID ? MTB_NONE : 0u;
     }
-    B.count = (uint8_t)half;
-    N.count = (uint8_t)half;
-    N.parent = B.parent;
+    int ol = 0;
+    bool isblk = false;
+    if (lane < MTB_MAXCH) {
+      const uint32_t c = V.f[F_ID][lane];
+      ol = child_olen(c, (int)V.f[F_LEN][lane], (int)V.f[F_RSEQ][lane]);
+      isblk = !(c & MTB_LEAF);
+      if (lane >= half) set_parent(c, nb, lane - half);
+    }
+    const int lenAll = csum8(ol);
+    const int lenL = csum8(lane < half ? ol : 0);
+    const uint32_t vpar = V.parent;
+    if (lane == 0) {
+      blk[b].count = half;
+      blk[b].len = lenL;
+      blk[nb].count = half;
+      blk[nb].len = lenAll - lenL;
+      blk[nb].parent = vpar;
+      V.count = half;  // (all views are cleared after fix_overflow)
+    }
     wsync();
-    rebuild(b);
-    rebuild(nb);
+    sp_lenL = (uint32_t)lenL;
+    sp_lenR = (uint32_t)(lenAll - lenL);
+    sp_loffL = sp_lcntL = sp_lcapL = sp_loffR = sp_lcntR = sp_lcapR = 0;
+    sp_internal = __ballot(isblk) != 0;  // the halves' lists are rebuilt by the caller
+    // the segment placed by the insert walk moves with the right half
+    if (level == ins_depth && ins_slot >= half) {
+      ins_blk = nb;
+      ins_slot -= half;
+      ins_scour = -1;
+    }
     return nb;
   }
-  // updateRoot (mergeTree.ts:1268-1277)
-  __device__ __forceinline__ void grow_root(uint32_t left, uint32_t right) {
-    const uint32_t r = alloc_blk();
-    if (err) return;
-    Blk& R = blk[r];
-    R.child[0] = left;
-    R.child[1] = right;
-    R.count = 2;
-    blk[left].parent = r;
-    blk[left].index = 0;
-    blk[right].parent = r;
-    blk[right].index = 1;
+  __device__ __forceinline__ void stage_block_child(uint32_t id, uint32_t len, uint32_t loff, uint32_t lcnt, uint32_t lcap) {
+    if (lane < 8) {
+      uint32_t v = 0;
+      if (lane == F_ID) v = id;
+      if (lane == F_LEN) v = len;
+      if (lane == F_SEQ) v = loff;
+      if (lane == F_RSEQ) v = lcnt;
+      if (lane == F_CLI) v = lcap;
+      sh->nseg[lane] = v;
+    }
     wsync();
-    rebuild(r);
-    root = r;
   }
-  // After inserting into block sh->path[d] (the leaf-level block), split every full block on the path.
+  // After inserting into the block at depth d, split every full block on the path; a root split grows
+  // the tree by one level (updateRoot, mergeTree.ts:1268-1277).
   __device__ __forceinline__ void fix_overflow(int d) {
+    if (sh->v[d].count >= MTB_MAXCH) fix_overflow_slow(d);
+  }
+  // Split every full block on the path, from depth d upwards.  Written as a state machine with a
+  // single list-rebuild site (the halves of an internal split, the new root, the parent).
+  __device__ __forceinline__ void fix_overflow_slow(int d) {
     int level = d;
-    uint32_t cur = sh->path[level];
-    while (!err && blk[cur].count >= MTB_MAXCH) {
-      const uint32_t nb = split_block(cur);
-      if (err) return;
-      if (level == 0) {
-        grow_root(cur, nb);
+    int phase = 0;  // 0 split `level` | 1 rebuild left half | 2 rebuild right half | 3 link | 4 parent done | 5 root done
+    uint32_t b = MTB_NONE, nb = MTB_NONE;
+    while (!err) {
+      if (phase == 0) {
+        if (sh->v[level].count < MTB_MAXCH) break;
+        b = sh->v[level].b;
+        nb = split_block(level);
+        if (err) break;
+        phase = sp_internal ? 1 : 3;
+        continue;
+      }
+      uint32_t X, ooff = 0, ocnt = 0, ocap = 0;
+      const int L = level - 1;
+      if (phase == 1) {
+        X = b;
+        meta_of(level, ooff, ocnt, ocap);
+        phase = 2;
+      } else if (phase == 2) {
+        X = nb;
+        phase = 3;
+      } else if (level == 0) {
+        // new root with children (b, nb) (updateRoot, mergeTree.ts:1268-1277)
+        X = alloc_blk();
+        if (err) break;
+        if (lane == 0) {
+          FBlk& Rb = blk[X];
+          Rb.f[F_ID][0] = b;
+          Rb.f[F_LEN][0] = sp_lenL;
+          Rb.f[F_SEQ][0] = sp_loffL;
+          Rb.f[F_RSEQ][0] = sp_lcntL;
+          Rb.f[F_CLI][0] = sp_lcapL;
+          Rb.f[F_ID][1] = nb;
+          Rb.f[F_LEN][1] = sp_lenR;
+          Rb.f[F_SEQ][1] = sp_loffR;
+          Rb.f[F_RSEQ][1] = sp_lcntR;
+          Rb.f[F_CLI][1] = sp_lcapR;
+          Rb.count = 2;
+          Rb.len = (int32_t)(sp_lenL + sp_lenR);
+          blk[b].parent = X;
+          blk[b].index = 0;
+          blk[nb].parent = X;
+          blk[nb].index = 1;
+        }
+        wsync();
+        phase = 5;
+      } else {
+        // link (b, nb) into the parent at depth level-1, then rebuild the parent's list
+        const int k = sh->slot[L];
+        View& P = sh->v[L];
+        if (lane == 0) {
+          P.f[F_LEN][k] = sp_lenL;
+          P.f[F_SEQ][k] = sp_loffL;
+          P.f[F_RSEQ][k] = sp_lcntL;
+          P.f[F_CLI][k] = sp_lcapL;
+          FBlk& PB = blk[P.b];
+          PB.f[F_LEN][k] = sp_lenL;
+          PB.f[F_SEQ][k] = sp_loffL;
+          PB.f[F_RSEQ][k] = sp_lcntL;
+          PB.f[F_CLI][k] = sp_lcapL;
+        }
+        wsync();
+        stage_block_child(nb, sp_lenR, sp_loffR, sp_lcntR, sp_lcapR);
+        insert_slot(L, k + 1);
+        X = P.b;
+        meta_of(L, ooff, ocnt, ocap);
+        phase = 4;
+      }
+      uint32_t a, c2, e;
+      rebuild(X, ooff, ocap, a, c2, e);
+      if (err) break;
+      if (phase == 2) {
+        sp_loffL = a;
+        sp_lcntL = c2;
+        sp_lcapL = e;
+      } else if (phase == 3) {
+        sp_loffR = a;
+        sp_lcntR = c2;
+        sp_lcapR = e;
+      } else if (phase == 4) {
+        if (lane == 0) set_meta(L, a, c2, e);
+        wsync();
+        level = L;
+        phase = 0;
+      } else {  // phase 5: the new root
+        root = X;
+        if (lane == 0) {
+          sh->path[0] = X;
+          sh->rmeta[0] = a;
+          sh->rmeta[1] = c2;
+          sh->rmeta[2] = e;
+          blk[X].loff = a;
+          blk[X].lcnt = c2;
+          blk[X].lcap = e;
+        }
+        wsync();
         break;
       }
-      const uint32_t p = sh->path[level - 1];
-      insert_child(p, blk[cur].index + 1, nb, -1);
-      cur = p;
-      level--;
     }
-    if (struct_changed) cache_clear();
-  }
-
-  // BaseSegment.splitAt (mergeTreeNodes.ts:481-510) + TextSegment.createSplitSegmentAt
-  __device__ __forceinline__ uint32_t split_seg(uint32_t sid, int at) {
-    const uint32_t r = alloc_seg();
-    if (err) return 0;
-    Seg t = seg[sid];
-    t.len -= at;
-    t.text += (uint32_t)at;
-    seg[r] = t;
-    seg[sid].len = at;
-    n_mod += 2;
-    wsync();
-    return r;
+    view_clear();
   }
 
   // ------------------------------------------------------------------ insertingWalk
   // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
-  // mode 1: blockInsert of candidate `cand` (seq S).  Returns false if the candidate was not placed.
+  // mode 1: blockInsert of the staged segment sh->nseg (seq S).  Returns false if it was not placed.
   // `resume`: start at the leaf-level block reached by the previous walk (same (R, C) and position, no
   // block split since): internal-level decisions of both walks are identical (blocks tie-break the same
   // way in both modes and a segment split changes no block length).
-  __device__ __forceinline__ bool walk(int pos, int R, int C, int S, bool insertMode, uint32_t cand, int candLen,
-                                       bool resume = false) {
+  __device__ __forceinline__ bool walk(int pos, int R, int C, int S, bool insertMode, int candLen, bool resume = false) {
     uint32_t b = root;
     int p = pos;
     int d = 0;
@@ -595,12 +886,21 @@ struct Eng {
     walk_depth = -1;
     struct_changed = false;
     while (true) {
-      if (d >= MTB_MAXDEPTH) { fail(DERR_DEPTH); return false; }
-      sh->path[d] = b;
-      sh->pp[d] = p;
-      uint32_t cid;
-      int clen, cseq;
-      const int count = child_info(b, d, R, C, cid, clen, cseq);
+      if (d >= MTB_VDEPTH) { fail(DERR_DEPTH); return false; }
+      if (lane == 0) {
+        sh->path[d] = b;
+        sh->pp[d] = p;
+      }
+      wsync();
+      const int count = load_view(d, b, R, C);
+      const View& V = sh->v[d];
+      uint32_t cid = MTB_NONE;
+      int clen = 0, cseq = 0;
+      if (lane < count) {
+        cid = V.f[F_ID][lane];
+        clen = V.rl[lane];
+        cseq = (int)V.f[F_SEQ][lane];
+      }
       const int def = (lane < count && clen > 0) ? clen : 0;
       const int incl = cscan8(def);
       const int pj = p - (incl - def);
@@ -608,10 +908,13 @@ struct Eng {
       const bool tie = isBlk || (insertMode && pj == 0 && S > cseq);
       const bool qual = lane < count && clen != MTB_UNDEF && (pj < clen || (pj == clen && tie));
       const unsigned long long m = __ballot(qual);
+      int at;
       if (m) {
         const int j = first_set(m);
         const uint32_t cj = rlu(cid, j);
         const int pjj = rl(pj, j);
+        if (lane == 0) sh->slot[d] = j;
+        wsync();
         if (!(cj & MTB_LEAF)) {
           b = cj;
           p = pjj;
@@ -619,40 +922,66 @@ struct Eng {
           continue;
         }
         walk_depth = d;
-        if (insertMode) {
-          insert_child(b, j, cand | MTB_LEAF, d);
-        } else {
+        if (!insertMode) {
           if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
-          const uint32_t sid = cj & ~MTB_LEAF;
-          if (seg[sid].text & MTB_MARKER) return true;  // markers never split
-          const uint32_t r = split_seg(sid, pjj);
+          if (V.f[F_TEXT][j] & MTB_MARKER) return true;  // markers never split
+          split_seg(d, j, pjj);
           if (err) return false;
-          insert_child(b, j + 1, r | MTB_LEAF, d);
-          fix_overflow(d);
+          pending_fix = d;  // (handled by the caller, after the walk)
           return true;
         }
+        at = j;
       } else {
         const int total = rl(incl, 7);
         if (p - total == 0) walk_depth = d;
         if (p - total != 0 || !insertMode) return !insertMode;
-        insert_child(b, count, cand | MTB_LEAF, d);
+        at = count;
       }
-      // candidate inserted into block b at depth d: propagate its length and window entry
-      cache_clear();
-      path_update(d + 1, candLen, S, C, WK_MAIN, candLen);
-      fix_overflow(d);
+      // blockInsert: place the staged segment at slot `at` of the block at depth d
+      ins_depth = d;
+      ins_slot = at;
+      ins_blk = b;
+      ins_scour = V.scour;
+      if (lane == 0) sh->slot[d] = at;
+      wsync();
+      insert_slot(d, at);
+      add_len_levels(0, d, d, candLen);
+      append_levels(0, d, S, C, WK_MAIN, candLen);
+      pending_fix = d;
       return true;
     }
   }
+  // BaseSegment.splitAt (mergeTreeNodes.ts:481-510) + TextSegment.createSplitSegmentAt (textSegment.ts:106):
+  // the segment in slot j of the block at depth d is cut at offset `at`; the right half goes to slot j + 1.
+  __device__ __forceinline__ void split_seg(int d, int j, int at) {
+    const uint32_t r = alloc_seg();
+    if (err) return;
+    View& V = sh->v[d];
+    if (lane < 8) {
+      uint32_t v = V.f[lane][j];
+      if (lane == F_ID) v = MTB_LEAF | r;
+      if (lane == F_LEN) v = v - (uint32_t)at;
+      if (lane == F_TEXT) v = v + (uint32_t)at;
+      sh->nseg[lane] = v;
+    }
+    wsync();
+    if (lane == 0) {
+      V.f[F_LEN][j] = (uint32_t)at;
+      blk[V.b].f[F_LEN][j] = (uint32_t)at;
+    }
+    n_mod += 2;
+    wsync();
+    insert_slot(d, j + 1);
+  }
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
-  __device__ __forceinline__ Lru hget(uint32_t k) const { return heap_lds ? sh->heap[k] : heap[k]; }
+  __device__ __forceinline__ Lru hget(uint32_t k) const { return heap_lds ? sh->heap[k] : sh->gheap[k]; }
   __device__ __forceinline__ void hset(uint32_t k, Lru v) {
     if (heap_lds) sh->heap[k] = v;
-    else heap[k] = v;
+    else sh->gheap[k] = v;
   }
   __device__ __forceinline__ void heap_spill() {  // LDS -> global slice
-    for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) heap[i] = sh->heap[i];
+    for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) sh->gheap[i] = sh->heap[i];
     heap_lds = false;
     wsync();
   }
@@ -698,7 +1027,7 @@ struct Eng {
   // addToLRUSet (mergeTree.ts:741-751); `b` is the segment's parent block, `scour` its needsScour
   __device__ __forceinline__ bool lru_add(uint32_t sid, uint32_t b, int scour, int seqv) {
     if (seqv > curSeq && scour != 1) {
-      blk[b].scour = 1;
+      if (lane == 0) blk[b].scour = 1;
       heap_add(sid, seqv);
       return true;
     }
@@ -707,7 +1036,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ properties
   __device__ __forceinline__ const uint32_t* props_ptr(uint32_t h) const {
-    return (h & MTB_GPROPS) ? (T.pool + (h & ~MTB_GPROPS)) : (aux + h);
+    return (h & MTB_GPROPS) ? (sh->tab.pool + (h & ~MTB_GPROPS)) : (aux + h);
   }
   // matchProperties (properties.ts:71-96) on interned property sets
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
@@ -722,7 +1051,7 @@ struct Eng {
       for (uint32_t q = 0; q < nb; q++) {
         if (pb[1 + 2 * q] == k) {
           found = true;
-          if (T.val_class[pa[2 + 2 * i]] != T.val_class[pb[2 + 2 * q]]) return false;
+          if (sh->tab.val_class[pa[2 + 2 * i]] != sh->tab.val_class[pb[2 + 2 * q]]) return false;
           break;
         }
       }
@@ -734,7 +1063,10 @@ struct Eng {
   // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
   __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
     if (old == memo_old && memo_new) return memo_new;
-    const uint32_t* op = T.pool + T.pidx[2 * opId];
+    return props_apply_slow(old, opId, rewrite);
+  }
+  __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite) {
+    const uint32_t* op = sh->tab.pool + sh->tab.pidx[2 * opId];
     const uint32_t nop = op[0];
     uint32_t n = 0;
     if (old) {
@@ -756,7 +1088,7 @@ struct Eng {
         for (uint32_t q = 0; q < nop; q++) {
           if (op[1 + 2 * q] == k) {
             const uint32_t v = op[2 + 2 * q];
-            keep = v != MTB_NONE && !T.val_falsy[v];
+            keep = v != MTB_NONE && !sh->tab.val_falsy[v];
           }
         }
         if (keep) {
@@ -790,12 +1122,12 @@ struct Eng {
         sh->pv[at] = v;
         wsync();
       } else if (n < 64) {
-        const uint32_t rank = T.key_rank[k];
+        const uint32_t rank = sh->tab.key_rank[k];
         uint32_t ins = n;
         if (rank != MTB_NONE) {
           ins = 0;
           while (ins < n) {
-            const uint32_t r2 = T.key_rank[sh->pk[ins]];
+            const uint32_t r2 = sh->tab.key_rank[sh->pk[ins]];
             if (r2 == MTB_NONE || r2 > rank) break;
             ins++;
           }
@@ -827,196 +1159,377 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ nodeMap (remove / annotate)
+  // The segments of one leaf-level block (depth d) touched by [start, end), all lanes at once (the
+  // boundaries were split beforehand, so each segment is wholly in or out of the range).  `pos` is the
+  // position at the start of the block; returns the block's total visible length.
+  __device__ __forceinline__ int map_leaf_block(int d, int pos, int start, int end, int S, int C, bool remove, uint32_t opId,
+                                bool rewrite) {
+    View& V = sh->v[d];
+    const uint32_t b = V.b;
+    const int count = V.count;
+    int rlj = 0;
+    if (lane < count) rlj = V.rl[lane];
+    const int def = (lane < count && rlj > 0) ? rlj : 0;
+    const int incl = cscan8(def);
+    const int total = rl(incl, 7);
+    const int sj = pos + incl - def;
+    const bool visit = lane < count && rlj > 0 && sj < end && start < sj + rlj;
+    const unsigned long long vm = __ballot(visit);
+    if (!vm) return total;
+    n_mod += (uint32_t)__popcll(vm);
+    uint32_t id = MTB_NONE, cli = 0, props = 0;
+    int len = 0, rseq = -1;
+    if (lane < count) {
+      id = V.f[F_ID][lane];
+      len = (int)V.f[F_LEN][lane];
+      rseq = (int)V.f[F_RSEQ][lane];
+      cli = V.f[F_CLI][lane];
+      props = V.f[F_PROPS][lane];
+    }
+    if (remove) {
+      // fresh removes: removedSeq = S, removedClientIds = [C] (mergeTree.ts:1978-1995)
+      const bool fresh = visit && rseq < 0;
+      int dl = 0;
+      if (fresh) {
+        const uint32_t ncli = (cli & 0xFFFF) | ((uint32_t)C << 16);
+        V.f[F_RSEQ][lane] = (uint32_t)S;
+        V.f[F_CLI][lane] = ncli;
+        V.f[F_RCX][lane] = 0;
+        FBlk& B = blk[b];
+        B.f[F_RSEQ][lane] = (uint32_t)S;
+        B.f[F_CLI][lane] = ncli;
+        B.f[F_RCX][lane] = 0;
+        const int before = local_len(len, -1);
+        const int after = local_len(len, S);
+        dl = (after == MTB_UNDEF ? 0 : after) - (before == MTB_UNDEF ? 0 : before);
+      }
+      const int dsum = csum8(dl);
+      if (lane == 0) sh->acc[d] += dsum;
+      wsync();
+      // overlapping removes (already removed): append C to removedClientIds (copy-on-write list) and an
+      // OVERLAP entry on every ancestor list (no observer-length change)
+      unsigned long long om = __ballot(visit && rseq >= 0);
+      while (om) {
+        const int t = first_set(om);
+        om &= om - 1;
+        const uint32_t orcx = V.f[F_RCX][t];
+        const uint32_t oldn = orcx ? aux[orcx] : 0;
+        const uint32_t h = alloc_aux(oldn + 2);
+        if (err) return 0;
+        for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[orcx + 1 + i];
+        if (lane == 0) {
+          aux[h] = oldn + 1;
+          aux[h + 1 + oldn] = (uint32_t)C;
+          V.f[F_RCX][t] = h;
+          blk[b].f[F_RCX][t] = h;
+        }
+        wsync();
+        append_levels(0, d, rl(rseq, t), C, WK_OVERLAP, rl(len, t));
+        if (err) return 0;
+      }
+    } else {
+      // annotate: one new property set per distinct old set (memoized per op)
+      unsigned long long am = vm;
+      while (am) {
+        const int t = first_set(am);
+        const uint32_t old = rlu(props, t);
+        const uint32_t np = props_apply(old, opId, rewrite);
+        if (err) return 0;
+        const bool mine = visit && props == old;
+        if (mine) {
+          V.f[F_PROPS][lane] = np;
+          blk[b].f[F_PROPS][lane] = np;
+        }
+        am &= ~__ballot(mine);
+        wsync();
+      }
+    }
+    // addToLRUSet for the first visited segment (the block's needsScour then becomes true)
+    const int t = first_set(vm);
+    const uint32_t tid = rlu(id, t);
+    if (S > curSeq && V.scour != 1) {
+      if (lane == 0) {
+        V.scour = 1;
+        blk[b].scour = 1;
+      }
+      wsync();
+      heap_add(tid & ~MTB_LEAF, S);
+    }
+    if (lane == 0) V.rlv = 0;
+    wsync();
+    return total;
+  }
   // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958).
   // Emulates depthFirstNodeWalk (mergeTreeNodeWalk.ts:35) with an explicit stack; block post-actions
-  // (blockUpdateLength) become one flush of the accumulated observer-length delta per block.
-  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId,
-                                           bool rewrite) {
+  // (blockUpdateLength) become one flush of the accumulated observer-length delta per block into its
+  // parent's slot and list.
+  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
     if (end == start) return;
     int pos = 0;
     int d = 0;
     bool exiting = false;
-    auto enter = [&](uint32_t b) {
-      uint32_t cid;
-      int clen, cseq;
-      child_info(b, d, R, C, cid, clen, cseq);
-      sh->path[d] = b;
-      sh->sidx[d] = 0;
-      sh->acc[d] = 0;
-      wsync();
-    };
-    enter(root);
+    if (lane == 0) {
+      sh->path[0] = root;
+      sh->sidx[0] = 0;
+      sh->acc[0] = 0;
+    }
+    wsync();
+    load_view(0, root, R, C);
     while (!err) {
-      const int idx = sh->sidx[d];
-      if (exiting || idx >= sh->ccount[d]) {
-        // post-order: flush this block's accumulated observer-length delta
+      View& V = sh->v[d];
+      const int count = V.count;
+      int idx = sh->sidx[d];
+      if (!exiting && idx == 0 && count > 0 && (V.f[F_ID][0] & MTB_LEAF)) {
+        // a block of segments: every touched segment at once
+        pos += map_leaf_block(d, pos, start, end, S, C, remove, opId, rewrite);
+        if (err) return;
+        if (pos >= end) exiting = true;
+        idx = count;
+        if (lane == 0) sh->sidx[d] = count;
+        wsync();
+      }
+      if (exiting || idx >= count) {
+        // post-order: flush this block's accumulated observer-length delta into its parent
         const int a = sh->acc[d];
         if (a != 0) {
-          const uint32_t b = sh->path[d];
-          const uint32_t keep = sh->path[0];
-          sh->path[0] = b;
-          wsync();
-          path_update(1, a, S, C, WK_MAIN, a);
-          sh->path[0] = keep;
-          if (d > 0) sh->acc[d - 1] += a;
+          if (d > 0) {
+            const int L = d - 1;
+            const int k = sh->slot[L];
+            if (lane == 0) {
+              const int v = (int)sh->v[L].f[F_LEN][k] + a;
+              sh->v[L].f[F_LEN][k] = (uint32_t)v;
+              blk[sh->path[L]].f[F_LEN][k] = (uint32_t)v;
+              sh->acc[L] += a;
+            }
+            wsync();
+            append_levels(L, d, S, C, WK_MAIN, a);
+          }
+          if (lane == 0) {
+            const int v = sh->v[d].len + a;
+            sh->v[d].len = v;
+            blk[sh->path[d]].len = v;
+          }
           wsync();
         }
         if (d == 0) break;
         d--;
         continue;
       }
-      sh->sidx[d] = idx + 1;
+      if (lane == 0) sh->sidx[d] = idx + 1;
       wsync();
       if (end <= pos) {
         exiting = true;
         continue;
       }
-      const int len = sh->clen[d][idx];
+      const int len = V.rl[idx];
       if (len == MTB_UNDEF || len == 0) continue;
       const int nextPos = pos + len;
       if (start >= nextPos) {
         pos = nextPos;
         continue;
       }
-      const uint32_t c = sh->cid[d][idx];
-      if (!(c & MTB_LEAF)) {
-        if (d + 1 >= MTB_MAXDEPTH) { fail(DERR_DEPTH); return; }
-        d++;
-        enter(c);
-        continue;
+      const uint32_t c = V.f[F_ID][idx];
+      if (c & MTB_LEAF) { fail(DERR_SHAPE); return; }
+      if (d + 1 >= MTB_VDEPTH) { fail(DERR_DEPTH); return; }
+      if (lane == 0) {
+        sh->slot[d] = idx;
+        sh->path[d + 1] = c;
+        sh->sidx[d + 1] = 0;
+        sh->acc[d + 1] = 0;
       }
-      const uint32_t sid = c & ~MTB_LEAF;
-      const Seg s = seg[sid];
-      n_mod += 1;
-      if (remove) {
-        if (s.rseq >= 0) {
-          // overlapping remove: append C to removedClientIds (copy-on-write list) and add an OVERLAP
-          // window entry on every ancestor (no observer-length change)
-          const uint32_t oldn = s.rcx ? aux[s.rcx] : 0;
-          const uint32_t h = alloc_aux(oldn + 2);
-          if (err) return;
-          for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[s.rcx + 1 + i];
-          aux[h] = oldn + 1;
-          aux[h + 1 + oldn] = (uint32_t)C;
-          seg[sid].rcx = h;
-          wsync();
-          path_update(d + 1, 0, s.rseq, C, WK_OVERLAP, s.len);
-        } else {
-          const int before = local_len(s);
-          seg[sid].rseq = S;
-          seg[sid].rc0 = (int16_t)C;
-          seg[sid].rcx = 0;
-          Seg s2 = s;
-          s2.rseq = S;
-          const int after = local_len(s2);
-          const int dl = (after == MTB_UNDEF ? 0 : after) - (before == MTB_UNDEF ? 0 : before);
-          sh->acc[d] += dl;
-          wsync();
-        }
-      } else {
-        const uint32_t np = props_apply(s.props, opId, rewrite);
-        if (err) return;
-        seg[sid].props = np;
-      }
-      if (lru_add(sid, sh->path[d], sh->cscour[d], S)) sh->cscour[d] = 1;
       wsync();
-      pos = nextPos;
+      d++;
+      load_view(d, c, R, C);
     }
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
   __device__ __forceinline__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
+    uint16_t* const txt = sh->gtext;
     for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
   }
-  // scourNode (zamboni.ts:122-193) for block `node`: kept children are appended to sh->hold[nh..].
-  // Every child record (and the last UTF-16 unit of every text) is fetched at once, lane-parallel;
-  // the sequential keep/drop/append decisions then run on registers (shuffles), and the text of each
-  // run of appended segments is written with one parallel copy (TextSegment.append, textSegment.ts:84).
-  __device__ __forceinline__ int scour(uint32_t node, int nh) {
-    const Blk& B = blk[node];
-    const int count = B.count;
-    uint32_t c = MTB_NONE;
-    Seg s;
-    s.len = 0;
-    s.seq = 0;
-    s.rseq = -1;
-    s.props = 0;
-    s.text = 0;
-    uint16_t last = 0;
+  __device__ __forceinline__ void stage_rec(uint32_t b) {
+    PROF_CNT(CN_ZRECORD, 1);
+    const uint32_t* src = bw(b);
+    const uint32_t w = src[lane];
+    const uint32_t h = lane < 4 ? src[FB_HDR + lane] : 0u;
+    const int hc = rl((int)h, 0), hs = rl((int)h, 3);
+    const uint32_t hp = rlu(h, 1), hi = rlu(h, 2);
+    (&sh->zr.f[0][0])[lane] = w;
+    if (lane == 0) {
+      sh->zr.count = hc;
+      sh->zr.parent = hp;
+      sh->zr.index = hi;
+      sh->zr.scour = hs;
+    }
+    wsync();
+  }
+  // Stage the records of blocks ids[r] (r < nrec, ids in lane r) into sh->pr[r]: lane (r, s) fetches
+  // slot s of block r, so up to 8 blocks arrive with one round trip.
+  __device__ __forceinline__ void stage_recs(int nrec, uint32_t ids) {
+    const int r = lane >> 3, s = lane & 7;
+    uint32_t id = MTB_NONE;
+#pragma unroll
+    for (int q = 0; q < MTB_MAXCH; q++)
+      if (q == r) id = rlu(ids, q);
+    uint32_t w[8];
+    uint32_t h = 0;
+    if (r < nrec) {
+      const uint32_t* src = bw(id);
+#pragma unroll
+      for (int q = 0; q < 8; q++) w[q] = src[q * 8 + s];
+      if (s < 4) h = src[FB_HDR + s];
+    }
+    if (r < nrec) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) sh->pr[r].f[q][s] = w[q];
+      if (s == 0) sh->pr[r].count = (int)h;
+      if (s == 1) sh->pr[r].parent = h;
+      if (s == 2) sh->pr[r].index = h;
+      if (s == 3) sh->pr[r].scour = (int)h;
+    }
+    wsync();
+  }
+  // Property-set signature of a segment, for matchProperties (properties.ts:71-96) without
+  // dependent loads: number of keys and up to two (key, value class) pairs.
+  struct PSig {
+    uint32_t n, k0, c0, k1, c1;
+  };
+  __device__ __forceinline__ PSig psig_of(uint32_t h) const {
+    PSig g;
+    g.n = 0;
+    g.k0 = g.c0 = g.k1 = g.c1 = 0;
+    if (h) {
+      const uint32_t* p = props_ptr(h);  // pools carry >= 4 words of tail padding
+      g.n = p[0];
+      g.k0 = p[1];
+      const uint32_t v0 = p[2];
+      g.k1 = p[3];
+      const uint32_t v1 = p[4];
+      if (g.n >= 1) g.c0 = sh->tab.val_class[v0];
+      if (g.n >= 2) g.c1 = sh->tab.val_class[v1];
+    }
+    return g;
+  }
+  // scourNode (zamboni.ts:122-193) over the staged records sh->pr[0..nrec), each one a block whose kept
+  // children (all 8 fields) are appended, record after record, to sh->hold[.][nh..].  Lane (r, s)
+  // evaluates child s of record r; the sequential keep/drop/append decisions then run on readlane
+  // values, and the text of each run of appended segments is written with one parallel copy
+  // (TextSegment.append, textSegment.ts:84).
+  __device__ __forceinline__ int scour(int nrec, int nh) {
+    const uint64_t ts0 = PROF_T();
+    PROF_CNT(CN_SCOUR, nrec);
+    const int r = lane >> 3, s = lane & 7;
+    const int count = r < nrec ? sh->pr[r].count : 0;
+    uint32_t f[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) f[q] = 0;
+    f[F_ID] = MTB_NONE;
     int kind = 0;  // 0 hold+reset, 1 drop (tombstone below MSN), 2 acked text/marker (may append)
-    if (lane < count) {
-      c = B.child[lane];
-      if (c & MTB_LEAF) {
-        s = seg[c & ~MTB_LEAF];
-        if (s.rseq >= 0) kind = s.rseq > minSeq ? 0 : 1;
-        else if (s.seq <= minSeq) kind = 2;
-        if (kind == 2 && !(s.text & MTB_MARKER) && s.len > 0) last = txt[s.text + s.len - 1];
+    uint16_t last = 0;
+    PSig g;
+    g.n = 0;
+    g.k0 = g.c0 = g.k1 = g.c1 = 0;
+    if (s < count) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) f[q] = sh->pr[r].f[q][s];
+      if (f[F_ID] & MTB_LEAF) {
+        const int rseq = (int)f[F_RSEQ];
+        if (rseq >= 0) kind = rseq > minSeq ? 0 : 1;
+        else if ((int)f[F_SEQ] <= minSeq) kind = 2;
+        if (kind == 2) {
+          if (hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0) last = sh->gtext[f[F_TEXT] + f[F_LEN] - 1];
+          g = psig_of(f[F_PROPS]);
+        }
       }
     }
-    // sequential decisions (uniform), values pulled from lane k by shuffles
-    int prev = -1;            // lane index of the current append target
-    int prevLen = 0;          // its (growing) length
-    uint16_t prevLast = 0;    // its (growing) last unit
-    bool prevMarker = false;
-    uint32_t prevProps = 0;
-    int target = -1;          // per lane: lane it was appended into (-1 kept / dropped)
-    int newLen = 0;           // per lane: final length if it is an append target
-    for (int k = 0; k < count; k++) {
-      const int kk = rl(kind, k);
-      const int klen = rl(s.len, k);
-      const uint32_t ktext = rlu(s.text, k);
-      const uint32_t kprops = rlu(s.props, k);
-      const uint16_t klast = (uint16_t)rl((int)last, k);
-      if (kk == 1) {
-        prev = -1;
-        continue;
-      }
-      if (kk == 2) {
+    int target = -1;  // per lane: lane it was appended into (-1 kept / dropped)
+    int newLen = 0;   // per lane: final length if it is an append target
+    for (int rr = 0; rr < nrec; rr++) {
+      const int cnt = rl(count, rr * 8);
+      // sequential decisions (uniform), values pulled from lane rr*8 + k
+      int prev = -1;          // lane of the current append target
+      int prevLen = 0;        // its (growing) length
+      uint16_t prevLast = 0;  // its (growing) last unit
+      bool prevMarker = false;
+      for (int k = 0; k < cnt; k++) {
+        const int L = rr * 8 + k;
+        const int kk = rl(kind, L);
+        if (kk == 1) {
+          prev = -1;
+          continue;
+        }
+        if (kk != 2) {
+          prev = -1;
+          continue;
+        }
+        const int klen = rl((int)f[F_LEN], L);
+        const uint32_t ktext = rlu(f[F_TEXT], L);
+        const uint16_t klast = (uint16_t)rl((int)last, L);
         const bool kmarker = (ktext & MTB_MARKER) != 0;
         bool ok = false;
         if (prev >= 0 && klen > 0 && !prevMarker && !kmarker && prevLast != (uint16_t)'\n' &&
-            (prevLen <= 256 || klen <= 256))
-          ok = props_match(prevProps, kprops);
+            (prevLen <= 256 || klen <= 256)) {
+          // matchProperties(prev, k)
+          const uint32_t pa = rlu(f[F_PROPS], prev), pb = rlu(f[F_PROPS], L);
+          if (pa == pb) {
+            ok = true;
+          } else {
+            const uint32_t na = rlu(g.n, prev), nb = rlu(g.n, L);
+            if (na != nb) {
+              ok = false;
+            } else if (na == 0) {
+              ok = true;
+            } else if (na > 2) {
+              ok = props_match(pa, pb);
+            } else {
+              const uint32_t ak0 = rlu(g.k0, prev), ac0 = rlu(g.c0, prev), bk0 = rlu(g.k0, L), bc0 = rlu(g.c0, L);
+              if (na == 1) {
+                ok = ak0 == bk0 && ac0 == bc0;
+              } else {
+                const uint32_t ak1 = rlu(g.k1, prev), ac1 = rlu(g.c1, prev), bk1 = rlu(g.k1, L), bc1 = rlu(g.c1, L);
+                ok = (ak0 == bk0 && ac0 == bc0 && ak1 == bk1 && ac1 == bc1) ||
+                     (ak0 == bk1 && ac0 == bc1 && ak1 == bk0 && ac1 == bc0);
+              }
+            }
+          }
+        }
         if (ok) {
-          if (lane == k) target = prev;
+          if (lane == L) target = prev;
           prevLen += klen;
           prevLast = klast;
           if (lane == prev) newLen = prevLen;
         } else {
-          prev = klen > 0 ? k : -1;
+          prev = klen > 0 ? L : -1;
           prevLen = klen;
           prevLast = klast;
           prevMarker = kmarker;
-          prevProps = kprops;
-          if (lane == k) newLen = klen;
+          if (lane == L) newLen = klen;
         }
-        continue;
       }
-      prev = -1;
     }
     // targets that received appends: build their new text
-    const bool isTarget = lane < count && kind == 2 && target < 0 && newLen != s.len;
+    const bool isTarget = s < count && kind == 2 && target < 0 && newLen != (int)f[F_LEN];
     unsigned long long tm = __ballot(isTarget);
     while (tm) {
       const int t = first_set(tm);
       tm &= tm - 1;
       // members of the run: t and every lane whose target is t, in order
       const unsigned long long run = __ballot(lane == t || target == t);
-      const uint32_t ttext = rlu(s.text, t);
-      const int tlen = rl(s.len, t);
+      const uint32_t ttext = rlu(f[F_TEXT], t);
+      const int tlen = rl((int)f[F_LEN], t);
       const int total = rl(newLen, t);
       // contiguous in the arena already?
       bool contiguous = true;
       {
         uint32_t expect = ttext + (uint32_t)tlen;
-        unsigned long long r = run & ~(1ull << t);
-        while (r) {
-          const int q = first_set(r);
-          r &= r - 1;
-          const uint32_t qt = rlu(s.text, q);
-          const int ql = rl(s.len, q);
+        unsigned long long rm = run & ~(1ull << t);
+        while (rm) {
+          const int q = first_set(rm);
+          rm &= rm - 1;
+          const uint32_t qt = rlu(f[F_TEXT], q);
           if (qt != expect) contiguous = false;
-          expect = qt + (uint32_t)ql;
+          expect = qt + (uint32_t)rl((int)f[F_LEN], q);
         }
       }
       uint32_t dst = ttext;
@@ -1032,43 +1545,100 @@ struct Eng {
         } else {
           w = ttext + (uint32_t)tlen;
         }
-        unsigned long long r = run & ~(1ull << t);
-        while (r) {
-          const int q = first_set(r);
-          r &= r - 1;
-          const uint32_t qt = rlu(s.text, q);
-          const int ql = rl(s.len, q);
+        unsigned long long rm = run & ~(1ull << t);
+        while (rm) {
+          const int q = first_set(rm);
+          rm &= rm - 1;
+          const uint32_t qt = rlu(f[F_TEXT], q);
+          const int ql = rl((int)f[F_LEN], q);
           copy_text(w, qt, (uint32_t)ql);
           w += (uint32_t)ql;
         }
         text_used += need;
       }
       if (lane == t) {
-        seg[c & ~MTB_LEAF].text = dst;
-        seg[c & ~MTB_LEAF].len = total;
+        f[F_TEXT] = dst;
+        f[F_LEN] = (uint32_t)total;
       }
       wsync();
     }
-    // unlink dropped / appended segments, compact the kept ones into hold[]
-    const bool keep = lane < count && kind != 1 && target < 0;
-    if (lane < count && !keep) seg[c & ~MTB_LEAF].parent = MTB_NONE;
+    // unlink dropped / appended segments, compact the kept ones (record-major order) into hold[]
+    const bool keep = s < count && kind != 1 && target < 0;
+    if (s < count && !keep) segp[f[F_ID] & ~MTB_LEAF] = MTB_NONE;
     const unsigned long long km = __ballot(keep);
-    if (keep) sh->hold[nh + rank_below(km)] = c;
+    if (keep) {
+      const uint32_t at = nh + rank_below(km);
+#pragma unroll
+      for (int q = 0; q < 8; q++) sh->hold[q][at] = f[q];
+    }
     wsync();
+    PROF_ADD(PH_SCOUR, ts0);
     return nh + __popcll(km);
+  }
+  // Write hold[.][from, from+n) as the children of block nb (slots 0..n-1, the rest cleared), point the
+  // children at nb and return their observer-view length.
+  __device__ __forceinline__ int place_children(uint32_t nb, int from, int n) {
+    const int fld = lane >> 3, s = lane & 7;
+    uint32_t v = fld == F_ID ? MTB_NONE : 0u;
+    if (s < n) v = sh->hold[fld][from + s];
+    bw(nb)[lane] = v;
+    int ol = 0;
+    if (lane < n) {
+      const uint32_t c = sh->hold[F_ID][from + lane];
+      set_parent(c, nb, lane);
+      ol = child_olen(c, (int)sh->hold[F_LEN][from + lane], (int)sh->hold[F_RSEQ][from + lane]);
+    }
+    const int len = csum8(ol);
+    if (lane == 0) blk[nb].count = (uint32_t)n;
+    wsync();
+    return len;
+  }
+  // Store block P's window-list metadata where it lives (its parent's slot, or its own header).
+  __device__ __forceinline__ void store_meta_of(uint32_t P, uint32_t parent, uint32_t index, uint32_t loff, uint32_t lcnt, uint32_t lcap) {
+    if (lane == 0) {
+      if (parent == MTB_NONE) {
+        blk[P].loff = loff;
+        blk[P].lcnt = lcnt;
+        blk[P].lcap = lcap;
+        if (P == root) {
+          sh->rmeta[0] = loff;
+          sh->rmeta[1] = lcnt;
+          sh->rmeta[2] = lcap;
+        }
+      } else {
+        FBlk& G = blk[parent];
+        G.f[F_SEQ][index] = loff;
+        G.f[F_RSEQ][index] = lcnt;
+        G.f[F_CLI][index] = lcap;
+      }
+    }
+    wsync();
   }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
   __device__ __forceinline__ void pack_parent(uint32_t parent) {
     while (!err) {
-      Blk& P = blk[parent];
-      const int pc = P.count;
-      int nh = 0;
-      for (int i = 0; i < pc; i++) {
-        const uint32_t cb = P.child[i];
-        nh = scour(cb, nh);
-        free_blk(cb);
+      PROF_CNT(CN_PACK, 1);
+      stage_rec(parent);
+      const int pc = sh->zr.count;
+      const uint32_t pparent = sh->zr.parent, pindex = sh->zr.index;
+      const uint32_t kids = lane < pc ? sh->zr.f[F_ID][lane] : MTB_NONE;
+      const uint32_t kloff = lane < pc ? sh->zr.f[F_SEQ][lane] : 0u, kcap = lane < pc ? sh->zr.f[F_CLI][lane] : 0u;
+      // P's own list metadata (its parent's slot, or the root header)
+      uint32_t ploff, pcap;
+      if (pparent == MTB_NONE) {
+        ploff = blk[parent].loff;
+        pcap = blk[parent].lcap;
+      } else {
+        ploff = blk[pparent].f[F_SEQ][pindex];
+        pcap = blk[pparent].f[F_CLI][pindex];
       }
-      wsync();
+      stage_recs(pc, kids);
+      const int nh = scour(pc, 0);
+      if (err) return;
+      for (int i = 0; i < pc; i++) {
+        free_blk(rlu(kids, i));
+        list_free(rlu(kloff, i), rlu(kcap, i));
+      }
       int cc = 0;
       if (nh > 0) {
         cc = nh / (MTB_MAXCH / 2);
@@ -1085,26 +1655,44 @@ struct Eng {
           }
           const uint32_t nb = alloc_blk();
           if (err) return;
-          Blk& N = blk[nb];
-          if (lane < n) {
-            const uint32_t c = sh->hold[taken + lane];
-            N.child[lane] = c;
-            set_parent(c, nb, lane);
+          const int len = place_children(nb, taken, n);
+          bool kblk = false;
+          if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
+          uint32_t a = 0, c2 = 0, e = 0;
+          if (__ballot(kblk)) {
+            rebuild(nb, 0, 0, a, c2, e);
+            if (err) return;
           }
-          N.count = (uint8_t)n;
-          N.parent = parent;
-          N.index = (uint8_t)q;
-          P.child[q] = nb;
+          if (lane == 0) {
+            blk[nb].parent = parent;
+            blk[nb].index = (uint32_t)q;
+            blk[nb].len = len;
+            FBlk& P = blk[parent];
+            P.f[F_ID][q] = nb;
+            P.f[F_LEN][q] = (uint32_t)len;
+            P.f[F_SEQ][q] = a;
+            P.f[F_RSEQ][q] = c2;
+            P.f[F_CLI][q] = e;
+            P.f[F_RCX][q] = 0;
+            P.f[F_PROPS][q] = 0;
+            P.f[F_TEXT][q] = 0;
+          }
           wsync();
           taken += n;
-          rebuild(nb);
         }
       }
-      if (lane < MTB_MAXCH && lane >= cc) P.child[lane] = MTB_NONE;
-      P.count = (uint8_t)cc;
+      {
+        const int fld = lane >> 3, s = lane & 7;
+        if (s >= cc) bw(parent)[lane] = fld == F_ID ? MTB_NONE : 0u;
+      }
+      if (lane == 0) blk[parent].count = (uint32_t)cc;
       wsync();
-      if (cc < MTB_MAXCH / 2 && P.parent != MTB_NONE) {
-        parent = P.parent;
+      uint32_t a, c2, e;
+      rebuild(parent, ploff, pcap, a, c2, e);
+      if (err) return;
+      store_meta_of(parent, pparent, pindex, a, c2, e);
+      if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {
+        parent = pparent;
         continue;
       }
       break;
@@ -1117,24 +1705,20 @@ struct Eng {
       const Lru top = hget(1);
       if (top.maxSeq > minSeq) break;
       heap_get();
-      const uint32_t b = seg[top.seg].parent;
-      if (b != MTB_NONE && blk[b].scour != 0) {
-        const int count = blk[b].count;
-        const int nh = scour(b, 0);
-        Blk& B = blk[b];
-        B.scour = 0;
-        if (nh < count) {
-          if (lane < nh) {
-            const uint32_t c = sh->hold[lane];
-            B.child[lane] = c;
-            if (!(c & MTB_LEAF)) blk[c].index = (uint8_t)lane;
-          }
-          if (lane < MTB_MAXCH && lane >= nh) B.child[lane] = MTB_NONE;
-          B.count = (uint8_t)nh;
-          wsync();
-          if (nh < MTB_MAXCH / 2 && B.parent != MTB_NONE) pack_parent(B.parent);
-        }
-        wsync();
+      const uint32_t b = segp[top.seg];
+      if (b == MTB_NONE) continue;
+      stage_recs(1, b);
+      if (sh->pr[0].scour == 0) continue;
+      const int count = sh->pr[0].count;
+      const uint32_t parent = sh->pr[0].parent;
+      const int nh = scour(1, 0);
+      if (err) return;
+      if (lane == 0) blk[b].scour = 0;
+      wsync();
+      // nh == count: nothing was dropped or appended, the record is unchanged
+      if (nh < count) {
+        place_children(b, 0, nh);
+        if (nh < MTB_MAXCH / 2 && parent != MTB_NONE) pack_parent(parent);
       }
     }
   }
@@ -1147,60 +1731,83 @@ struct Eng {
       zamboni();
     }
   }
+  // block splits requested by the last walk (one call site keeps the split code out of the walk)
+  __device__ __forceinline__ void settle() {
+    if (pending_fix >= 0) {
+      const int d = pending_fix;
+      pending_fix = -1;
+      if (!err) fix_overflow(d);
+    }
+  }
+  __device__ __forceinline__ void zamboni_p() {
+    const uint64_t t0 = PROF_T();
+    zamboni();
+    PROF_ADD(PH_ZAMBONI, t0);
+  }
   __device__ __forceinline__ void apply(const mtb_op& o) {
+    const uint64_t tA = PROF_T();
     memo_old = MTB_NONE;
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)o.client;
     switch (o.type) {
       case MTB_OP_INSERT: {
         ops_applied++;
-        cache_clear();
-        walk((int)o.pos1, R, C, -2, false, 0, 0);  // ensureIntervalBoundary
+        view_clear();
+        uint64_t t0 = PROF_T();
+        walk((int)o.pos1, R, C, -2, false, 0);  // ensureIntervalBoundary
+        settle();
+        PROF_ADD(PH_BOUNDARY, t0);
         if (err) return;
         const bool marker = (o.flags & MTB_F_MARKER) != 0;
         const int len = marker ? 1 : (int)o.pos2;
         if (len > 0) {
+          t0 = PROF_T();
           const uint32_t sid = alloc_seg();
           if (err) return;
-          Seg s;
-          s.len = len;
-          s.seq = S;
-          s.rseq = -1;
-          s.props = o.props ? (MTB_GPROPS | T.pidx[2 * o.props + 1]) : 0;
-          s.text = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
-          s.parent = MTB_NONE;
-          s.rcx = 0;
-          s.client = (int16_t)C;
-          s.rc0 = -1;
-          seg[sid] = s;
+          if (lane < 8) {
+            uint32_t v = 0;
+            if (lane == F_ID) v = MTB_LEAF | sid;
+            if (lane == F_LEN) v = (uint32_t)len;
+            if (lane == F_SEQ) v = (uint32_t)S;
+            if (lane == F_RSEQ) v = (uint32_t)-1;
+            if (lane == F_CLI) v = ((uint32_t)C & 0xFFFF) | 0xFFFF0000u;  // removedClientIds[0] = none
+            if (lane == F_PROPS) v = o.props ? (MTB_GPROPS | sh->tab.pidx[2 * o.props + 1]) : 0;
+            if (lane == F_TEXT) v = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
+            sh->nseg[lane] = v;
+          }
           wsync();
           n_mod += 1;
-          text_bytes += marker ? 0 : 2ull * (uint64_t)len;
-          if (!walk((int)o.pos1, R, C, S, true, sid, len, true)) {
+          text_bytes += marker ? 0u : 2u * (uint32_t)len;
+          if (!walk((int)o.pos1, R, C, S, true, len, true)) {
             fail(DERR_INSERT);
             return;
           }
-          if (S > minSeq) {  // saveIfLocal (mergeTree.ts:1617-1637)
-            const uint32_t pb = seg[sid].parent;
-            lru_add(sid, pb, blk[pb].scour, S);
-          }
+          settle();
+          if (S > minSeq) lru_add(sid, ins_blk, ins_scour, S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          PROF_ADD(PH_INSERT, t0);
         }
-        zamboni();
+        zamboni_p();
         break;
       }
       case MTB_OP_REMOVE:
       case MTB_OP_ANNOTATE: {
         ops_applied++;
-        cache_clear();
-        walk((int)o.pos1, R, C, -2, false, 0, 0);
-        walk((int)o.pos2, R, C, -2, false, 0, 0);
+        view_clear();
+        uint64_t t0 = PROF_T();
+        walk((int)o.pos1, R, C, -2, false, 0);
+        settle();
+        walk((int)o.pos2, R, C, -2, false, 0);
+        settle();
+        PROF_ADD(PH_BOUNDARY, t0);
         if (err) return;
+        t0 = PROF_T();
         node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
-        zamboni();
+        PROF_ADD(PH_NODEMAP, t0);
+        zamboni_p();
         break;
       }
       case MTB_OP_ACK:
-        zamboni();
+        zamboni_p();
         break;
       default:
         break;
@@ -1210,8 +1817,11 @@ struct Eng {
       if (!(curSeq <= S)) { fail(DERR_ASSERT_SEQ); return; }
       curSeq = S;
       if (!((int)o.msn <= S)) { fail(DERR_ASSERT_MSN); return; }
+      const uint64_t t0 = PROF_T();
       set_min_seq((int)o.msn);
+      PROF_ADD(PH_ZAMBONI, t0);
     }
+    PROF_ADD(PH_TOTAL, tA);
   }
 };
 
@@ -1220,33 +1830,34 @@ struct Eng {
 using namespace mtbk;
 
 #ifndef MTB_WAVES_PER_SIMD
-#define MTB_WAVES_PER_SIMD 3
+#define MTB_WAVES_PER_SIMD 4
 #endif
-extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD) mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs,
-                                                                   const mtb_op* ops, Seg* segs, Blk* blks, WEnt* lists,
-                                                                   uint16_t* text, Lru* heap, uint32_t* aux,
-                                                                   uint32_t* freel, Tables tables) {
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                      WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
   __shared__ Scratch sh;
   const uint32_t doc = blockIdx.x;
   if (doc >= ndocs) return;
   DocState* ds = &docs[doc];
   Eng e;
   e.ds = ds;
-  e.seg = segs + ds->seg_base;
+  e.segp = segp + ds->seg_base;
   e.blk = blks + ds->blk_base;
   e.lst = lists + ds->list_base;
-  e.txt = text + ds->text_base;
-  e.heap = heap + ds->heap_base;
   e.aux = aux + ds->aux_base;
-  e.fre = freel + ds->free_base;
-  e.ops = ops + ds->op_base;
-  e.T = tables;
+  Lru* const gheap = heap + ds->heap_base;
+  const mtb_op* const dops = ops + ds->op_base;
+  sh.tab = tables;  // (every lane stores the same values)
+  sh.gheap = gheap;
+  sh.gfree = freel + ds->free_base;
+  sh.gtext = text + ds->text_base;
   e.sh = &sh;
   e.lane = lane_id();
   e.minSeq = ds->min_seq;
   e.curSeq = ds->cur_seq;
   e.root = ds->root;
   e.newMode = ds->new_mode != 0;
+  e.hasNL = (ds->flags & DSF_NEWLINE) != 0;
   e.seg_used = ds->seg_used;
   e.blk_used = ds->blk_used;
   e.free_top = ds->free_top;
@@ -1255,28 +1866,59 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD) mtb_replay_
   e.heap_cnt = ds->heap_cnt;
   e.aux_used = ds->aux_used;
   e.err = ds->err;
-  e.n_mod = ds->n_mod;
-  e.ops_applied = ds->ops_applied;
-  e.text_bytes = ds->text_bytes;
+  e.n_mod = 0;
+  e.ops_applied = 0;
+  e.text_bytes = 0;
   uint32_t k = ds->op_next;
   const uint32_t n = ds->n_ops;
   e.walk_depth = -1;
   e.struct_changed = false;
-  // bring the LRU heap into LDS when it fits
+  e.pending_fix = -1;
+  e.sp_internal = false;
+  sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
+  sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
+  for (int i = 0; i < NPH; i++) e.prof[i] = 0;
+  for (int i = 0; i < NCN; i++) e.evc[i] = 0;
+  // root window-list metadata, the list free heads and the LRU heap (while it fits) into LDS
+  if (e.lane < 3) sh.rmeta[e.lane] = (&e.blk[e.root].loff)[e.lane];
+  if (e.list_used == 0) {
+    if (e.lane < MTB_LCLASSES) sh.lfree[e.lane] = MTB_NONE;
+    e.list_used = MTB_LIST_RESERVED;
+  } else if (e.lane < MTB_LCLASSES) {
+    sh.lfree[e.lane] = reinterpret_cast<const uint32_t*>(e.lst)[e.lane];
+  }
+  if (e.lane == 0) sh.path[0] = e.root;
   e.heap_lds = e.heap_cnt + 1 < MTB_LDS_HEAP;
   if (e.heap_lds)
-    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) sh.heap[i] = e.heap[i];
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) sh.heap[i] = gheap[i];
+  e.view_clear();
   __syncthreads();
   if (k < n) {
-    mtb_op cur = e.ops[k];
+    // op records are read one dword per lane (lanes 0..7), the next one in flight while applying
+    const uint32_t* opw = reinterpret_cast<const uint32_t*>(dops);
+    uint32_t cw = e.lane < 8 ? opw[k * 8 + e.lane] : 0u;
     for (; k < n && !e.err; k++) {
-      const mtb_op nxt = e.ops[k + 1 < n ? k + 1 : k];  // prefetch the next record
+      const uint32_t nk = k + 1 < n ? k + 1 : k;
+      const uint32_t nw = e.lane < 8 ? opw[nk * 8 + e.lane] : 0u;  // prefetch the next record
+      mtb_op cur;
+      const uint32_t w0 = rlu(cw, 0);
+      cur.type = (uint8_t)(w0 & 0xFF);
+      cur.flags = (uint8_t)((w0 >> 8) & 0xFF);
+      cur.client = (uint16_t)(w0 >> 16);
+      cur.seq = rlu(cw, 1);
+      cur.ref_seq = rlu(cw, 2);
+      cur.msn = rlu(cw, 3);
+      cur.pos1 = rlu(cw, 4);
+      cur.pos2 = rlu(cw, 5);
+      cur.payload = rlu(cw, 6);
+      cur.props = rlu(cw, 7);
       e.apply(cur);
-      cur = nxt;
+      cw = nw;
     }
   }
   if (e.heap_lds)
-    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) e.heap[i] = sh.heap[i];
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) gheap[i] = sh.heap[i];
+  if (e.lane < MTB_LCLASSES) reinterpret_cast<uint32_t*>(e.lst)[e.lane] = sh.lfree[e.lane];
   __syncthreads();
   if (e.lane == 0) {
     ds->min_seq = e.minSeq;
@@ -1289,9 +1931,13 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD) mtb_replay_
     ds->text_used = e.text_used;
     ds->heap_cnt = e.heap_cnt;
     ds->aux_used = e.aux_used;
-    ds->n_mod = e.n_mod;
-    ds->ops_applied = e.ops_applied;
-    ds->text_bytes = e.text_bytes;
+    ds->n_mod += e.n_mod;
+    ds->ops_applied += e.ops_applied;
+    ds->text_bytes += e.text_bytes;
+#ifdef MTB_PROFILE
+    for (int i = 0; i < NPH; i++) ds->prof[i] += e.prof[i];
+    for (int i = 0; i < NCN; i++) ds->cnt[i] += e.evc[i];
+#endif
     if (e.err && !ds->err) {
       ds->err = e.err;
       ds->err_op = k;
@@ -1300,18 +1946,19 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD) mtb_replay_
   }
 }
 
-hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, Seg* segs, Blk* blks,
-                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
-  hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segs, blks, lists, text, heap,
+hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                             FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                             Tables tables) {
+  hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
                      aux, freel, tables);
   return hipGetLastError();
 }
 
 // Rewind every document to its post-init state (benchmark / re-replay utility): restores the
-// DocState header, the root block and the initial segment; ops and payload stay resident.
-extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, Seg* segs,
-                                             const Seg* pseg, Blk* blks, const Blk* pblk) {
-  // one 64-lane wave per document: lanes copy the 256-byte header, the root block and the initial segment
+// DocState header, the root block and the initial segment's parent; ops and payload stay resident.
+extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, uint32_t* segp,
+                                             const uint32_t* psegp, FBlk* blks, const FBlk* pblk) {
+  // one 64-lane wave per document: lanes copy the 256-byte header and the 320-byte root block
   const uint32_t i = blockIdx.x;
   const int l = threadIdx.x;
   if (i >= ndocs) return;
@@ -1319,13 +1966,16 @@ extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pri
   uint32_t* dst = reinterpret_cast<uint32_t*>(docs + i);
   dst[l] = src[l];
   const uint64_t bb = pristine[i].blk_base, sb = pristine[i].seg_base;
-  if (l < 16) reinterpret_cast<uint32_t*>(blks + bb)[l] = reinterpret_cast<const uint32_t*>(pblk + i)[l];
-  if (pristine[i].seg_used && l < 8) reinterpret_cast<uint32_t*>(segs + sb)[l] = reinterpret_cast<const uint32_t*>(pseg + i)[l];
+  const uint32_t* ps = reinterpret_cast<const uint32_t*>(pblk + i);
+  uint32_t* bd = reinterpret_cast<uint32_t*>(blks + bb);
+  bd[l] = ps[l];
+  if (l < 16) bd[64 + l] = ps[64 + l];
+  if (pristine[i].seg_used && l == 0) segp[sb] = psegp[i];
 }
 
-hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, Seg* segs,
-                             const Seg* pseg, Blk* blks, const Blk* pblk) {
-  hipLaunchKernelGGL(mtb_rewind_kernel, dim3(ndocs), dim3(64), 0, stream, docs, pristine, ndocs, segs, pseg, blks, pblk);
+hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs, const DocState* pristine, uint32_t* segp,
+                             const uint32_t* psegp, FBlk* blks, const FBlk* pblk) {
+  hipLaunchKernelGGL(mtb_rewind_kernel, dim3(ndocs), dim3(64), 0, stream, docs, pristine, ndocs, segp, psegp, blks, pblk);
   return hipGetLastError();
 }
 
