@@ -54,7 +54,7 @@ def build_napi(force=False):
 
 if __name__ == "__main__":
     if "--variants" in sys.argv:  # occupancy variants for tuning runs (MTB_LIB=...)
-        for w in (2, 3, 4):
+        for w in (4, 5, 6):
             print(build(force=True, out=os.path.join(HERE, f"libmtb_w{w}.so"), defines=[f"MTB_WAVES_PER_SIMD={w}"]))
     print(build(force="--force" in sys.argv))
     print(build_napi(force="--force" in sys.argv))

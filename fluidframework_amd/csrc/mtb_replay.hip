@@ -81,6 +81,16 @@ __device__ __forceinline__ int cscan8(int v) {
 __device__ __forceinline__ int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 __device__ __forceinline__ uint32_t rlu(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
 __device__ __forceinline__ int csum8(int v) { return rl(cscan8(v), 7); }
+// Uniform values read from LDS or from a wave-uniform global address: readfirstlane moves them to
+// SGPRs, so they cost no VGPR and branches on them stay scalar.
+__device__ __forceinline__ int U(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t U(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+template <class T>
+__device__ __forceinline__ T* UP(T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = U((uint32_t)v), hi = U((uint32_t)(v >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -130,10 +140,14 @@ struct Scratch {  // LDS, one per wave
   uint32_t* gfree;             // free-block stack
   uint16_t* gtext;             // UTF-16 text arena
   Rec zr;                      // zamboni / pack / rebuild record
-  Rec pr[MTB_MAXCH];           // scour inputs: the block(s) being scoured (packParent: all siblings)
-  uint32_t hold[8][64];        // scour / pack: kept children, [field][i]
-  uint32_t pk[64];             // props edit scratch
-  uint32_t pv[64];
+  union {
+    Rec pr[MTB_MAXCH];         // scour inputs: the block(s) being scoured (packParent: all siblings)
+    uint32_t hold[8][64];      // scour output: kept children, [field][i] (inputs are in registers by then)
+    struct {
+      uint32_t pk[64];         // props edit scratch (annotate; never live during a scour)
+      uint32_t pv[64];
+    };
+  };
   Lru heap[MTB_LDS_HEAP];      // LRU heap while it fits (index 0 unused)
 };
 
@@ -190,7 +204,7 @@ struct Eng {
     uint32_t b;
     if (free_top > 0) {
       free_top--;
-      b = sh->gfree[free_top];
+      b = U(UP(sh->gfree)[free_top]);
     } else {
       if (blk_used >= ds->blk_cap) { fail(DERR_CAP_BLK); return 0; }
       b = blk_used++;
@@ -208,7 +222,7 @@ struct Eng {
     return b;
   }
   __device__ __forceinline__ void free_blk(uint32_t b) {
-    sh->gfree[free_top] = b;
+    UP(sh->gfree)[free_top] = b;
     free_top++;
   }
   __device__ __forceinline__ uint32_t alloc_aux(uint32_t n) {
@@ -270,24 +284,26 @@ struct Eng {
   // Window-list metadata of the block at depth d of the current path (root: rmeta).
   __device__ __forceinline__ void meta_of(int d, uint32_t& loff, uint32_t& lcnt, uint32_t& lcap) const {
     if (d == 0) {
-      loff = sh->rmeta[0];
-      lcnt = sh->rmeta[1];
-      lcap = sh->rmeta[2];
+      loff = U(sh->rmeta[0]);
+      lcnt = U(sh->rmeta[1]);
+      lcap = U(sh->rmeta[2]);
     } else {
       const View& P = sh->v[d - 1];
-      const int k = sh->slot[d - 1];
-      loff = P.f[F_SEQ][k];
-      lcnt = P.f[F_RSEQ][k];
-      lcap = P.f[F_CLI][k];
+      const int k = U(sh->slot[d - 1]);
+      loff = U(P.f[F_SEQ][k]);
+      lcnt = U(P.f[F_RSEQ][k]);
+      lcap = U(P.f[F_CLI][k]);
     }
   }
   // Fetch block b (depth d of the current path) together with its window list, and compute its
   // children's lengths in the (R, C) view.  Returns the child count.
   __device__ __forceinline__ int load_view(int d, uint32_t b, int R, int C) {
     View& V = sh->v[d];
-    if (V.b == b && V.rlv) return V.count;
-    if (V.b == b) {  // record still valid (e.g. after a segment split): recompute lengths from LDS
-      const int count = V.count;
+    const uint32_t vb = U(V.b);
+    const int vrlv = U(V.rlv);
+    if (vb == b && vrlv) return U(V.count);
+    if (vb == b) {  // record still valid (e.g. after a segment split): recompute lengths from LDS
+      const int count = U(V.count);
       bool segs = true;
       if (lane < count) segs = (V.f[F_ID][lane] & MTB_LEAF) != 0;
       if (__ballot(!segs) == 0) {
@@ -367,9 +383,9 @@ struct Eng {
     cap = list_class_cap(want);
     const int c = list_class(cap);
     if (c < MTB_LCLASSES) {
-      const uint32_t head = sh->lfree[c];
+      const uint32_t head = U(sh->lfree[c]);
       if (head != MTB_NONE) {
-        const uint32_t next = reinterpret_cast<const uint32_t*>(&lst[head])[0];
+        const uint32_t next = U(reinterpret_cast<const uint32_t*>(&lst[head])[0]);
         wsync();
         if (lane == 0) sh->lfree[c] = next;
         wsync();
@@ -389,7 +405,7 @@ struct Eng {
     const int c = list_class(cap);
     if (c >= MTB_LCLASSES) return;
     if (lane == 0) {
-      reinterpret_cast<uint32_t*>(&lst[off])[0] = sh->lfree[c];
+      reinterpret_cast<uint32_t*>(&lst[off])[0] = U(sh->lfree[c]);
       sh->lfree[c] = off;
     }
     wsync();
@@ -538,7 +554,7 @@ struct Eng {
     Rec& Z = sh->zr;
     const uint32_t* src = bw(P);
     const uint32_t w = src[lane];
-    const int count = (int)src[FB_HDR];
+    const int count = U((int)src[FB_HDR]);
     (&Z.f[0][0])[lane] = w;
     wsync();
     // lane (k, s): segment child s of block child k
@@ -674,8 +690,8 @@ struct Eng {
   // (insertingWalk shift, mergeTree.ts:1831-1837).  Updates the record, the view and the parents.
   __device__ __forceinline__ void insert_slot(int d, int k) {
     View& V = sh->v[d];
-    const uint32_t b = V.b;
-    const int count = V.count;
+    const uint32_t b = U(V.b);
+    const int count = U(V.count);
     const int fld = lane >> 3, s = lane & 7;
     uint32_t nv = (&V.f[0][0])[lane];
     if (s == k) nv = sh->nseg[fld];
@@ -706,7 +722,7 @@ struct Eng {
     const uint32_t nb = alloc_blk();
     if (err) return 0;
     View& V = sh->v[level];
-    const uint32_t b = V.b;
+    const uint32_t b = U(V.b);
     const int half = MTB_MAXCH / 2;
     const int fld = lane >> 3, s = lane & 7;
     const uint32_t val = (&V.f[0][0])[lane];
@@ -724,7 +740,7 @@ struct Eng {
     }
     const int lenAll = csum8(ol);
     const int lenL = csum8(lane < half ? ol : 0);
-    const uint32_t vpar = V.parent;
+    const uint32_t vpar = U(V.parent);
     if (lane == 0) {
       blk[b].count = half;
       blk[b].len = lenL;
@@ -739,7 +755,7 @@ struct Eng {
     sp_loffL = sp_lcntL = sp_lcapL = sp_loffR = sp_lcntR = sp_lcapR = 0;
     sp_internal = __ballot(isblk) != 0;  // the halves' lists are rebuilt by the caller
     // the segment placed by the insert walk moves with the right half
-    if (level == ins_depth && ins_slot >= half) {
+    if (level == U(ins_depth) && U(ins_slot) >= half) {
       ins_blk = nb;
       ins_slot -= half;
       ins_scour = -1;
@@ -761,7 +777,7 @@ struct Eng {
   // After inserting into the block at depth d, split every full block on the path; a root split grows
   // the tree by one level (updateRoot, mergeTree.ts:1268-1277).
   __device__ __forceinline__ void fix_overflow(int d) {
-    if (sh->v[d].count >= MTB_MAXCH) fix_overflow_slow(d);
+    if (U(sh->v[d].count) >= MTB_MAXCH) fix_overflow_slow(d);
   }
   // Split every full block on the path, from depth d upwards.  Written as a state machine with a
   // single list-rebuild site (the halves of an internal split, the new root, the parent).
@@ -771,8 +787,8 @@ struct Eng {
     uint32_t b = MTB_NONE, nb = MTB_NONE;
     while (!err) {
       if (phase == 0) {
-        if (sh->v[level].count < MTB_MAXCH) break;
-        b = sh->v[level].b;
+        if (U(sh->v[level].count) < MTB_MAXCH) break;
+        b = U(sh->v[level].b);
         nb = split_block(level);
         if (err) break;
         phase = sp_internal ? 1 : 3;
@@ -814,7 +830,7 @@ struct Eng {
         phase = 5;
       } else {
         // link (b, nb) into the parent at depth level-1, then rebuild the parent's list
-        const int k = sh->slot[L];
+        const int k = U(sh->slot[L]);
         View& P = sh->v[L];
         if (lane == 0) {
           P.f[F_LEN][k] = sp_lenL;
@@ -830,7 +846,7 @@ struct Eng {
         wsync();
         stage_block_child(nb, sp_lenR, sp_loffR, sp_lcntR, sp_lcapR);
         insert_slot(L, k + 1);
-        X = P.b;
+        X = U(P.b);
         meta_of(L, ooff, ocnt, ocap);
         phase = 4;
       }
@@ -880,8 +896,8 @@ struct Eng {
     int d = 0;
     if (resume && walk_depth >= 0 && !struct_changed) {
       d = walk_depth;
-      b = sh->path[d];
-      p = sh->pp[d];
+      b = U(sh->path[d]);
+      p = U(sh->pp[d]);
     }
     walk_depth = -1;
     struct_changed = false;
@@ -924,7 +940,7 @@ struct Eng {
         walk_depth = d;
         if (!insertMode) {
           if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
-          if (V.f[F_TEXT][j] & MTB_MARKER) return true;  // markers never split
+          if (U(V.f[F_TEXT][j]) & MTB_MARKER) return true;  // markers never split
           split_seg(d, j, pjj);
           if (err) return false;
           pending_fix = d;  // (handled by the caller, after the walk)
@@ -941,7 +957,7 @@ struct Eng {
       ins_depth = d;
       ins_slot = at;
       ins_blk = b;
-      ins_scour = V.scour;
+      ins_scour = U(V.scour);
       if (lane == 0) sh->slot[d] = at;
       wsync();
       insert_slot(d, at);
@@ -975,10 +991,15 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
-  __device__ __forceinline__ Lru hget(uint32_t k) const { return heap_lds ? sh->heap[k] : sh->gheap[k]; }
+  __device__ __forceinline__ Lru hget(uint32_t k) const {
+    Lru x = heap_lds ? sh->heap[k] : UP(sh->gheap)[k];
+    x.seg = U(x.seg);
+    x.maxSeq = U(x.maxSeq);
+    return x;
+  }
   __device__ __forceinline__ void hset(uint32_t k, Lru v) {
     if (heap_lds) sh->heap[k] = v;
-    else sh->gheap[k] = v;
+    else UP(sh->gheap)[k] = v;
   }
   __device__ __forceinline__ void heap_spill() {  // LDS -> global slice
     for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) sh->gheap[i] = sh->heap[i];
@@ -1036,7 +1057,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ properties
   __device__ __forceinline__ const uint32_t* props_ptr(uint32_t h) const {
-    return (h & MTB_GPROPS) ? (sh->tab.pool + (h & ~MTB_GPROPS)) : (aux + h);
+    return (h & MTB_GPROPS) ? (UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : (aux + h);
   }
   // matchProperties (properties.ts:71-96) on interned property sets
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
@@ -1062,16 +1083,17 @@ struct Eng {
   // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157).
   // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
   __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
-    if (old == memo_old && memo_new) return memo_new;
+    const uint32_t mo = U(memo_old), mn = U(memo_new);
+    if (old == mo && mn) return mn;
     return props_apply_slow(old, opId, rewrite);
   }
   __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite) {
-    const uint32_t* op = sh->tab.pool + sh->tab.pidx[2 * opId];
-    const uint32_t nop = op[0];
+    const uint32_t* op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * opId]);
+    const uint32_t nop = U(op[0]);
     uint32_t n = 0;
     if (old) {
       const uint32_t* po = props_ptr(old);
-      n = po[0];
+      n = U(po[0]);
       if (n > 64) n = 64;
       for (uint32_t i = lane; i < n; i += 64) {
         sh->pk[i] = po[1 + 2 * i];
@@ -1165,8 +1187,8 @@ struct Eng {
   __device__ __forceinline__ int map_leaf_block(int d, int pos, int start, int end, int S, int C, bool remove, uint32_t opId,
                                 bool rewrite) {
     View& V = sh->v[d];
-    const uint32_t b = V.b;
-    const int count = V.count;
+    const uint32_t b = U(V.b);
+    const int count = U(V.count);
     int rlj = 0;
     if (lane < count) rlj = V.rl[lane];
     const int def = (lane < count && rlj > 0) ? rlj : 0;
@@ -1212,8 +1234,8 @@ struct Eng {
       while (om) {
         const int t = first_set(om);
         om &= om - 1;
-        const uint32_t orcx = V.f[F_RCX][t];
-        const uint32_t oldn = orcx ? aux[orcx] : 0;
+        const uint32_t orcx = U(V.f[F_RCX][t]);
+        const uint32_t oldn = orcx ? U(aux[orcx]) : 0;
         const uint32_t h = alloc_aux(oldn + 2);
         if (err) return 0;
         for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[orcx + 1 + i];
@@ -1247,7 +1269,7 @@ struct Eng {
     // addToLRUSet for the first visited segment (the block's needsScour then becomes true)
     const int t = first_set(vm);
     const uint32_t tid = rlu(id, t);
-    if (S > curSeq && V.scour != 1) {
+    if (S > curSeq && U(V.scour) != 1) {
       if (lane == 0) {
         V.scour = 1;
         blk[b].scour = 1;
@@ -1277,9 +1299,9 @@ struct Eng {
     load_view(0, root, R, C);
     while (!err) {
       View& V = sh->v[d];
-      const int count = V.count;
-      int idx = sh->sidx[d];
-      if (!exiting && idx == 0 && count > 0 && (V.f[F_ID][0] & MTB_LEAF)) {
+      const int count = U(V.count);
+      int idx = U(sh->sidx[d]);
+      if (!exiting && idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
         // a block of segments: every touched segment at once
         pos += map_leaf_block(d, pos, start, end, S, C, remove, opId, rewrite);
         if (err) return;
@@ -1290,11 +1312,11 @@ struct Eng {
       }
       if (exiting || idx >= count) {
         // post-order: flush this block's accumulated observer-length delta into its parent
-        const int a = sh->acc[d];
+        const int a = U(sh->acc[d]);
         if (a != 0) {
           if (d > 0) {
             const int L = d - 1;
-            const int k = sh->slot[L];
+            const int k = U(sh->slot[L]);
             if (lane == 0) {
               const int v = (int)sh->v[L].f[F_LEN][k] + a;
               sh->v[L].f[F_LEN][k] = (uint32_t)v;
@@ -1321,14 +1343,14 @@ struct Eng {
         exiting = true;
         continue;
       }
-      const int len = V.rl[idx];
+      const int len = U(V.rl[idx]);
       if (len == MTB_UNDEF || len == 0) continue;
       const int nextPos = pos + len;
       if (start >= nextPos) {
         pos = nextPos;
         continue;
       }
-      const uint32_t c = V.f[F_ID][idx];
+      const uint32_t c = U(V.f[F_ID][idx]);
       if (c & MTB_LEAF) { fail(DERR_SHAPE); return; }
       if (d + 1 >= MTB_VDEPTH) { fail(DERR_DEPTH); return; }
       if (lane == 0) {
@@ -1345,7 +1367,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
   __device__ __forceinline__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
-    uint16_t* const txt = sh->gtext;
+    uint16_t* const txt = UP(sh->gtext);
     for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
   }
   __device__ __forceinline__ void stage_rec(uint32_t b) {
@@ -1406,8 +1428,9 @@ struct Eng {
       const uint32_t v0 = p[2];
       g.k1 = p[3];
       const uint32_t v1 = p[4];
-      if (g.n >= 1) g.c0 = sh->tab.val_class[v0];
-      if (g.n >= 2) g.c1 = sh->tab.val_class[v1];
+      const uint32_t* vc = UP(sh->tab.val_class);
+      if (g.n >= 1) g.c0 = vc[v0];
+      if (g.n >= 2) g.c1 = vc[v1];
     }
     return g;
   }
@@ -1438,7 +1461,7 @@ struct Eng {
         if (rseq >= 0) kind = rseq > minSeq ? 0 : 1;
         else if ((int)f[F_SEQ] <= minSeq) kind = 2;
         if (kind == 2) {
-          if (hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0) last = sh->gtext[f[F_TEXT] + f[F_LEN] - 1];
+          if (hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0) last = UP(sh->gtext)[f[F_TEXT] + f[F_LEN] - 1];
           g = psig_of(f[F_PROPS]);
         }
       }
@@ -1619,18 +1642,18 @@ struct Eng {
     while (!err) {
       PROF_CNT(CN_PACK, 1);
       stage_rec(parent);
-      const int pc = sh->zr.count;
-      const uint32_t pparent = sh->zr.parent, pindex = sh->zr.index;
+      const int pc = U(sh->zr.count);
+      const uint32_t pparent = U(sh->zr.parent), pindex = U(sh->zr.index);
       const uint32_t kids = lane < pc ? sh->zr.f[F_ID][lane] : MTB_NONE;
       const uint32_t kloff = lane < pc ? sh->zr.f[F_SEQ][lane] : 0u, kcap = lane < pc ? sh->zr.f[F_CLI][lane] : 0u;
       // P's own list metadata (its parent's slot, or the root header)
       uint32_t ploff, pcap;
       if (pparent == MTB_NONE) {
-        ploff = blk[parent].loff;
-        pcap = blk[parent].lcap;
+        ploff = U(blk[parent].loff);
+        pcap = U(blk[parent].lcap);
       } else {
-        ploff = blk[pparent].f[F_SEQ][pindex];
-        pcap = blk[pparent].f[F_CLI][pindex];
+        ploff = U(blk[pparent].f[F_SEQ][pindex]);
+        pcap = U(blk[pparent].f[F_CLI][pindex]);
       }
       stage_recs(pc, kids);
       const int nh = scour(pc, 0);
@@ -1705,12 +1728,12 @@ struct Eng {
       const Lru top = hget(1);
       if (top.maxSeq > minSeq) break;
       heap_get();
-      const uint32_t b = segp[top.seg];
+      const uint32_t b = U(segp[top.seg]);
       if (b == MTB_NONE) continue;
       stage_recs(1, b);
-      if (sh->pr[0].scour == 0) continue;
-      const int count = sh->pr[0].count;
-      const uint32_t parent = sh->pr[0].parent;
+      if (U(sh->pr[0].scour) == 0) continue;
+      const int count = U(sh->pr[0].count);
+      const uint32_t parent = U(sh->pr[0].parent);
       const int nh = scour(1, 0);
       if (err) return;
       if (lane == 0) blk[b].scour = 0;
@@ -1771,7 +1794,7 @@ struct Eng {
             if (lane == F_SEQ) v = (uint32_t)S;
             if (lane == F_RSEQ) v = (uint32_t)-1;
             if (lane == F_CLI) v = ((uint32_t)C & 0xFFFF) | 0xFFFF0000u;  // removedClientIds[0] = none
-            if (lane == F_PROPS) v = o.props ? (MTB_GPROPS | sh->tab.pidx[2 * o.props + 1]) : 0;
+            if (lane == F_PROPS) v = o.props ? (MTB_GPROPS | UP(sh->tab.pidx)[2 * o.props + 1]) : 0;
             if (lane == F_TEXT) v = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
             sh->nseg[lane] = v;
           }
@@ -1783,7 +1806,7 @@ struct Eng {
             return;
           }
           settle();
-          if (S > minSeq) lru_add(sid, ins_blk, ins_scour, S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);  // saveIfLocal (mergeTree.ts:1617-1637)
           PROF_ADD(PH_INSERT, t0);
         }
         zamboni_p();
