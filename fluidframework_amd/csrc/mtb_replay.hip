@@ -96,6 +96,10 @@ __device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ __forceinline__ int first_set(unsigned long long m) { return __ffsll((long long)m) - 1; }
+// Branch hints: block splits, packParent, list re-allocation, overlapping removes, heap spills and errors
+// are rare; marking them lets the register allocator place spill code on those paths.
+#define COLD(x) __builtin_expect(!!(x), 0)
+#define HOT(x) __builtin_expect(!!(x), 1)
 
 __device__ __forceinline__ int cli_client(uint32_t cli) { return (int)(int16_t)(cli & 0xFFFF); }
 __device__ __forceinline__ int cli_rc0(uint32_t cli) { return (int)(int16_t)(cli >> 16); }
@@ -195,6 +199,7 @@ struct Eng {
   __device__ __forceinline__ void fail(int code) {
     if (!err) err = code;
   }
+  __device__ __forceinline__ bool bad() const { return COLD(err != 0); }
   __device__ __forceinline__ uint32_t alloc_seg() {
     if (seg_used >= ds->seg_cap) { fail(DERR_CAP_SEG); return 0; }
     return seg_used++;
@@ -446,7 +451,7 @@ struct Eng {
       n += __popcll(__ballot(keep));
     }
     const uint32_t no = list_alloc(2 * (n + extra), cap);
-    if (err) return 0;
+    if (bad()) return 0;
     uint32_t w = 0;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
@@ -505,7 +510,7 @@ struct Eng {
       }
     }
     unsigned long long m = __ballot(need);
-    wsync();
+    if (COLD(m))
     while (m) {
       const int d = first_set(m);
       m &= m - 1;
@@ -513,7 +518,7 @@ struct Eng {
       meta_of(d, loff, lcnt, lcap);
       uint32_t live, cap;
       const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
-      if (err) return;
+      if (bad()) return;
       if (lane == 0) {
         WEnt e;
         e.seq = seqv;
@@ -610,7 +615,7 @@ struct Eng {
     const uint32_t total = (uint32_t)(nder + novt + ltotal);
     uint32_t cap;
     const uint32_t no = list_alloc(total + total / 2 + 4, cap);
-    if (err) return;
+    if (bad()) return;
     // derived entries: insert (seq, client, +len), removal (removedSeq, rc0, -len)
     uint32_t wp = rank_below(b1) + rank_below(b2);
     if (ne) {
@@ -632,6 +637,7 @@ struct Eng {
     uint32_t wpos = (uint32_t)nder;
     // overlapping removers (rare): (removedSeq, c, OVERLAP, +len), lane by lane
     unsigned long long om = __ballot(nov > 0);
+    if (COLD(om))
     while (om) {
       const int t = first_set(om);
       om &= om - 1;
@@ -720,7 +726,7 @@ struct Eng {
     PROF_CNT(CN_SPLIT, 1);
     struct_changed = true;
     const uint32_t nb = alloc_blk();
-    if (err) return 0;
+    if (bad()) return 0;
     View& V = sh->v[level];
     const uint32_t b = U(V.b);
     const int half = MTB_MAXCH / 2;
@@ -777,7 +783,7 @@ struct Eng {
   // After inserting into the block at depth d, split every full block on the path; a root split grows
   // the tree by one level (updateRoot, mergeTree.ts:1268-1277).
   __device__ __forceinline__ void fix_overflow(int d) {
-    if (U(sh->v[d].count) >= MTB_MAXCH) fix_overflow_slow(d);
+    if (COLD(U(sh->v[d].count) >= MTB_MAXCH)) fix_overflow_slow(d);
   }
   // Split every full block on the path, from depth d upwards.  Written as a state machine with a
   // single list-rebuild site (the halves of an internal split, the new root, the parent).
@@ -942,7 +948,7 @@ struct Eng {
           if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
           if (U(V.f[F_TEXT][j]) & MTB_MARKER) return true;  // markers never split
           split_seg(d, j, pjj);
-          if (err) return false;
+          if (bad()) return false;
           pending_fix = d;  // (handled by the caller, after the walk)
           return true;
         }
@@ -971,7 +977,7 @@ struct Eng {
   // the segment in slot j of the block at depth d is cut at offset `at`; the right half goes to slot j + 1.
   __device__ __forceinline__ void split_seg(int d, int j, int at) {
     const uint32_t r = alloc_seg();
-    if (err) return;
+    if (bad()) return;
     View& V = sh->v[d];
     if (lane < 8) {
       uint32_t v = V.f[lane][j];
@@ -1008,7 +1014,7 @@ struct Eng {
   }
   __device__ __forceinline__ void heap_add(uint32_t s, int maxSeq) {
     if (heap_cnt + 1 >= ds->heap_cap) { fail(DERR_CAP_HEAP); return; }
-    if (heap_lds && heap_cnt + 1 >= MTB_LDS_HEAP) heap_spill();
+    if (COLD(heap_lds && heap_cnt + 1 >= MTB_LDS_HEAP)) heap_spill();
     uint32_t k = ++heap_cnt;
     Lru x;
     x.seg = s;
@@ -1084,7 +1090,7 @@ struct Eng {
   // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
   __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
     const uint32_t mo = U(memo_old), mn = U(memo_new);
-    if (old == mo && mn) return mn;
+    if (HOT(old == mo && mn)) return mn;
     return props_apply_slow(old, opId, rewrite);
   }
   __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite) {
@@ -1168,7 +1174,7 @@ struct Eng {
       }
     }
     const uint32_t h = alloc_aux(1 + 2 * n);
-    if (err) return 0;
+    if (bad()) return 0;
     aux[h] = n;
     for (uint32_t i = lane; i < n; i += 64) {
       aux[h + 1 + 2 * i] = sh->pk[i];
@@ -1231,13 +1237,14 @@ struct Eng {
       // overlapping removes (already removed): append C to removedClientIds (copy-on-write list) and an
       // OVERLAP entry on every ancestor list (no observer-length change)
       unsigned long long om = __ballot(visit && rseq >= 0);
+      if (COLD(om))
       while (om) {
         const int t = first_set(om);
         om &= om - 1;
         const uint32_t orcx = U(V.f[F_RCX][t]);
         const uint32_t oldn = orcx ? U(aux[orcx]) : 0;
         const uint32_t h = alloc_aux(oldn + 2);
-        if (err) return 0;
+        if (bad()) return 0;
         for (uint32_t i = lane; i < oldn; i += 64) aux[h + 1 + i] = aux[orcx + 1 + i];
         if (lane == 0) {
           aux[h] = oldn + 1;
@@ -1247,7 +1254,7 @@ struct Eng {
         }
         wsync();
         append_levels(0, d, rl(rseq, t), C, WK_OVERLAP, rl(len, t));
-        if (err) return 0;
+        if (bad()) return 0;
       }
     } else {
       // annotate: one new property set per distinct old set (memoized per op)
@@ -1256,7 +1263,7 @@ struct Eng {
         const int t = first_set(am);
         const uint32_t old = rlu(props, t);
         const uint32_t np = props_apply(old, opId, rewrite);
-        if (err) return 0;
+        if (bad()) return 0;
         const bool mine = visit && props == old;
         if (mine) {
           V.f[F_PROPS][lane] = np;
@@ -1304,7 +1311,7 @@ struct Eng {
       if (!exiting && idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
         // a block of segments: every touched segment at once
         pos += map_leaf_block(d, pos, start, end, S, C, remove, opId, rewrite);
-        if (err) return;
+        if (bad()) return;
         if (pos >= end) exiting = true;
         idx = count;
         if (lane == 0) sh->sidx[d] = count;
@@ -1657,7 +1664,7 @@ struct Eng {
       }
       stage_recs(pc, kids);
       const int nh = scour(pc, 0);
-      if (err) return;
+      if (bad()) return;
       for (int i = 0; i < pc; i++) {
         free_blk(rlu(kids, i));
         list_free(rlu(kloff, i), rlu(kcap, i));
@@ -1677,14 +1684,14 @@ struct Eng {
             rem--;
           }
           const uint32_t nb = alloc_blk();
-          if (err) return;
+          if (bad()) return;
           const int len = place_children(nb, taken, n);
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
           uint32_t a = 0, c2 = 0, e = 0;
           if (__ballot(kblk)) {
             rebuild(nb, 0, 0, a, c2, e);
-            if (err) return;
+            if (bad()) return;
           }
           if (lane == 0) {
             blk[nb].parent = parent;
@@ -1712,7 +1719,7 @@ struct Eng {
       wsync();
       uint32_t a, c2, e;
       rebuild(parent, ploff, pcap, a, c2, e);
-      if (err) return;
+      if (bad()) return;
       store_meta_of(parent, pparent, pindex, a, c2, e);
       if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {
         parent = pparent;
@@ -1735,13 +1742,13 @@ struct Eng {
       const int count = U(sh->pr[0].count);
       const uint32_t parent = U(sh->pr[0].parent);
       const int nh = scour(1, 0);
-      if (err) return;
+      if (bad()) return;
       if (lane == 0) blk[b].scour = 0;
       wsync();
       // nh == count: nothing was dropped or appended, the record is unchanged
       if (nh < count) {
         place_children(b, 0, nh);
-        if (nh < MTB_MAXCH / 2 && parent != MTB_NONE) pack_parent(parent);
+        if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);
       }
     }
   }
@@ -1756,7 +1763,7 @@ struct Eng {
   }
   // block splits requested by the last walk (one call site keeps the split code out of the walk)
   __device__ __forceinline__ void settle() {
-    if (pending_fix >= 0) {
+    if (COLD(pending_fix >= 0)) {
       const int d = pending_fix;
       pending_fix = -1;
       if (!err) fix_overflow(d);
@@ -1780,13 +1787,13 @@ struct Eng {
         walk((int)o.pos1, R, C, -2, false, 0);  // ensureIntervalBoundary
         settle();
         PROF_ADD(PH_BOUNDARY, t0);
-        if (err) return;
+        if (bad()) return;
         const bool marker = (o.flags & MTB_F_MARKER) != 0;
         const int len = marker ? 1 : (int)o.pos2;
         if (len > 0) {
           t0 = PROF_T();
           const uint32_t sid = alloc_seg();
-          if (err) return;
+          if (bad()) return;
           if (lane < 8) {
             uint32_t v = 0;
             if (lane == F_ID) v = MTB_LEAF | sid;
@@ -1822,7 +1829,7 @@ struct Eng {
         walk((int)o.pos2, R, C, -2, false, 0);
         settle();
         PROF_ADD(PH_BOUNDARY, t0);
-        if (err) return;
+        if (bad()) return;
         t0 = PROF_T();
         node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
         PROF_ADD(PH_NODEMAP, t0);
@@ -1835,7 +1842,7 @@ struct Eng {
       default:
         break;
     }
-    if (err) return;
+    if (bad()) return;
     if (o.flags & MTB_F_LAST) {  // updateSeqNumbers (client.ts:877-887)
       if (!(curSeq <= S)) { fail(DERR_ASSERT_SEQ); return; }
       curSeq = S;
