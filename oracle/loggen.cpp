@@ -80,7 +80,8 @@ static std::vector<std::string> props_table(int nclients, int nkeys) {
   t.push_back("{\"bold\":null}");  // 2
   for (int w = 0; w <= nclients; w++) {   // 3 + w: {"client": tag}
     char buf[64];
-    snprintf(buf, sizeof buf, "{\"client\":\"%c\"}", 'A' + (w % 26));
+    if (w < 26) snprintf(buf, sizeof buf, "{\"client\":\"%c\"}", 'A' + w);
+    else snprintf(buf, sizeof buf, "{\"client\":\"%c%d\"}", 'A' + (w % 26), w / 26);  // unique beyond 26 writers
     t.push_back(buf);
   }
   for (int k = 1; k < nkeys; k++)        // extra keys for annotate-heavy configs
