@@ -496,6 +496,48 @@ void MergeTree::insertSegments(int pos, Seg* seg, int refSeq, int clientId, int 
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
 
+// insertSegments with a batch of segments (mergeTree.ts:1397-1427): one ensureIntervalBoundary, each
+// segment placed by blockInsert at an advancing position (insertPos += cachedLength, :1664-1684), one
+// zamboni at the end.
+void MergeTree::insertSegmentsBatch(int pos, const std::vector<Seg*>& segs, int refSeq, int clientId, int seq) {
+  ensureIntervalBoundary(pos, refSeq, clientId);
+  int insertPos = pos;
+  for (Seg* sg : segs) {
+    if (sg->cachedLength > 0) {
+      blockInsert(insertPos, refSeq, clientId, seq, sg);
+      insertPos += sg->cachedLength;
+    }
+  }
+  if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
+}
+
+// reloadFromSegments (mergeTree.ts:678-721)
+void MergeTree::reloadFromSegments(const std::vector<Seg*>& segs) {
+  if (window.collaborating) fail_assert("0x049", "Trying to reload from segments while collaborating!");
+  const int maxChildren = MaxNodesInBlock - 1;
+  if (segs.empty()) {
+    root = makeBlock(0);
+    return;
+  }
+  std::vector<Node*> nodes(segs.begin(), segs.end());
+  while (true) {
+    const size_t blockCount = (nodes.size() + maxChildren - 1) / maxChildren;
+    std::vector<Node*> blocks;
+    size_t ni = 0;
+    for (size_t bi = 0; bi < blockCount; bi++) {
+      Block* b = makeBlock(0);
+      for (int ci = 0; ci < maxChildren && ni < nodes.size(); ci++, ni++) b->assignChild(nodes[ni], b->childCount++);
+      blockUpdate(b);
+      blocks.push_back(b);
+    }
+    if (blocks.size() == 1) {
+      root = static_cast<Block*>(blocks[0]);
+      return;
+    }
+    nodes = blocks;
+  }
+}
+
 // blockUpdate (mergeTree.ts:2392-2417): cachedLength = sum(nodeTotalLength ?? 0)
 void MergeTree::blockUpdate(Block* b) {
   int len = 0;
@@ -1438,6 +1480,85 @@ std::string Doc::dumpSegments() {
   };
   rec(mt.root);
   return out;
+}
+
+// Client.load -> SnapshotLoader (snapshotLoader.ts:41-257) for SnapshotV1 chunks.
+void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId) {
+  auto findBlob = [&](const std::string& id) -> const std::string& {
+    for (auto& b : blobs)
+      if (b.first == id) return b.second;
+    throw OracleError(-1, "missing blob " + id);
+  };
+  auto num = [](const JVal* v, int dflt) { return v && v->t == JVal::Num ? (int)v->num : dflt; };
+  // specToSegment (snapshotLoader.ts:94-131)
+  auto specToSegment = [&](const JVal& spec) -> Seg* {
+    const bool mergeInfo = spec.t == JVal::Obj && obj_get(spec.obj, u"json") != nullptr;  // hasMergeInfo
+    if (!mergeInfo) {
+      Seg* s = makeSegFromSpec(mt, spec);
+      s->seq = UniversalSeq;
+      s->clientId = NonCollabClient;
+      return s;
+    }
+    Seg* s = makeSegFromSpec(mt, *obj_get(spec.obj, u"json"));
+    const JVal* client = obj_get(spec.obj, u"client");
+    s->clientId = client && client->t == JVal::Str ? getOrAddShortClientId(u16_to_utf8(client->str)) : NonCollabClient;
+    const JVal* seq = obj_get(spec.obj, u"seq");
+    s->seq = seq && seq->t == JVal::Num ? (int)seq->num : UniversalSeq;
+    const JVal* rseq = obj_get(spec.obj, u"removedSeq");
+    if (rseq && rseq->t == JVal::Num) {
+      s->removed = true;
+      s->removedSeq = (int)rseq->num;
+    }
+    const JVal* rc = obj_get(spec.obj, u"removedClient");
+    if (rc && rc->t == JVal::Str) s->removedClientIds = {getOrAddShortClientId(u16_to_utf8(rc->str))};
+    const JVal* rcs = obj_get(spec.obj, u"removedClientIds");
+    if (rcs && rcs->t == JVal::Arr) {
+      s->removedClientIds.clear();
+      for (auto& c : rcs->arr) s->removedClientIds.push_back(getOrAddShortClientId(u16_to_utf8(c.str)));
+    }
+    return s;
+  };
+  // loadHeader (snapshotLoader.ts:133-167)
+  const JVal header = json_parse(findBlob("header"));
+  if (header.t != JVal::Obj) throw OracleError(-8, "header chunk is not an object");
+  const JVal* hsegs = obj_get(header.obj, u"segments");
+  const JVal* md = obj_get(header.obj, u"headerMetadata");
+  if (!hsegs || hsegs->t != JVal::Arr || !md || md->t != JVal::Obj) throw OracleError(-8, "header metadata not available");
+  std::vector<Seg*> segs;
+  for (auto& sp : hsegs->arr) segs.push_back(specToSegment(sp));
+  mt.reloadFromSegments(segs);
+  const int seqNum = num(obj_get(md->obj, u"sequenceNumber"), 0);
+  const int minSeqNum = num(obj_get(md->obj, u"minSequenceNumber"), seqNum);
+  startOrUpdateCollaboration(observerId, minSeqNum, seqNum);
+  // loadBody (snapshotLoader.ts:169-248)
+  const JVal* ocm = obj_get(md->obj, u"orderedChunkMetadata");
+  std::vector<Seg*> body;
+  if (ocm && ocm->t == JVal::Arr) {
+    for (size_t ci = 1; ci < ocm->arr.size(); ci++) {
+      const JVal* id = obj_get(ocm->arr[ci].obj, u"id");
+      const JVal chunk = json_parse(findBlob(u16_to_utf8(id->str)));
+      const JVal* cs = obj_get(chunk.obj, u"segments");
+      if (cs && cs->t == JVal::Arr)
+        for (auto& sp : cs->arr) body.push_back(specToSegment(sp));
+    }
+  }
+  std::vector<Seg*> batch;
+  auto append = [&](const std::vector<Seg*>& v, int cli, int seq) {
+    mt.insertSegmentsBatch(mt.root->cachedLength, v, UniversalSeq, cli, seq);
+  };
+  auto flushBatch = [&] {
+    if (!batch.empty()) append(batch, NonCollabClient, UniversalSeq);
+    batch.clear();
+  };
+  for (Seg* sg : body) {
+    if (sg->clientId == NonCollabClient && sg->seq == UniversalSeq) {
+      batch.push_back(sg);
+    } else {
+      flushBatch();
+      append({sg}, sg->clientId, sg->seq);
+    }
+  }
+  flushBatch();
 }
 
 uint64_t fnv1a64(const std::string& s) {

@@ -156,6 +156,10 @@ class MergeTree {
   void startCollaboration(int localClientId, int minSeq, int currentSeq);
   void setMinSeq(int minSeq);
   void insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq);
+  // insertSegments with several segments (mergeTree.ts:1397-1427 over blockInsert :1594-1685)
+  void insertSegmentsBatch(int pos, const std::vector<Seg*>& segs, int refSeq, int clientId, int seq);
+  // reloadFromSegments (mergeTree.ts:678-721): bottom-up B-tree, MaxNodesInBlock - 1 children per block
+  void reloadFromSegments(const std::vector<Seg*>& segs);
   void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
   void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
   void zamboniSegments();
@@ -231,6 +235,9 @@ class Doc {
   void applyRecord(const Record& r, const uint16_t* text, const std::vector<std::string>& propsJson);
   void applyRecordParsed(const Record& r, const uint16_t* text, const std::vector<std::optional<JVal>>& props);
 
+  // Client.load of a SnapshotV1 summary (snapshotLoader.ts:41-257): header -> reloadFromSegments ->
+  // startOrUpdateCollaboration(observer, minSeq, seq) -> body chunks appended through insertSegments.
+  void loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId);
   // SnapshotV1 (snapshotV1.ts:46-312) -> (blob path, content) list + ISummaryTreeWithStats JSON
   std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);
   // canonical segment dump used for engine parity (one JSON object per line)

@@ -136,5 +136,14 @@ int orc_dump_segments(orc_doc* d, char** out, size_t* len) {
   return guard(d, [&] { *out = dupstr(d->doc.dumpSegments(), len); });
 }
 uint64_t orc_checksum(orc_doc* d) { return fnv1a64(d->doc.dumpSegments()); }
+// Client.load of a SnapshotV1 summary: blobs_json = [[path, content], ...] (as orc_summarize_v1 returns)
+int orc_load_v1(orc_doc* d, const char* blobs_json, size_t len, const char* observer_id) {
+  return guard(d, [&] {
+    JVal v = json_parse(blobs_json, len);
+    std::vector<std::pair<std::string, std::string>> blobs;
+    for (auto& p : v.arr) blobs.push_back({u16_to_utf8(p.arr[0].str), u16_to_utf8(p.arr[1].str)});
+    d->doc.loadV1(blobs, observer_id);
+  });
+}
 
 }  // extern "C"

@@ -50,6 +50,7 @@ def lib():
         L.orc_dump_segments.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_checksum.restype = ctypes.c_uint64
         L.orc_checksum.argtypes = [vp]
+        L.orc_load_v1.argtypes = [vp, cp, sz, cp]
         _LIB = L
     return _LIB
 
@@ -173,6 +174,11 @@ class OracleDoc:
 
     def checksum(self):
         return self._L.orc_checksum(self._h)
+
+    def load_v1(self, blobs, observer_id):
+        """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""
+        raw = json.dumps([list(b) for b in blobs]).encode()
+        self._chk(self._L.orc_load_v1(self._h, raw, len(raw), observer_id.encode()))
 
 
 def msg_from_compact(m):

@@ -143,3 +143,39 @@ def test_group_op_members_share_seq():
     assert o.get_text() == "hello world"
     dump = o.dump_segments().splitlines()
     assert any('"bold":true' in line for line in dump)
+
+
+# ---- SnapshotV1 load (snapshotLoader.ts:41-220) ----
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations",
+                                  "withIntervals"])
+def test_snapshot_v1_load_roundtrip(name):
+    """Loading a committed reference summary and summarizing it again reproduces the same bytes."""
+    blobs = snapshot_fixture(name)
+    o = OracleDoc()
+    o.load_v1(blobs, "snapshot")
+    got = o.summarize_v1(0, 0)
+    assert [list(b) for b in got["blobs"]] == blobs
+
+
+@pytest.mark.parametrize("idx", [0, 4, 11, 18, 25, 29])
+@pytest.mark.parametrize("cut", [16, 40])
+def test_snapshot_v1_load_mid_stream_then_continue(idx, cut):
+    """Summarize an observer after `cut` groups, load the summary into a fresh client, keep replaying:
+    the loaded client matches the reference's golden text after every later group."""
+    name, d = FIXTURES[idx]
+    a = OracleDoc()
+    a.insert_text_local(0, d["initialText"])
+    a.start_collab("A")
+    groups = d["groups"]
+    for g in groups[:cut]:
+        for m in g["msgs"]:
+            a.apply_msg(msg_from_compact(m))
+    blobs = a.summarize_v1()["blobs"]
+    b = OracleDoc()
+    b.load_v1([list(x) for x in blobs], "A")
+    assert b.get_text() == groups[cut - 1]["resultText"]
+    for gi in range(cut, len(groups)):
+        for m in groups[gi]["msgs"]:
+            b.apply_msg(msg_from_compact(m))
+        assert b.get_text() == groups[gi]["resultText"], f"{name}: group {gi}"
