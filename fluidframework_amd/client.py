@@ -99,6 +99,20 @@ class MergeTreeBatch:
         buf = ctypes.create_string_buffer(raw, max(2, len(raw)))
         self._chk(self._L.mtb_doc_init(self._h, doc, buf, len(raw) // 2, observer_long_id.encode(), min_seq, cur_seq))
 
+    def load_v1(self, doc, blobs, observer_long_id="snapshot"):
+        """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""
+        pairs = [(p.encode(), c.encode("utf-8") if isinstance(c, str) else bytes(c)) for p, c in blobs]
+        arr = (_lib.MtbBlob * max(1, len(pairs)))()
+        keep = []
+        for i, (p, c) in enumerate(pairs):
+            buf = ctypes.create_string_buffer(c, max(1, len(c)))
+            keep.append(buf)
+            arr[i].path = p
+            arr[i].content = ctypes.cast(buf, ctypes.c_void_p)
+            arr[i].content_len = len(c)
+        self._chk(self._L.mtb_doc_load_v1(self._h, doc, arr, len(pairs), observer_long_id.encode()))
+        self._dirty = True
+
     def replay(self):
         """Replay every pending op of every document (blocking).  Returns the stats dict."""
         st = _lib.MtbStats()
@@ -218,6 +232,17 @@ class Client:
             raise MergeTreeError(-6, "unsupported: re-keying the observer id")
         self._b.init_doc(self._doc, "".join(self._initial), longClientId, minSeq, currentSeq)
         self.longClientId = longClientId
+
+    def load(self, storage, clientId=None):
+        """Client.load (client.ts:1007) from a SnapshotV1 summary.  `storage` maps blob path -> content (a
+        dict, or [(path, content), ...]); `clientId` is the runtime's client id (the reference falls back
+        to "snapshot", snapshotLoader.ts:154).  The body is appended by the next replay."""
+        if self.longClientId is not None or self._initial:
+            raise MergeTreeError(-1, "document already initialised")
+        blobs = list(storage.items()) if isinstance(storage, dict) else list(storage)
+        longId = clientId if clientId is not None else "snapshot"
+        self._b.load_v1(self._doc, blobs, longId)
+        self.longClientId = longId
 
     def applyMsg(self, msg, local=False):
         if local:

@@ -22,6 +22,20 @@
 #define MTB_UNDEF (-1)
 #define MTB_MARKER 0x80000000u  // Seg.text flag: marker, low bits = refType + 1 (0 = undefined)
 #define MTB_GPROPS 0x80000000u  // props handle flag: batch-global table (else per-doc aux arena)
+#define MTB_NOKEY ((int32_t)0x80000000)
+// Window lists are allocated in power-of-two capacities (8 << class) from the document's list slice;
+// released lists go to a per-class free stack whose heads live in the slice's first 16 words.
+#define MTB_LCLASSES 16
+#define MTB_LIST_RESERVED 4  // WEnt entries (16 words) reserved for the heads
+
+// Internal record type (never accepted from mtb_append_ops): one body segment of a SnapshotV1 load,
+// appended by insertSegments(root length, [segs], UniversalSeq, client, seq) (snapshotLoader.ts:187-220).
+//   client = inserting client (NonCollabClient = 0xFFFE), seq = its seq, ref_seq = removedSeq (0xFFFFFFFF =
+//   none), msn = removedClientIds[0] (0xFFFF = none), pos1 = aux offset of further removers, pos2 = text
+//   length (marker: refType as for inserts), payload = text offset, props = props id.
+#define MTB_OP_LOADSEG 5
+#define MTB_F_LDFIRST 0x10  // first segment of an insertSegments batch: ensureIntervalBoundary at the root length
+#define MTB_F_LDLAST 0x20   // last segment of the batch: zamboniSegments
 
 // ---- device records -------------------------------------------------------------------------
 // A tree node ("fat block", 320 B).  Besides its children's ids it holds the hot fields of every

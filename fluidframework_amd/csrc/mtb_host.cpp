@@ -35,6 +35,9 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables);
+hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                           FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                           Tables tables);
 
 namespace {
 
@@ -173,6 +176,30 @@ struct Interner {
   }
 };
 
+// ------------------------------------------------------------------ SnapshotV1 load image
+// A segment read from a summary chunk by SnapshotLoader.specToSegment (snapshotLoader.ts:94-131).
+struct LoadSeg {
+  uint32_t len = 0;     // cachedLength (markers 1)
+  uint32_t text = 0;    // text offset (header: initial-text arena, body: payload) or MTB_MARKER | (refType + 1)
+  uint32_t props = 0;   // props id (0 = none)
+  int32_t seq = 0;      // UniversalSequenceNumber unless the spec carries merge info
+  int32_t rseq = -1;    // removedSeq, -1 = not removed
+  int16_t client = -2;  // NonCollabClient unless the spec names one
+  int16_t rc0 = -1;     // removedClientIds[0] (-1 = none)
+  uint32_t rcx = 0;     // aux offset of the further removers [n, c1..cn] (0 = none)
+  bool marker = false;
+};
+// The header segments rebuilt as a tree (reloadFromSegments, mergeTree.ts:678-721) with the window
+// lists startCollaboration's recursive combine gives every internal block (partialLengths.ts:256-338),
+// laid out as the device slices hold them.
+struct LoadImage {
+  std::vector<uint32_t> segp;  // parent block of each header segment
+  std::vector<FBlk> blks;
+  std::vector<WEnt> lists;     // entry 0..MTB_LIST_RESERVED-1: the free-list heads
+  std::vector<uint32_t> aux;   // word 0 unused, then the overlapping-remover lists
+  uint32_t root = 0;
+};
+
 // ------------------------------------------------------------------ host mirror of a document
 struct HostDoc {
   std::vector<std::string> longIds;
@@ -186,6 +213,9 @@ struct HostDoc {
   int64_t lastSeq = 0;            // last appended message seq (host-side 0x038 check)
   uint64_t totalOps = 0;          // all records ever appended (capacity sizing)
   uint64_t totalPayload = 0;
+  // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
+  bool loaded = false;
+  LoadImage img;
   // device mirror
   DocState st{};
   bool onDevice = false;
@@ -227,6 +257,18 @@ struct DevBuf {
   }
 };
 
+// A list of (src offset, dst offset, length) chunks moved by one kernel launch.
+struct Chunks {
+  std::vector<uint64_t> src, dst;
+  std::vector<uint32_t> len;
+  void add(uint64_t s, uint64_t d, uint64_t n) {
+    if (!n) return;
+    src.push_back(s);
+    dst.push_back(d);
+    len.push_back((uint32_t)n);
+  }
+};
+
 }  // namespace
 
 struct mtb_batch {
@@ -257,6 +299,9 @@ struct mtb_batch {
   DevBuf<DocState> dPristine;
   DevBuf<uint32_t> dPSeg;
   DevBuf<FBlk> dPBlk;
+  DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
+  Chunks pxSave[4], pxRestore[4];
+  bool residentLoad = false;        // the resident records start with LOADSEG records
   // batched moves: chunk tables and host->device staging
   DevBuf<uint64_t> dMvSrc, dMvDst;
   DevBuf<uint32_t> dMvLen, dStageW;
@@ -383,6 +428,192 @@ void pack_delta(mtb_batch* b, HostDoc& d, const hj::Value& op, mtb_op base, std:
   }
 }
 
+// ------------------------------------------------------------------ SnapshotV1 load (host side)
+// specToSegment (snapshotLoader.ts:94-131) over the segment spec of textSegment.ts / Marker.make: a
+// spec with merge info is {json, client?, seq?, removedSeq?, removedClient?, removedClientIds?}; its
+// client ids are interned in the order they are met.  Text goes to `sink` (offsets are into it).
+LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<uint16_t>& sink) {
+  LoadSeg g;
+  const bool mergeInfo = spec.kind == hj::Value::kObj && member(spec, u"json");
+  const hj::Value& js = mergeInfo ? *member(spec, u"json") : spec;
+  const hj::Value* props = nullptr;
+  const U16* text = nullptr;
+  if (js.kind == hj::Value::kStr) {
+    text = &js.s;
+  } else if (js.kind == hj::Value::kObj && member(js, u"text")) {
+    const hj::Value* tv = member(js, u"text");
+    if (tv->kind != hj::Value::kStr) raise(MTB_E_UNSUPPORTED, "unsupported: non-string text segment");
+    text = &tv->s;
+    props = member(js, u"props");
+  } else if (js.kind == hj::Value::kObj && member(js, u"marker")) {
+    const hj::Value* mk = member(js, u"marker");
+    const hj::Value* rt = mk ? member(*mk, u"refType") : nullptr;
+    g.marker = true;
+    g.len = 1;
+    g.text = MTB_MARKER | ((rt && rt->kind == hj::Value::kNum) ? (uint32_t)rt->n + 1 : 0u);
+    props = member(js, u"props");
+  } else {
+    raise(MTB_E_PARSE, "Unrecognized IJSONSegment type");
+  }
+  if (text) {
+    g.len = (uint32_t)text->size();
+    g.text = (uint32_t)sink.size();
+    sink.insert(sink.end(), text->begin(), text->end());
+  }
+  if (props && props->truthy()) {
+    if (props->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: non-object segment props");
+    g.props = b->in.props(*props);
+  }
+  if (!mergeInfo) return g;  // seq = UniversalSequenceNumber, client = NonCollabClient
+  auto cid = [&](const hj::Value& v) -> int16_t {
+    if (v.kind != hj::Value::kStr) raise(MTB_E_PARSE, "client id in a segment spec is not a string");
+    return (int16_t)d.client(hj::to_utf8(v.s.data(), v.s.size()));
+  };
+  const hj::Value* c = member(spec, u"client");
+  if (c && c->kind == hj::Value::kStr) g.client = cid(*c);
+  const hj::Value* sq = member(spec, u"seq");
+  if (sq && sq->kind == hj::Value::kNum) g.seq = (int32_t)sq->n;
+  const hj::Value* rs = member(spec, u"removedSeq");
+  if (rs && rs->kind == hj::Value::kNum) g.rseq = (int32_t)rs->n;
+  std::vector<int16_t> rcs;
+  const hj::Value* rc = member(spec, u"removedClient");
+  if (rc && rc->kind == hj::Value::kStr) rcs = {cid(*rc)};
+  const hj::Value* rcl = member(spec, u"removedClientIds");
+  if (rcl && rcl->kind == hj::Value::kArr) {
+    rcs.clear();
+    for (auto& x : rcl->items) rcs.push_back(cid(x));
+  }
+  if (!rcs.empty()) g.rc0 = rcs[0];
+  if (rcs.size() > 1) {
+    if (d.img.aux.empty()) d.img.aux.push_back(0);  // aux word 0 means "no list"
+    g.rcx = (uint32_t)d.img.aux.size();
+    d.img.aux.push_back((uint32_t)(rcs.size() - 1));
+    for (size_t i = 1; i < rcs.size(); i++) d.img.aux.push_back((uint32_t)(int32_t)rcs[i]);
+  }
+  return g;
+}
+
+uint32_t seg_cli_word(const LoadSeg& g) { return ((uint32_t)(uint16_t)g.client) | ((uint32_t)(uint16_t)g.rc0 << 16); }
+
+// reloadFromSegments (mergeTree.ts:678-721): the segments bottom-up, MaxNodesInBlock-1 = 7 children per
+// block, followed by startCollaboration's combine of every block (the window list of a block whose
+// children are blocks holds, per child slot, the entries derived from that child's leaves: insert
+// (seq, client, +len) for seq > minSeq, removal (removedSeq, removedClientIds[0], -len) and overlapping
+// removers (removedSeq, c, OVERLAP, +len) for removedSeq > minSeq — the same derivation the kernel's
+// list rebuild uses).
+void build_load_image(mtb_batch* b, HostDoc& d, const std::vector<LoadSeg>& hdr) {
+  LoadImage& im = d.img;
+  if (im.aux.empty()) im.aux.push_back(0);
+  const int32_t minSeq = (int32_t)d.min0;
+  im.segp.assign(hdr.size(), MTB_NONE);
+  im.blks.clear();
+  im.lists.assign(MTB_LIST_RESERVED, WEnt{});
+  for (auto& e : im.lists) e.seq = e.ck = e.delta = e.pad = (int32_t)MTB_NONE;  // empty free-list heads
+  auto blank = [] {
+    FBlk f{};
+    for (int k = 0; k < MTB_MAXCH; k++) f.f[F_ID][k] = MTB_NONE;
+    f.parent = MTB_NONE;
+    f.scour = -1;  // needsScour undefined
+    f.lseq = MTB_NOKEY;
+    return f;
+  };
+  struct Node {
+    uint32_t id;
+    int32_t olen;
+    uint32_t loff = 0, lcnt = 0, lcap = 0;
+    std::vector<WEnt> ents;  // untagged entries of the subtree
+  };
+  auto derived = [&](const LoadSeg& g, std::vector<WEnt>& out) {
+    if (g.seq > minSeq) out.push_back(WEnt{g.seq, (int32_t)WE_KEY((uint32_t)(uint16_t)g.client, WK_MAIN, 0), (int32_t)g.len, 0});
+    if (g.rseq >= 0 && g.rseq > minSeq) {
+      out.push_back(WEnt{g.rseq, (int32_t)WE_KEY((uint32_t)(uint16_t)g.rc0, WK_MAIN, 0), -(int32_t)g.len, 0});
+      if (g.rcx)
+        for (uint32_t i = 0; i < im.aux[g.rcx]; i++)
+          out.push_back(WEnt{g.rseq, (int32_t)WE_KEY(im.aux[g.rcx + 1 + i] & 0xFFFF, WK_OVERLAP, 0), (int32_t)g.len, 0});
+    }
+  };
+  std::vector<Node> level;
+  for (size_t i = 0; i < hdr.size(); i++) {
+    Node n;
+    n.id = MTB_LEAF | (uint32_t)i;
+    n.olen = hdr[i].rseq >= 0 ? 0 : (int32_t)hdr[i].len;  // localNetLength ?? 0
+    derived(hdr[i], n.ents);
+    level.push_back(std::move(n));
+  }
+  const uint32_t maxChildren = MTB_MAXCH - 1;
+  while (true) {
+    std::vector<Node> up;
+    const size_t nb = level.empty() ? 1 : (level.size() + maxChildren - 1) / maxChildren;
+    size_t ni = 0;
+    for (size_t bi = 0; bi < nb; bi++) {
+      const uint32_t id = (uint32_t)im.blks.size();
+      FBlk f = blank();
+      Node n;
+      n.id = id;
+      n.olen = 0;
+      bool internal = false;
+      uint32_t k = 0;
+      for (; k < maxChildren && ni < level.size(); k++, ni++) {
+        Node& c = level[ni];
+        f.f[F_ID][k] = c.id;
+        if (c.id & MTB_LEAF) {
+          const LoadSeg& g = hdr[c.id & ~MTB_LEAF];
+          f.f[F_LEN][k] = g.len;
+          f.f[F_SEQ][k] = (uint32_t)g.seq;
+          f.f[F_RSEQ][k] = (uint32_t)g.rseq;
+          f.f[F_CLI][k] = seg_cli_word(g);
+          f.f[F_RCX][k] = g.rcx;
+          f.f[F_PROPS][k] = g.props ? (MTB_GPROPS | b->in.pidx[2 * g.props + 1]) : 0u;
+          f.f[F_TEXT][k] = g.text;
+          im.segp[c.id & ~MTB_LEAF] = id;
+        } else {
+          internal = true;
+          f.f[F_LEN][k] = (uint32_t)c.olen;
+          f.f[F_SEQ][k] = c.loff;
+          f.f[F_RSEQ][k] = c.lcnt;
+          f.f[F_CLI][k] = c.lcap;
+          im.blks[c.id].parent = id;
+          im.blks[c.id].index = k;
+        }
+        n.olen += c.olen;
+      }
+      f.count = k;
+      f.len = n.olen;
+      if (internal) {
+        // the block's window list: its children's entries tagged with their slot
+        uint32_t cnt = 0;
+        for (size_t j = ni - k; j < ni; j++) cnt += (uint32_t)level[j].ents.size();
+        uint32_t cap = 8;
+        while (cap < cnt + cnt / 2 + 4) cap <<= 1;
+        n.loff = (uint32_t)im.lists.size();
+        n.lcnt = cnt;
+        n.lcap = cap;
+        for (size_t j = ni - k; j < ni; j++)
+          for (WEnt e : level[j].ents) {
+            e.ck |= (int32_t)((j - (ni - k)) << 20);
+            im.lists.push_back(e);
+          }
+        im.lists.resize(n.loff + cap, WEnt{});
+      }
+      for (size_t j = ni - k; j < ni; j++) {
+        n.ents.insert(n.ents.end(), level[j].ents.begin(), level[j].ents.end());
+        std::vector<WEnt>().swap(level[j].ents);
+      }
+      im.blks.push_back(f);
+      up.push_back(std::move(n));
+    }
+    if (up.size() == 1) {
+      im.root = up[0].id;
+      FBlk& r = im.blks[im.root];
+      r.loff = up[0].loff;
+      r.lcnt = up[0].lcnt;
+      r.lcap = up[0].lcap;
+      break;
+    }
+    level = std::move(up);
+  }
+}
+
 // ------------------------------------------------------------------ device management
 void ensure_stream(mtb_batch* b) {
   if (b->stream) return;
@@ -394,17 +625,6 @@ void ensure_stream(mtb_batch* b) {
   HIPCHK(hipEventCreate(&b->ev1));
 }
 
-// A list of (src offset, dst offset, length) chunks moved by one kernel launch.
-struct Chunks {
-  std::vector<uint64_t> src, dst;
-  std::vector<uint32_t> len;
-  void add(uint64_t s, uint64_t d, uint64_t n) {
-    if (!n) return;
-    src.push_back(s);
-    dst.push_back(d);
-    len.push_back((uint32_t)n);
-  }
-};
 void upload_chunks(mtb_batch* b, const Chunks& c) {
   b->dMvSrc.ensure(c.src.size());
   b->dMvDst.ensure(c.dst.size());
@@ -457,6 +677,17 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
   c.text = (uint32_t)(5 * (payload + init) + 4096);
   c.heap = (uint32_t)(n + 256);
   c.aux = (uint32_t)(16 * n + 4096);
+  return c;
+}
+// caps_for plus what a loaded summary already occupies (header segments, blocks, lists, aux words)
+Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
+  Caps c = caps_for(n, payload, d.initText.size());
+  if (d.loaded) {
+    c.seg += (uint32_t)d.img.segp.size();
+    c.blk += (uint32_t)d.img.blks.size() + (uint32_t)d.img.segp.size() / 4;
+    c.list += (uint32_t)d.img.lists.size() * 2;
+    c.aux += (uint32_t)d.img.aux.size();
+  }
   return c;
 }
 bool fits(const DocState& s, const Caps& c) {
@@ -529,19 +760,44 @@ void device_init(mtb_batch* b) {
   std::vector<Caps> want(b->ndocs);
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
-    want[i] = caps_for(d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()), d.initText.size());
+    want[i] = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
   }
   layout(b, want);
   // initial state: root block (+ the detached initial text segment), collaboration started
   std::vector<uint32_t> recs;
   std::vector<uint16_t> texts;
-  Chunks segc, blkc, txtc;
+  Chunks segc, blkc, txtc, lstc, auxc;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
     s.new_mode = b->opts.new_length_calc;
     s.min_seq = (int32_t)d.min0;
     s.cur_seq = (int32_t)d.cur0;
+    if (d.loaded) {
+      // the reloaded header tree, its window lists and overlap lists, and the header text
+      const LoadImage& im = d.img;
+      s.root = im.root;
+      s.blk_used = (uint32_t)im.blks.size();
+      s.seg_used = (uint32_t)im.segp.size();
+      s.list_used = (uint32_t)im.lists.size();
+      s.aux_used = (uint32_t)im.aux.size();
+      s.heap_cnt = 0;
+      s.text_used = (uint32_t)d.initText.size();
+      segc.add(recs.size(), s.seg_base, im.segp.size());
+      recs.insert(recs.end(), im.segp.begin(), im.segp.end());
+      blkc.add(recs.size(), s.blk_base * (sizeof(FBlk) / 4), im.blks.size() * (sizeof(FBlk) / 4));
+      const uint32_t* bwds = reinterpret_cast<const uint32_t*>(im.blks.data());
+      recs.insert(recs.end(), bwds, bwds + im.blks.size() * (sizeof(FBlk) / 4));
+      lstc.add(recs.size(), s.list_base * (sizeof(WEnt) / 4), im.lists.size() * (sizeof(WEnt) / 4));
+      const uint32_t* lwds = reinterpret_cast<const uint32_t*>(im.lists.data());
+      recs.insert(recs.end(), lwds, lwds + im.lists.size() * (sizeof(WEnt) / 4));
+      auxc.add(recs.size(), s.aux_base, im.aux.size());
+      recs.insert(recs.end(), im.aux.begin(), im.aux.end());
+      txtc.add(texts.size(), s.text_base, d.initText.size());
+      texts.insert(texts.end(), d.initText.begin(), d.initText.end());
+      d.onDevice = true;
+      continue;
+    }
     s.root = 0;
     s.blk_used = 1;
     s.aux_used = 1;
@@ -574,8 +830,14 @@ void device_init(mtb_batch* b) {
     recs.insert(recs.end(), w, w + sizeof(FBlk) / 4);
     d.onDevice = true;
   }
-  scatter_words(b, recs, b->dSegs.p, segc);
-  scatter_words(b, recs, b->dBlks.p, blkc);
+  if (!recs.empty()) {  // one upload, then one move per pool
+    b->dStageW.ensure(recs.size());
+    HIPCHK(hipMemcpyAsync(b->dStageW.p, recs.data(), recs.size() * 4, hipMemcpyHostToDevice, b->stream));
+    move_words(b, b->dStageW.p, b->dSegs.p, segc);
+    move_words(b, b->dStageW.p, b->dBlks.p, blkc);
+    move_words(b, b->dStageW.p, b->dLists.p, lstc);
+    move_words(b, b->dStageW.p, b->dAux.p, auxc);
+  }
   scatter_u16(b, texts, b->dText.p, txtc);
   b->dDocs.ensure(b->ndocs);
   b->devInit = true;
@@ -681,6 +943,27 @@ void capture_pristine(mtb_batch* b) {
   }
   move_words(b, b->dBlks.p, b->dPBlk.p, bc);
   move_words(b, b->dSegs.p, b->dPSeg.p, sc);
+  // documents loaded from a summary: their whole initial tree, window lists and overlap lists
+  for (auto& c : b->pxSave) c = Chunks{};
+  for (auto& c : b->pxRestore) c = Chunks{};
+  uint64_t px = 0;
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    if (!b->docs[i].loaded) continue;
+    const DocState& s = b->hst[i];
+    const uint64_t base[4] = {s.blk_base * (sizeof(FBlk) / 4), s.seg_base, s.list_base * (sizeof(WEnt) / 4), s.aux_base};
+    const uint64_t len[4] = {(uint64_t)s.blk_used * (sizeof(FBlk) / 4), s.seg_used, (uint64_t)s.list_used * (sizeof(WEnt) / 4),
+                             s.aux_used};
+    for (int k = 0; k < 4; k++) {
+      b->pxSave[k].add(base[k], px, len[k]);
+      b->pxRestore[k].add(px, base[k], len[k]);
+      px += len[k];
+    }
+  }
+  if (px) {
+    b->dPX.ensure(px);
+    void* pools[4] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p};
+    for (int k = 0; k < 4; k++) move_words(b, pools[k], b->dPX.p, b->pxSave[k]);
+  }
   b->haveRewind = true;
 }
 
@@ -694,9 +977,9 @@ void replay(mtb_batch* b, mtb_stats* out) {
     for (uint32_t i = 0; i < b->ndocs; i++) {
       HostDoc& d = b->docs[i];
       const DocState& s = b->hst[i];
-      Caps need = caps_for(d.totalOps, d.totalPayload + s.text_used, d.initText.size());
+      Caps need = doc_caps(d, d.totalOps, d.totalPayload + s.text_used);
       if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap) {
-        want[i] = caps_for(2 * d.totalOps, 2 * (d.totalPayload + s.text_used), d.initText.size());
+        want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
         grow = true;
       } else {
         want[i] = Caps{0, 0, 0, 0, 0, 0};
@@ -712,6 +995,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
   }
   std::vector<mtb_op> ops;
   ops.reserve(total);
+  bool anyLoad = false;
   std::vector<uint16_t> pay;
   pay.reserve(totalPay);
   Chunks payc;
@@ -732,8 +1016,9 @@ void replay(mtb_batch* b, mtb_stats* out) {
     s.op_base = ops.size();
     s.n_ops = (uint32_t)d.pending.size();
     s.op_next = 0;
+    if (!d.pending.empty() && d.pending[0].type == MTB_OP_LOADSEG) anyLoad = true;
     for (mtb_op o : d.pending) {
-      if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_MARKER)) o.payload += base;
+      if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER)) o.payload += base;
       ops.push_back(o);
     }
   }
@@ -748,7 +1033,11 @@ void replay(mtb_batch* b, mtb_stats* out) {
   t.val_class = b->dValClass.p;
   t.val_falsy = b->dValFalsy.p;
   t.key_rank = b->dKeyRank.p;
+  b->residentLoad = anyLoad;
   HIPCHK(hipEventRecord(b->ev0, b->stream));
+  if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
+    HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                           b->dHeap.p, b->dAux.p, b->dFree.p, t));
   HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                            b->dHeap.p, b->dAux.p, b->dFree.p, t));
   HIPCHK(hipEventRecord(b->ev1, b->stream));
@@ -1150,6 +1439,93 @@ int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_
   });
 }
 
+// Client.load of a SnapshotV1 summary (client.ts:1007 -> SnapshotLoader.initialize, snapshotLoader.ts:41-257).
+int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
+    if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
+    if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
+    auto blob = [&](const std::string& path) -> hj::Value {
+      for (uint32_t i = 0; i < nblobs; i++)
+        if (blobs[i].path && path == blobs[i].path) {
+          if (!blobs[i].content && blobs[i].content_len) raise(MTB_E_ARG, "null blob content");
+          return hj::parse(blobs[i].content ? blobs[i].content : "", blobs[i].content_len);
+        }
+      raise(MTB_E_ARG, "summary blob not found: " + path);
+    };
+    // loadHeader (snapshotLoader.ts:133-167)
+    const hj::Value header = blob("header");
+    const hj::Value* hsegs = member(header, u"segments");
+    const hj::Value* md = member(header, u"headerMetadata");
+    if (!hsegs || hsegs->kind != hj::Value::kArr || !md || md->kind != hj::Value::kObj)
+      raise(MTB_E_PARSE, "header metadata not available");
+    std::vector<LoadSeg> hdr;
+    for (auto& sp : hsegs->items) hdr.push_back(load_spec(b, d, sp, d.initText));
+    auto num = [&](const char16_t* k, double dflt) {
+      const hj::Value* v = member(*md, k);
+      return v && v->kind == hj::Value::kNum ? v->n : dflt;
+    };
+    const double seqNum = num(u"sequenceNumber", 0);
+    const double minSeqNum = num(u"minSequenceNumber", seqNum);
+    if (seqNum < 0 || minSeqNum < 0 || seqNum > 2147483647.0 || minSeqNum > seqNum)
+      raise(MTB_E_PARSE, "invalid header sequence numbers");
+    // startOrUpdateCollaboration(runtime.clientId ?? "snapshot", minSeq, seq) (snapshotLoader.ts:154)
+    d.observer = observer_long_id;
+    d.client(d.observer);
+    d.min0 = (uint32_t)minSeqNum;
+    d.cur0 = (uint32_t)seqNum;
+    d.lastSeq = (int64_t)seqNum;
+    // loadBody (snapshotLoader.ts:169-220): chunks 1.. of orderedChunkMetadata, appended at the end
+    std::vector<LoadSeg> body;
+    const hj::Value* ocm = member(*md, u"orderedChunkMetadata");
+    if (ocm && ocm->kind == hj::Value::kArr)
+      for (size_t ci = 1; ci < ocm->items.size(); ci++) {
+        const hj::Value* id = member(ocm->items[ci], u"id");
+        if (!id || id->kind != hj::Value::kStr) raise(MTB_E_PARSE, "chunk metadata without an id");
+        const hj::Value chunk = blob(hj::to_utf8(id->s.data(), id->s.size()));
+        const hj::Value* cs = member(chunk, u"segments");
+        if (cs && cs->kind == hj::Value::kArr)
+          for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload));
+      }
+    build_load_image(b, d, hdr);
+    // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
+    // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
+    std::vector<mtb_op> recs;
+    size_t i = 0;
+    while (i < body.size()) {
+      const bool universal = body[i].client == -2 && body[i].seq == 0;
+      size_t j = i + 1;
+      if (universal)
+        while (j < body.size() && body[j].client == -2 && body[j].seq == 0) j++;
+      for (size_t k = i; k < j; k++) {
+        const LoadSeg& g = body[k];
+        if (g.rseq >= 0 && g.client != -2)
+          raise(MTB_E_UNSUPPORTED, "unsupported: removed body segment inserted by a collaborating client "
+                                   "(blockUpdateLength's incremental path, mergeTree.ts:2419-2431)");
+        mtb_op r{};
+        r.type = MTB_OP_LOADSEG;
+        r.flags = (uint8_t)((g.marker ? MTB_F_MARKER : 0) | (k == i ? MTB_F_LDFIRST : 0) | (k + 1 == j ? MTB_F_LDLAST : 0));
+        r.client = (uint16_t)g.client;
+        r.seq = (uint32_t)g.seq;
+        r.ref_seq = (uint32_t)g.rseq;
+        r.msn = (uint16_t)g.rc0;
+        r.pos1 = g.rcx;
+        r.pos2 = g.marker ? (g.text & ~MTB_MARKER) - 1 : g.len;  // marker: refType (0xFFFFFFFF = undefined)
+        r.payload = g.marker ? 0 : g.text;
+        r.props = g.props;
+        recs.push_back(r);
+      }
+      i = j;
+    }
+    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
+    d.totalOps += recs.size();
+    d.totalPayload = d.payload.size();
+    d.loaded = true;
+    d.inited = true;
+  });
+}
+
 int mtb_add_client(mtb_batch* b, uint32_t doc, const char* long_id) {
   return guarded(b, [&] { docref(b, doc).client(long_id ? long_id : ""); });
 }
@@ -1248,6 +1624,8 @@ int mtb_rewind(mtb_batch* b) {
     for (auto& d : b->docs)
       if (!d.pending.empty()) raise(MTB_E_ARG, "rewind with pending (unreplayed) ops");
     HIPCHK(mtb_launch_rewind(b->stream, b->ndocs, b->dDocs.p, b->dPristine.p, b->dSegs.p, b->dPSeg.p, b->dBlks.p, b->dPBlk.p));
+    void* pools[4] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p};
+    for (int k = 0; k < 4; k++) move_words(b, b->dPX.p, pools[k], b->pxRestore[k]);
     HIPCHK(hipStreamSynchronize(b->stream));
     b->hst = b->hPristine;
     for (auto& d : b->docs) d.cached = false;
@@ -1265,6 +1643,9 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
     t.val_falsy = b->dValFalsy.p;
     t.key_rank = b->dKeyRank.p;
     HIPCHK(hipEventRecord(b->ev0, b->stream));
+    if (b->residentLoad)
+      HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t));
     HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
     HIPCHK(hipEventRecord(b->ev1, b->stream));

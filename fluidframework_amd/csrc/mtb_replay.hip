@@ -51,11 +51,6 @@ enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, N
 
 #define MTB_LDS_HEAP 128
 #define MTB_VDEPTH 12  // depth of the LDS path cache; 4^12 segments per document is far beyond any input
-#define MTB_NOKEY ((int32_t)0x80000000)
-// Window lists are allocated in power-of-two capacities (8 << class) from the document's list slice;
-// released lists go to a per-class free stack whose heads live in the slice's first 16 words.
-#define MTB_LCLASSES 16
-#define MTB_LIST_RESERVED 4  // WEnt entries (16 words) reserved for the heads
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // Cross-lane hand-off inside the single wave that owns a document.  A wavefront's vector-memory and
@@ -171,6 +166,9 @@ struct Scratch {  // LDS, one per wave
 #define memo_old sh->memo[0]
 #define memo_new sh->memo[1]
 
+// LD: the summary-load variant, which applies only the LOADSEG records at the head of each document's
+// records (mtb_load_kernel); the replay variant never sees one and carries none of that code.
+template <bool LD>
 struct Eng {
   DocState* ds;
   uint32_t* segp;  // parent block of each segment
@@ -191,7 +189,8 @@ struct Eng {
   int walk_depth;               // depth of the leaf-level block reached by the last walk (-1: none)
   bool struct_changed;          // a block split / root growth happened since the last walk started
   bool sp_internal;
-  int pending_fix;              // depth of a block that reached MaxNodesInBlock children (-1: none)
+  int pending_fix;
+  int ld_pos;                   // insertSegments' advancing insert position within a LOADSEG batch              // depth of a block that reached MaxNodesInBlock children (-1: none)
   uint64_t prof[NPH];
   uint32_t evc[NCN];
 
@@ -339,17 +338,21 @@ struct Eng {
     const int hsc = rl((int)h, 3), hlen = rl((int)h, 4);
     wsync();
     PROF_CNT(CN_ENTRIES, lcnt);
-    // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength)
-    if ((uint32_t)lane < lcnt && e0.seq > R) {
+    // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength).  Entries at or
+    // below minSeq sit in the reference's minLength whatever refSeq is, so the scan threshold is
+    // max(refSeq, minSeq) (only a summary load's body inserts, at refSeq 0, ever see refSeq < minSeq).
+    const int Rl = R > minSeq ? R : minSeq;
+    const int Cm = C & 0xFFFF;
+    if ((uint32_t)lane < lcnt && e0.seq > Rl) {
       const int c = e0.ck & 0xFFFF, kind = (e0.ck >> 16) & 0xF;
-      if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[(e0.ck >> 20) & 7], e0.delta);
+      if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e0.ck >> 20) & 7], e0.delta);
     }
     for (uint32_t base = 64; base < lcnt; base += 64) {
       if (base + lane < lcnt) {
         const WEnt e = lst[loff + base + lane];
-        if (e.seq > R) {
+        if (e.seq > Rl) {
           const int c = e.ck & 0xFFFF, kind = (e.ck >> 16) & 0xF;
-          if ((kind == WK_MAIN && c != C) || (kind == WK_OVERLAP && c == C)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
+          if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
         }
       }
     }
@@ -890,6 +893,23 @@ struct Eng {
     view_clear();
   }
 
+  // Window-list entries for a summary segment placed by a LOADSEG insert: blockUpdateLength's combine
+  // (mergeTree.ts:2419-2431) recomputes the path blocks' partials from their leaves, which is what the
+  // derived entries give (the host admits removed body segments only for NonCollabClient, whose inserts
+  // take that path; a client segment's incremental update equals the same entries when unremoved).
+  __device__ __forceinline__ void load_entries(int d, int S, int C) {
+    const int len = (int)U(sh->nseg[F_LEN]);
+    const int rseq = (int)U(sh->nseg[F_RSEQ]);
+    const uint32_t cli = U(sh->nseg[F_CLI]);
+    const uint32_t rcx = U(sh->nseg[F_RCX]);
+    if (S > minSeq) append_levels(0, d, S, C, WK_MAIN, len);
+    if (rseq >= 0 && rseq > minSeq) {
+      append_levels(0, d, rseq, cli_rc0(cli), WK_MAIN, -len);
+      const uint32_t n = rcx ? U(aux[rcx]) : 0u;
+      for (uint32_t i = 0; i < n && !err; i++) append_levels(0, d, rseq, (int)U(aux[rcx + 1 + i]), WK_OVERLAP, len);
+    }
+  }
+
   // ------------------------------------------------------------------ insertingWalk
   // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
   // mode 1: blockInsert of the staged segment sh->nseg (seq S).  Returns false if it was not placed.
@@ -968,7 +988,8 @@ struct Eng {
       wsync();
       insert_slot(d, at);
       add_len_levels(0, d, d, candLen);
-      append_levels(0, d, S, C, WK_MAIN, candLen);
+      if constexpr (LD) load_entries(d, S, C);
+      else append_levels(0, d, S, C, WK_MAIN, candLen);
       pending_fix = d;
       return true;
     }
@@ -1774,11 +1795,58 @@ struct Eng {
     zamboni();
     PROF_ADD(PH_ZAMBONI, t0);
   }
+  // One body segment of a SnapshotV1 load: insertSegments(root length, batch, UniversalSeq, C, S)
+  // (snapshotLoader.ts:201-220, mergeTree.ts:1397-1427): ensureIntervalBoundary at the batch start, the
+  // segment placed at the batch's advancing position in the (refSeq 0, C) view, zamboni at the batch end.
+  __device__ __forceinline__ void apply_loadseg(const mtb_op& o, int S, int C) {
+    view_clear();
+    const bool first = (o.flags & MTB_F_LDFIRST) != 0;
+    if (first) {
+      ld_pos = U(blk[root].len);
+      walk(ld_pos, 0, C, -2, false, 0);
+      settle();
+      if (bad()) return;
+    }
+    const bool marker = (o.flags & MTB_F_MARKER) != 0;
+    const int len = marker ? 1 : (int)o.pos2;
+    const int rseq = (int)o.ref_seq;
+    if (len > 0) {
+      const uint32_t sid = alloc_seg();
+      if (bad()) return;
+      if (lane < 8) {
+        uint32_t v = 0;
+        if (lane == F_ID) v = MTB_LEAF | sid;
+        if (lane == F_LEN) v = (uint32_t)len;
+        if (lane == F_SEQ) v = (uint32_t)S;
+        if (lane == F_RSEQ) v = (uint32_t)rseq;
+        if (lane == F_CLI) v = ((uint32_t)C & 0xFFFF) | (o.msn << 16);
+        if (lane == F_RCX) v = o.pos1;
+        if (lane == F_PROPS) v = o.props ? (MTB_GPROPS | UP(sh->tab.pidx)[2 * o.props + 1]) : 0;
+        if (lane == F_TEXT) v = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
+        sh->nseg[lane] = v;
+      }
+      wsync();
+      n_mod += 1;
+      const bool ok = walk(ld_pos, 0, C, S, true, rseq >= 0 ? 0 : len, first);
+      if (!ok) {
+        fail(DERR_INSERT);
+        return;
+      }
+      settle();
+      if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);
+      ld_pos += len;
+    }
+    if (o.flags & MTB_F_LDLAST) zamboni_p();
+  }
   __device__ __forceinline__ void apply(const mtb_op& o) {
     const uint64_t tA = PROF_T();
     memo_old = MTB_NONE;
     memo_new = 0;
-    const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)o.client;
+    const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)(int16_t)o.client;
+    if constexpr (LD) {
+      apply_loadseg(o, S, C);
+      return;
+    }
     switch (o.type) {
       case MTB_OP_INSERT: {
         ops_applied++;
@@ -1862,14 +1930,14 @@ using namespace mtbk;
 #ifndef MTB_WAVES_PER_SIMD
 #define MTB_WAVES_PER_SIMD 4
 #endif
-extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
-    mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
-                      WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
-  __shared__ Scratch sh;
+template <bool LD>
+__device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops,
+                                           uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap,
+                                           uint32_t* aux, uint32_t* freel, const Tables& tables) {
   const uint32_t doc = blockIdx.x;
   if (doc >= ndocs) return;
   DocState* ds = &docs[doc];
-  Eng e;
+  Eng<LD> e;
   e.ds = ds;
   e.segp = segp + ds->seg_base;
   e.blk = blks + ds->blk_base;
@@ -1904,6 +1972,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   e.walk_depth = -1;
   e.struct_changed = false;
   e.pending_fix = -1;
+  e.ld_pos = 0;
   e.sp_internal = false;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
@@ -1942,6 +2011,9 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
       cur.pos2 = rlu(cw, 5);
       cur.payload = rlu(cw, 6);
       cur.props = rlu(cw, 7);
+      if constexpr (LD) {
+        if (cur.type != MTB_OP_LOADSEG) break;  // the summary body precedes every op
+      }
       e.apply(cur);
       cw = nw;
     }
@@ -1972,14 +2044,35 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
       ds->err = e.err;
       ds->err_op = k;
     }
-    ds->op_next = e.err ? k : n;
+    ds->op_next = k;
   }
+}
+
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                      WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  replay_doc<false>(sh, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
+// SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                    WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  replay_doc<true>(sh, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
 
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables) {
   hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
+                     aux, freel, tables);
+  return hipGetLastError();
+}
+hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                           FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                           Tables tables) {
+  hipLaunchKernelGGL(mtb_load_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
                      aux, freel, tables);
   return hipGetLastError();
 }

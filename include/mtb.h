@@ -9,6 +9,7 @@
  *
  * Interfaces replaced (reference file:line -> entry point here):
  *   Client ctor / startOrUpdateCollaboration   client.ts:107, :1133      -> mtb_batch_create, mtb_doc_init
+ *   Client.load (SnapshotV1 summary)           client.ts:1007            -> mtb_doc_load_v1
  *   Client.applyMsg(ISequencedDocumentMessage) client.ts:858              -> mtb_apply_msg_json (JSON) or
  *                                                                           mtb_append_ops (pre-packed records)
  *   (replay of the appended ops; synchronous in the reference)            -> mtb_replay
@@ -111,6 +112,17 @@ void mtb_free(void* p);
  * and startOrUpdateCollaboration(observer_long_id, min_seq, cur_seq) (client.ts:1133). */
 int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_t n_units,
                  const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq);
+
+/* Client.load of a SnapshotV1 summary (client.ts:1007 -> SnapshotLoader, snapshotLoader.ts:41-257): the
+ * blobs are the summary's [path, content] pairs (as mtb_summarize_v1 returns them; "header" plus the
+ * chunks orderedChunkMetadata names).  The header segments are reloaded into a tree
+ * (reloadFromSegments, mergeTree.ts:678), collaboration starts as startOrUpdateCollaboration(
+ * observer_long_id, minSequenceNumber, sequenceNumber) (the reference passes runtime.clientId ??
+ * "snapshot"), and the body chunks are appended on the GPU by the next replay, ahead of any op applied
+ * after this call.  Instead of mtb_doc_init.  A removed body segment inserted by a collaborating client
+ * is rejected with MTB_E_UNSUPPORTED. */
+int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs,
+                    const char* observer_long_id);
 
 /* Client.applyMsg(msg) with msg = JSON.stringify(ISequencedDocumentMessage).  Validates, interns the
  * long client id and props, packs records and appends them to the document (no GPU work). */

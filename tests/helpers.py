@@ -34,3 +34,104 @@ def first_diff(a, b):
         if x != y:
             return f"line {i}:\n  gpu   : {x[:300]}\n  oracle: {y[:300]}"
     return f"length differs: {len(la)} vs {len(lb)} lines"
+
+
+def records_to_msgs(ops_bytes, n, text_bytes, props_json, long_ids):
+    """Turn packed 32-byte records (mtb_op layout) back into ISequencedDocumentMessages: records sharing a
+    seq up to the one flagged LAST form one message (a GROUP op when there are several)."""
+    import struct
+    text = text_bytes.decode("utf-16-le", "surrogatepass")
+    msgs, cur = [], []
+    for k in range(n):
+        t, fl, c, seq, ref, msn, p1, p2, pay, pr = struct.unpack_from("<BBHIIIIIII", ops_bytes, 32 * k)
+        if t == 0:
+            if fl & 0x02:
+                seg = {"marker": {"refType": p2} if p2 != 0xFFFFFFFF else {}}
+                if pr:
+                    seg["props"] = json.loads(props_json[pr])
+            else:
+                seg = text[pay:pay + p2]
+                if pr or fl & 0x08:
+                    seg = {"text": seg}
+                    if pr:
+                        seg["props"] = json.loads(props_json[pr])
+            op = {"type": 0, "pos1": p1, "seg": seg}
+        elif t in (1, 2):
+            op = {"type": t, "pos1": p1, "pos2": p2}
+            if t == 2:
+                op["props"] = json.loads(props_json[pr])
+                if fl & 0x04:
+                    op["combiningOp"] = {"name": "rewrite"}
+        else:
+            raise ValueError(f"record type {t} has no message form here")
+        cur.append(op)
+        if fl & 0x01:
+            contents = cur[0] if len(cur) == 1 else {"type": 3, "ops": cur}
+            msgs.append({"clientId": long_ids[c], "sequenceNumber": seq, "referenceSequenceNumber": ref,
+                         "minimumSequenceNumber": msn, "type": "op", "contents": contents})
+            cur = []
+    assert not cur, "trailing records without a LAST flag"
+    return msgs
+
+
+def make_v1_summary(seed, n_segments, chunk_len, msn, seq, n_clients=4, p_removed=0.25, p_client=0.0,
+                    client_body=False, client_removed=False):
+    """A constructed SnapshotV1 summary (snapshotV1.ts layout) for load tests: text / marker / props
+    segments; NonCollab segments removed above the MSN by 1-3 clients; optionally segments inserted above
+    the MSN by clients (header only unless `client_body`).  Returns [(path, content), ...]."""
+    import random
+    rng = random.Random(seed)
+    clients = [f"client-{k}" for k in range(n_clients)]
+    segs = []
+    for i in range(n_segments):
+        r = rng.random()
+        if r < 0.1:
+            spec = {"marker": {"refType": rng.choice([0, 1, 2])}, "props": {"markerId": f"m{i}"}}
+            ln = 1
+        else:
+            t = "".join(rng.choice("abcdefgh \n") for _ in range(rng.randint(1, 12)))
+            spec = t if r < 0.75 else {"text": t, "props": rng.choice([{"bold": True}, {"color": "red"}, {"bold": True, "k": 1}])}
+            ln = len(t)
+        segs.append([spec, ln])
+    out = []
+    for i, (spec, ln) in enumerate(segs):
+        u = rng.random()
+        if u < p_removed:
+            rs = rng.randint(msn + 1, seq)
+            rcs = rng.sample(clients, rng.randint(1, 3))
+            out.append(({"json": spec, "removedSeq": rs, "removedClientIds": rcs}, ln))
+        elif u < p_removed + p_client:
+            s = rng.randint(msn + 1, seq)
+            m = {"json": spec, "client": rng.choice(clients), "seq": s}
+            if client_removed and rng.random() < 0.3 and s < seq:
+                m["removedSeq"] = rng.randint(s + 1, seq)
+                m["removedClientIds"] = [rng.choice(clients)]
+            out.append((m, ln))
+        else:
+            out.append((spec, ln))
+    chunks, cur, cur_len = [], [], 0
+    for spec, ln in out:
+        cur.append(spec)
+        cur_len += ln
+        if cur_len >= chunk_len:
+            chunks.append(cur)
+            cur, cur_len = [], 0
+    if cur or not chunks:
+        chunks.append(cur)
+    if not client_body:  # keep client-inserted segments in the header chunk
+        for c in chunks[1:]:
+            for k, spec in enumerate(c):
+                if isinstance(spec, dict) and "client" in spec:
+                    c[k] = spec["json"]
+    ids = ["header"] + [f"body_{k}" for k in range(len(chunks) - 1)]
+    blobs = []
+    start = 0
+    for k, c in enumerate(chunks):
+        o = {"version": "1", "segmentCount": len(c), "length": 0, "segments": c, "startIndex": start}
+        if k == 0:
+            o["headerMetadata"] = {"minSequenceNumber": msn, "sequenceNumber": seq,
+                                   "orderedChunkMetadata": [{"id": x} for x in ids],
+                                   "totalLength": 0, "totalSegmentCount": len(out)}
+        start += len(c)
+        blobs.append([ids[k], json.dumps(o, separators=(",", ":"))])
+    return blobs
