@@ -41,6 +41,8 @@ export declare class MergeTreeBatch {
 export declare class Client {
   insertTextLocal(pos: number, text: string): void;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
+  load(runtime: { clientId?: string } | undefined,
+       storage: { readBlob(path: string): Promise<ArrayBufferLike | Uint8Array | string> }): Promise<{ catchupOpsP: Promise<unknown[]> }>;
   applyMsg(msg: ISequencedDocumentMessage | string, local?: boolean): void;
   getText(start?: number, end?: number): string;
   getLength(): number;

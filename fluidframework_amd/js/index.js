@@ -139,6 +139,28 @@ class Client {
     this.longClientId = longClientId;
   }
 
+  /**
+   * Client.load (client.ts:1007) of a SnapshotV1 summary through SnapshotLoader (snapshotLoader.ts:41):
+   * `storage.readBlob(path)` gives the blob contents (string, Uint8Array or ArrayBuffer);
+   * `runtime.clientId` becomes the observer id ("snapshot" when absent, snapshotLoader.ts:154).  The
+   * header is rebuilt at once; the body chunks are appended by the next flush.  Catch-up ops do not
+   * exist in the V1 format, so `catchupOpsP` resolves to [].
+   */
+  async load(runtime, storage) {
+    if (this.longClientId !== undefined || this.initial) throw new Error("document already initialised");
+    const text = (x) => (typeof x === "string" ? x : Buffer.from(x instanceof ArrayBuffer ? new Uint8Array(x) : x).toString("utf8"));
+    const header = text(await storage.readBlob("header"));
+    const blobs = [["header", header]];
+    const md = JSON.parse(header).headerMetadata;
+    const ids = md && Array.isArray(md.orderedChunkMetadata) ? md.orderedChunkMetadata.slice(1).map((c) => c.id) : [];
+    for (const id of ids) blobs.push([id, text(await storage.readBlob(id))]);
+    const longId = runtime && runtime.clientId !== undefined ? runtime.clientId : "snapshot";
+    native.loadV1(this.batch.handle, this.doc, blobs, longId);
+    this.longClientId = longId;
+    this.batch.dirty = true;
+    return { catchupOpsP: Promise.resolve([]) };
+  }
+
   // ---- op application ---------------------------------------------------------------------------
   /** Client.applyMsg (client.ts:858): `msg` is an ISequencedDocumentMessage (object or JSON text). */
   applyMsg(msg, local = false) {

@@ -175,6 +175,51 @@ static napi_value js_doc_init(napi_env env, napi_callback_info info) {
   return undef(env);
 }
 
+/* loadV1(h, doc, [[path, content], ...], observerLongId)               client.ts:1007, snapshotLoader.ts:41 */
+static napi_value js_load_v1(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc, n = 0;
+  if (!b || !get_u32(env, argv[1], &doc)) return NULL;
+  if (napi_get_array_length(env, argv[2], &n) != napi_ok) {
+    napi_throw_type_error(env, NULL, "expected an array of [path, content] pairs");
+    return NULL;
+  }
+  mtb_blob* blobs = (mtb_blob*)calloc(n ? n : 1, sizeof(mtb_blob));
+  char* id = NULL;
+  int ok = 1;
+  for (uint32_t i = 0; i < n && ok; i++) {
+    napi_value pair, p, c;
+    ok = napi_get_element(env, argv[2], i, &pair) == napi_ok && napi_get_element(env, pair, 0, &p) == napi_ok &&
+         napi_get_element(env, pair, 1, &c) == napi_ok;
+    if (!ok) {
+      napi_throw_type_error(env, NULL, "expected [path, content]");
+      break;
+    }
+    size_t len = 0;
+    blobs[i].path = get_utf8(env, p, NULL);
+    blobs[i].content = blobs[i].path ? get_utf8(env, c, &len) : NULL;
+    blobs[i].content_len = len;
+    ok = blobs[i].path && blobs[i].content;
+  }
+  int rc = 0;
+  if (ok) {
+    id = get_utf8(env, argv[3], NULL);
+    if (id) rc = mtb_doc_load_v1(b, doc, blobs, n, id);
+    else ok = 0;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    free((void*)blobs[i].path);
+    free((void*)blobs[i].content);
+  }
+  free(blobs);
+  free(id);
+  if (!ok) return NULL;
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
 /* applyMsg(h, doc, JSON.stringify(ISequencedDocumentMessage))          client.ts:858 */
 static napi_value js_apply_msg(napi_env env, napi_callback_info info) {
   napi_value argv[3];
@@ -473,7 +518,7 @@ static napi_value init(napi_env env, napi_value exports) {
     const char* name;
     napi_callback fn;
   } fns[] = {
-      {"create", js_create},           {"docInit", js_doc_init},
+      {"create", js_create},           {"docInit", js_doc_init},       {"loadV1", js_load_v1},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

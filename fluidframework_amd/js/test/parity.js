@@ -18,6 +18,16 @@ const zlib = require("zlib");
 const { MergeTreeBatch, native } = require("..");
 
 const GOLDEN = path.join(__dirname, "..", "..", "..", "tests", "golden", "replay");
+const SNAPSHOTS = path.join(__dirname, "..", "..", "..", "tests", "golden", "snapshots_v1");
+
+function snapshotBlobs(name) {
+  return JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(SNAPSHOTS, `${name}.json.gz`))).toString("utf8")).blobs;
+}
+/** IChannelStorageService over [[path, content], ...] */
+function storageOf(blobs) {
+  const m = new Map(blobs);
+  return { readBlob: async (p) => Buffer.from(m.get(p), "utf8"), contains: async (p) => m.has(p) };
+}
 
 function loadFixtures() {
   return fs.readdirSync(GOLDEN).filter((f) => f.endsWith(".json.gz")).sort().map((f) => ({
@@ -34,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId"];
+    "clientLongId", "loadV1"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -52,6 +62,12 @@ function cpuChecks() {
   assert.throws(() => b2.client(0).applyMsg(toMsg(["B", 4, 0, 0, { type: 0, pos1: 0, seg: "y" }])), /0x038/);
   // no CPU fallback
   assert.throws(() => batch.flush(), (e) => e.code === -2);
+  // Client.load packs the summary on the host; the body append still needs the GPU
+  const b3 = new MergeTreeBatch(1);
+  b3.client(0).load(undefined, storageOf(snapshotBlobs("withMarkers"))).then(() => {
+    assert.throws(() => b3.flush(), (e) => e.code === -2);
+    console.log("js cpu checks ok: summary load packed, flush fails with MTB_E_NODEV");
+  }).catch((e) => { console.error(e); process.exit(1); });
   console.log("js cpu checks ok: 30 logs packed, flush fails with MTB_E_NODEV");
 }
 
@@ -83,6 +99,19 @@ async function gpuChecks() {
   assert.strictEqual(c0.getLength(), c0.getText().length);
   assert.strictEqual(c0.getCurrentSeq(), fx[0].log.groups[ngroups - 1].msgs.slice(-1)[0][1]);
   console.log(`js gpu parity ok: ${checked} text checkpoints over ${fx.length} reference logs`);
+  // Client.load: every document's summary loads into a fresh batch and summarizes back to the same bytes
+  const loaded = new MergeTreeBatch(fx.length);
+  const sums = fx.map((_, i) => batch.summarizeV1(i).blobs);
+  for (let i = 0; i < fx.length; i++) await loaded.client(i).load({ clientId: "A" }, storageOf(sums[i]));
+  await loaded.flushAsync();
+  fx.forEach(({ name, log }, i) => {
+    assert.strictEqual(loaded.client(i).getText(), log.groups[ngroups - 1].resultText, `${name}: text after load`);
+    assert.deepStrictEqual(loaded.summarizeV1(i).blobs, sums[i], `${name}: summary after load`);
+  });
+  const ref = new MergeTreeBatch(1);
+  await ref.client(0).load(undefined, storageOf(snapshotBlobs("withMarkers")));
+  assert.deepStrictEqual(ref.summarizeV1(0, 0, 0).blobs, snapshotBlobs("withMarkers"));
+  console.log(`js gpu load ok: ${fx.length} summaries + the withMarkers reference summary round-trip`);
 }
 
 if (process.argv.includes("--cpu")) {

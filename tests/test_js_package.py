@@ -3,7 +3,8 @@
 CPU: the addon loads, exposes one function per C-ABI entry point, packs all 30 reference replay logs
 through Client.applyMsg, keeps the reference's assert text (0x038) and fails loudly without a GPU.
 GPU: node replays the 30 reference logs (client.replay.spec.ts style) and checks the text after every
-group, through both flush() and the thread-pool flushAsync().
+group, through both flush() and the thread-pool flushAsync(); then Client.load(runtime, storage) of
+every document's summary (and of a committed reference summary) summarizes back to the same bytes.
 """
 import os
 import shutil
@@ -31,10 +32,14 @@ def test_js_package_cpu():
     import torch
     if torch.cuda.is_available():
         pytest.skip("a GPU is present (the CPU check expects MTB_E_NODEV)")
-    assert "js cpu checks ok" in _node("--cpu")
+    out = _node("--cpu")
+    assert "js cpu checks ok: 30 logs packed" in out
+    assert "js cpu checks ok: summary load packed" in out
 
 
 @needs_node
 @pytest.mark.gpu
 def test_js_package_replays_reference_logs_on_gpu():
-    assert "js gpu parity ok" in _node()
+    out = _node()
+    assert "js gpu parity ok" in out
+    assert "js gpu load ok" in out
