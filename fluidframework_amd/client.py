@@ -113,6 +113,28 @@ class MergeTreeBatch:
         self._chk(self._L.mtb_doc_load_v1(self._h, doc, arr, len(pairs), observer_long_id.encode()))
         self._dirty = True
 
+    def load_v1_many(self, docs, summaries, observer_long_ids, threads=16):
+        """load_v1 for many documents, parsed on `threads` host threads (mtb_docs_load_v1)."""
+        n = len(docs)
+        arrs, keep = [], []
+        for blobs in summaries:
+            arr = (_lib.MtbBlob * max(1, len(blobs)))()
+            for i, (p, c) in enumerate(blobs):
+                pb = p.encode()
+                cb = c.encode("utf-8") if isinstance(c, str) else bytes(c)
+                buf = ctypes.create_string_buffer(cb, max(1, len(cb)))
+                keep += [pb, buf]
+                arr[i].path = pb
+                arr[i].content = ctypes.cast(buf, ctypes.c_void_p)
+                arr[i].content_len = len(cb)
+            arrs.append(arr)
+        ptrs = (ctypes.POINTER(_lib.MtbBlob) * max(1, n))(*[ctypes.cast(a, ctypes.POINTER(_lib.MtbBlob)) for a in arrs])
+        counts = (ctypes.c_uint32 * max(1, n))(*[len(x) for x in summaries])
+        ids = (ctypes.c_uint32 * max(1, n))(*docs)
+        obs = (ctypes.c_char_p * max(1, n))(*[o.encode() for o in observer_long_ids])
+        self._chk(self._L.mtb_docs_load_v1(self._h, n, ids, ptrs, counts, obs, threads))
+        self._dirty = True
+
     def replay(self):
         """Replay every pending op of every document (blocking).  Returns the stats dict."""
         st = _lib.MtbStats()

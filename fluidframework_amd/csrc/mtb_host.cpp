@@ -15,7 +15,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -149,7 +152,10 @@ struct Interner {
   // props object -> id with (a) op-props list for annotate, (b) property set for insert specs.
   uint32_t props(const hj::Value& obj) {
     if (obj.kind != hj::Value::kObj) raise(MTB_E_PARSE, "props is not an object");
-    std::string js = hj::dump(obj);
+    return props_keyed(hj::dump(obj), obj);
+  }
+  // `js` = hj::dump(obj) (computed by the caller, e.g. outside a lock)
+  uint32_t props_keyed(const std::string& js, const hj::Value& obj) {
     auto it = propsByJson.find(js);
     if (it != propsByJson.end()) return it->second;
     std::vector<std::pair<uint32_t, uint32_t>> kv;
@@ -432,7 +438,13 @@ void pack_delta(mtb_batch* b, HostDoc& d, const hj::Value& op, mtb_op base, std:
 // specToSegment (snapshotLoader.ts:94-131) over the segment spec of textSegment.ts / Marker.make: a
 // spec with merge info is {json, client?, seq?, removedSeq?, removedClient?, removedClientIds?}; its
 // client ids are interned in the order they are met.  Text goes to `sink` (offsets are into it).
-LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<uint16_t>& sink) {
+// Props interning for parallel loads: a per-thread cache in front of the batch's (locked) props table.
+struct PropsCache {
+  std::mutex* mu = nullptr;
+  std::unordered_map<std::string, uint32_t> ids;
+};
+
+LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<uint16_t>& sink, PropsCache* pc) {
   LoadSeg g;
   const bool mergeInfo = spec.kind == hj::Value::kObj && member(spec, u"json");
   const hj::Value& js = mergeInfo ? *member(spec, u"json") : spec;
@@ -462,7 +474,21 @@ LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<u
   }
   if (props && props->truthy()) {
     if (props->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: non-object segment props");
-    g.props = b->in.props(*props);
+    if (pc) {  // parallel loads share the batch's props table
+      std::string js = hj::dump(*props);
+      auto it = pc->ids.find(js);
+      if (it != pc->ids.end()) {
+        g.props = it->second;
+      } else {
+        {
+          std::lock_guard<std::mutex> lk(*pc->mu);
+          g.props = b->in.props_keyed(js, *props);
+        }
+        pc->ids.emplace(std::move(js), g.props);
+      }
+    } else {
+      g.props = b->in.props(*props);
+    }
   }
   if (!mergeInfo) return g;  // seq = UniversalSequenceNumber, client = NonCollabClient
   auto cid = [&](const hj::Value& v) -> int16_t {
@@ -501,7 +527,7 @@ uint32_t seg_cli_word(const LoadSeg& g) { return ((uint32_t)(uint16_t)g.client) 
 // (seq, client, +len) for seq > minSeq, removal (removedSeq, removedClientIds[0], -len) and overlapping
 // removers (removedSeq, c, OVERLAP, +len) for removedSeq > minSeq — the same derivation the kernel's
 // list rebuild uses).
-void build_load_image(mtb_batch* b, HostDoc& d, const std::vector<LoadSeg>& hdr) {
+void build_load_image(HostDoc& d, const std::vector<LoadSeg>& hdr) {
   LoadImage& im = d.img;
   if (im.aux.empty()) im.aux.push_back(0);
   const int32_t minSeq = (int32_t)d.min0;
@@ -563,7 +589,7 @@ void build_load_image(mtb_batch* b, HostDoc& d, const std::vector<LoadSeg>& hdr)
           f.f[F_RSEQ][k] = (uint32_t)g.rseq;
           f.f[F_CLI][k] = seg_cli_word(g);
           f.f[F_RCX][k] = g.rcx;
-          f.f[F_PROPS][k] = g.props ? (MTB_GPROPS | b->in.pidx[2 * g.props + 1]) : 0u;
+          f.f[F_PROPS][k] = g.props;  // props id; resolve_load_props turns it into the device handle
           f.f[F_TEXT][k] = g.text;
           im.segp[c.id & ~MTB_LEAF] = id;
         } else {
@@ -612,6 +638,100 @@ void build_load_image(mtb_batch* b, HostDoc& d, const std::vector<LoadSeg>& hdr)
     }
     level = std::move(up);
   }
+}
+
+// Header segments' props ids -> global property-set handles (after every parallel load has interned).
+void resolve_load_props(mtb_batch* b, HostDoc& d) {
+  for (FBlk& f : d.img.blks)
+    for (uint32_t k = 0; k < f.count; k++)
+      if ((f.f[F_ID][k] & MTB_LEAF) && f.f[F_PROPS][k]) f.f[F_PROPS][k] = MTB_GPROPS | b->in.pidx[2 * f.f[F_PROPS][k] + 1];
+}
+
+// Client.load of one SnapshotV1 summary into the fresh document d (client.ts:1007 -> SnapshotLoader,
+// snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in parallel.
+void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
+              PropsCache* pc) {
+  if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
+  if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
+  if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
+  auto blob = [&](const std::string& path) -> hj::Value {
+    for (uint32_t i = 0; i < nblobs; i++)
+      if (blobs[i].path && path == blobs[i].path) {
+        if (!blobs[i].content && blobs[i].content_len) raise(MTB_E_ARG, "null blob content");
+        return hj::parse(blobs[i].content ? blobs[i].content : "", blobs[i].content_len);
+      }
+    raise(MTB_E_ARG, "summary blob not found: " + path);
+  };
+  // loadHeader (snapshotLoader.ts:133-167)
+  const hj::Value header = blob("header");
+  const hj::Value* hsegs = member(header, u"segments");
+  const hj::Value* md = member(header, u"headerMetadata");
+  if (!hsegs || hsegs->kind != hj::Value::kArr || !md || md->kind != hj::Value::kObj)
+    raise(MTB_E_PARSE, "header metadata not available");
+  std::vector<LoadSeg> hdr;
+  hdr.reserve(hsegs->items.size());
+  for (auto& sp : hsegs->items) hdr.push_back(load_spec(b, d, sp, d.initText, pc));
+  auto num = [&](const char16_t* k, double dflt) {
+    const hj::Value* v = member(*md, k);
+    return v && v->kind == hj::Value::kNum ? v->n : dflt;
+  };
+  const double seqNum = num(u"sequenceNumber", 0);
+  const double minSeqNum = num(u"minSequenceNumber", seqNum);
+  if (seqNum < 0 || minSeqNum < 0 || seqNum > 2147483647.0 || minSeqNum > seqNum)
+    raise(MTB_E_PARSE, "invalid header sequence numbers");
+  // startOrUpdateCollaboration(runtime.clientId ?? "snapshot", minSeq, seq) (snapshotLoader.ts:154)
+  d.observer = observer_long_id;
+  d.client(d.observer);
+  d.min0 = (uint32_t)minSeqNum;
+  d.cur0 = (uint32_t)seqNum;
+  d.lastSeq = (int64_t)seqNum;
+  // loadBody (snapshotLoader.ts:169-220): chunks 1.. of orderedChunkMetadata, appended at the end
+  std::vector<LoadSeg> body;
+  const hj::Value* ocm = member(*md, u"orderedChunkMetadata");
+  if (ocm && ocm->kind == hj::Value::kArr)
+    for (size_t ci = 1; ci < ocm->items.size(); ci++) {
+      const hj::Value* id = member(ocm->items[ci], u"id");
+      if (!id || id->kind != hj::Value::kStr) raise(MTB_E_PARSE, "chunk metadata without an id");
+      const hj::Value chunk = blob(hj::to_utf8(id->s.data(), id->s.size()));
+      const hj::Value* cs = member(chunk, u"segments");
+      if (cs && cs->kind == hj::Value::kArr)
+        for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload, pc));
+    }
+  build_load_image(d, hdr);
+  // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
+  // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
+  std::vector<mtb_op>& recs = d.pending;
+  recs.reserve(body.size());
+  size_t i = 0;
+  while (i < body.size()) {
+    const bool universal = body[i].client == -2 && body[i].seq == 0;
+    size_t j = i + 1;
+    if (universal)
+      while (j < body.size() && body[j].client == -2 && body[j].seq == 0) j++;
+    for (size_t k = i; k < j; k++) {
+      const LoadSeg& g = body[k];
+      if (g.rseq >= 0 && g.client != -2)
+        raise(MTB_E_UNSUPPORTED, "unsupported: removed body segment inserted by a collaborating client "
+                                 "(blockUpdateLength's incremental path, mergeTree.ts:2419-2431)");
+      mtb_op r{};
+      r.type = MTB_OP_LOADSEG;
+      r.flags = (uint8_t)((g.marker ? MTB_F_MARKER : 0) | (k == i ? MTB_F_LDFIRST : 0) | (k + 1 == j ? MTB_F_LDLAST : 0));
+      r.client = (uint16_t)g.client;
+      r.seq = (uint32_t)g.seq;
+      r.ref_seq = (uint32_t)g.rseq;
+      r.msn = (uint16_t)g.rc0;
+      r.pos1 = g.rcx;
+      r.pos2 = g.marker ? (g.text & ~MTB_MARKER) - 1 : g.len;  // marker: refType (0xFFFFFFFF = undefined)
+      r.payload = g.marker ? 0 : g.text;
+      r.props = g.props;
+      recs.push_back(r);
+    }
+    i = j;
+  }
+  d.totalOps += recs.size();
+  d.totalPayload = d.payload.size();
+  d.loaded = true;
+  d.inited = true;
 }
 
 // ------------------------------------------------------------------ device management
@@ -1443,86 +1563,62 @@ int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_
 int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
-    if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
-    if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
-    if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
-    auto blob = [&](const std::string& path) -> hj::Value {
-      for (uint32_t i = 0; i < nblobs; i++)
-        if (blobs[i].path && path == blobs[i].path) {
-          if (!blobs[i].content && blobs[i].content_len) raise(MTB_E_ARG, "null blob content");
-          return hj::parse(blobs[i].content ? blobs[i].content : "", blobs[i].content_len);
-        }
-      raise(MTB_E_ARG, "summary blob not found: " + path);
-    };
-    // loadHeader (snapshotLoader.ts:133-167)
-    const hj::Value header = blob("header");
-    const hj::Value* hsegs = member(header, u"segments");
-    const hj::Value* md = member(header, u"headerMetadata");
-    if (!hsegs || hsegs->kind != hj::Value::kArr || !md || md->kind != hj::Value::kObj)
-      raise(MTB_E_PARSE, "header metadata not available");
-    std::vector<LoadSeg> hdr;
-    for (auto& sp : hsegs->items) hdr.push_back(load_spec(b, d, sp, d.initText));
-    auto num = [&](const char16_t* k, double dflt) {
-      const hj::Value* v = member(*md, k);
-      return v && v->kind == hj::Value::kNum ? v->n : dflt;
-    };
-    const double seqNum = num(u"sequenceNumber", 0);
-    const double minSeqNum = num(u"minSequenceNumber", seqNum);
-    if (seqNum < 0 || minSeqNum < 0 || seqNum > 2147483647.0 || minSeqNum > seqNum)
-      raise(MTB_E_PARSE, "invalid header sequence numbers");
-    // startOrUpdateCollaboration(runtime.clientId ?? "snapshot", minSeq, seq) (snapshotLoader.ts:154)
-    d.observer = observer_long_id;
-    d.client(d.observer);
-    d.min0 = (uint32_t)minSeqNum;
-    d.cur0 = (uint32_t)seqNum;
-    d.lastSeq = (int64_t)seqNum;
-    // loadBody (snapshotLoader.ts:169-220): chunks 1.. of orderedChunkMetadata, appended at the end
-    std::vector<LoadSeg> body;
-    const hj::Value* ocm = member(*md, u"orderedChunkMetadata");
-    if (ocm && ocm->kind == hj::Value::kArr)
-      for (size_t ci = 1; ci < ocm->items.size(); ci++) {
-        const hj::Value* id = member(ocm->items[ci], u"id");
-        if (!id || id->kind != hj::Value::kStr) raise(MTB_E_PARSE, "chunk metadata without an id");
-        const hj::Value chunk = blob(hj::to_utf8(id->s.data(), id->s.size()));
-        const hj::Value* cs = member(chunk, u"segments");
-        if (cs && cs->kind == hj::Value::kArr)
-          for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload));
-      }
-    build_load_image(b, d, hdr);
-    // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
-    // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
-    std::vector<mtb_op> recs;
-    size_t i = 0;
-    while (i < body.size()) {
-      const bool universal = body[i].client == -2 && body[i].seq == 0;
-      size_t j = i + 1;
-      if (universal)
-        while (j < body.size() && body[j].client == -2 && body[j].seq == 0) j++;
-      for (size_t k = i; k < j; k++) {
-        const LoadSeg& g = body[k];
-        if (g.rseq >= 0 && g.client != -2)
-          raise(MTB_E_UNSUPPORTED, "unsupported: removed body segment inserted by a collaborating client "
-                                   "(blockUpdateLength's incremental path, mergeTree.ts:2419-2431)");
-        mtb_op r{};
-        r.type = MTB_OP_LOADSEG;
-        r.flags = (uint8_t)((g.marker ? MTB_F_MARKER : 0) | (k == i ? MTB_F_LDFIRST : 0) | (k + 1 == j ? MTB_F_LDLAST : 0));
-        r.client = (uint16_t)g.client;
-        r.seq = (uint32_t)g.seq;
-        r.ref_seq = (uint32_t)g.rseq;
-        r.msn = (uint16_t)g.rc0;
-        r.pos1 = g.rcx;
-        r.pos2 = g.marker ? (g.text & ~MTB_MARKER) - 1 : g.len;  // marker: refType (0xFFFFFFFF = undefined)
-        r.payload = g.marker ? 0 : g.text;
-        r.props = g.props;
-        recs.push_back(r);
-      }
-      i = j;
+    try {
+      load_one(b, d, blobs, nblobs, observer_long_id, nullptr);
+    } catch (...) {
+      if (!d.onDevice) d = HostDoc{};  // leave the slot fresh
+      throw;
     }
-    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
-    d.totalOps += recs.size();
-    d.totalPayload = d.payload.size();
-    d.loaded = true;
-    d.inited = true;
+    resolve_load_props(b, d);
+  });
+}
+
+// Many documents at once: blobs are parsed and headers rebuilt on `threads` host threads (the batch's
+// props table is shared under a lock).  On failure the first failing document's error is returned and
+// that document (and every other failing one) is left fresh; the others are loaded.
+int mtb_docs_load_v1(mtb_batch* b, uint32_t n, const uint32_t* docs, const mtb_blob* const* blobs,
+                     const uint32_t* nblobs, const char* const* observer_long_ids, uint32_t threads) {
+  return guarded(b, [&] {
+    if (n && (!docs || !blobs || !nblobs || !observer_long_ids)) raise(MTB_E_ARG, "null argument");
+    for (uint32_t i = 0; i < n; i++) docref(b, docs[i]);
+    std::vector<uint8_t> seen(b->ndocs, 0);
+    for (uint32_t i = 0; i < n; i++) {
+      if (seen[docs[i]]) raise(MTB_E_ARG, "document listed twice");
+      seen[docs[i]] = 1;
+    }
+    std::mutex mu;
+    std::atomic<uint32_t> next{0};
+    std::vector<int> codes(n, 0);
+    std::vector<std::string> msgs(n);
+    auto work = [&] {
+      PropsCache pc;
+      pc.mu = &mu;
+      for (uint32_t i = next++; i < n; i = next++) {
+        HostDoc& d = b->docs[docs[i]];
+        try {
+          load_one(b, d, blobs[i], nblobs[i], observer_long_ids[i], &pc);
+        } catch (const MtbError& e) {
+          codes[i] = e.code;
+          msgs[i] = e.msg;
+        } catch (const hj::ParseError& e) {
+          codes[i] = MTB_E_PARSE;
+          msgs[i] = std::string("JSON: ") + e.what();
+        } catch (const std::exception& e) {
+          codes[i] = MTB_E_ARG;
+          msgs[i] = e.what();
+        }
+        if (codes[i] && !d.onDevice) d = HostDoc{};
+      }
+    };
+    const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, n));
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+    for (uint32_t i = 0; i < n; i++)
+      if (!codes[i]) resolve_load_props(b, b->docs[docs[i]]);
+    for (uint32_t i = 0; i < n; i++)
+      if (codes[i]) raise(codes[i], "document " + std::to_string(docs[i]) + ": " + msgs[i]);
   });
 }
 

@@ -123,6 +123,11 @@ int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_
  * is rejected with MTB_E_UNSUPPORTED. */
 int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs,
                     const char* observer_long_id);
+/* mtb_doc_load_v1 for n documents at once, the blobs parsed and the headers rebuilt on `threads` host
+ * threads (no reference counterpart: the reference loads one channel at a time).  Documents whose load
+ * fails are left fresh; the first failure's error is returned. */
+int mtb_docs_load_v1(mtb_batch* b, uint32_t n, const uint32_t* docs, const mtb_blob* const* blobs,
+                     const uint32_t* nblobs, const char* const* observer_long_ids, uint32_t threads);
 
 /* Client.applyMsg(msg) with msg = JSON.stringify(ISequencedDocumentMessage).  Validates, interns the
  * long client id and props, packs records and appends them to the document (no GPU work). */

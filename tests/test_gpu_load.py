@@ -153,10 +153,12 @@ def test_constructed_summaries_with_removals_in_header_and_body(new_mode):
     from pyoracle import OracleDoc
     n = 16
     B = _batch(n, new_length_calc=new_mode)
-    oracles, tails = [], []
+    oracles, tails, sums = [], [], []
     for i in range(n):
-        blobs = make_v1_summary(100 + i, 300 + 40 * i, 250, 10, 40, p_removed=0.3)
-        B[i].load(blobs, "obs")
+        sums.append(make_v1_summary(100 + i, 300 + 40 * i, 250, 10, 40, p_removed=0.3))
+    B.load_v1_many(list(range(n)), sums, ["obs"] * n, threads=4)  # the parallel host path
+    for i in range(n):
+        blobs = sums[i]
         o = OracleDoc(new_length_calc=new_mode)
         o.load_v1(blobs, "obs")
         oracles.append(o)

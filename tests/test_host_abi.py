@@ -91,9 +91,9 @@ def test_packed_records_replay_to_golden_text(idx):
     assert o.get_text() == d["groups"][-1]["resultText"], name
 
 
-def _has_client(B, i):
+def _has_client(B, i, doc=0):
     try:
-        B.client_long_id(0, i)
+        B.client_long_id(doc, i)
         return True
     except Exception:
         return False
@@ -166,3 +166,35 @@ def test_summary_load_interns_header_clients_first():
     B[0].load(blobs, "obs")
     got = [B.client_long_id(0, k) for k in range(len(order) + 1)]
     assert got == order + ["obs"]
+
+
+def test_parallel_summary_load_packs_like_single_loads():
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from helpers import make_v1_summary, snapshot_fixture
+    sums = [make_v1_summary(s, 300, 200, 10, 40, p_removed=0.3, p_client=0.1) for s in range(12)]
+    sums.append(snapshot_fixture("withAnnotations"))
+    A = MergeTreeBatch(len(sums))
+    for i, bl in enumerate(sums):
+        A.load_v1(i, bl, "obs")
+    B = MergeTreeBatch(len(sums))
+    B.load_v1_many(list(range(len(sums))), sums, ["obs"] * len(sums), threads=6)
+    def recs(M, i):  # props ids depend on interning order (threads): compare their JSON
+        import struct
+        ops, n, payload = M.export_pending(i)
+        out = []
+        for k in range(n):
+            r = list(struct.unpack_from("<BBHIIIIIII", ops, 32 * k))
+            r[9] = M.props_json(r[9]) if r[9] else None
+            out.append(r)
+        return out, payload
+    for i in range(len(sums)):
+        assert recs(A, i) == recs(B, i)
+        assert [A.client_long_id(i, k) for k in range(64) if _has_client(A, k, i)] == \
+            [B.client_long_id(i, k) for k in range(64) if _has_client(B, k, i)]
+    # a failing document is reported and left fresh; the others load
+    bad = [("body_0", "{}")]
+    C = MergeTreeBatch(3)
+    with pytest.raises(MergeTreeError, match="document 1: summary blob not found"):
+        C.load_v1_many([0, 1, 2], [sums[0], bad, sums[1]], ["obs"] * 3, threads=3)
+    C.load_v1(1, sums[2], "obs")
+    assert recs(C, 0) == recs(A, 0)
