@@ -774,11 +774,33 @@ void scatter_words(mtb_batch* b, const std::vector<uint32_t>& host, void* dst, c
   HIPCHK(hipMemcpyAsync(b->dStageW.p, host.data(), host.size() * 4, hipMemcpyHostToDevice, b->stream));
   move_words(b, b->dStageW.p, dst, c);
 }
-void scatter_u16(mtb_batch* b, const std::vector<uint16_t>& host, uint16_t* dst, const Chunks& c) {
+void scatter_u16(mtb_batch* b, const uint16_t* host, size_t n, uint16_t* dst, const Chunks& c) {
   if (c.len.empty()) return;
-  b->dStageH.ensure(host.size());
-  HIPCHK(hipMemcpyAsync(b->dStageH.p, host.data(), host.size() * 2, hipMemcpyHostToDevice, b->stream));
+  b->dStageH.ensure(n);
+  HIPCHK(hipMemcpyAsync(b->dStageH.p, host, n * 2, hipMemcpyHostToDevice, b->stream));
   move_u16(b, b->dStageH.p, dst, c);
+}
+void scatter_u16(mtb_batch* b, const std::vector<uint16_t>& host, uint16_t* dst, const Chunks& c) {
+  scatter_u16(b, host.data(), host.size(), dst, c);
+}
+// f(i) for every document i, on up to 16 host threads (documents are independent)
+template <class F>
+void parallel_docs(uint32_t n, F&& f) {
+  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint32_t nt = std::min<uint32_t>(std::min<uint32_t>(16, hw), std::max<uint32_t>(1, n / 64));
+  if (nt <= 1) {
+    for (uint32_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  auto work = [&] {
+    for (uint32_t i = next.fetch_add(64); i < n; i = next.fetch_add(64))
+      for (uint32_t j = i; j < std::min(n, i + 64); j++) f(j);
+  };
+  std::vector<std::thread> ts;
+  for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
 }
 
 // Per-document slice capacities from the record count (see DESIGN.md "HBM layout").  `n` is the
@@ -1087,9 +1109,30 @@ void capture_pristine(mtb_batch* b) {
   b->haveRewind = true;
 }
 
+// MTB_TIMING=1: host-side phase times of each replay call on stderr
+struct PhaseClock {
+  bool on = getenv("MTB_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    char buf[96];
+    snprintf(buf, sizeof buf, " %s %.1f", what, std::chrono::duration<double, std::milli>(n - t).count());
+    line += buf;
+    t = n;
+  }
+  ~PhaseClock() {
+    if (on) fprintf(stderr, "mtb_timing ms:%s\n", line.c_str());
+  }
+};
+
 void replay(mtb_batch* b, mtb_stats* out) {
+  PhaseClock pc;
   if (!b->devInit) device_init(b);
+  pc.mark("device_init");
   upload_tables(b);
+  pc.mark("tables");
   // grow the slices of documents whose appended records no longer fit (2x headroom)
   {
     std::vector<Caps> want(b->ndocs);
@@ -1108,45 +1151,54 @@ void replay(mtb_batch* b, mtb_stats* out) {
     if (grow) layout(b, want);
   }
   // gather pending ops of every document into one buffer
-  uint64_t total = 0, totalPay = 0;
-  for (auto& d : b->docs) {
-    total += d.pending.size();
-    totalPay += d.payload.size();
-  }
-  std::vector<mtb_op> ops;
-  ops.reserve(total);
+  // per-document offsets first, then every document's records and payload copied in parallel
   bool anyLoad = false;
-  std::vector<uint16_t> pay;
-  pay.reserve(totalPay);
   Chunks payc;
+  std::vector<uint64_t> opOff(b->ndocs, 0), payOff(b->ndocs, 0);
+  uint64_t nOps = 0, nPay = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
     if (s.err) continue;
-    // payload goes after the text already in the arena; rebase record offsets
-    const uint32_t base = s.text_used;
-    payc.add(pay.size(), s.text_base + base, d.payload.size());
-    pay.insert(pay.end(), d.payload.begin(), d.payload.end());
+    opOff[i] = nOps;
+    payOff[i] = nPay;
+    // payload goes after the text already in the arena
+    payc.add(nPay, s.text_base + s.text_used, d.payload.size());
+    nOps += d.pending.size();
+    nPay += d.payload.size();
+    if (!d.pending.empty() && d.pending[0].type == MTB_OP_LOADSEG) anyLoad = true;
+  }
+  std::unique_ptr<mtb_op[]> ops(new mtb_op[nOps + 1]);
+  std::unique_ptr<uint16_t[]> pay(new uint16_t[nPay + 1]);
+  parallel_docs(b->ndocs, [&](uint32_t i) {
+    HostDoc& d = b->docs[i];
+    DocState& s = b->hst[i];
+    if (s.err) return;
+    const uint32_t base = s.text_used;  // rebase record payload offsets into the arena
+    std::copy(d.payload.begin(), d.payload.end(), pay.get() + payOff[i]);
     s.text_used += (uint32_t)d.payload.size();
     if (!(s.flags & DSF_NEWLINE)) {
       bool nl = std::find(d.payload.begin(), d.payload.end(), (uint16_t)'\n') != d.payload.end();
       if (!nl) nl = std::find(d.initText.begin(), d.initText.end(), (uint16_t)'\n') != d.initText.end();
       if (nl) s.flags |= DSF_NEWLINE;
     }
-    s.op_base = ops.size();
+    s.op_base = opOff[i];
     s.n_ops = (uint32_t)d.pending.size();
     s.op_next = 0;
-    if (!d.pending.empty() && d.pending[0].type == MTB_OP_LOADSEG) anyLoad = true;
+    mtb_op* out = ops.get() + opOff[i];
     for (mtb_op o : d.pending) {
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER)) o.payload += base;
-      ops.push_back(o);
+      *out++ = o;
     }
-  }
-  scatter_u16(b, pay, b->dText.p, payc);
-  b->dOps.ensure(ops.size() + 1);
-  if (!ops.empty()) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.data(), ops.size() * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
+  });
+  pc.mark("gather");
+  scatter_u16(b, pay.get(), nPay, b->dText.p, payc);
+  b->dOps.ensure(nOps + 1);
+  if (nOps) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.get(), nOps * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+  pc.mark("upload");
   if (!b->haveRewind) capture_pristine(b);
+  pc.mark("pristine");
   Tables t;
   t.pool = b->dPool.p;
   t.pidx = b->dPidx.p;
@@ -1166,6 +1218,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
+  pc.mark("kernels");
   mtb_stats st{};
   st.kernel_ms = ms;
   int firstErr = 0;
