@@ -3,4 +3,4 @@
 The hot path -- applying sequenced merge-tree ops (`Client.applyMsg`) and producing the SnapshotV1
 summary -- runs as hand-written HIP kernels on gfx950 behind the C ABI in include/mtb.h.
 """
-from .client import Client, MergeTreeBatch, MergeTreeError, UsageError  # noqa: F401
+from .client import Client, MatrixBatch, MergeTreeBatch, MergeTreeError, SharedMatrix, UsageError  # noqa: F401

@@ -41,9 +41,9 @@ def _check(L, h, rc):
 class MergeTreeBatch:
     """A batch of independent merge-tree documents replayed together on one MI355X."""
 
-    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0):
+    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0, _flags=0):
         self._L = _lib.lib()
-        opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, 0)
+        opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, int(_flags))
         h = ctypes.c_void_p()
         rc = self._L.mtb_batch_create(ctypes.byref(opts), ndocs, 1 << device, ctypes.byref(h))
         if rc != 0:
@@ -293,3 +293,57 @@ class Client:
         msn = -1 if minimumSequenceNumber is None else minimumSequenceNumber
         seq = -1 if lastSequenceNumber is None else lastSequenceNumber
         return self._b.summarize_v1(self._doc, msn, seq)[1]
+
+
+MTB_BATCH_MATRIX = 1
+
+
+class MatrixBatch(MergeTreeBatch):
+    """A batch of SharedMatrix observers (matrix.ts): matrix m is the PermutationVector documents 2m (rows)
+    and 2m+1 (cols).  Vector ops and setCell handle allocation replay on the GPU; cell values are not kept."""
+
+    def __init__(self, nmatrices, new_length_calc=False, chunk_size=0, device=0):
+        super().__init__(2 * nmatrices, new_length_calc=new_length_calc, chunk_size=chunk_size, device=device,
+                         _flags=MTB_BATCH_MATRIX)
+        self.nmatrices = nmatrices
+        self._matrices = [SharedMatrix(self, m) for m in range(nmatrices)]
+
+    def matrix(self, m):
+        return self._matrices[m]
+
+    __getitem__ = matrix
+
+    def init_matrix(self, m, observer_long_id, min_seq=0, cur_seq=0):
+        self._chk(self._L.mtb_matrix_init(self._h, m, observer_long_id.encode(), min_seq, cur_seq))
+
+    def apply_matrix_msg(self, m, msg):
+        s = msg if isinstance(msg, (bytes, bytearray)) else (msg.encode() if isinstance(msg, str) else json.dumps(msg).encode())
+        self._chk(self._L.mtb_matrix_apply_msg_json(self._h, m, s, len(s)))
+        self._dirty = True
+
+
+class SharedMatrix:
+    """SharedMatrix observer slot: startOrUpdateCollaboration / applyMsg (processCore, matrix.ts:636) and
+    the two PermutationVector summaries (permutationvector.ts:310)."""
+
+    def __init__(self, batch, m):
+        self._b = batch
+        self._m = m
+
+    def startOrUpdateCollaboration(self, longClientId, minSeq=0, currentSeq=0):
+        self._b.init_matrix(self._m, longClientId, minSeq, currentSeq)
+
+    def applyMsg(self, msg):
+        self._b.apply_matrix_msg(self._m, msg)
+
+    @property
+    def rows_doc(self):
+        return 2 * self._m
+
+    @property
+    def cols_doc(self):
+        return 2 * self._m + 1
+
+    def summarize(self):
+        """{"rows": (blobs, summary), "cols": (blobs, summary)} of the two PermutationVectors."""
+        return {"rows": self._b.summarize_v1(self.rows_doc), "cols": self._b.summarize_v1(self.cols_doc)}

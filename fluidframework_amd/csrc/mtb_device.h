@@ -36,6 +36,10 @@
 #define MTB_OP_LOADSEG 5
 #define MTB_F_LDFIRST 0x10  // first segment of an insertSegments batch: ensureIntervalBoundary at the root length
 #define MTB_F_LDLAST 0x20   // last segment of the batch: zamboniSegments
+// PermutationVector documents (matrix/src/permutationvector.ts): segments carry a storage-handle start
+// in the F_TEXT field instead of a text offset; their handle table lives in the (otherwise unused) text
+// arena as u32 words [length, handles[0], handles[1], ...] (handletable.ts: handles[0] = free-list head).
+#define MTB_HANDLE_UNALLOC 0x80000000u  // Handle.unallocated (-0x80000000)
 
 // ---- device records -------------------------------------------------------------------------
 // A tree node ("fat block", 320 B).  Besides its children's ids it holds the hot fields of every
@@ -154,5 +158,7 @@ struct Tables {
 #define DERR_ASSERT_MSN 9  // 0x039 / 0x04e / 0x04f
 #define DERR_DEPTH 10
 #define DERR_SHAPE 11      // a block mixing segment and block children (never produced by the reference)
+#define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
+#define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

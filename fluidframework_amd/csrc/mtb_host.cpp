@@ -41,6 +41,9 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
+hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                             FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                             Tables tables);
 
 namespace {
 
@@ -221,6 +224,9 @@ struct HostDoc {
   uint64_t totalPayload = 0;
   // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
   bool loaded = false;
+  // PermutationVector (matrix batches): segments carry handles; the handle table lives in the text arena
+  bool perm = false;
+  uint64_t totalSetcell = 0;
   LoadImage img;
   // device mirror
   DocState st{};
@@ -306,8 +312,9 @@ struct mtb_batch {
   DevBuf<uint32_t> dPSeg;
   DevBuf<FBlk> dPBlk;
   DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
-  Chunks pxSave[4], pxRestore[4];
+  Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
+  bool matrix = false;              // MTB_BATCH_MATRIX: documents 2m / 2m+1 are matrix m's rows / cols
   // batched moves: chunk tables and host->device staging
   DevBuf<uint64_t> dMvSrc, dMvDst;
   DevBuf<uint32_t> dMvLen, dStageW;
@@ -380,6 +387,15 @@ void pack_delta(mtb_batch* b, HostDoc& d, const hj::Value& op, mtb_op base, std:
     r.type = MTB_OP_INSERT;
     const U16* text = nullptr;
     const hj::Value* props = nullptr;
+    if (d.perm) {  // PermutationSegment.fromJSONObject([length, start]) (permutationvector.ts:45-48)
+      if (seg->kind != hj::Value::kArr || seg->items.empty() || seg->items[0].kind != hj::Value::kNum ||
+          seg->items[0].n < 0 || seg->items[0].n > 1e9 || seg->items[0].n != std::floor(seg->items[0].n))
+        raise(MTB_E_PARSE, "PermutationVector insert without a [length, start] segment");
+      r.flags |= MTB_F_PERMSEG;
+      r.pos2 = (uint32_t)seg->items[0].n;
+      out.push_back(r);
+      return;
+    }
     if (seg->kind == hj::Value::kStr) {
       text = &seg->s;
     } else if (seg->kind == hj::Value::kObj && member(*seg, u"text")) {
@@ -651,6 +667,7 @@ void resolve_load_props(mtb_batch* b, HostDoc& d) {
 // snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in parallel.
 void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
               PropsCache* pc) {
+  if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: summary load into a matrix batch (PermutationVector.load)");
   if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
   if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
   if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
@@ -824,6 +841,7 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
 // caps_for plus what a loaded summary already occupies (header segments, blocks, lists, aux words)
 Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
   Caps c = caps_for(n, payload, d.initText.size());
+  if (d.perm) c.text = (uint32_t)(2 * (d.totalSetcell + 4) + 64);  // the handle table (u32 words)
   if (d.loaded) {
     c.seg += (uint32_t)d.img.segp.size();
     c.blk += (uint32_t)d.img.blks.size() + (uint32_t)d.img.segp.size() / 4;
@@ -848,7 +866,7 @@ void layout(mtb_batch* b, const std::vector<Caps>& want) {
     s.seg_cap = std::max(s.seg_cap, c.seg);
     s.blk_cap = std::max(s.blk_cap, c.blk);
     s.list_cap = std::max(s.list_cap, c.list);
-    s.text_cap = std::max(s.text_cap, c.text);
+    s.text_cap = std::max(s.text_cap, (c.text + 1) & ~1u);  // even: text slices stay u32-aligned (handle tables)
     s.heap_cap = std::max(s.heap_cap, c.heap);
     s.aux_cap = std::max(s.aux_cap, c.aux);
     s.seg_base = seg; seg += s.seg_cap;
@@ -940,6 +958,12 @@ void device_init(mtb_batch* b) {
       d.onDevice = true;
       continue;
     }
+    if (d.perm) {
+      s.flags |= DSF_PERM;
+      const uint16_t ht[4] = {1, 0, 1, 0};  // u32 [length 1, handles[0] = 1] (handletable.ts:22)
+      txtc.add(texts.size(), s.text_base, 4);
+      texts.insert(texts.end(), ht, ht + 4);
+    }
     s.root = 0;
     s.blk_used = 1;
     s.aux_used = 1;
@@ -966,7 +990,7 @@ void device_init(mtb_batch* b) {
       txtc.add(texts.size(), s.text_base, d.initText.size());
       texts.insert(texts.end(), d.initText.begin(), d.initText.end());
     }
-    s.text_used = (uint32_t)d.initText.size();
+    s.text_used = d.perm ? 4u : (uint32_t)d.initText.size();
     blkc.add(recs.size(), s.blk_base * (sizeof(FBlk) / 4), sizeof(FBlk) / 4);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&root);
     recs.insert(recs.end(), w, w + sizeof(FBlk) / 4);
@@ -1090,12 +1114,16 @@ void capture_pristine(mtb_batch* b) {
   for (auto& c : b->pxRestore) c = Chunks{};
   uint64_t px = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
-    if (!b->docs[i].loaded) continue;
+    if (!b->docs[i].loaded && !b->docs[i].perm) continue;
     const DocState& s = b->hst[i];
-    const uint64_t base[4] = {s.blk_base * (sizeof(FBlk) / 4), s.seg_base, s.list_base * (sizeof(WEnt) / 4), s.aux_base};
-    const uint64_t len[4] = {(uint64_t)s.blk_used * (sizeof(FBlk) / 4), s.seg_used, (uint64_t)s.list_used * (sizeof(WEnt) / 4),
-                             s.aux_used};
-    for (int k = 0; k < 4; k++) {
+    const bool ld = b->docs[i].loaded;
+    // loaded documents: their whole initial tree; PermutationVectors: their handle table (text words)
+    const uint64_t base[5] = {s.blk_base * (sizeof(FBlk) / 4), s.seg_base, s.list_base * (sizeof(WEnt) / 4), s.aux_base,
+                              s.text_base / 2};
+    const uint64_t len[5] = {ld ? (uint64_t)s.blk_used * (sizeof(FBlk) / 4) : 0, ld ? s.seg_used : 0,
+                             ld ? (uint64_t)s.list_used * (sizeof(WEnt) / 4) : 0, ld ? s.aux_used : 0,
+                             b->docs[i].perm ? s.text_used / 2 : 0};
+    for (int k = 0; k < 5; k++) {
       b->pxSave[k].add(base[k], px, len[k]);
       b->pxRestore[k].add(px, base[k], len[k]);
       px += len[k];
@@ -1103,8 +1131,8 @@ void capture_pristine(mtb_batch* b) {
   }
   if (px) {
     b->dPX.ensure(px);
-    void* pools[4] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p};
-    for (int k = 0; k < 4; k++) move_words(b, pools[k], b->dPX.p, b->pxSave[k]);
+    void* pools[5] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p, b->dText.p};
+    for (int k = 0; k < 5; k++) move_words(b, pools[k], b->dPX.p, b->pxSave[k]);
   }
   b->haveRewind = true;
 }
@@ -1141,7 +1169,8 @@ void replay(mtb_batch* b, mtb_stats* out) {
       HostDoc& d = b->docs[i];
       const DocState& s = b->hst[i];
       Caps need = doc_caps(d, d.totalOps, d.totalPayload + s.text_used);
-      if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap) {
+      if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap ||
+          (d.perm && 2 * (d.totalSetcell + 4) > s.text_cap)) {
         want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
         grow = true;
       } else {
@@ -1210,8 +1239,9 @@ void replay(mtb_batch* b, mtb_stats* out) {
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
     HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                            b->dHeap.p, b->dAux.p, b->dFree.p, t));
-  HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
-                           b->dHeap.p, b->dAux.p, b->dFree.p, t));
+  HIPCHK((b->matrix ? mtb_launch_matrix : mtb_launch_replay)(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p,
+                                                            b->dBlks.p, b->dLists.p, b->dText.p, b->dHeap.p, b->dAux.p,
+                                                            b->dFree.p, t));
   HIPCHK(hipEventRecord(b->ev1, b->stream));
   HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
@@ -1346,12 +1376,28 @@ void rc_list(const HostDoc& d, const Seg& s, std::vector<int>& out) {
     for (uint32_t i = 0; i < d.aux[s.rcx]; i++) out.push_back((int)d.aux[s.rcx + 1 + i]);
 }
 
+// PermutationSegment.toJSONObject (permutationvector.ts:107): [length, start]
+std::string perm_json(int len, uint32_t start) { return "[" + std::to_string(len) + "," + std::to_string((int32_t)start) + "]"; }
+// HandleTable.getSummaryContent (handletable.ts:82): the handles array, from the text-arena words
+std::string handle_table_json(const HostDoc& d) {
+  auto word = [&](size_t k) { return (uint32_t)d.text[2 * k] | ((uint32_t)d.text[2 * k + 1] << 16); };
+  const uint32_t L = d.text.size() >= 2 ? word(0) : 0;
+  std::string o = "[";
+  for (uint32_t k = 0; k < L && 2 * (k + 2) <= d.text.size(); k++) {
+    if (k) o += ',';
+    o += std::to_string(word(1 + k));
+  }
+  return o + "]";
+}
+
 std::string dump_doc(mtb_batch* b, uint32_t i) {
   download_doc(b, i);
   const HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
   std::string o = "{\"minSeq\":" + std::to_string(s.min_seq) + ",\"currentSeq\":" + std::to_string(s.cur_seq) +
-                  ",\"length\":" + std::to_string(d.blks[s.root].len) + "}\n";
+                  ",\"length\":" + std::to_string(d.blks[s.root].len);
+  if (d.perm) o += ",\"handles\":" + handle_table_json(d);
+  o += "}\n";
   std::vector<FlatSeg> fl;
   flatten(d, s.root, fl, true);
   std::vector<int> rc;
@@ -1363,7 +1409,9 @@ std::string dump_doc(mtb_batch* b, uint32_t i) {
       o += std::to_string(f.path[k]);
     }
     o += "],";
-    if (is_marker(g)) {
+    if (d.perm) {
+      o += "\"P\"," + perm_json(g.len, g.text);
+    } else if (is_marker(g)) {
       const uint32_t rt = g.text & ~MTB_MARKER;
       o += "\"M\",";
       o += rt == 0 ? "null" : std::to_string(rt - 1);
@@ -1371,11 +1419,18 @@ std::string dump_doc(mtb_batch* b, uint32_t i) {
       o += "\"T\",";
       hj::quote(o, reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len);
     }
-    o += ',' + std::to_string(g.seq) + ',' + std::to_string(g.client) + ',' + std::to_string(seg_removed(g) ? g.rseq : -1) + ",[";
+    // PermutationVectors name clients by long id: their short ids depend on setCell interning order
+    auto cl = [&](int c) {
+      if (!d.perm) return std::to_string(c);
+      std::string q;
+      hj::quote(q, hj::from_utf8(d.longId(c)));
+      return q;
+    };
+    o += ',' + std::to_string(g.seq) + ',' + cl(g.client) + ',' + std::to_string(seg_removed(g) ? g.rseq : -1) + ",[";
     rc_list(d, g, rc);
     for (size_t k = 0; k < rc.size(); k++) {
       if (k) o += ',';
-      o += std::to_string(rc[k]);
+      o += cl(rc[k]);
     }
     o += "],";
     PropView pv = props_of(b, d, g.props);
@@ -1425,8 +1480,10 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
     bool marker = false;
     uint32_t refType = 0;
     uint32_t props = 0;
+    uint32_t start = 0;  // PermutationSegment
   };
   auto textOf = [&](const Seg& g) { return U16(reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len); };
+  const bool perm = d.perm;
   auto json_of = [&](bool marker, uint32_t refType, const U16& text, uint32_t props) {
     std::string o;
     PropView pv = props_of(b, d, props);
@@ -1451,7 +1508,7 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
   std::unique_ptr<Prev> prev;
   auto pushPrev = [&]() {
     if (!prev) return;
-    segJson.push_back(json_of(prev->marker, prev->refType, prev->text, prev->props));
+    segJson.push_back(perm ? perm_json(prev->len, prev->start) : json_of(prev->marker, prev->refType, prev->text, prev->props));
     segLen.push_back(prev->len);
     prev.reset();
   };
@@ -1460,7 +1517,20 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
     const Seg& g = d.segs[f.id];
     if (seg_removed(g) && g.rseq <= minSeq) continue;  // elided
     if (g.seq <= minSeq && !seg_removed(g)) {
-      const bool marker = is_marker(g);
+      const bool marker = !perm && is_marker(g);
+      if (perm) {  // PermutationSegment.canAppend: both unallocated, or contiguous handles
+        if (prev && (prev->start == MTB_HANDLE_UNALLOC ? g.text == MTB_HANDLE_UNALLOC : g.text == prev->start + (uint32_t)prev->len)) {
+          prev->len += g.len;
+          prev->live = false;
+        } else {
+          pushPrev();
+          prev.reset(new Prev());
+          prev->live = true;
+          prev->len = g.len;
+          prev->start = g.text;
+        }
+        continue;
+      }
       if (!prev) {
         prev.reset(new Prev());
         prev->live = true;
@@ -1492,7 +1562,8 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
     }
     pushPrev();
     std::string o = "{\"json\":";
-    o += json_of(is_marker(g), is_marker(g) ? (g.text & ~MTB_MARKER) : 0, is_marker(g) ? U16() : textOf(g), g.props);
+    if (perm) o += perm_json(g.len, g.text);
+    else o += json_of(is_marker(g), is_marker(g) ? (g.text & ~MTB_MARKER) : 0, is_marker(g) ? U16() : textOf(g), g.props);
     if (g.seq > minSeq) {
       o += ",\"seq\":" + std::to_string(g.seq) + ",\"client\":";
       hj::quote(o, hj::from_utf8(d.longId(g.client)));
@@ -1562,9 +1633,74 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
     totalBytes += utf8_byte_length(blobs[k].second);
   }
   tree += "}";
+  if (perm) {
+    // PermutationVector.summarize (permutationvector.ts:310-325): {segments: <SnapshotV1>, handleTable}
+    const std::string ht = handle_table_json(d);
+    std::string outer = "{\"segments\":{\"type\":1,\"tree\":" + tree + "},\"handleTable\":{\"type\":2,\"content\":";
+    hj::quote(outer, hj::from_utf8(ht));
+    outer += "}}";
+    totalBytes += utf8_byte_length(ht);
+    summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + outer + "},\"stats\":{\"treeNodeCount\":2,\"blobNodeCount\":" +
+                  std::to_string(blobs.size() + 1) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
+                  ",\"unreferencedBlobSize\":0}}";
+    for (auto& bl : blobs) bl.first = "segments/" + bl.first;
+    blobs.push_back({"handleTable", ht});
+    return;
+  }
   summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
                 std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
                 ",\"unreferencedBlobSize\":0}}";
+}
+
+// Client.applyMsg (client.ts:858-887) -> records appended to d
+void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
+  {
+    if (msg.kind != hj::Value::kObj) raise(MTB_E_PARSE, "message is not an object");
+    const hj::Value* cid = member(msg, u"clientId");
+    if (!cid || cid->kind != hj::Value::kStr) raise(MTB_E_UNSUPPORTED, "unsupported: message without a string clientId");
+    const std::string longId = hj::to_utf8(cid->s.data(), cid->s.size());
+    mtb_op base{};
+    base.client = d.client(longId);
+    base.seq = u32field(msg, u"sequenceNumber", "sequenceNumber");
+    base.ref_seq = u32field(msg, u"referenceSequenceNumber", "referenceSequenceNumber");
+    base.msn = u32field(msg, u"minimumSequenceNumber", "minimumSequenceNumber");
+    if ((int64_t)base.seq < d.lastSeq) raise(MTB_E_ASSERT, "0x038 Incoming op sequence# < local collabWindow's currentSequence#");
+    if (base.msn > base.seq) raise(MTB_E_ASSERT, "0x039 Incoming op sequence# < minSequence#");
+    std::vector<mtb_op> recs;
+    const size_t payloadBefore = d.payload.size();
+    const hj::Value* type = member(msg, u"type");
+    const bool isOp = type && type->kind == hj::Value::kStr && type->s == u"op";
+    const hj::Value* contents = member(msg, u"contents");
+    if (isOp) {
+      if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
+      if (longId == d.observer) {
+        // ack path with no pending local segments: one zamboni per member (client.ts:866, mergeTree.ts:1283)
+        const hj::Value* t = member(*contents, u"type");
+        size_t members = 1;
+        if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
+          const hj::Value* ops = member(*contents, u"ops");
+          members = ops && ops->kind == hj::Value::kArr ? ops->items.size() : 0;
+        }
+        for (size_t k = 0; k < members; k++) {
+          mtb_op r = base;
+          r.type = MTB_OP_ACK;
+          recs.push_back(r);
+        }
+      } else {
+        pack_delta(b, d, *contents, base, recs);
+      }
+    }
+    if (recs.empty()) {
+      mtb_op r = base;
+      r.type = MTB_OP_NOOP;
+      recs.push_back(r);
+    }
+    recs.back().flags |= MTB_F_LAST;
+    d.totalPayload += d.payload.size() - payloadBefore;
+    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
+    d.totalOps += recs.size();
+    d.lastSeq = base.seq;
+  }
 }
 
 char* dup(const std::string& s) {
@@ -1583,6 +1719,11 @@ int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_ma
   if (!out || ndocs == 0) return MTB_E_ARG;
   auto* b = new mtb_batch();
   if (opts) b->opts = *opts;
+  b->matrix = (b->opts.flags & MTB_BATCH_MATRIX) != 0;
+  if (b->matrix && (ndocs & 1)) {
+    delete b;
+    return MTB_E_ARG;  // a matrix batch holds (rows, cols) pairs
+  }
   b->ndocs = ndocs;
   b->docs.resize(ndocs);
   b->device = 0;
@@ -1599,6 +1740,7 @@ void mtb_free(void* p) { free(p); }
 int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_t n_units, const char* observer_long_id,
                  uint32_t min_seq, uint32_t cur_seq) {
   return guarded(b, [&] {
+    if (b->matrix) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_init");
     HostDoc& d = docref(b, doc);
     if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
     if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
@@ -1688,54 +1830,84 @@ int mtb_intern_props(mtb_batch* b, const char* json, size_t len, uint32_t* id_ou
 
 int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json, size_t len) {
   return guarded(b, [&] {
+    if (b->matrix) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_apply_msg_json");
     HostDoc& d = docref(b, doc);
     if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    apply_msg(b, d, hj::parse(json, len));
+  });
+}
+
+// SharedMatrix.processCore (matrix.ts:636-697): a vector op goes to its PermutationVector's applyMsg
+// (with that vector's updateSeqNumbers); a remote setCell becomes a SETCELL record in both vectors
+// (adjusted, exchanged and allocated on the GPU); a local setCell is an ack with no vector effect.
+int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json, size_t len) {
+  return guarded(b, [&] {
+    if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
+    if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    HostDoc& R = b->docs[2 * matrix];
+    HostDoc& C = b->docs[2 * matrix + 1];
+    if (!R.inited || !C.inited) raise(MTB_E_ARG, "mtb_matrix_init must be called first");
     hj::Value msg = hj::parse(json, len);
     if (msg.kind != hj::Value::kObj) raise(MTB_E_PARSE, "message is not an object");
+    const hj::Value* type = member(msg, u"type");
+    const hj::Value* contents = member(msg, u"contents");
+    if (!type || type->kind != hj::Value::kStr || type->s != u"op") return;  // not routed to processCore
+    if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
+    const hj::Value* target = member(*contents, u"target");
+    if (target && target->kind == hj::Value::kStr && (target->s == u"rows" || target->s == u"cols")) {
+      apply_msg(b, target->s == u"rows" ? R : C, msg);
+      return;
+    }
+    const hj::Value* t = member(*contents, u"type");
+    if (!t || t->kind != hj::Value::kNum || (int)t->n != 2)
+      raise(MTB_E_ASSERT, "0x021 SharedMatrix message contents have unexpected type!");
     const hj::Value* cid = member(msg, u"clientId");
     if (!cid || cid->kind != hj::Value::kStr) raise(MTB_E_UNSUPPORTED, "unsupported: message without a string clientId");
     const std::string longId = hj::to_utf8(cid->s.data(), cid->s.size());
+    if (longId == R.observer) return;  // ack of a local set (matrix.ts:660-667)
     mtb_op base{};
-    base.client = d.client(longId);
+    base.type = MTB_OP_SETCELL;
     base.seq = u32field(msg, u"sequenceNumber", "sequenceNumber");
     base.ref_seq = u32field(msg, u"referenceSequenceNumber", "referenceSequenceNumber");
     base.msn = u32field(msg, u"minimumSequenceNumber", "minimumSequenceNumber");
-    if ((int64_t)base.seq < d.lastSeq) raise(MTB_E_ASSERT, "0x038 Incoming op sequence# < local collabWindow's currentSequence#");
-    if (base.msn > base.seq) raise(MTB_E_ASSERT, "0x039 Incoming op sequence# < minSequence#");
-    std::vector<mtb_op> recs;
-    const size_t payloadBefore = d.payload.size();
-    const hj::Value* type = member(msg, u"type");
-    const bool isOp = type && type->kind == hj::Value::kStr && type->s == u"op";
-    const hj::Value* contents = member(msg, u"contents");
-    if (isOp) {
-      if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
-      if (longId == d.observer) {
-        // ack path with no pending local segments: one zamboni per member (client.ts:866, mergeTree.ts:1283)
-        const hj::Value* t = member(*contents, u"type");
-        size_t members = 1;
-        if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
-          const hj::Value* ops = member(*contents, u"ops");
-          members = ops && ops->kind == hj::Value::kArr ? ops->items.size() : 0;
-        }
-        for (size_t k = 0; k < members; k++) {
-          mtb_op r = base;
-          r.type = MTB_OP_ACK;
-          recs.push_back(r);
-        }
-      } else {
-        pack_delta(b, d, *contents, base, recs);
-      }
+    const uint32_t row = u32field(*contents, u"row", "row"), col = u32field(*contents, u"col", "col");
+    mtb_op r = base, c = base;
+    r.client = R.client(longId);  // getOrAddShortClientId in adjustPosition (client.ts:1070)
+    r.pos1 = row;
+    r.pos2 = R.client(R.observer);
+    c.client = C.client(longId);
+    c.pos1 = col;
+    c.pos2 = C.client(C.observer);
+    R.pending.push_back(r);
+    C.pending.push_back(c);
+    for (HostDoc* d : {&R, &C}) {
+      d->totalOps++;
+      d->totalSetcell++;
     }
-    if (recs.empty()) {
-      mtb_op r = base;
-      r.type = MTB_OP_NOOP;
-      recs.push_back(r);
+  });
+}
+
+// SharedMatrix observers (rows = document 2m, cols = 2m + 1) in a MTB_BATCH_MATRIX batch:
+// startOrUpdateCollaboration on both PermutationVectors (matrix.ts:102-118 construct them empty).
+int mtb_matrix_init(mtb_batch* b, uint32_t matrix, const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq) {
+  return guarded(b, [&] {
+    if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
+    if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
+    for (int k = 0; k < 2; k++) {
+      HostDoc& d = b->docs[2 * matrix + k];
+      if (d.inited || d.onDevice) raise(MTB_E_ARG, "matrix already initialised");
     }
-    recs.back().flags |= MTB_F_LAST;
-    d.totalPayload += d.payload.size() - payloadBefore;
-    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
-    d.totalOps += recs.size();
-    d.lastSeq = base.seq;
+    for (int k = 0; k < 2; k++) {
+      HostDoc& d = b->docs[2 * matrix + k];
+      d.perm = true;
+      d.observer = observer_long_id;
+      d.client(d.observer);
+      d.min0 = min_seq;
+      d.cur0 = cur_seq;
+      d.lastSeq = cur_seq;
+      d.inited = true;
+    }
   });
 }
 
@@ -1748,8 +1920,14 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
     d.totalPayload += payload_len;
     for (uint32_t k = 0; k < n; k++) {
       mtb_op o = ops[k];
-      if (o.type > MTB_OP_ACK) raise(MTB_E_ARG, "bad record type");
-      if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_MARKER)) {
+      if (o.type > MTB_OP_ACK && !(b->matrix && o.type == MTB_OP_SETCELL)) raise(MTB_E_ARG, "bad record type");
+      if (d.perm && o.type == MTB_OP_INSERT && !(o.flags & MTB_F_PERMSEG)) raise(MTB_E_ARG, "PermutationVector insert without MTB_F_PERMSEG");
+      if (!d.perm && (o.flags & MTB_F_PERMSEG)) raise(MTB_E_ARG, "MTB_F_PERMSEG outside a matrix batch");
+      if (o.type == MTB_OP_SETCELL) {
+        if (o.flags & MTB_F_LAST) raise(MTB_E_ARG, "SETCELL records never carry MTB_F_LAST");
+        d.totalSetcell++;
+      }
+      if (o.type == MTB_OP_INSERT && !(o.flags & (MTB_F_MARKER | MTB_F_PERMSEG))) {
         if ((uint64_t)o.payload + o.pos2 > payload_len) raise(MTB_E_ARG, "record payload out of range");
         o.payload += base;
       }
@@ -1773,8 +1951,8 @@ int mtb_rewind(mtb_batch* b) {
     for (auto& d : b->docs)
       if (!d.pending.empty()) raise(MTB_E_ARG, "rewind with pending (unreplayed) ops");
     HIPCHK(mtb_launch_rewind(b->stream, b->ndocs, b->dDocs.p, b->dPristine.p, b->dSegs.p, b->dPSeg.p, b->dBlks.p, b->dPBlk.p));
-    void* pools[4] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p};
-    for (int k = 0; k < 4; k++) move_words(b, b->dPX.p, pools[k], b->pxRestore[k]);
+    void* pools[5] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p, b->dText.p};
+    for (int k = 0; k < 5; k++) move_words(b, b->dPX.p, pools[k], b->pxRestore[k]);
     HIPCHK(hipStreamSynchronize(b->stream));
     b->hst = b->hPristine;
     for (auto& d : b->docs) d.cached = false;
@@ -1795,8 +1973,9 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
-    HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
-                             b->dHeap.p, b->dAux.p, b->dFree.p, t));
+    HIPCHK((b->matrix ? mtb_launch_matrix : mtb_launch_replay)(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p,
+                                                              b->dBlks.p, b->dLists.p, b->dText.p, b->dHeap.p, b->dAux.p,
+                                                              b->dFree.p, t));
     HIPCHK(hipEventRecord(b->ev1, b->stream));
     HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));

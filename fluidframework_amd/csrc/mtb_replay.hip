@@ -166,9 +166,11 @@ struct Scratch {  // LDS, one per wave
 #define memo_old sh->memo[0]
 #define memo_new sh->memo[1]
 
-// LD: the summary-load variant, which applies only the LOADSEG records at the head of each document's
-// records (mtb_load_kernel); the replay variant never sees one and carries none of that code.
-template <bool LD>
+// Engine variants: MODE_REPLAY (mtb_replay_kernel); MODE_LOAD applies only the LOADSEG records at
+// the head of each document's records (mtb_load_kernel); MODE_MATRIX replays SharedMatrix vector pairs
+// with setCell handle allocation (mtb_matrix_kernel).  Each variant carries only its own code.
+enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2 };
+template <int MODE>
 struct Eng {
   DocState* ds;
   uint32_t* segp;  // parent block of each segment
@@ -190,7 +192,10 @@ struct Eng {
   bool struct_changed;          // a block split / root growth happened since the last walk started
   bool sp_internal;
   int pending_fix;
-  int ld_pos;                   // insertSegments' advancing insert position within a LOADSEG batch              // depth of a block that reached MaxNodesInBlock children (-1: none)
+  int ld_pos;                   // insertSegments' advancing insert position within a LOADSEG batch
+  static constexpr bool isPerm = MODE == MODE_MATRIX;  // matrix batches hold PermutationVectors only
+  int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
+  int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
   uint64_t prof[NPH];
   uint32_t evc[NCN];
 
@@ -966,7 +971,7 @@ struct Eng {
         walk_depth = d;
         if (!insertMode) {
           if (pjj <= 0) return true;  // splitLeafSegment: pos 0 -> no change
-          if (U(V.f[F_TEXT][j]) & MTB_MARKER) return true;  // markers never split
+          if (!isPerm && (U(V.f[F_TEXT][j]) & MTB_MARKER)) return true;  // markers never split
           split_seg(d, j, pjj);
           if (bad()) return false;
           pending_fix = d;  // (handled by the caller, after the walk)
@@ -988,7 +993,7 @@ struct Eng {
       wsync();
       insert_slot(d, at);
       add_len_levels(0, d, d, candLen);
-      if constexpr (LD) load_entries(d, S, C);
+      if constexpr (MODE == MODE_LOAD) load_entries(d, S, C);
       else append_levels(0, d, S, C, WK_MAIN, candLen);
       pending_fix = d;
       return true;
@@ -1004,7 +1009,8 @@ struct Eng {
       uint32_t v = V.f[lane][j];
       if (lane == F_ID) v = MTB_LEAF | r;
       if (lane == F_LEN) v = v - (uint32_t)at;
-      if (lane == F_TEXT) v = v + (uint32_t)at;
+      // text offset + at; PermutationSegment: start + at unless unallocated (permutationvector.ts:126-140)
+      if (lane == F_TEXT && !(isPerm && v == MTB_HANDLE_UNALLOC)) v = v + (uint32_t)at;
       sh->nseg[lane] = v;
     }
     wsync();
@@ -1501,6 +1507,7 @@ struct Eng {
       // sequential decisions (uniform), values pulled from lane rr*8 + k
       int prev = -1;          // lane of the current append target
       int prevLen = 0;        // its (growing) length
+      uint32_t prevStart = 0; // its PermutationSegment start
       uint16_t prevLast = 0;  // its (growing) last unit
       bool prevMarker = false;
       for (int k = 0; k < cnt; k++) {
@@ -1519,7 +1526,11 @@ struct Eng {
         const uint16_t klast = (uint16_t)rl((int)last, L);
         const bool kmarker = (ktext & MTB_MARKER) != 0;
         bool ok = false;
-        if (prev >= 0 && klen > 0 && !prevMarker && !kmarker && prevLast != (uint16_t)'\n' &&
+        if (isPerm) {
+          // PermutationSegment.canAppend (permutationvector.ts:117-123): both unallocated, or contiguous
+          ok = prev >= 0 && klen > 0 &&
+               (prevStart == MTB_HANDLE_UNALLOC ? ktext == MTB_HANDLE_UNALLOC : ktext == prevStart + (uint32_t)prevLen);
+        } else if (prev >= 0 && klen > 0 && !prevMarker && !kmarker && prevLast != (uint16_t)'\n' &&
             (prevLen <= 256 || klen <= 256)) {
           // matchProperties(prev, k)
           const uint32_t pa = rlu(f[F_PROPS], prev), pb = rlu(f[F_PROPS], L);
@@ -1555,6 +1566,7 @@ struct Eng {
           prevLen = klen;
           prevLast = klast;
           prevMarker = kmarker;
+          prevStart = ktext;
           if (lane == L) newLen = klen;
         }
       }
@@ -1562,6 +1574,13 @@ struct Eng {
     // targets that received appends: build their new text
     const bool isTarget = s < count && kind == 2 && target < 0 && newLen != (int)f[F_LEN];
     unsigned long long tm = __ballot(isTarget);
+    if (isPerm) {  // BaseSegment.append: the length only (mergeTreeNodes.ts:527-545)
+      if (isTarget) f[F_LEN] = (uint32_t)newLen;
+      tm = 0;
+      // unlinked tombstones return their handles, in scour order (permutationvector.ts:418-441)
+      unsigned long long dm = __ballot(s < count && kind == 1 && (int)f[F_TEXT] >= 1);
+      if (COLD(dm)) handles_free_lanes(dm, f[F_TEXT], (int)f[F_LEN]);
+    }
     while (tm) {
       const int t = first_set(tm);
       tm &= tm - 1;
@@ -1749,6 +1768,142 @@ struct Eng {
       break;
     }
   }
+  // ------------------------------------------------------------------ PermutationVector handles
+  // HandleTable (matrix/src/handletable.ts) in the text arena: u32 [length, handles[0..length)].
+  __device__ __forceinline__ uint32_t* htab() const { return reinterpret_cast<uint32_t*>(UP(sh->gtext)); }
+  // free(start + i) for every lane of `m` in lane order (handletable.ts:55-58)
+  __device__ __forceinline__ void handles_free_lanes(unsigned long long m, uint32_t start, int len) {
+    uint32_t* ht = htab();
+    while (m) {
+      const int t = first_set(m);
+      m &= m - 1;
+      const uint32_t st = rlu(start, t);
+      const int n = rl(len, t);
+      if (lane == 0) {
+        uint32_t head = ht[1];
+        for (int i = 0; i < n; i++) {
+          ht[1 + st + i] = head;  // handles[h] = next
+          head = st + (uint32_t)i;
+        }
+        ht[1] = head;
+      }
+      wsync();
+    }
+  }
+  // allocate (handletable.ts:36-41): the free-list head, growing the table when it is exhausted
+  __device__ __forceinline__ uint32_t handle_alloc() {
+    uint32_t* ht = htab();
+    const uint32_t L = U(ht[0]);
+    const uint32_t fr = U(ht[1]);
+    const uint32_t next = fr < L ? U(ht[1 + fr]) : fr + 1;  // handles[free] ?? free + 1
+    if (fr >= L && 2u * (L + 2u) > ds->text_cap) {
+      fail(DERR_CAP_TEXT);
+      return 0;
+    }
+    wsync();
+    if (lane == 0) {
+      ht[1] = next;
+      ht[1 + fr] = 0;
+      if (fr >= L) ht[0] = L + 1;
+    }
+    if (fr >= L) text_used = 2u * (L + 2u);
+    wsync();
+    return fr;
+  }
+  // getContainingSegment(pos, refSeq, clientId) (mergeTree.ts:787-813, nodeMap :2531-2582): the first
+  // leaf with a non-zero (R, C) length whose span holds pos.  Leaves the path in the views; returns the
+  // depth of the leaf-level block (or -1), its slot, the offset in the segment and the segment's local
+  // position (getPosition in the observer's view, mergeTree.ts:1240).
+  __device__ __forceinline__ int find_seg(int pos, int R, int C, int& slot, int& offset, int& lpos) {
+    uint32_t b = root;
+    int p = pos, d = 0, lp = 0;
+    while (true) {
+      if (d >= MTB_VDEPTH) { fail(DERR_DEPTH); return -1; }
+      if (lane == 0) {
+        sh->path[d] = b;
+        sh->pp[d] = p;
+      }
+      wsync();
+      const int count = load_view(d, b, R, C);
+      const View& V = sh->v[d];
+      int clen = 0, ol = 0;
+      uint32_t cid = MTB_NONE;
+      if (lane < count) {
+        cid = V.f[F_ID][lane];
+        clen = V.rl[lane];
+        ol = child_olen(cid, (int)V.f[F_LEN][lane], (int)V.f[F_RSEQ][lane]);
+      }
+      const int def = clen > 0 ? clen : 0;  // nodeMap skips undefined and zero lengths
+      const int incl = cscan8(def);
+      const int pj = p - (incl - def);
+      const unsigned long long m = __ballot(lane < count && def > 0 && pj < def);
+      if (!m) return -1;
+      const int j = first_set(m);
+      lp += csum8(lane < j ? ol : 0);
+      if (lane == 0) sh->slot[d] = j;
+      wsync();
+      const uint32_t cj = rlu(cid, j);
+      const int pjj = rl(pj, j);
+      if (!(cj & MTB_LEAF)) {
+        b = cj;
+        p = pjj;
+        d++;
+        continue;
+      }
+      slot = j;
+      offset = pjj;
+      lpos = lp + pjj;
+      return d;
+    }
+  }
+  // adjustPosition (permutationvector.ts:209-226): the op's position in the observer's view, or -1
+  // when it lands on no segment or on a removed one
+  __device__ __forceinline__ int adjust_position(int pos, int R, int C) {
+    view_clear();
+    int j, off, lp;
+    const int d = find_seg(pos, R, C, j, off, lp);
+    if (d < 0 || bad()) return -1;
+    if ((int)U(sh->v[d].f[F_RSEQ][j]) >= 0) return -1;
+    return lp;
+  }
+  // getAllocatedHandle (permutationvector.ts:183-207) at local position pos: nothing when the position
+  // already has a handle, else walkSegments(pos, pos + 1, splitRange) isolates it and it gets one
+  __device__ __forceinline__ void allocated_handle(int pos, int Cl) {
+    view_clear();
+    int j, off, lp;
+    int d = find_seg(pos, curSeq, Cl, j, off, lp);
+    if (d < 0 || bad()) { fail(DERR_HANDLE); return; }
+    if ((int)U(sh->v[d].f[F_TEXT][j]) >= 1) return;  // start + offset is valid
+    walk(pos, curSeq, Cl, -2, false, 0);  // ensureIntervalBoundary(pos) and (pos + 1), local view
+    settle();
+    if (bad()) return;
+    view_clear();
+    walk(pos + 1, curSeq, Cl, -2, false, 0);
+    settle();
+    if (bad()) return;
+    view_clear();
+    d = find_seg(pos, curSeq, Cl, j, off, lp);
+    if (d < 0 || bad() || off != 0 || (int)U(sh->v[d].f[F_LEN][j]) != 1) { fail(DERR_HANDLE); return; }
+    const uint32_t h = handle_alloc();
+    if (bad()) return;
+    if (lane == 0) {
+      sh->v[d].f[F_TEXT][j] = h;
+      blk[sh->v[d].b].f[F_TEXT][j] = h;
+    }
+    n_mod += 1;
+    wsync();
+  }
+  // SharedMatrix setCell (matrix.ts:668-676) on this wave's vector: adjust, exchange with the partner
+  // wave (the other vector of the same matrix) through LDS, allocate when both positions survive.
+  // Both waves meet one barrier per setCell record, errors included.
+  __device__ __forceinline__ void setcell(const mtb_op& o, int par) {
+    const int adj = err ? -1 : adjust_position((int)o.pos1, (int)o.ref_seq, (int)(int16_t)o.client);
+    if (lane == 0) xch[par * 2 + wv] = adj;
+    __syncthreads();
+    const int other = U(xch[par * 2 + (wv ^ 1)]);
+    if (!err && adj >= 0 && other >= 0) allocated_handle(adj, (int)o.pos2);
+  }
+
   // zamboniSegments (zamboni.ts:19-60)
   __device__ __forceinline__ void zamboni() {
     for (int i = 0; i < 2 && !err; i++) {
@@ -1843,7 +1998,7 @@ struct Eng {
     memo_old = MTB_NONE;
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)(int16_t)o.client;
-    if constexpr (LD) {
+    if constexpr (MODE == MODE_LOAD) {
       apply_loadseg(o, S, C);
       return;
     }
@@ -1870,12 +2025,14 @@ struct Eng {
             if (lane == F_RSEQ) v = (uint32_t)-1;
             if (lane == F_CLI) v = ((uint32_t)C & 0xFFFF) | 0xFFFF0000u;  // removedClientIds[0] = none
             if (lane == F_PROPS) v = o.props ? (MTB_GPROPS | UP(sh->tab.pidx)[2 * o.props + 1]) : 0;
-            if (lane == F_TEXT) v = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1)) : o.payload;
+            if (lane == F_TEXT)
+              v = marker ? (MTB_MARKER | (o.pos2 == 0xFFFFFFFFu ? 0u : o.pos2 + 1))
+                         : ((o.flags & MTB_F_PERMSEG) ? MTB_HANDLE_UNALLOC : o.payload);  // onDelta resets remote handles
             sh->nseg[lane] = v;
           }
           wsync();
           n_mod += 1;
-          text_bytes += marker ? 0u : 2u * (uint32_t)len;
+          text_bytes += (marker || (o.flags & MTB_F_PERMSEG)) ? 0u : 2u * (uint32_t)len;
           if (!walk((int)o.pos1, R, C, S, true, len, true)) {
             fail(DERR_INSERT);
             return;
@@ -1930,14 +2087,16 @@ using namespace mtbk;
 #ifndef MTB_WAVES_PER_SIMD
 #define MTB_WAVES_PER_SIMD 4
 #endif
-template <bool LD>
-__device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops,
-                                           uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap,
-                                           uint32_t* aux, uint32_t* freel, const Tables& tables) {
-  const uint32_t doc = blockIdx.x;
+template <int MODE>
+__device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* xch, int wv, DocState* __restrict__ docs,
+                                           uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
+                                           uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                                           const Tables& tables) {
   if (doc >= ndocs) return;
   DocState* ds = &docs[doc];
-  Eng<LD> e;
+  Eng<MODE> e;
+  e.xch = xch;
+  e.wv = wv;
   e.ds = ds;
   e.segp = segp + ds->seg_base;
   e.blk = blks + ds->blk_base;
@@ -1969,6 +2128,7 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ d
   e.text_bytes = 0;
   uint32_t k = ds->op_next;
   const uint32_t n = ds->n_ops;
+  uint32_t errk = n;  // MODE_MATRIX: index after the record that failed
   e.walk_depth = -1;
   e.struct_changed = false;
   e.pending_fix = -1;
@@ -1996,7 +2156,9 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ d
     // op records are read one dword per lane (lanes 0..7), the next one in flight while applying
     const uint32_t* opw = reinterpret_cast<const uint32_t*>(dops);
     uint32_t cw = e.lane < 8 ? opw[k * 8 + e.lane] : 0u;
-    for (; k < n && !e.err; k++) {
+    int par = 0;  // MODE_MATRIX: setCell exchange parity
+    // a matrix wave keeps walking its records after an error: its partner waits for it at every setCell
+    for (; k < n && (MODE == MODE_MATRIX || !e.err); k++) {
       const uint32_t nk = k + 1 < n ? k + 1 : k;
       const uint32_t nw = e.lane < 8 ? opw[nk * 8 + e.lane] : 0u;  // prefetch the next record
       mtb_op cur;
@@ -2011,10 +2173,25 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ d
       cur.pos2 = rlu(cw, 5);
       cur.payload = rlu(cw, 6);
       cur.props = rlu(cw, 7);
-      if constexpr (LD) {
+      if constexpr (MODE == MODE_LOAD) {
         if (cur.type != MTB_OP_LOADSEG) break;  // the summary body precedes every op
       }
+      if constexpr (MODE == MODE_MATRIX) {
+        if (cur.type == MTB_OP_SETCELL) {
+          e.setcell(cur, par);
+          par ^= 1;
+          cw = nw;
+          continue;
+        }
+        if (e.err) {
+          cw = nw;
+          continue;
+        }
+      }
       e.apply(cur);
+      if constexpr (MODE == MODE_MATRIX) {
+        if (e.err && errk == n) errk = k + 1;
+      }
       cw = nw;
     }
   }
@@ -2042,7 +2219,7 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, DocState* __restrict__ d
 #endif
     if (e.err && !ds->err) {
       ds->err = e.err;
-      ds->err_op = k;
+      ds->err_op = MODE == MODE_MATRIX ? errk : k;
     }
     ds->op_next = k;
   }
@@ -2052,14 +2229,25 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                       WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
   __shared__ Scratch sh;
-  replay_doc<false>(sh, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+  replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
 // SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                     WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
   __shared__ Scratch sh;
-  replay_doc<true>(sh, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+  replay_doc<MODE_LOAD>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
+// SharedMatrix batches: one 128-lane workgroup per matrix, wave 0 = rows vector (document 2m), wave 1 =
+// cols vector (document 2m + 1); setCell records meet at a workgroup barrier (matrix.ts:668-676).
+extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
+    mtb_matrix_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                      WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh[2];
+  __shared__ int32_t xch[4];
+  const int wv = (int)(threadIdx.x >> 6);
+  replay_doc<MODE_MATRIX>(sh[wv], 2 * blockIdx.x + (uint32_t)wv, xch, wv, docs, ndocs, ops, segp, blks, lists, text,
+                          heap, aux, freel, tables);
 }
 
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
@@ -2067,6 +2255,13 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              Tables tables) {
   hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
                      aux, freel, tables);
+  return hipGetLastError();
+}
+hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
+                             FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
+                             Tables tables) {
+  hipLaunchKernelGGL(mtb_matrix_kernel, dim3((ndocs + 1) / 2), dim3(128), 0, stream, docs, ndocs, ops, segp, blks, lists,
+                     text, heap, aux, freel, tables);
   return hipGetLastError();
 }
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,

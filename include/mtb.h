@@ -38,13 +38,17 @@ enum {
   MTB_OP_REMOVE = 1,   /* ops.ts:59 REMOVE   [pos1, pos2) */
   MTB_OP_ANNOTATE = 2, /* ops.ts:60 ANNOTATE [pos1, pos2), props = op-props id */
   MTB_OP_NOOP = 3,     /* non-"op" message, or a member with no merge-tree effect */
-  MTB_OP_ACK = 4       /* op authored by the observer itself (client.ts:866 ack path): zamboni only */
+  MTB_OP_ACK = 4,      /* op authored by the observer itself (client.ts:866 ack path): zamboni only */
+  MTB_OP_SETCELL = 6   /* SharedMatrix setCell (matrix.ts:668-676), in both vectors' records: pos1 = the
+                          row (rows vector) or col (cols vector), pos2 = the observer's short id; no
+                          updateSeqNumbers.  Only in matrix batches. */
 };
 enum {
   MTB_F_LAST = 0x01,    /* run updateSeqNumbers(msn, seq) after this record (client.ts:874) */
   MTB_F_MARKER = 0x02,  /* insert: Marker segment, pos2 = refType (0xFFFFFFFF = undefined) */
   MTB_F_REWRITE = 0x04, /* annotate: combiningOp {name:"rewrite"} */
-  MTB_F_SEGOBJ = 0x08   /* insert: seg given as {text, props?} object (props id may be 0) */
+  MTB_F_SEGOBJ = 0x08,  /* insert: seg given as {text, props?} object (props id may be 0) */
+  MTB_F_PERMSEG = 0x40  /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
 };
 typedef struct mtb_op {
   uint8_t type;
@@ -63,8 +67,10 @@ typedef struct mtb_options {
   int32_t new_length_calc; /* IMergeTreeOptions.mergeTreeUseNewLengthCalculations (mergeTree.ts:413) */
   int32_t chunk_size;      /* IMergeTreeOptions.mergeTreeSnapshotChunkSize, 0 -> 10000 */
   int32_t threads_per_doc; /* reserved (64) */
-  int32_t flags;           /* reserved */
+  int32_t flags;           /* MTB_BATCH_MATRIX: a batch of SharedMatrix observers (mtb_matrix_*) */
 } mtb_options;
+
+#define MTB_BATCH_MATRIX 1 /* mtb_options.flags: documents 2m / 2m+1 are matrix m's rows / cols PermutationVectors */
 
 typedef struct mtb_stats {
   uint64_t ops_applied;     /* delta ops applied (each GROUP member counts once) */
@@ -139,6 +145,16 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n,
 int mtb_add_client(mtb_batch* b, uint32_t doc, const char* long_id);
 /* Intern a props object (JSON text); id 0 is reserved for "none". */
 int mtb_intern_props(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* id_out);
+
+/* ---- SharedMatrix (MTB_BATCH_MATRIX batches; matrix.ts, permutationvector.ts) ----
+ * Matrix m owns documents 2m (rows) and 2m+1 (cols), each a PermutationVector observer: remote
+ * insert/remove of rows/cols are merge-tree ops on that vector; a remote setCell adjusts (row, col)
+ * into the observer's view (adjustPosition, permutationvector.ts:209) and allocates storage handles
+ * (getAllocatedHandle, :183) on the GPU.  The cell values (SparseArray2D) are not kept.  mtb_summarize_v1
+ * and mtb_dump_segments on a vector document give PermutationVector.summarize (:310): blobs
+ * "segments/header", "segments/body_i", "handleTable". */
+int mtb_matrix_init(mtb_batch* b, uint32_t matrix, const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq);
+int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json_utf8, size_t len);
 
 /* Replay every pending op of every document on the GPU(s).  Blocking. */
 int mtb_replay(mtb_batch* b, mtb_stats* out);

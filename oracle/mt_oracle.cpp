@@ -308,10 +308,17 @@ bool MergeTree::breakTie(int pos, Node* node, int seq) {
 Seg* MergeTree::splitAt(Seg* s, int pos) {
   if (pos <= 0 || s->isMarker) return nullptr;  // Marker.createSplitSegmentAt -> undefined
   Seg* r = newSeg();
-  r->text = s->text.substr(pos);
-  s->text.resize(pos);
-  s->cachedLength = (int)s->text.size();
-  r->cachedLength = (int)r->text.size();
+  if (s->perm) {  // PermutationSegment.createSplitSegmentAt (permutationvector.ts:126-140)
+    r->perm = true;
+    r->start = s->start == HandleUnallocated ? HandleUnallocated : s->start + pos;
+    r->cachedLength = s->cachedLength - pos;
+    s->cachedLength = pos;
+  } else {
+    r->text = s->text.substr(pos);
+    s->text.resize(pos);
+    s->cachedLength = (int)s->text.size();
+    r->cachedLength = (int)r->text.size();
+  }
   if (s->hasPropManager && s->props) {  // copyPropertiesTo
     r->hasPropManager = true;
     r->props = *s->props;
@@ -832,6 +839,8 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
 
 // ---------------------------------------------------------------- zamboni (MT/zamboni.ts)
 static bool canAppend(const Seg* a, const Seg* b) {  // TextSegment.canAppend (textSegment.ts:71-78)
+  if (a->perm)  // PermutationSegment.canAppend (permutationvector.ts:117-123): contiguous handles
+    return a->start == HandleUnallocated ? b->start == HandleUnallocated : b->start == a->start + a->cachedLength;
   if (a->isMarker || b->isMarker) return false;
   if (!a->text.empty() && a->text.back() == u'\n') return false;
   return a->cachedLength <= TextSegmentGranularity || b->cachedLength <= TextSegmentGranularity;
@@ -862,8 +871,12 @@ void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {  // zamboni.t
     if (c->leaf) {
       Seg* s = static_cast<Seg*>(c);
       if (s->removed) {
-        if (s->removedSeq > window.minSeq) hold.push_back(s);
-        else s->parent = nullptr;  // unlink
+        if (s->removedSeq > window.minSeq) {
+          hold.push_back(s);
+        } else {
+          if (onUnlink) onUnlink(s);  // MergeTreeMaintenanceType.UNLINK
+          s->parent = nullptr;        // unlink
+        }
         prev = nullptr;
       } else {
         if (s->seq <= window.minSeq) {
@@ -1024,6 +1037,14 @@ JObj propsFromSpec(const JVal* spec) {
 }
 
 static Seg* makeSegFromSpec(MergeTree& mt, const JVal& spec) {  // testClient.ts:38-50 specToSegment
+  if (spec.t == JVal::Arr) {  // PermutationSegment.fromJSONObject([length, start]) (permutationvector.ts:45-48)
+    if (spec.arr.size() < 2 || spec.arr[0].t != JVal::Num) throw OracleError(-8, "bad PermutationSegment spec");
+    Seg* s = mt.newSeg();
+    s->perm = true;
+    s->cachedLength = (int)spec.arr[0].num;
+    s->start = spec.arr[1].t == JVal::Num ? (int)spec.arr[1].num : HandleUnallocated;
+    return s;
+  }
   if (spec.t == JVal::Str) {
     Seg* s = mt.newSeg();
     s->text = spec.str;
@@ -1079,6 +1100,10 @@ void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
       const JVal* spec = obj_get(op.obj, u"seg");
       if (js_falsy(spec)) return;
       Seg* s = makeSegFromSpec(mt, *spec);
+      if (perm != s->perm) fail_unsupported(perm ? "non-permutation segment in a PermutationVector" : "PermutationSegment in a SharedString");
+      // PermutationVector.onDelta (permutationvector.ts:346-357): a remote insert's handle allocation is
+      // dropped; the reset happens before insertSegments' zamboni, so inserting unallocated is the same
+      if (s->perm) s->start = HandleUnallocated;
       mt.insertSegments(pos, s, refSeq, client, seq);
       break;
     }
@@ -1237,6 +1262,13 @@ void Doc::removeRangeLocal(int start, int end) {
 
 // ---------------------------------------------------------------- SnapshotV1 (snapshotV1.ts)
 static JVal segJson(const Seg* s) {  // TextSegment.toJSONObject / Marker.toJSONObject
+  if (s->perm) {  // PermutationSegment.toJSONObject: [length, start]
+    JVal a;
+    a.t = JVal::Arr;
+    a.arr.push_back(JVal::number(s->cachedLength));
+    a.arr.push_back(JVal::number(s->start));
+    return a;
+  }
   if (s->isMarker) {
     JVal o;
     o.t = JVal::Obj;
@@ -1388,6 +1420,56 @@ std::vector<std::pair<std::string, std::string>> Doc::summarizeV1(std::string* s
   std::vector<std::pair<std::string, std::string>> blobs;
   blobs.push_back({"header", chunkJson(chunks[0], true)});
   for (size_t i = 1; i < chunks.size(); i++) blobs.push_back({"body_" + std::to_string(i - 1), chunkJson(chunks[i], false)});
+  if (perm) {
+    // PermutationVector.summarize (permutationvector.ts:310-325): {segments: <SnapshotV1>, handleTable}
+    std::string inner;
+    std::vector<std::pair<std::string, std::string>> segBlobs = blobs;
+    std::string ht = handleTableJson();
+    if (summaryJson) {
+      JVal tree;
+      tree.t = JVal::Obj;
+      int64_t total = 0;
+      for (auto& b : segBlobs) {
+        JVal blob;
+        blob.t = JVal::Obj;
+        blob.obj.push_back({u"type", JVal::number(2)});
+        blob.obj.push_back({u"content", JVal::string(utf8_to_u16(b.second))});
+        obj_set(tree.obj, utf8_to_u16(b.first), blob);
+        total += utf8ByteLength(b.second);
+      }
+      JVal segs;
+      segs.t = JVal::Obj;
+      segs.obj.push_back({u"type", JVal::number(1)});
+      segs.obj.push_back({u"tree", tree});
+      JVal htb;
+      htb.t = JVal::Obj;
+      htb.obj.push_back({u"type", JVal::number(2)});
+      htb.obj.push_back({u"content", JVal::string(utf8_to_u16(ht))});
+      JVal outer;
+      outer.t = JVal::Obj;
+      outer.obj.push_back({u"segments", segs});
+      outer.obj.push_back({u"handleTable", htb});
+      JVal summary;
+      summary.t = JVal::Obj;
+      summary.obj.push_back({u"type", JVal::number(1)});
+      summary.obj.push_back({u"tree", outer});
+      JVal stats;
+      stats.t = JVal::Obj;
+      stats.obj.push_back({u"treeNodeCount", JVal::number(2)});
+      stats.obj.push_back({u"blobNodeCount", JVal::number((double)segBlobs.size() + 1)});
+      stats.obj.push_back({u"handleNodeCount", JVal::number(0)});
+      stats.obj.push_back({u"totalBlobSize", JVal::number((double)(total + utf8ByteLength(ht)))});
+      stats.obj.push_back({u"unreferencedBlobSize", JVal::number(0)});
+      JVal all;
+      all.t = JVal::Obj;
+      all.obj.push_back({u"summary", summary});
+      all.obj.push_back({u"stats", stats});
+      *summaryJson = json_stringify(all);
+    }
+    for (auto& b : blobs) b.first = "segments/" + b.first;
+    blobs.push_back({"handleTable", ht});
+    return blobs;
+  }
   if (summaryJson) {
     // ISummaryTreeWithStats (summaryUtils.ts:138-198)
     JVal tree;
@@ -1431,6 +1513,7 @@ std::string Doc::dumpSegments() {
     h.obj.push_back({u"minSeq", JVal::number(mt.window.minSeq)});
     h.obj.push_back({u"currentSeq", JVal::number(mt.window.currentSeq)});
     h.obj.push_back({u"length", JVal::number(mt.length())});
+    if (perm) h.obj.push_back({u"handles", json_parse(handleTableJson())});
     out += json_stringify(h);
     out.push_back('\n');
   }
@@ -1447,20 +1530,25 @@ std::string Doc::dumpSegments() {
         p.t = JVal::Arr;
         for (int x : path) p.arr.push_back(JVal::number(x));
         row.arr.push_back(p);
-        if (s->isMarker) {
+        if (s->perm) {
+          row.arr.push_back(JVal::string(u"P"));
+          row.arr.push_back(segJson(s));
+        } else if (s->isMarker) {
           row.arr.push_back(JVal::string(u"M"));
           row.arr.push_back(s->refType >= 0 ? JVal::number(s->refType) : JVal::null());
         } else {
           row.arr.push_back(JVal::string(u"T"));
           row.arr.push_back(JVal::string(s->text));
         }
+        // PermutationVectors name clients by long id (setCell interning order is lazy, matrix.ts:669-672)
+        auto cl = [&](int c) { return perm ? JVal::string(utf8_to_u16(getLongClientId(c))) : JVal::number(c); };
         row.arr.push_back(JVal::number(s->seq));
-        row.arr.push_back(JVal::number(s->clientId));
+        row.arr.push_back(cl(s->clientId));
         row.arr.push_back(JVal::number(s->removed ? s->removedSeq : -1));
         JVal rc;
         rc.t = JVal::Arr;
         if (s->removed)
-          for (int c2 : s->removedClientIds) rc.arr.push_back(JVal::number(c2));
+          for (int c2 : s->removedClientIds) rc.arr.push_back(cl(c2));
         row.arr.push_back(rc);
         if (s->props && !s->props->empty()) {  // {} and undefined are interchangeable (snapshotV1.ts:199)
           JVal pr;
@@ -1559,6 +1647,123 @@ void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, 
     }
   }
   flushBatch();
+}
+
+// ---------------------------------------------------------------- PermutationVector / SharedMatrix
+// getContainingSegment (mergeTree.ts:787-813): the first leaf of nodeMap over [pos, pos + 1)
+Seg* MergeTree::containingSegment(int pos, int refSeq, int clientId, int* offset) {
+  Seg* found = nullptr;
+  int off = 0;
+  nodeMap(
+      refSeq, clientId,
+      [&](Seg* s, int, int start, int) {
+        found = s;
+        off = start;
+        return false;
+      },
+      [](Block*) {}, pos, pos + 1);
+  if (offset) *offset = off;
+  return found;
+}
+// getPosition (mergeTree.ts:1240-1262) in the local view: lengths of everything before the node
+int MergeTree::localPosition(Seg* s) {
+  int total = 0;
+  Node* node = s;
+  for (Block* parent = s->parent; parent; node = parent, parent = parent->parent)
+    for (int i = 0; i < parent->childCount && parent->children[i] != node; i++) {
+      int l = nodeLength(parent->children[i], window.currentSeq, window.clientId);
+      total += l == UNDEF_LEN ? 0 : l;
+    }
+  return total;
+}
+
+void Doc::enablePermutation() {
+  perm = true;
+  // onMaintenance (permutationvector.ts:418-441): handles of unlinked segments back to the free list
+  mt.onUnlink = [this](Seg* s) {
+    if (s->perm && s->start >= 1)
+      for (int i = 0; i < s->cachedLength; i++) freeHandle(s->start + i);
+  };
+}
+int Doc::allocateHandle() {
+  const int64_t free = handles[0];
+  const int64_t next = free < (int64_t)handles.size() ? handles[free] : free + 1;  // `?? free + 1`
+  handles[0] = next;
+  if (free == (int64_t)handles.size()) handles.push_back(0);
+  else handles[free] = 0;
+  return (int)free;
+}
+void Doc::freeHandle(int h) {
+  handles[h] = handles[0];
+  handles[0] = h;
+}
+int Doc::adjustPosition(int pos, int refSeq, const std::string& longClientId) {
+  const int client = getOrAddShortClientId(longClientId);  // getClientSequenceArgsForMessage
+  int offset = 0;
+  Seg* s = mt.containingSegment(pos, refSeq, client, &offset);
+  if (!s || s->removed) return -1;
+  return mt.localPosition(s) + offset;
+}
+int Doc::getAllocatedHandle(int pos) {
+  int offset = 0;
+  Seg* s = mt.containingSegment(pos, mt.window.currentSeq, mt.window.clientId, &offset);
+  if (!s) throw OracleError(-4, "0x027 Trying to get handle of out-of-bounds position!");
+  if (s->start >= 1) return s->start + offset;  // getMaybeHandle: start + offset (handlecache.ts:79)
+  // walkSegments(pos, pos + 1, splitRange = true) in the local view
+  mt.boundary(pos, mt.window.currentSeq, mt.window.clientId);
+  mt.boundary(pos + 1, mt.window.currentSeq, mt.window.clientId);
+  Seg* t = mt.containingSegment(pos, mt.window.currentSeq, mt.window.clientId, &offset);
+  if (!t || t->cachedLength != 1 || offset != 0) throw OracleError(-4, "handle allocation did not isolate one position");
+  const int h = allocateHandle();
+  if (t->start != HandleUnallocated) throw OracleError(-4, "0x024 Start of PermutationSegment already allocated!");
+  t->start = h;
+  mt.counters.segsTouched += 1;
+  return h;
+}
+std::string Doc::handleTableJson() const {
+  std::string o = "[";
+  for (size_t i = 0; i < handles.size(); i++) {
+    if (i) o += ",";
+    o += std::to_string(handles[i]);
+  }
+  return o + "]";
+}
+
+// SharedMatrix.processCore (matrix.ts:636-697): vector ops go to their PermutationVector's applyMsg;
+// a remote setCell adjusts (row, col) into the local view and allocates both handles when both survive.
+void MatrixDoc::applyMsg(const JVal& msg) {
+  if (msg.t != JVal::Obj) throw OracleError(-8, "message is not an object");
+  const JVal* type = obj_get(msg.obj, u"type");
+  const JVal* contents = obj_get(msg.obj, u"contents");
+  if (!type || type->t != JVal::Str || type->str != u"op" || !contents || contents->t != JVal::Obj) return;
+  const JVal* target = obj_get(contents->obj, u"target");
+  if (target && target->t == JVal::Str && target->str == u"rows") return rows.applyMsg(msg);
+  if (target && target->t == JVal::Str && target->str == u"cols") return cols.applyMsg(msg);
+  const JVal* t = obj_get(contents->obj, u"type");
+  if (!t || t->t != JVal::Num || (int)t->num != 2) throw OracleError(-4, "0x021 SharedMatrix message contents have unexpected type!");
+  const JVal* cid = obj_get(msg.obj, u"clientId");
+  if (!cid || cid->t != JVal::Str) fail_unsupported("message without string clientId");
+  const std::string longId = u16_to_utf8(cid->str);
+  if (rows.longClientId && longId == *rows.longClientId) return;  // ack of a local set
+  const JVal* ref = obj_get(msg.obj, u"referenceSequenceNumber");
+  const JVal* r = obj_get(contents->obj, u"row");
+  const JVal* c = obj_get(contents->obj, u"col");
+  if (!ref || ref->t != JVal::Num || !r || r->t != JVal::Num || !c || c->t != JVal::Num)
+    throw OracleError(-8, "bad setCell message");
+  const int refSeq = (int)ref->num;
+  const int ar = rows.adjustPosition((int)r->num, refSeq, longId);
+  if (ar < 0) {
+    cellsDropped++;
+    return;
+  }
+  const int ac = cols.adjustPosition((int)c->num, refSeq, longId);
+  if (ac < 0) {
+    cellsDropped++;
+    return;
+  }
+  rows.getAllocatedHandle(ar);
+  cols.getAllocatedHandle(ac);
+  cellsSet++;
 }
 
 uint64_t fnv1a64(const std::string& s) {

@@ -11,6 +11,7 @@
 #pragma once
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <optional>
@@ -41,8 +42,12 @@ struct Node {
   explicit Node(bool l) : leaf(l) {}
 };
 
+constexpr int HandleUnallocated = INT32_MIN;  // Handle.unallocated (matrix/src/handletable.ts:11)
+
 struct Seg : Node {
   bool isMarker = false;
+  bool perm = false;               // PermutationSegment (matrix/src/permutationvector.ts:41)
+  int start = HandleUnallocated;   // PermutationSegment._start
   int refType = -1;                // -1 = undefined
   u16str text;                     // TextSegment text (markers: empty)
   int seq = UniversalSeq;          // BaseSegment.seq default (mergeTreeNodes.ts:368)
@@ -163,6 +168,12 @@ class MergeTree {
   void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
   void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
   void zamboniSegments();
+  // MergeTreeMaintenanceType.UNLINK observer (zamboni.ts:139-148)
+  std::function<void(Seg*)> onUnlink;
+  // getContainingSegment (mergeTree.ts:787-813) and getPosition (:1240) for PermutationVector
+  Seg* containingSegment(int pos, int refSeq, int clientId, int* offset);
+  int localPosition(Seg* s);
+  void boundary(int pos, int refSeq, int clientId) { ensureIntervalBoundary(pos, refSeq, clientId); }
 
   // text / walks
   u16str getText();
@@ -242,6 +253,35 @@ class Doc {
   std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);
   // canonical segment dump used for engine parity (one JSON object per line)
   std::string dumpSegments();
+
+  // ---- PermutationVector (matrix/src/permutationvector.ts) when `perm` is set
+  bool perm = false;
+  std::vector<int64_t> handles{1};  // HandleTable.handles (handletable.ts:22): [0] = head of the free list
+  int allocateHandle();              // handletable.ts:36-41
+  void freeHandle(int h);            // handletable.ts:55-58
+  // adjustPosition (permutationvector.ts:209-226): the op's position in the local view, or -1
+  int adjustPosition(int pos, int refSeq, const std::string& longClientId);
+  // getAllocatedHandle (permutationvector.ts:183-207)
+  int getAllocatedHandle(int pos);
+  std::string handleTableJson() const;
+  void enablePermutation();
+};
+
+// SharedMatrix observer over two PermutationVectors (matrix/src/matrix.ts:636-697); the cell store
+// (SparseArray2D) is not restated.
+struct MatrixDoc {
+  Doc& rows;
+  Doc& cols;
+  MatrixDoc(Doc& r, Doc& c) : rows(r), cols(c) {
+    rows.enablePermutation();
+    cols.enablePermutation();
+  }
+  void startOrUpdateCollaboration(const std::string& id, int minSeq, int curSeq) {
+    rows.startOrUpdateCollaboration(id, minSeq, curSeq);
+    cols.startOrUpdateCollaboration(id, minSeq, curSeq);
+  }
+  void applyMsg(const JVal& msg);
+  uint64_t cellsSet = 0, cellsDropped = 0;
 };
 
 uint64_t fnv1a64(const std::string& s);

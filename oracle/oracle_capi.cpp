@@ -44,7 +44,33 @@ static std::optional<JObj> parseProps(const char* json) {
   return propsFromSpec(&v);
 }
 
+struct orc_matrix {
+  orc_doc rows, cols;
+  MatrixDoc m;
+  std::string err;
+  explicit orc_matrix(const Options& o) : rows(o), cols(o), m(rows.doc, cols.doc) {}
+};
+
 extern "C" {
+
+// SharedMatrix observer: two PermutationVector documents (rows = 0, cols = 1) reachable as orc_doc
+orc_matrix* orc_matrix_create(int new_length_calc, int chunk_size) {
+  Options o;
+  o.newLengthCalc = new_length_calc != 0;
+  if (chunk_size > 0) o.chunkSize = chunk_size;
+  return new orc_matrix(o);
+}
+void orc_matrix_destroy(orc_matrix* m) { delete m; }
+orc_doc* orc_matrix_vector(orc_matrix* m, int which) { return which ? &m->cols : &m->rows; }
+const char* orc_matrix_last_error(orc_matrix* m) { return m->err.c_str(); }
+int orc_matrix_start_collab(orc_matrix* m, const char* long_id, int min_seq, int cur_seq) {
+  return guard(&m->rows, [&] { m->m.startOrUpdateCollaboration(long_id, min_seq, cur_seq); });
+}
+int orc_matrix_apply_msg_json(orc_matrix* m, const char* json, size_t len) {
+  int rc = guard(&m->rows, [&] { m->m.applyMsg(json_parse(json, len)); });
+  if (rc) m->err = m->rows.err;
+  return rc;
+}
 
 orc_doc* orc_create(int new_length_calc, int chunk_size, int verify) {
   Options o;

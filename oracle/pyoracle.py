@@ -51,6 +51,15 @@ def lib():
         L.orc_checksum.restype = ctypes.c_uint64
         L.orc_checksum.argtypes = [vp]
         L.orc_load_v1.argtypes = [vp, cp, sz, cp]
+        L.orc_matrix_create.restype = vp
+        L.orc_matrix_create.argtypes = [i, i]
+        L.orc_matrix_destroy.argtypes = [vp]
+        L.orc_matrix_vector.restype = vp
+        L.orc_matrix_vector.argtypes = [vp, i]
+        L.orc_matrix_last_error.restype = cp
+        L.orc_matrix_last_error.argtypes = [vp]
+        L.orc_matrix_start_collab.argtypes = [vp, cp, i, i]
+        L.orc_matrix_apply_msg_json.argtypes = [vp, cp, sz]
         _LIB = L
     return _LIB
 
@@ -186,3 +195,46 @@ def msg_from_compact(m):
     cid, seq, ref, msn, contents = m
     return {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,
             "minimumSequenceNumber": msn, "type": "op", "contents": contents}
+
+
+class _VectorView(OracleDoc):
+    """One PermutationVector of an OracleMatrix (borrowed handle: never destroyed on its own)."""
+
+    def __init__(self, L, h):
+        self._L = L
+        self._h = h
+
+    def close(self):
+        self._h = None
+
+
+class OracleMatrix:
+    """SharedMatrix observer (matrix.ts:636-697) over two PermutationVectors: rows (0) and cols (1)."""
+
+    def __init__(self, new_length_calc=False, chunk_size=0):
+        self._L = lib()
+        self._h = self._L.orc_matrix_create(int(new_length_calc), int(chunk_size))
+        self.rows = _VectorView(self._L, self._L.orc_matrix_vector(self._h, 0))
+        self.cols = _VectorView(self._L, self._L.orc_matrix_vector(self._h, 1))
+
+    def close(self):
+        if self._h:
+            self._L.orc_matrix_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise OracleError(rc, self._L.orc_matrix_last_error(self._h).decode())
+
+    def start_collab(self, long_id, min_seq=0, cur_seq=0):
+        self._chk(self._L.orc_matrix_start_collab(self._h, long_id.encode(), min_seq, cur_seq))
+
+    def apply_msg(self, msg):
+        raw = msg if isinstance(msg, (bytes, bytearray)) else json.dumps(msg).encode()
+        self._chk(self._L.orc_matrix_apply_msg_json(self._h, raw, len(raw)))

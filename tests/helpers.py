@@ -135,3 +135,47 @@ def make_v1_summary(seed, n_segments, chunk_len, msn, seq, n_clients=4, p_remove
         start += len(c)
         blobs.append([ids[k], json.dumps(o, separators=(",", ":"))])
     return blobs
+
+
+UNALLOCATED = -2147483648  # Handle.unallocated (matrix/src/handletable.ts:11)
+
+
+def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, new_mode=False):
+    """A SharedMatrix op stream (matrix.ts message shapes) valid in each author's (refSeq, client) view:
+    row/col inserts and removes of 1..max_count, and setCell at a row/col inside the author's view.
+    Generated by driving the oracle as the observer; returns the messages."""
+    import random
+    from pyoracle import OracleMatrix
+    rng = random.Random(seed)
+    m = OracleMatrix(new_length_calc=new_mode)
+    m.start_collab("obs")
+    clients = [f"w{k}" for k in range(n_clients)]
+    ref = {c: 0 for c in clients}
+    msgs, seq = [], 0
+
+    def vlen(doc, w, r):
+        doc.add_client(w)
+        return doc.remote_length(r, doc.client_ids().index(w))
+
+    for _ in range(n_msgs):
+        w = rng.choice(clients)
+        ref[w] = max(ref[w], seq - rng.randint(0, lag))
+        r = ref[w]
+        seq += 1
+        rl, cl = vlen(m.rows, w, r), vlen(m.cols, w, r)
+        if rng.random() < p_set and rl > 0 and cl > 0:
+            contents = {"type": 2, "row": rng.randrange(rl), "col": rng.randrange(cl), "value": rng.randint(0, 99)}
+        else:
+            target = rng.choice(["rows", "cols"])
+            ln = rl if target == "rows" else cl
+            if ln == 0 or rng.random() < 0.6:
+                contents = {"type": 0, "pos1": rng.randint(0, ln), "seg": [rng.randint(1, max_count), UNALLOCATED],
+                            "target": target}
+            else:
+                p1 = rng.randrange(ln)
+                contents = {"type": 1, "pos1": p1, "pos2": min(ln, p1 + rng.randint(1, max_count)), "target": target}
+        msg = {"clientId": w, "sequenceNumber": seq, "referenceSequenceNumber": r,
+               "minimumSequenceNumber": min(ref.values()), "type": "op", "contents": contents}
+        m.apply_msg(msg)
+        msgs.append(msg)
+    return msgs

@@ -198,3 +198,33 @@ def test_parallel_summary_load_packs_like_single_loads():
         C.load_v1_many([0, 1, 2], [sums[0], bad, sums[1]], ["obs"] * 3, threads=3)
     C.load_v1(1, sums[2], "obs")
     assert recs(C, 0) == recs(A, 0)
+
+
+def test_matrix_messages_pack_per_vector():
+    """SharedMatrix.processCore routing (matrix.ts:636-697): vector ops to their vector (with its
+    updateSeqNumbers), remote setCell to both vectors as SETCELL records, local setCell dropped."""
+    import struct
+    from fluidframework_amd import MatrixBatch, MergeTreeError
+    from helpers import make_matrix_log
+    msgs = make_matrix_log(9, 200, n_clients=3)
+    B = MatrixBatch(1)
+    B[0].startOrUpdateCollaboration("obs")
+    for m in msgs:
+        B[0].applyMsg(m)
+    B[0].applyMsg({"clientId": "obs", "sequenceNumber": 10 ** 6, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                   "type": "op", "contents": {"type": 2, "row": 0, "col": 0, "value": 1}})
+    recs = []
+    for doc in (0, 1):
+        ops, n, _ = B.export_pending(doc)
+        recs.append([struct.unpack_from("<BBHIIIIIII", ops, 32 * k) for k in range(n)])
+    sets = [m for m in msgs if m["contents"]["type"] == 2]
+    for doc, target, coord in ((0, "rows", "row"), (1, "cols", "col")):
+        r = recs[doc]
+        sc = [x for x in r if x[0] == 6]
+        assert [x[6] for x in sc] == [m["contents"][coord] for m in sets]
+        assert all(not (x[1] & 1) for x in sc)  # no updateSeqNumbers
+        vec = [x for x in r if x[0] != 6]
+        assert [x[3] for x in vec] == [m["sequenceNumber"] for m in msgs if m["contents"].get("target") == target]
+        assert all(x[1] & 0x40 for x in vec if x[0] == 0)  # MTB_F_PERMSEG
+    with pytest.raises(MergeTreeError, match="mtb_matrix"):
+        B.init_doc(0, "", "x")

@@ -179,3 +179,38 @@ def test_snapshot_v1_load_mid_stream_then_continue(idx, cut):
         for m in groups[gi]["msgs"]:
             b.apply_msg(msg_from_compact(m))
         assert b.get_text() == groups[gi]["resultText"], f"{name}: group {gi}"
+
+
+# ---- SharedMatrix PermutationVectors (matrix/src/permutationvector.ts, handletable.ts) ----
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_matrix_oracle_handle_table_invariants(seed):
+    """Allocated handles are distinct and marked 0 in the table; the free list threads every other slot
+    and ends at the table's length (handletable.ts:36-58)."""
+    import json
+    from helpers import make_matrix_log
+    from pyoracle import OracleMatrix
+    msgs = make_matrix_log(seed, 600, n_clients=4, lag=12)
+    o = OracleMatrix()
+    o.start_collab("obs")
+    for m in msgs:
+        o.apply_msg(m)
+    for vec in (o.rows, o.cols):
+        lines = vec.dump_segments().splitlines()
+        table = json.loads(lines[0])["handles"]
+        owned = []
+        for ln in lines[1:]:
+            row = json.loads(ln)
+            length, start = row[2]
+            if start >= 1:
+                owned += range(start, start + length)
+        assert len(owned) == len(set(owned))
+        assert all(table[h] == 0 for h in owned)
+        free, h = [], table[0]
+        while h < len(table):
+            free.append(h)
+            h = table[h]
+        assert h == len(table)
+        assert not set(free) & set(owned)
+        # removed-but-not-yet-unlinked segments may still own handles
+        assert len(free) + len(owned) == len(table) - 1
