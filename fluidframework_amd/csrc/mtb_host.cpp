@@ -1179,6 +1179,12 @@ void replay(mtb_batch* b, mtb_stats* out) {
     }
     if (grow) layout(b, want);
   }
+  // a matrix whose vector failed is failed as a whole (its waves must agree on every setCell barrier)
+  if (b->matrix)
+    for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
+      const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
+      if (e) b->hst[i].err = b->hst[i + 1].err = e;
+    }
   // gather pending ops of every document into one buffer
   // per-document offsets first, then every document's records and payload copied in parallel
   bool anyLoad = false;
@@ -1188,7 +1194,11 @@ void replay(mtb_batch* b, mtb_stats* out) {
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
-    if (s.err) continue;
+    if (s.err) {  // sticky: nothing more runs for this document
+      s.n_ops = 0;
+      s.op_next = 0;
+      continue;
+    }
     opOff[i] = nOps;
     payOff[i] = nPay;
     // payload goes after the text already in the arena
@@ -1249,6 +1259,11 @@ void replay(mtb_batch* b, mtb_stats* out) {
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
   pc.mark("kernels");
+  if (b->matrix)
+    for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
+      const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
+      if (e) b->hst[i].err = b->hst[i + 1].err = e;
+    }
   mtb_stats st{};
   st.kernel_ms = ms;
   int firstErr = 0;
