@@ -50,6 +50,21 @@ struct loggen_cfg {
   int32_t new_length_calc;
   int32_t min_length;     // insert whenever the author's view is shorter than this
   int32_t annotate_keys;  // number of distinct annotate keys (>=1); key 0 is "client"
+  int32_t pct_set;        // matrix logs: percent of messages that are setCell
+  int32_t max_count;      // matrix logs: rows/cols per insert/remove (1..max_count)
+};
+
+// Per-matrix output (SharedMatrix logs): the records of each PermutationVector (0 rows, 1 cols), with
+// setCell records present in both.  Free with loggen_matrix_free.
+struct loggen_matrix {
+  void* ops[2];
+  uint32_t n_ops[2];
+  uint32_t n_msgs;
+  uint32_t n_sets;
+  uint16_t client_writer[2][256];  // per vector: short id -> writer index (0 = observer)
+  uint32_t n_short[2];
+  uint64_t checksum[2];            // oracle's final canonical dump checksums
+  int32_t error;
 };
 
 // Per-document output.  All arrays are malloc'd; free with loggen_free.
@@ -257,6 +272,205 @@ int loggen_generate_batch(const loggen_cfg* cfg, uint32_t doc_begin, uint32_t do
   for (int rc : rcs)
     if (rc) return rc;
   return 0;
+}
+
+// ---- SharedMatrix logs: row/col inserts and removes of 1..max_count and setCell,
+// every op valid in its author's view; the generator's oracle is a MatrixDoc observer fed the messages.
+static JVal jobj(std::initializer_list<std::pair<const char16_t*, JVal>> kv) {
+  JVal o;
+  o.t = JVal::Obj;
+  for (auto& p : kv) o.obj.push_back({p.first, p.second});
+  return o;
+}
+static int gen_matrix_one(const loggen_cfg& cfg, uint32_t index, loggen_matrix* out) {
+  memset(out, 0, sizeof *out);
+  const int K = cfg.n_clients;
+  if (K < 1 || K > 250) return -1;
+  SplitMix64 rng(cfg.seed * 0x9E3779B97F4A7C15ull ^ (0xA24BAED4963EE407ull * (index + 1)));
+  SplitMix64 seeder(rng.next());
+  rng = SplitMix64(seeder.next());
+  Options o;
+  o.newLengthCalc = cfg.new_length_calc != 0;
+  Doc rowsDoc(o), colsDoc(o);
+  MatrixDoc mat(rowsDoc, colsDoc);
+  std::vector<Doc::Record> recs[2];
+  try {
+    mat.startOrUpdateCollaboration("obs", 0, 0);
+    std::vector<int> vshort[2] = {std::vector<int>(K + 1, -1), std::vector<int>(K + 1, -1)};
+    for (int v = 0; v < 2; v++) {
+      vshort[v][0] = 0;
+      out->client_writer[v][0] = 0;
+      out->n_short[v] = 1;
+    }
+    auto shortIn = [&](int v, int w) {
+      if (vshort[v][w] < 0) {
+        vshort[v][w] = (int)out->n_short[v];
+        out->client_writer[v][out->n_short[v]++] = (uint16_t)w;
+      }
+      return (uint16_t)vshort[v][w];
+    };
+    std::vector<uint32_t> refSeq(K + 1, 0);
+    uint32_t cur = 0;
+    const int maxc = std::max(1, cfg.max_count);
+    for (int m = 0; m < cfg.n_ops; m++) {
+      const int w = (int)rng.range(1, K);
+      const std::string name = "c" + std::to_string(w);
+      const uint32_t lagv = rng.below((uint32_t)cfg.lag + 1);
+      const uint32_t cand = cur > lagv ? cur - lagv : 0;
+      if (cand > refSeq[w]) refSeq[w] = cand;
+      const uint32_t r = refSeq[w], seq = cur + 1;
+      uint32_t msn = UINT32_MAX;
+      for (int k = 1; k <= K; k++) msn = std::min(msn, refSeq[k]);
+      const int rl = rowsDoc.mt.getLength((int)r, rowsDoc.getOrAddShortClientId(name));
+      const int cl = colsDoc.mt.getLength((int)r, colsDoc.getOrAddShortClientId(name));
+      JVal contents;
+      Doc::Record rec{};
+      rec.seq = seq;
+      rec.refSeq = r;
+      rec.msn = msn;
+      if ((int)rng.below(100) < cfg.pct_set && rl > 0 && cl > 0) {
+        const uint32_t row = rng.below((uint32_t)rl), col = rng.below((uint32_t)cl);
+        contents = jobj({{u"type", JVal::number(2)}, {u"row", JVal::number(row)}, {u"col", JVal::number(col)},
+                         {u"value", JVal::number(m)}});
+        rec.type = 6;  // MTB_OP_SETCELL, no updateSeqNumbers
+        for (int v = 0; v < 2; v++) {
+          Doc::Record x = rec;
+          x.client = shortIn(v, w);
+          x.pos1 = v ? col : row;
+          x.pos2 = 0;  // the observer's short id
+          recs[v].push_back(x);
+        }
+        out->n_sets++;
+      } else {
+        const int v = (int)rng.below(2);
+        const int ln = v ? cl : rl;
+        const char16_t* target = v ? u"cols" : u"rows";
+        if (ln == 0 || rng.below(100) < 60) {
+          const uint32_t pos = rng.below((uint32_t)ln + 1), cnt = rng.range(1, (uint32_t)maxc);
+          JVal seg;
+          seg.t = JVal::Arr;
+          seg.arr.push_back(JVal::number(cnt));
+          seg.arr.push_back(JVal::number(HandleUnallocated));
+          contents = jobj({{u"type", JVal::number(0)}, {u"pos1", JVal::number(pos)}, {u"seg", seg},
+                           {u"target", JVal::string(target)}});
+          rec.type = 0;
+          rec.flags = 0x01 | 0x40;  // MTB_F_LAST | MTB_F_PERMSEG
+          rec.pos1 = pos;
+          rec.pos2 = cnt;
+        } else {
+          const uint32_t p1 = rng.below((uint32_t)ln);
+          const uint32_t p2 = std::min<uint32_t>((uint32_t)ln, p1 + rng.range(1, (uint32_t)maxc));
+          contents = jobj({{u"type", JVal::number(1)}, {u"pos1", JVal::number(p1)}, {u"pos2", JVal::number(p2)},
+                           {u"target", JVal::string(target)}});
+          rec.type = 1;
+          rec.flags = 0x01;
+          rec.pos1 = p1;
+          rec.pos2 = p2;
+        }
+        rec.client = shortIn(v, w);
+        recs[v].push_back(rec);
+      }
+      JVal msg = jobj({{u"clientId", JVal::string(utf8_to_u16(name))}, {u"sequenceNumber", JVal::number(seq)},
+                       {u"referenceSequenceNumber", JVal::number(r)}, {u"minimumSequenceNumber", JVal::number(msn)},
+                       {u"type", JVal::string(u"op")}, {u"contents", contents}});
+      mat.applyMsg(msg);
+      cur = seq;
+      out->n_msgs++;
+    }
+  } catch (const OracleError& e) {
+    fprintf(stderr, "loggen matrix %u: %s\n", index, e.what());
+    out->error = e.code;
+    return e.code;
+  }
+  for (int v = 0; v < 2; v++) {
+    out->n_ops[v] = (uint32_t)recs[v].size();
+    out->ops[v] = malloc(recs[v].size() * sizeof(Doc::Record) + 1);
+    memcpy(out->ops[v], recs[v].data(), recs[v].size() * sizeof(Doc::Record));
+  }
+  out->checksum[0] = fnv1a64(rowsDoc.dumpSegments());
+  out->checksum[1] = fnv1a64(colsDoc.dumpSegments());
+  return 0;
+}
+
+int loggen_matrix_generate_batch(const loggen_cfg* cfg, uint32_t begin, uint32_t end, int threads, loggen_matrix* out) {
+  const uint32_t n = end - begin;
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> ts;
+  std::vector<int> rcs(threads, 0);
+  for (int t = 0; t < threads; t++)
+    ts.emplace_back([&, t] {
+      for (uint32_t i = t; i < n; i += threads) {
+        const int rc = gen_matrix_one(*cfg, begin + i, &out[i]);
+        if (rc) rcs[t] = rc;
+      }
+    });
+  for (auto& th : ts) th.join();
+  for (int rc : rcs)
+    if (rc) return rc;
+  return 0;
+}
+
+void loggen_matrix_free(loggen_matrix* m) {
+  for (int v = 0; v < 2; v++) {
+    free(m->ops[v]);
+    m->ops[v] = nullptr;
+  }
+}
+
+// CPU baseline for matrix logs: the oracle replays each vector's records; setCell records of the two
+// streams pair up in order (adjust rows, adjust cols, allocate both when both survive).
+static void matrix_cpu_one(const loggen_cfg& cfg, const loggen_matrix& m, uint64_t ck[2]) {
+  Options o;
+  o.newLengthCalc = cfg.new_length_calc != 0;
+  Doc rows(o), cols(o);
+  MatrixDoc mat(rows, cols);
+  mat.startOrUpdateCollaboration("obs", 0, 0);
+  Doc* vec[2] = {&rows, &cols};
+  for (int v = 0; v < 2; v++)
+    for (uint32_t s = 1; s < m.n_short[v]; s++) vec[v]->getOrAddShortClientId("c" + std::to_string(m.client_writer[v][s]));
+  const Doc::Record* r[2] = {static_cast<const Doc::Record*>(m.ops[0]), static_cast<const Doc::Record*>(m.ops[1])};
+  uint32_t k[2] = {0, 0};
+  static const std::vector<std::optional<JVal>> noProps(1);
+  while (k[0] < m.n_ops[0] || k[1] < m.n_ops[1]) {
+    for (int v = 0; v < 2; v++)
+      while (k[v] < m.n_ops[v] && r[v][k[v]].type != 6) vec[v]->applyRecordParsed(r[v][k[v]++], nullptr, noProps);
+    if (k[0] >= m.n_ops[0] || k[1] >= m.n_ops[1]) continue;
+    const Doc::Record& a = r[0][k[0]++];
+    const Doc::Record& b = r[1][k[1]++];
+    const int ar = rows.adjustPosition((int)a.pos1, (int)a.refSeq, rows.getLongClientId(a.client));
+    if (ar < 0) continue;
+    const int ac = cols.adjustPosition((int)b.pos1, (int)b.refSeq, cols.getLongClientId(b.client));
+    if (ac < 0) continue;
+    rows.getAllocatedHandle(ar);
+    cols.getAllocatedHandle(ac);
+  }
+  ck[0] = fnv1a64(rows.dumpSegments());
+  ck[1] = fnv1a64(cols.dumpSegments());
+}
+
+double loggen_matrix_cpu_replay(const loggen_cfg* cfg, const loggen_matrix* mats, uint32_t n, int threads, int32_t* mismatches) {
+  if (threads < 1) threads = 1;
+  std::vector<int> bad(threads, 0);
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; t++)
+    ts.emplace_back([&, t] {
+      for (uint32_t i = t; i < n; i += threads) {
+        uint64_t ck[2];
+        try {
+          matrix_cpu_one(*cfg, mats[i], ck);
+          if (ck[0] != mats[i].checksum[0] || ck[1] != mats[i].checksum[1]) bad[t]++;
+        } catch (const OracleError&) {
+          bad[t]++;
+        }
+      }
+    });
+  for (auto& th : ts) th.join();
+  auto t1 = std::chrono::steady_clock::now();
+  int b = 0;
+  for (int v : bad) b += v;
+  if (mismatches) *mismatches = b;
+  return std::chrono::duration<double>(t1 - t0).count();
 }
 
 void loggen_free(loggen_doc* d) {

@@ -1195,7 +1195,10 @@ void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::ve
     case 0: {
       mt.counters.ops++;
       Seg* s = mt.newSeg();
-      if (r.flags & 0x02) {
+      if (r.flags & 0x40) {  // PermutationSegment (inserted unallocated, permutationvector.ts:346-357)
+        s->perm = true;
+        s->cachedLength = (int)r.pos2;
+      } else if (r.flags & 0x02) {
         s->isMarker = true;
         s->cachedLength = 1;
         s->refType = r.pos2 == 0xFFFFFFFFu ? -1 : (int)r.pos2;

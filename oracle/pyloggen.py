@@ -14,7 +14,7 @@ class LoggenCfg(ctypes.Structure):
                 ("lag", ctypes.c_int32), ("initial_len", ctypes.c_int32), ("pct_insert", ctypes.c_int32),
                 ("pct_remove", ctypes.c_int32), ("pct_group", ctypes.c_int32),
                 ("new_length_calc", ctypes.c_int32), ("min_length", ctypes.c_int32),
-                ("annotate_keys", ctypes.c_int32)]
+                ("annotate_keys", ctypes.c_int32), ("pct_set", ctypes.c_int32), ("max_count", ctypes.c_int32)]
 
 
 class LoggenDoc(ctypes.Structure):
@@ -26,9 +26,21 @@ class LoggenDoc(ctypes.Structure):
                 ("final_segments", ctypes.c_uint32), ("error", ctypes.c_int32)]
 
 
+class LoggenMatrix(ctypes.Structure):
+    _fields_ = [("ops", ctypes.c_void_p * 2), ("n_ops", ctypes.c_uint32 * 2), ("n_msgs", ctypes.c_uint32),
+                ("n_sets", ctypes.c_uint32), ("client_writer", (ctypes.c_uint16 * 256) * 2),
+                ("n_short", ctypes.c_uint32 * 2), ("checksum", ctypes.c_uint64 * 2), ("error", ctypes.c_int32)]
+
+
 def _lib():
     L = _oracle_lib()
     if not getattr(L, "_loggen_ready", False):
+        L.loggen_matrix_generate_batch.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.c_uint32,
+                                                   ctypes.c_int, ctypes.POINTER(LoggenMatrix)]
+        L.loggen_matrix_free.argtypes = [ctypes.POINTER(LoggenMatrix)]
+        L.loggen_matrix_cpu_replay.restype = ctypes.c_double
+        L.loggen_matrix_cpu_replay.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.POINTER(LoggenMatrix), ctypes.c_uint32,
+                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
         L.loggen_generate.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.POINTER(LoggenDoc)]
         L.loggen_generate_batch.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.POINTER(LoggenDoc)]
@@ -43,9 +55,9 @@ def _lib():
 
 
 def make_cfg(seed=1, n_clients=8, n_ops=1000, lag=128, initial_len=64, pct_insert=50, pct_remove=30,
-             pct_group=5, new_length_calc=False, min_length=1, annotate_keys=1):
+             pct_group=5, new_length_calc=False, min_length=1, annotate_keys=1, pct_set=40, max_count=8):
     return LoggenCfg(seed, n_clients, n_ops, lag, initial_len, pct_insert, pct_remove, pct_group,
-                     int(new_length_calc), min_length, annotate_keys)
+                     int(new_length_calc), min_length, annotate_keys, pct_set, max_count)
 
 
 class LogBatch:
@@ -97,6 +109,47 @@ class LogBatch:
             for i in range(self.n):
                 L.loggen_free(ctypes.byref(self.docs[i]))
             self.docs = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MatrixLogBatch:
+    """Generated SharedMatrix logs for matrices [begin, end): per matrix the rows / cols record streams
+    (setCell records in both), their client tables and the oracle's final checksums."""
+
+    def __init__(self, cfg, begin, end, threads=None):
+        self.cfg = cfg
+        self.n = end - begin
+        self.mats = (LoggenMatrix * self.n)()
+        threads = threads or min(16, os.cpu_count() or 1)
+        rc = _lib().loggen_matrix_generate_batch(ctypes.byref(cfg), begin, end, threads, self.mats)
+        if rc != 0:
+            raise RuntimeError(f"loggen matrix failed rc={rc}")
+
+    def ops_bytes(self, i, v):
+        m = self.mats[i]
+        return ctypes.string_at(m.ops[v], m.n_ops[v] * 32)
+
+    def client_ids(self, i, v):
+        m = self.mats[i]
+        return ["obs"] + [f"c{m.client_writer[v][s]}" for s in range(1, m.n_short[v])]
+
+    def cpu_replay(self, n=None, threads=1):
+        bad = ctypes.c_int32()
+        n = self.n if n is None else n
+        secs = _lib().loggen_matrix_cpu_replay(ctypes.byref(self.cfg), self.mats, n, threads, ctypes.byref(bad))
+        return secs, bad.value
+
+    def close(self):
+        if self.mats is not None:
+            L = _lib()
+            for i in range(self.n):
+                L.loggen_matrix_free(ctypes.byref(self.mats[i]))
+            self.mats = None
 
     def __del__(self):
         try:
