@@ -52,3 +52,14 @@ export declare class Client {
   summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }): unknown;
 }
 export declare const TestClient: typeof Client;
+
+/** A batch of SharedMatrix observers (rows / cols PermutationVectors replayed on the GPU). */
+export declare class MatrixBatch extends MergeTreeBatch {
+  constructor(nmatrices: number, options?: { mergeTreeUseNewLengthCalculations?: boolean; mergeTreeSnapshotChunkSize?: number; device?: number });
+  matrix(m: number): SharedMatrix;
+}
+export declare class SharedMatrix {
+  startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
+  applyMsg(msg: ISequencedDocumentMessage | string): void;
+  summarizeVectors(): { rows: { blobs: [string, string][]; summary: unknown }; cols: { blobs: [string, string][]; summary: unknown } };
+}

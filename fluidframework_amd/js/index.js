@@ -28,16 +28,19 @@ function unsupported(what) {
   return e;
 }
 
+const MTB_BATCH_MATRIX = 1;
+
 class MergeTreeBatch {
   /**
    * @param {number} ndocs documents in the batch
    * @param {object} [options] IMergeTreeOptions subset: mergeTreeUseNewLengthCalculations
    *   (mergeTree.ts:413), mergeTreeSnapshotChunkSize (snapshotV1.ts:37); plus `device` (GPU index)
    */
-  constructor(ndocs, options = {}) {
-    this.ndocs = ndocs;
-    this.handle = native.create(ndocs, options.mergeTreeUseNewLengthCalculations ? 1 : 0,
-      options.mergeTreeSnapshotChunkSize || 0, options.device || 0);
+  constructor(ndocs, options = {}, _rawDocs = undefined, _flags = 0) {
+    const n = _rawDocs === undefined ? ndocs : _rawDocs;
+    this.ndocs = n;
+    this.handle = native.create(n, options.mergeTreeUseNewLengthCalculations ? 1 : 0,
+      options.mergeTreeSnapshotChunkSize || 0, options.device || 0, _flags);
     this.dirty = false;
     this.busy = false;
     this.lastStats = undefined;
@@ -215,7 +218,45 @@ class Client {
   }
 }
 
+/**
+ * A batch of SharedMatrix observers (matrix.ts): matrix m is the PermutationVector documents 2m (rows)
+ * and 2m+1 (cols).  Row/col ops and setCell handle allocation replay on the GPU (one workgroup per
+ * matrix); cell values are not kept.
+ */
+class MatrixBatch extends MergeTreeBatch {
+  constructor(nmatrices, options = {}) {
+    super(0, options, 2 * nmatrices, MTB_BATCH_MATRIX);
+    this.matrices = [];
+    for (let m = 0; m < nmatrices; m++) this.matrices.push(new SharedMatrix(this, m));
+  }
+
+  matrix(m) { return this.matrices[m]; }
+}
+
+/** SharedMatrix observer slot: processCore (matrix.ts:636) and the PermutationVector summaries. */
+class SharedMatrix {
+  constructor(batch, m) {
+    this.batch = batch;
+    this.m = m;
+  }
+
+  startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
+    native.matrixInit(this.batch.handle, this.m, longClientId, minSeq, currentSeq);
+  }
+
+  applyMsg(msg) {
+    this.batch.checkIdle();
+    native.matrixApplyMsg(this.batch.handle, this.m, typeof msg === "string" ? msg : JSON.stringify(msg));
+    this.batch.dirty = true;
+  }
+
+  /** PermutationVector.summarize (permutationvector.ts:310) of rows and cols. */
+  summarizeVectors() {
+    return { rows: this.batch.summarizeV1(2 * this.m), cols: this.batch.summarizeV1(2 * this.m + 1) };
+  }
+}
+
 /** TestClient alias: the same observer slot plus getText (testClient.ts:54). */
 const TestClient = Client;
 
-module.exports = { MergeTreeBatch, Client, TestClient, native };
+module.exports = { MergeTreeBatch, MatrixBatch, SharedMatrix, Client, TestClient, native };

@@ -134,17 +134,22 @@ static void batch_finalize(napi_env env, void* data, void* hint) {
 
 /* create(ndocs, newLengthCalc, chunkSize, device) -> handle            client.ts:107 ctor */
 static napi_value js_create(napi_env env, napi_callback_info info) {
-  napi_value argv[4];
-  if (!get_args(env, info, 4, argv)) return NULL;
-  uint32_t ndocs, nl, chunk, dev;
+  napi_value argv[5];
+  size_t argc = 5;
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 4) {
+    napi_throw_type_error(env, NULL, "wrong number of arguments");
+    return NULL;
+  }
+  uint32_t ndocs, nl, chunk, dev, flags = 0;
   if (!get_u32(env, argv[0], &ndocs) || !get_u32(env, argv[1], &nl) || !get_u32(env, argv[2], &chunk) ||
-      !get_u32(env, argv[3], &dev))
+      !get_u32(env, argv[3], &dev) || (argc > 4 && !get_u32(env, argv[4], &flags)))
     return NULL;
   mtb_options o;
   memset(&o, 0, sizeof o);
   o.new_length_calc = (int32_t)nl;
   o.chunk_size = (int32_t)chunk;
   o.threads_per_doc = 64;
+  o.flags = (int32_t)flags;
   mtb_batch* b = NULL;
   int rc = mtb_batch_create(&o, ndocs, 1u << dev, &b);
   if (rc) return throw_rc(env, b, rc);
@@ -216,6 +221,37 @@ static napi_value js_load_v1(napi_env env, napi_callback_info info) {
   free(blobs);
   free(id);
   if (!ok) return NULL;
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
+/* matrixInit(h, matrix, observerLongId, minSeq, curSeq)                matrix.ts:102-118 */
+static napi_value js_matrix_init(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t m, mn, cur;
+  if (!b || !get_u32(env, argv[1], &m) || !get_u32(env, argv[3], &mn) || !get_u32(env, argv[4], &cur)) return NULL;
+  char* id = get_utf8(env, argv[2], NULL);
+  if (!id) return NULL;
+  int rc = mtb_matrix_init(b, m, id, mn, cur);
+  free(id);
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
+/* matrixApplyMsg(h, matrix, JSON.stringify(ISequencedDocumentMessage))  matrix.ts:636 */
+static napi_value js_matrix_apply_msg(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t m;
+  if (!b || !get_u32(env, argv[1], &m)) return NULL;
+  size_t n = 0;
+  char* json = get_utf8(env, argv[2], &n);
+  if (!json) return NULL;
+  int rc = mtb_matrix_apply_msg_json(b, m, json, n);
+  free(json);
   if (rc) return throw_rc(env, b, rc);
   return undef(env);
 }
@@ -519,6 +555,7 @@ static napi_value init(napi_env env, napi_value exports) {
     napi_callback fn;
   } fns[] = {
       {"create", js_create},           {"docInit", js_doc_init},       {"loadV1", js_load_v1},
+      {"matrixInit", js_matrix_init},  {"matrixApplyMsg", js_matrix_apply_msg},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

@@ -15,7 +15,7 @@ const fs = require("fs");
 const path = require("path");
 const zlib = require("zlib");
 
-const { MergeTreeBatch, native } = require("..");
+const { MergeTreeBatch, MatrixBatch, native } = require("..");
 
 const GOLDEN = path.join(__dirname, "..", "..", "..", "tests", "golden", "replay");
 const SNAPSHOTS = path.join(__dirname, "..", "..", "..", "tests", "golden", "snapshots_v1");
@@ -44,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId", "loadV1"];
+    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -108,6 +108,18 @@ async function gpuChecks() {
     assert.strictEqual(loaded.client(i).getText(), log.groups[ngroups - 1].resultText, `${name}: text after load`);
     assert.deepStrictEqual(loaded.summarizeV1(i).blobs, sums[i], `${name}: summary after load`);
   });
+  // SharedMatrix through the drop-in surface: a matrix log replayed twice, in one batch of two matrices
+  const mlog = JSON.parse(fs.readFileSync(path.join(__dirname, "matrix_log.json"), "utf8"));
+  const mb = new MatrixBatch(2);
+  for (let m = 0; m < 2; m++) {
+    mb.matrix(m).startOrUpdateCollaboration("obs");
+    for (const msg of mlog) mb.matrix(m).applyMsg(msg);
+  }
+  mb.flush();
+  const v0 = mb.matrix(0).summarizeVectors(), v1 = mb.matrix(1).summarizeVectors();
+  assert.deepStrictEqual(v0, v1);
+  assert.strictEqual(v0.rows.blobs[v0.rows.blobs.length - 1][0], "handleTable");
+  console.log("js gpu matrix ok");
   const ref = new MergeTreeBatch(1);
   await ref.client(0).load(undefined, storageOf(snapshotBlobs("withMarkers")));
   assert.deepStrictEqual(ref.summarizeV1(0, 0, 0).blobs, snapshotBlobs("withMarkers"));

@@ -43,3 +43,4 @@ def test_js_package_replays_reference_logs_on_gpu():
     out = _node()
     assert "js gpu parity ok" in out
     assert "js gpu load ok" in out
+    assert "js gpu matrix ok" in out
