@@ -1668,6 +1668,16 @@ Seg* MergeTree::containingSegment(int pos, int refSeq, int clientId, int* offset
   if (offset) *offset = off;
   return found;
 }
+void MergeTree::mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f) {
+  const int end = blockLength(root, refSeq, clientId);
+  nodeMap(
+      refSeq, clientId,
+      [&](Seg* s, int, int, int) {
+        f(s);
+        return true;
+      },
+      [](Block*) {}, 0, end == UNDEF_LEN ? 0 : end);
+}
 // getPosition (mergeTree.ts:1240-1262) in the local view: lengths of everything before the node
 int MergeTree::localPosition(Seg* s) {
   int total = 0;
@@ -1767,6 +1777,139 @@ void MatrixDoc::applyMsg(const JVal& msg) {
   rows.getAllocatedHandle(ar);
   cols.getAllocatedHandle(ac);
   cellsSet++;
+}
+
+// ---------------------------------------------------------------- SnapshotLegacy (snapshotlegacy.ts)
+std::vector<std::pair<std::string, std::string>> Doc::summarizeLegacy(const std::string& catchUpJson, std::string* summaryJson) {
+  MergeTree& t = mt;
+  const int seq = t.window.minSeq;  // extractSync (snapshotlegacy.ts:205-259): everything at the MSN
+  const int headerLen = t.getLength(seq, NonCollabClient);
+  std::vector<Seg> segs;  // coalesced copies (prev.clone().append(segment.clone()))
+  Seg* prevLive = nullptr;
+  std::optional<Seg> prevClone;
+  auto flushPrev = [&] {
+    if (prevClone) segs.push_back(*prevClone);
+    else if (prevLive) segs.push_back(*prevLive);
+    prevClone.reset();
+    prevLive = nullptr;
+  };
+  t.mapAll(seq, NonCollabClient, [&](Seg* s) {
+    if (s->seq != UnassignedSeq && s->seq <= seq && (!s->removed || s->removedSeq == UnassignedSeq || s->removedSeq > seq)) {
+      Seg* prev = prevClone ? &*prevClone : prevLive;
+      if (prev && canAppend(prev, s) && matchSegProps(prev, s)) {
+        Seg c = *prev;
+        if (c.props) c.hasPropManager = true;
+        c.text += s->text;
+        c.cachedLength += s->cachedLength;
+        prevClone = std::move(c);
+        prevLive = nullptr;
+      } else {
+        flushPrev();
+        prevLive = s;
+      }
+    }
+  });
+  flushPrev();
+  int totalLength = 0;
+  for (Seg& s : segs) {
+    totalLength += s.cachedLength;
+    if (s.props && s.props->empty()) {  // properties {} -> undefined (mutates the live segment in the reference)
+      s.props.reset();
+      s.hasPropManager = false;
+    }
+  }
+  // live segments normalized the same way
+  t.walkAllSegments([&](Seg* s) {
+    if (s->seq != UnassignedSeq && s->seq <= seq && s->props && s->props->empty()) {
+      s->props.reset();
+      s->hasPropManager = false;
+    }
+  });
+  const int segmentsTotalLength = headerLen != totalLength ? totalLength : headerLen;  // SegmentsTotalLengthMismatch
+  const int chunkSize = t.options.chunkSize;
+  struct Chunk { int start = 0, count = 0, length = 0; };
+  auto take = [&](int approx, int start) {  // getSeqLengthSegs (snapshotlegacy.ts:66-117)
+    Chunk c;
+    c.start = start;
+    while (c.length < approx && start + c.count < (int)segs.size()) c.length += segs[start + c.count++].cachedLength;
+    return c;
+  };
+  const int total = (int)segs.size();
+  auto chunkJson = [&](const Chunk& c, bool header) {
+    JVal o;
+    o.t = JVal::Obj;
+    o.obj.push_back({u"chunkStartSegmentIndex", JVal::number(c.start)});
+    o.obj.push_back({u"chunkSegmentCount", JVal::number(c.count)});
+    o.obj.push_back({u"chunkLengthChars", JVal::number(c.length)});
+    o.obj.push_back({u"totalLengthChars", JVal::number(segmentsTotalLength)});
+    o.obj.push_back({u"totalSegmentCount", JVal::number(total)});
+    o.obj.push_back({u"chunkSequenceNumber", JVal::number(seq)});
+    JVal texts;
+    texts.t = JVal::Arr;
+    for (int i = 0; i < c.count; i++) texts.arr.push_back(segJson(&segs[c.start + i]));
+    o.obj.push_back({u"segmentTexts", texts});
+    if (header) {  // buildHeaderMetadataForLegacyChunk (snapshotChunks.ts:178-200); minSequenceNumber undefined
+      JVal h;
+      h.t = JVal::Obj;
+      JVal ids;
+      ids.t = JVal::Arr;
+      ids.arr.push_back(json_parse(std::string("{\"id\":\"header\"}")));
+      if (c.length < segmentsTotalLength) ids.arr.push_back(json_parse(std::string("{\"id\":\"body\"}")));
+      h.obj.push_back({u"orderedChunkMetadata", ids});
+      h.obj.push_back({u"sequenceNumber", JVal::number(seq)});
+      h.obj.push_back({u"totalLength", JVal::number(segmentsTotalLength)});
+      h.obj.push_back({u"totalSegmentCount", JVal::number(total)});
+      o.obj.push_back({u"headerMetadata", h});
+    }
+    return json_stringify(o);
+  };
+  // emit (snapshotlegacy.ts:122-203)
+  std::vector<std::pair<std::string, std::string>> blobs;
+  const Chunk c1 = take(chunkSize, 0);
+  blobs.push_back({"header", chunkJson(c1, true)});
+  int length = c1.length, count = c1.count;
+  if (c1.count < total) {
+    const Chunk c2 = take(segmentsTotalLength, c1.count);
+    blobs.push_back({"body", chunkJson(c2, false)});
+    length += c2.length;
+    count += c2.count;
+  }
+  if (length != segmentsTotalLength) fail_assert("0x05d", "emit: mismatch in segmentsTotalLength");
+  if (count != total) fail_assert("0x05e", "emit: mismatch in totalSegmentCount");
+  if (!catchUpJson.empty()) {
+    JVal cu = json_parse(catchUpJson);
+    if (cu.t == JVal::Arr && !cu.arr.empty()) blobs.push_back({"catchupOps", json_stringify(cu)});
+  }
+  if (summaryJson) {
+    JVal tree;
+    tree.t = JVal::Obj;
+    int64_t bytes = 0;
+    for (auto& b : blobs) {
+      JVal blob;
+      blob.t = JVal::Obj;
+      blob.obj.push_back({u"type", JVal::number(2)});
+      blob.obj.push_back({u"content", JVal::string(utf8_to_u16(b.second))});
+      obj_set(tree.obj, utf8_to_u16(b.first), blob);
+      bytes += utf8ByteLength(b.second);
+    }
+    JVal summary;
+    summary.t = JVal::Obj;
+    summary.obj.push_back({u"type", JVal::number(1)});
+    summary.obj.push_back({u"tree", tree});
+    JVal stats;
+    stats.t = JVal::Obj;
+    stats.obj.push_back({u"treeNodeCount", JVal::number(1)});
+    stats.obj.push_back({u"blobNodeCount", JVal::number((double)blobs.size())});
+    stats.obj.push_back({u"handleNodeCount", JVal::number(0)});
+    stats.obj.push_back({u"totalBlobSize", JVal::number((double)bytes)});
+    stats.obj.push_back({u"unreferencedBlobSize", JVal::number(0)});
+    JVal all;
+    all.t = JVal::Obj;
+    all.obj.push_back({u"summary", summary});
+    all.obj.push_back({u"stats", stats});
+    *summaryJson = json_stringify(all);
+  }
+  return blobs;
 }
 
 uint64_t fnv1a64(const std::string& s) {

@@ -174,6 +174,8 @@ class MergeTree {
   Seg* containingSegment(int pos, int refSeq, int clientId, int* offset);
   int localPosition(Seg* s);
   void boundary(int pos, int refSeq, int clientId) { ensureIntervalBoundary(pos, refSeq, clientId); }
+  // mapRange(action, refSeq, clientId) over the whole tree (mergeTree.ts mapRange -> nodeMap)
+  void mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f);
 
   // text / walks
   u16str getText();
@@ -251,6 +253,9 @@ class Doc {
   void loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId);
   // SnapshotV1 (snapshotV1.ts:46-312) -> (blob path, content) list + ISummaryTreeWithStats JSON
   std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);
+  // SnapshotLegacy (snapshotlegacy.ts:122-259): header / body chunks at the MSN, plus the catch-up
+  // messages blob when `catchUpJson` is a non-empty JSON array
+  std::vector<std::pair<std::string, std::string>> summarizeLegacy(const std::string& catchUpJson, std::string* summaryJson);
   // canonical segment dump used for engine parity (one JSON object per line)
   std::string dumpSegments();
 

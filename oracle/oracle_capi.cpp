@@ -158,6 +158,25 @@ int orc_summarize_v1(orc_doc* d, int msn, int seq, char** out, size_t* len) {
     *out = dupstr(s, len);
   });
 }
+// Client.summarize without newMergeTreeSnapshotFormat (client.ts:999-1003): SnapshotLegacy
+int orc_summarize_legacy(orc_doc* d, int msn, int seq, const char* catchup_json, char** out, size_t* len) {
+  return guard(d, [&] {
+    if (msn >= 0 && seq >= 0) d->doc.updateSeqNumbers(msn, seq);
+    std::string summary;
+    auto blobs = d->doc.summarizeLegacy(catchup_json ? catchup_json : "", &summary);
+    JVal arr;
+    arr.t = JVal::Arr;
+    for (auto& b : blobs) {
+      JVal pair;
+      pair.t = JVal::Arr;
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.first)));
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.second)));
+      arr.arr.push_back(pair);
+    }
+    std::string s = "{\"blobs\":" + json_stringify(arr) + ",\"summary\":" + summary + "}";
+    *out = dupstr(s, len);
+  });
+}
 int orc_dump_segments(orc_doc* d, char** out, size_t* len) {
   return guard(d, [&] { *out = dupstr(d->doc.dumpSegments(), len); });
 }

@@ -51,6 +51,7 @@ def lib():
         L.orc_checksum.restype = ctypes.c_uint64
         L.orc_checksum.argtypes = [vp]
         L.orc_load_v1.argtypes = [vp, cp, sz, cp]
+        L.orc_summarize_legacy.argtypes = [vp, i, i, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_matrix_create.restype = vp
         L.orc_matrix_create.argtypes = [i, i]
         L.orc_matrix_destroy.argtypes = [vp]
@@ -165,6 +166,18 @@ class OracleDoc:
         p = ctypes.c_void_p()
         n = ctypes.c_size_t()
         self._chk(self._L.orc_summarize_v1(self._h, msn, seq, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            raw = ctypes.string_at(p, n.value)
+        finally:
+            self._L.orc_free(p)
+        return json.loads(raw.decode("utf-8"))
+
+    def summarize_legacy(self, msn=-1, seq=-1, catchup=None):
+        """SnapshotLegacy summary (snapshotlegacy.ts): {"blobs": [[path, content]...], "summary": {...}}."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        cu = json.dumps(catchup, separators=(",", ":")).encode() if catchup else None
+        self._chk(self._L.orc_summarize_legacy(self._h, msn, seq, cu, ctypes.byref(p), ctypes.byref(n)))
         try:
             raw = ctypes.string_at(p, n.value)
         finally:

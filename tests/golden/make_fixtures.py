@@ -11,6 +11,8 @@ Outputs (data only: inputs and expected outputs, no reference source):
   tests/golden/replay/<name>.json.gz   {"initialText", "groups":[{"msgs":[[clientId,seq,refSeq,msn,contents]...],
                                          "resultText"}]}
   tests/golden/snapshots_v1/<name>.json.gz  {"blobs": [[path, contents], ...]} of the "content" subtree
+  packages/dds/sequence/src/test/snapshots/legacy/*.json  -- SnapshotLegacy summaries of the same strings
+  tests/golden/snapshots_legacy/<name>.json.gz  (same layout)
 """
 import gzip
 import json
@@ -46,9 +48,9 @@ def replay_fixtures():
         print("wrote", dst, os.path.getsize(dst))
 
 
-def snapshot_fixtures():
-    src = os.path.join(REF, "packages/dds/sequence/src/test/snapshots/v1")
-    out_dir = os.path.join(HERE, "snapshots_v1")
+def snapshot_fixtures(version="v1"):
+    src = os.path.join(REF, f"packages/dds/sequence/src/test/snapshots/{version}")
+    out_dir = os.path.join(HERE, f"snapshots_{version}")
     os.makedirs(out_dir, exist_ok=True)
     for name in sorted(os.listdir(src)):
         with open(os.path.join(src, name)) as f:
@@ -60,7 +62,7 @@ def snapshot_fixtures():
             blobs.append([e["path"], e["value"]["contents"]])
         dst = os.path.join(out_dir, name.replace(".json", ".json.gz"))
         with gzip.open(dst, "wt", compresslevel=9) as f:
-            json.dump({"source": f"packages/dds/sequence/src/test/snapshots/v1/{name}", "blobs": blobs}, f)
+            json.dump({"source": f"packages/dds/sequence/src/test/snapshots/{version}/{name}", "blobs": blobs}, f)
         print("wrote", dst, os.path.getsize(dst))
 
 
@@ -68,4 +70,5 @@ if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference checkout not present; fixtures are already committed")
     replay_fixtures()
-    snapshot_fixtures()
+    snapshot_fixtures("v1")
+    snapshot_fixtures("legacy")

@@ -17,8 +17,8 @@ def replay_fixtures():
     return out
 
 
-def snapshot_fixture(name):
-    with gzip.open(os.path.join(GOLDEN, "snapshots_v1", f"{name}.json.gz"), "rt") as fh:
+def snapshot_fixture(name, version="v1"):
+    with gzip.open(os.path.join(GOLDEN, f"snapshots_{version}", f"{name}.json.gz"), "rt") as fh:
         return json.load(fh)["blobs"]
 
 

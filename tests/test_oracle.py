@@ -214,3 +214,13 @@ def test_matrix_oracle_handle_table_invariants(seed):
         assert not set(free) & set(owned)
         # removed-but-not-yet-unlinked segments may still own handles
         assert len(free) + len(owned) == len(table) - 1
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations",
+                                  "withIntervals"])
+def test_snapshot_legacy_fixture_bytes(name):
+    """SnapshotLegacy (snapshotlegacy.ts:122-259) of the generateSharedStrings.ts recipes, byte-exact against
+    the reference's committed snapshots/legacy files (the interval-collection blob aside)."""
+    expected = snapshot_fixture(name, "legacy")
+    got = _build_detached(name).summarize_legacy(0, 0)
+    assert [list(b) for b in got["blobs"]] == expected
