@@ -219,6 +219,15 @@ class MergeTreeBatch:
         self._chk(self._L.mtb_doc_checksum(self._h, doc, ctypes.byref(out)))
         return out.value
 
+    def summarize_legacy(self, doc, msn=-1, seq=-1, catchup=None):
+        """SnapshotLegacy summary (snapshotlegacy.ts): (blobs, ISummaryTreeWithStats); `catchup` is the list of
+        messages above the MSN (SharedSegmentSequence.messagesSinceMSNChange)."""
+        self._ensure_flushed()
+        lst = _lib.MtbBlobList()
+        cu = json.dumps(catchup, separators=(",", ":")).encode() if catchup else None
+        self._chk(self._L.mtb_summarize_legacy(self._h, doc, msn, seq, cu, len(cu) if cu else 0, ctypes.byref(lst)))
+        return _blob_list(self._L, lst)
+
     def summarize_v1(self, doc, msn=-1, seq=-1):
         """SnapshotV1 summary: returns (blobs [(path, content)], ISummaryTreeWithStats dict)."""
         self._ensure_flushed()
@@ -231,6 +240,16 @@ class MergeTreeBatch:
         finally:
             self._L.mtb_blob_list_free(ctypes.byref(lst))
         return blobs, summary
+
+
+def _blob_list(L, lst):
+    try:
+        blobs = [(lst.blobs[i].path.decode(), ctypes.string_at(lst.blobs[i].content, lst.blobs[i].content_len).decode("utf-8"))
+                 for i in range(lst.count)]
+        summary = json.loads(ctypes.string_at(lst.summary_json, lst.summary_json_len).decode("utf-8"))
+    finally:
+        L.mtb_blob_list_free(ctypes.byref(lst))
+    return blobs, summary
 
 
 class Client:

@@ -1718,6 +1718,129 @@ void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
   }
 }
 
+// SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:122-259) over the downloaded document: every
+// segment in the MSN view (inserted at or below the MSN, not removed at or below it), coalesced with
+// canAppend + matchProperties, split into "header" (first mergeTreeSnapshotChunkSize chars) and "body",
+// plus the catch-up messages blob (sequence.ts:680-692) when given.
+void summarize_legacy(mtb_batch* b, uint32_t i, const std::string& catchUp, std::vector<std::pair<std::string, std::string>>& blobs,
+                      std::string& summaryJson) {
+  download_doc(b, i);
+  const HostDoc& d = b->docs[i];
+  const DocState& s = b->hst[i];
+  if (d.perm) raise(MTB_E_UNSUPPORTED, "unsupported: SnapshotLegacy of a PermutationVector (it forces SnapshotV1)");
+  const int seq = s.min_seq;
+  std::vector<FlatSeg> fl;
+  flatten(d, s.root, fl, false);
+  struct Piece {
+    bool marker = false;
+    uint32_t refType = 0;
+    U16 text;
+    int len = 0;
+    uint32_t props = 0;
+  };
+  std::vector<Piece> segs;
+  auto textOf = [&](const Seg& g) { return U16(reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len); };
+  bool havePrev = false;
+  Piece prev;
+  for (auto& f : fl) {
+    const Seg& g = d.segs[f.id];
+    if (g.len == 0) continue;  // mapRange skips zero-length nodes
+    if (!(g.seq <= seq && (!seg_removed(g) || g.rseq > seq))) continue;
+    const bool marker = is_marker(g);
+    if (havePrev) {
+      // TextSegment.canAppend (textSegment.ts:71-78) + matchProperties
+      const bool can = !prev.marker && !marker && !(prev.len > 0 && prev.text.back() == u'\n') &&
+                       (prev.len <= 256 || g.len <= 256) && props_match(b, props_of(b, d, prev.props), props_of(b, d, g.props));
+      if (can) {
+        prev.text += textOf(g);
+        prev.len += g.len;
+        continue;
+      }
+      segs.push_back(prev);
+    }
+    prev = Piece();
+    prev.marker = marker;
+    prev.refType = marker ? (g.text & ~MTB_MARKER) : 0;
+    if (!marker) prev.text = textOf(g);
+    prev.len = g.len;
+    prev.props = g.props;
+    havePrev = true;
+  }
+  if (havePrev) segs.push_back(prev);
+  auto json_of = [&](const Piece& p) {
+    std::string o;
+    PropView pv = props_of(b, d, p.props);
+    const bool hasProps = p.props && pv.n() > 0;  // {} -> undefined (snapshotlegacy.ts:236-243)
+    if (p.marker) {
+      o += "{\"marker\":{";
+      if (p.refType) o += "\"refType\":" + std::to_string(p.refType - 1);
+      o += "}";
+      if (hasProps) { o += ",\"props\":"; props_json(b, o, pv); }
+      o += "}";
+    } else if (hasProps) {
+      o += "{\"text\":";
+      hj::quote(o, p.text);
+      o += ",\"props\":";
+      props_json(b, o, pv);
+      o += "}";
+    } else {
+      hj::quote(o, p.text);
+    }
+    return o;
+  };
+  int total = 0;
+  for (auto& p : segs) total += p.len;
+  const int n = (int)segs.size();
+  const int chunkSize = b->opts.chunk_size > 0 ? b->opts.chunk_size : 10000;
+  struct Chunk { int start = 0, count = 0, length = 0; };
+  auto take = [&](int approx, int start) {  // getSeqLengthSegs
+    Chunk c;
+    c.start = start;
+    while (c.length < approx && start + c.count < n) c.length += segs[start + c.count++].len;
+    return c;
+  };
+  auto chunkText = [&](const Chunk& c, bool header) {
+    std::string o = "{\"chunkStartSegmentIndex\":" + std::to_string(c.start) + ",\"chunkSegmentCount\":" + std::to_string(c.count) +
+                    ",\"chunkLengthChars\":" + std::to_string(c.length) + ",\"totalLengthChars\":" + std::to_string(total) +
+                    ",\"totalSegmentCount\":" + std::to_string(n) + ",\"chunkSequenceNumber\":" + std::to_string(seq) +
+                    ",\"segmentTexts\":[";
+    for (int k = 0; k < c.count; k++) {
+      if (k) o += ',';
+      o += json_of(segs[c.start + k]);
+    }
+    o += "]";
+    if (header) {  // buildHeaderMetadataForLegacyChunk (snapshotChunks.ts:178-200); minSequenceNumber undefined
+      o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+      if (c.length < total) o += ",{\"id\":\"body\"}";
+      o += "],\"sequenceNumber\":" + std::to_string(seq) + ",\"totalLength\":" + std::to_string(total) +
+           ",\"totalSegmentCount\":" + std::to_string(n) + "}";
+    }
+    return o + "}";
+  };
+  blobs.clear();
+  const Chunk c1 = take(chunkSize, 0);
+  blobs.push_back({"header", chunkText(c1, true)});
+  if (c1.count < n) blobs.push_back({"body", chunkText(take(total, c1.count), false)});
+  if (!catchUp.empty()) {
+    hj::Value cu = hj::parse(catchUp.data(), catchUp.size());
+    if (cu.kind != hj::Value::kArr) raise(MTB_E_PARSE, "catch-up messages must be a JSON array");
+    if (!cu.items.empty()) blobs.push_back({"catchupOps", hj::dump(cu)});
+  }
+  std::string tree = "{";
+  uint64_t totalBytes = 0;
+  for (size_t k = 0; k < blobs.size(); k++) {
+    if (k) tree += ',';
+    tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
+    hj::quote(tree, hj::from_utf8(blobs[k].second));
+    tree += "}";
+    totalBytes += utf8_byte_length(blobs[k].second);
+  }
+  tree += "}";
+  summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
+                std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
+                ",\"unreferencedBlobSize\":0}}";
+}
+
 char* dup(const std::string& s) {
   char* p = (char*)malloc(s.size() + 1);
   memcpy(p, s.data(), s.size());
@@ -2062,6 +2185,46 @@ int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out) {
   return guarded(b, [&] {
     docref(b, doc);
     *out = fnv(dump_doc(b, doc));
+  });
+}
+
+namespace {
+void fill_blob_list(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& summary, mtb_blob_list* out) {
+  out->count = (uint32_t)blobs.size();
+  out->blobs = (mtb_blob*)calloc(blobs.size() ? blobs.size() : 1, sizeof(mtb_blob));
+  for (size_t k = 0; k < blobs.size(); k++) {
+    out->blobs[k].path = dup(blobs[k].first);
+    out->blobs[k].content = dup(blobs[k].second);
+    out->blobs[k].content_len = blobs[k].second.size();
+  }
+  out->summary_json = dup(summary);
+  out->summary_json_len = summary.size();
+}
+void summary_catch_up(mtb_batch* b, HostDoc& d, int64_t msn, int64_t seq) {
+  if (msn >= 0 && seq >= 0) {  // Client.summarize: updateSeqNumbers(deltaManager.MSN, lastSequenceNumber)
+    mtb_op r{};
+    r.type = MTB_OP_NOOP;
+    r.flags = MTB_F_LAST;
+    r.seq = (uint32_t)seq;
+    r.msn = (uint32_t)msn;
+    d.pending.push_back(r);
+    d.totalOps++;
+    replay(b, nullptr);
+  }
+}
+}  // namespace
+
+// Client.summarize without newMergeTreeSnapshotFormat (client.ts:999-1003)
+int mtb_summarize_legacy(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, const char* catchup_json, size_t catchup_len,
+                         mtb_blob_list* out) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!out) raise(MTB_E_ARG, "null output");
+    summary_catch_up(b, d, msn, seq);
+    std::vector<std::pair<std::string, std::string>> blobs;
+    std::string summary;
+    summarize_legacy(b, doc, catchup_json ? std::string(catchup_json, catchup_len) : std::string(), blobs, summary);
+    fill_blob_list(blobs, summary, out);
   });
 }
 

@@ -171,6 +171,12 @@ int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out);
 int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,
                      mtb_blob_list* out);
 void mtb_blob_list_free(mtb_blob_list* l);
+/* Client.summarize without newMergeTreeSnapshotFormat (client.ts:999-1003, snapshotlegacy.ts:122-259):
+ * "header" / "body" chunks of the segments at the MSN, plus a "catchupOps" blob holding
+ * `catchup_json` (a JSON array of the messages above the MSN that the caller keeps, as
+ * SharedSegmentSequence.messagesSinceMSNChange does, sequence.ts:680-748) when it is non-empty. */
+int mtb_summarize_legacy(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, const char* catchup_json,
+                         size_t catchup_len, mtb_blob_list* out);
 
 /* ---- benchmark / re-replay utilities (no reference counterpart) ----
  * mtb_rewind restores every document to its state before its first replay while keeping the op

@@ -1,0 +1,77 @@
+"""GPU parity of the SnapshotLegacy summary (snapshotlegacy.ts:122-259).
+
+The engine's legacy writer (mtb_summarize_legacy) reads the replayed tree and emits the header / body
+chunks at the MSN; the oracle's writer is pinned byte-exact by the reference's 6 snapshots/legacy files
+(tests/test_oracle.py).  Bar: blobs and ISummaryTreeWithStats byte-equal to the oracle after collaborative
+replay — the 30 reference logs at every 8th group and at the end, synthetic logs in both length modes, a
+small chunk size (header + body), and a catch-up messages blob.
+"""
+import pytest
+
+from helpers import msg_from_compact, replay_fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("chunk", [0, 64])
+def test_reference_logs_legacy_summaries(chunk):
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    fx = replay_fixtures()
+    B = MergeTreeBatch(len(fx), chunk_size=chunk)
+    oracles = []
+    for i, (_, d) in enumerate(fx):
+        B[i].insertTextLocal(0, d["initialText"])
+        B[i].startOrUpdateCollaboration("A")
+        o = OracleDoc(chunk_size=chunk)
+        o.insert_text_local(0, d["initialText"])
+        o.start_collab("A")
+        oracles.append(o)
+    ngroups = len(fx[0][1]["groups"])
+    for g in range(ngroups):
+        for i, (_, d) in enumerate(fx):
+            for m in d["groups"][g]["msgs"]:
+                B[i].applyMsg(msg_from_compact(m))
+                oracles[i].apply_msg(msg_from_compact(m))
+        if g % 8 == 7 or g == ngroups - 1:
+            B.flush()
+            for i, (name, _) in enumerate(fx):
+                gb, gs = B.summarize_legacy(i)
+                osum = oracles[i].summarize_legacy()
+                assert [list(x) for x in gb] == osum["blobs"], f"{name} group {g}: legacy blobs differ"
+                assert gs == osum["summary"], f"{name} group {g}: summary tree differs"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_synthetic_logs_legacy_summary_with_catch_up(new_mode):
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    from pyloggen import LogBatch, make_cfg
+    from helpers import records_to_msgs
+    cfg = make_cfg(seed=91 + int(new_mode), n_ops=1200, new_length_calc=new_mode)
+    lb = LogBatch(cfg, 0, 16)
+    props = lb.props_json()
+    B = MergeTreeBatch(lb.n, new_length_calc=new_mode, chunk_size=500)
+    oracles, tails = [], []
+    for i in range(lb.n):
+        tb = lb.doc_text_bytes(i)
+        il = lb.docs[i].initial_len
+        msgs = records_to_msgs(lb.doc_ops_bytes(i), lb.docs[i].n_ops, tb, props, lb.client_ids(i))
+        B[i].insertTextLocal(0, tb[: il * 2].decode("utf-16-le"))
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode, chunk_size=500)
+        o.insert_text_local(0, tb[: il * 2].decode("utf-16-le"))
+        o.start_collab("obs")
+        for m in msgs:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+        msn = msgs[-1]["minimumSequenceNumber"]
+        tails.append([dict(m, minimumSequenceNumber=msn) for m in msgs if m["sequenceNumber"] > msn])
+    B.flush()
+    for i in range(lb.n):
+        gb, gs = B.summarize_legacy(i, catchup=tails[i])
+        osum = oracles[i].summarize_legacy(catchup=tails[i])
+        assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy blobs differ"
+        assert gs == osum["summary"], f"doc {i}: summary tree differs"
+        assert any(p == "catchupOps" for p, _ in gb) == bool(tails[i])
