@@ -1502,74 +1502,108 @@ struct Eng {
     }
     int target = -1;  // per lane: lane it was appended into (-1 kept / dropped)
     int newLen = 0;   // per lane: final length if it is an append target
-    for (int rr = 0; rr < nrec; rr++) {
-      const int cnt = rl(count, rr * 8);
-      // sequential decisions (uniform), values pulled from lane rr*8 + k
-      int prev = -1;          // lane of the current append target
-      int prevLen = 0;        // its (growing) length
-      uint32_t prevStart = 0; // its PermutationSegment start
-      uint16_t prevLast = 0;  // its (growing) last unit
-      bool prevMarker = false;
-      for (int k = 0; k < cnt; k++) {
-        const int L = rr * 8 + k;
-        const int kk = rl(kind, L);
-        if (kk == 1) {
-          prev = -1;
-          continue;
-        }
-        if (kk != 2) {
-          prev = -1;
-          continue;
-        }
-        const int klen = rl((int)f[F_LEN], L);
-        const uint32_t ktext = rlu(f[F_TEXT], L);
-        const uint16_t klast = (uint16_t)rl((int)last, L);
-        const bool kmarker = (ktext & MTB_MARKER) != 0;
-        bool ok = false;
-        if (isPerm) {
-          // PermutationSegment.canAppend (permutationvector.ts:117-123): both unallocated, or contiguous
-          ok = prev >= 0 && klen > 0 &&
-               (prevStart == MTB_HANDLE_UNALLOC ? ktext == MTB_HANDLE_UNALLOC : ktext == prevStart + (uint32_t)prevLen);
-        } else if (prev >= 0 && klen > 0 && !prevMarker && !kmarker && prevLast != (uint16_t)'\n' &&
-            (prevLen <= 256 || klen <= 256)) {
-          // matchProperties(prev, k)
-          const uint32_t pa = rlu(f[F_PROPS], prev), pb = rlu(f[F_PROPS], L);
-          if (pa == pb) {
-            ok = true;
-          } else {
-            const uint32_t na = rlu(g.n, prev), nb = rlu(g.n, L);
-            if (na != nb) {
-              ok = false;
-            } else if (na == 0) {
-              ok = true;
-            } else if (na > 2) {
-              ok = props_match(pa, pb);
-            } else {
-              const uint32_t ak0 = rlu(g.k0, prev), ac0 = rlu(g.c0, prev), bk0 = rlu(g.k0, L), bc0 = rlu(g.c0, L);
-              if (na == 1) {
-                ok = ak0 == bk0 && ac0 == bc0;
-              } else {
-                const uint32_t ak1 = rlu(g.k1, prev), ac1 = rlu(g.c1, prev), bk1 = rlu(g.k1, L), bc1 = rlu(g.c1, L);
-                ok = (ak0 == bk0 && ac0 == bc0 && ak1 == bk1 && ac1 == bc1) ||
-                     (ak0 == bk1 && ac0 == bc1 && ak1 == bk0 && ac1 == bc0);
-              }
-            }
+    // Run decisions.  Lane-parallel: segment k joins the run of its left neighbour when both are acked
+    // non-empty segments that may append (TextSegment.canAppend: no marker, no trailing newline;
+    // matchProperties, an equivalence, so comparing with the left neighbour equals comparing with the
+    // run's head; PermutationSegment.canAppend: contiguous handles).  The length rule (run length <= 256
+    // or segment length <= 256) only cuts runs at segments longer than 256, and a cut there never
+    // un-cuts a later one, so one segmented scan settles it.  Property sets with more than two keys that
+    // need a full comparison fall back to the sequential form below.
+    const int klen0 = (int)f[F_LEN];
+    const bool cand = s < count && kind == 2 && klen0 > 0;
+    bool compat = false;
+    {
+      // Every DPP read runs with all lanes active (a read from an inactive lane yields 0), so the
+      // neighbour values are fetched in plain statements before any short-circuit combination.
+      const bool hasLeft = s > 0;  // row_shr:1 also reaches lane 7 of the previous group for s == 0
+      const int lcandv = dpp_shr_t<0x111>((int)cand);
+      const bool lcand = hasLeft & (lcandv != 0);
+      if (isPerm) {
+        const uint32_t lst = (uint32_t)dpp_shr_t<0x111>((int)f[F_TEXT]);
+        const int llen = dpp_shr_t<0x111>(klen0);
+        compat = cand && lcand &&
+                 (lst == MTB_HANDLE_UNALLOC ? f[F_TEXT] == MTB_HANDLE_UNALLOC : f[F_TEXT] == lst + (uint32_t)llen);
+      } else {
+        // each neighbour value is compared as soon as it is fetched: the results are lane masks (SGPRs)
+        const bool mk = (f[F_TEXT] & MTB_MARKER) != 0;
+        const int lmkv = dpp_shr_t<0x111>((int)mk);
+        const int llastv = dpp_shr_t<0x111>((int)last);
+        const bool base = cand & lcand & !mk & (lmkv == 0) & ((uint16_t)llastv != (uint16_t)'\n');
+        const bool sameH = f[F_PROPS] == (uint32_t)dpp_shr_t<0x111>((int)f[F_PROPS]);
+        const bool sameN = g.n == (uint32_t)dpp_shr_t<0x111>((int)g.n);
+        const bool k0k0 = g.k0 == (uint32_t)dpp_shr_t<0x111>((int)g.k0);
+        const bool c0c0 = g.c0 == (uint32_t)dpp_shr_t<0x111>((int)g.c0);
+        const bool k1k1 = g.k1 == (uint32_t)dpp_shr_t<0x111>((int)g.k1);
+        const bool c1c1 = g.c1 == (uint32_t)dpp_shr_t<0x111>((int)g.c1);
+        const bool k0k1 = g.k0 == (uint32_t)dpp_shr_t<0x111>((int)g.k1);
+        const bool c0c1 = g.c0 == (uint32_t)dpp_shr_t<0x111>((int)g.c1);
+        const bool k1k0 = g.k1 == (uint32_t)dpp_shr_t<0x111>((int)g.k0);
+        const bool c1c0 = g.c1 == (uint32_t)dpp_shr_t<0x111>((int)g.c0);
+        bool eq = sameH || (sameN && (g.n == 0 || (g.n == 1 && k0k0 && c0c0) ||
+                                      (g.n == 2 && ((k0k0 && c0c0 && k1k1 && c1c1) || (k0k1 && c0c1 && k1k0 && c1c0)))));
+        // more than two keys: a full matchProperties, one neighbour pair at a time (rare)
+        unsigned long long nf = __ballot(base && !sameH && sameN && g.n > 2);
+        if (COLD(nf)) {
+          while (nf) {
+            const int t = first_set(nf);
+            nf &= nf - 1;
+            const bool ok = props_match(rlu(f[F_PROPS], t - 1), rlu(f[F_PROPS], t));
+            if (lane == t) eq = ok;
           }
         }
-        if (ok) {
-          if (lane == L) target = prev;
-          prevLen += klen;
-          prevLast = klast;
-          if (lane == prev) newLen = prevLen;
-        } else {
-          prev = klen > 0 ? L : -1;
-          prevLen = klen;
-          prevLast = klast;
-          prevMarker = kmarker;
-          prevStart = ktext;
-          if (lane == L) newLen = klen;
+        compat = base && eq;
+        // length rule: the run length before this segment (segmented scan restarting at run heads)
+        int v = cand ? klen0 : 0;
+        int st = (!cand || !compat) ? 1 : 0;
+        {
+          const int pv = dpp_shr_t<0x111>(v), pst = dpp_shr_t<0x111>(st);
+          if (s >= 1 && !st) { v += pv; st = pst; }
         }
+        {
+          const int pv = dpp_shr_t<0x112>(v), pst = dpp_shr_t<0x112>(st);
+          if (s >= 2 && !st) { v += pv; st = pst; }
+        }
+        {
+          const int pv = dpp_shr_t<0x114>(v), pst = dpp_shr_t<0x114>(st);
+          if (s >= 4 && !st) { v += pv; st = pst; }
+        }
+        const int cum = v - (cand ? klen0 : 0);
+        if (compat && klen0 > 256 && cum > 256) compat = false;
       }
+    }
+    {
+    // run heads and each member's head (prefix max of head lanes within the 8-lane group)
+    const bool head = cand && !compat;
+    int hv = head ? lane : -1;
+    {
+      const int pv = dpp_shr_t<0x111>(hv + 1) - 1;
+      if (s >= 1) hv = max(hv, pv);
+    }
+    {
+      const int pv = dpp_shr_t<0x112>(hv + 1) - 1;
+      if (s >= 2) hv = max(hv, pv);
+    }
+    {
+      const int pv = dpp_shr_t<0x114>(hv + 1) - 1;
+      if (s >= 4) hv = max(hv, pv);
+    }
+    target = compat ? hv : -1;
+    newLen = cand ? klen0 : 0;
+    const int rcompat = dpp_shr_t<0x101>((int)compat);  // row_shl:1: does lane s + 1 join me?
+      const bool follower = (s < 7) & (rcompat != 0);
+    unsigned long long hm = __ballot(head && follower);
+    while (hm) {
+      const int t = first_set(hm);
+      hm &= hm - 1;
+      unsigned long long run = __ballot(target == t);
+      int tot = rl(klen0, t);
+      while (run) {
+        const int q = first_set(run);
+        run &= run - 1;
+        tot += rl(klen0, q);
+      }
+      if (lane == t) newLen = tot;
+    }
     }
     // targets that received appends: build their new text
     const bool isTarget = s < count && kind == 2 && target < 0 && newLen != (int)f[F_LEN];
