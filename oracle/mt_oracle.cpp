@@ -500,6 +500,7 @@ void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg
 void MergeTree::insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
   ensureIntervalBoundary(pos, refSeq, clientId);
   blockInsert(pos, refSeq, clientId, seq, seg);
+  if (onDelta && seg->parent && seg->cachedLength > 0) onDelta(0, {seg}, nullptr);
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
 
@@ -774,7 +775,9 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
   bool overwrite = false;
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
+  std::vector<Seg*> removed;  // removedSegments (mergeTree.ts:1973): fresh removals only
   auto markRemoved = [&](Seg* s, int, int, int) -> bool {
+    if (!s->removed) removed.push_back(s);
     if (s->removed) {
       overwrite = true;
       if (s->removedSeq == UnassignedSeq) fail_unsupported("local pending remove");
@@ -796,6 +799,7 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
     else blockUpdateLength(b, seq, clientId);
   };
   nodeMap(refSeq, clientId, markRemoved, post, start, end);
+  if (onDelta && !removed.empty()) onDelta(1, removed, nullptr);
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
 
@@ -823,7 +827,9 @@ static void applyProps(Seg* s, const JObj& newProps, bool rewrite) {
 void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq) {
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
+  std::vector<Seg*> annotated;
   auto annotate = [&](Seg* s, int, int, int) -> bool {
+    annotated.push_back(s);
     applyProps(s, props, rewrite);
     counters.segsTouched += 1;
     if (window.collaborating) {
@@ -834,6 +840,10 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
   };
   auto post = [&](Block*) {};
   nodeMap(refSeq, clientId, annotate, post, start, end);
+  if (onDelta && !annotated.empty()) {
+    if (rewrite) fail_unsupported("catch-up rewriting of a rewrite annotate");
+    onDelta(2, annotated, &props);
+  }
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
 
@@ -1141,7 +1151,112 @@ void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
 }
 
 // applyMsg (client.ts:858-875)
+static JVal jop(std::initializer_list<std::pair<const char16_t*, JVal>> kv) {
+  JVal o;
+  o.t = JVal::Obj;
+  for (auto& p : kv) o.obj.push_back({p.first, p.second});
+  return o;
+}
+static JVal segJson(const Seg* s);
+
+void Doc::processMinSequenceNumberChanged(int minSeq) {  // sequence.ts:737-748
+  size_t i = 0;
+  for (; i < messagesSinceMSNChange.size(); i++) {
+    const JVal* sq = obj_get(messagesSinceMSNChange[i].obj, u"sequenceNumber");
+    if (sq && sq->num > minSeq) break;
+  }
+  if (i) messagesSinceMSNChange.erase(messagesSinceMSNChange.begin(), messagesSinceMSNChange.begin() + (long)i);
+}
+std::string Doc::catchUpJson(int minSeq) {  // SharedSegmentSequence.summarizeCore (sequence.ts:676-692)
+  processMinSequenceNumberChanged(minSeq);
+  JVal arr;
+  arr.t = JVal::Arr;
+  for (JVal& m : messagesSinceMSNChange) {
+    obj_set(m.obj, u"minimumSequenceNumber", JVal::number(minSeq));
+    arr.arr.push_back(m);
+  }
+  return json_stringify(arr);
+}
+
 void Doc::applyMsg(const JVal& msg) {
+  if (catchUp && msg.t == JVal::Obj) {
+    // processMergeTreeMsg (sequence.ts:697-733): a message that did not see everything before it is
+    // stored rewritten from its deltas (createOpsFromDelta, sequence.ts:120-172) at refSeq = seq - 1
+    const JVal* type = obj_get(msg.obj, u"type");
+    const JVal* sq = obj_get(msg.obj, u"sequenceNumber");
+    const JVal* rs = obj_get(msg.obj, u"referenceSequenceNumber");
+    const JVal* ms = obj_get(msg.obj, u"minimumSequenceNumber");
+    if (type && type->t == JVal::Str && type->str == u"op" && sq && rs && ms) {
+      const int seqN = (int)sq->num;
+      const bool transform = (int)rs->num != seqN - 1;
+      std::vector<JVal> ops;
+      if (transform)
+        mt.onDelta = [&](int op, const std::vector<Seg*>& segs, const JObj* props) {
+          std::vector<JVal> evOps;  // per event
+          std::vector<std::pair<int, Seg*>> ranges;
+          for (Seg* s : segs) ranges.push_back({mt.localPosition(s), s});
+          for (auto& [position, s] : ranges) {
+            if (op == 2) {
+              JVal pv;
+              pv.t = JVal::Obj;
+              for (auto& kv : *props) {
+                const JVal* cur = s->props ? obj_get(*s->props, kv.first) : nullptr;
+                pv.obj.push_back({kv.first, cur && cur->t != JVal::Undef ? *cur : JVal::null()});
+              }
+              JVal* last = evOps.empty() ? nullptr : &evOps.back();
+              const JVal* lp2 = last ? obj_get(last->obj, u"pos2") : nullptr;
+              const JVal* lpr = last ? obj_get(last->obj, u"props") : nullptr;
+              if (lp2 && lp2->t == JVal::Num && (int)lp2->num == position && match_properties(lpr, &pv)) {
+                obj_set(last->obj, u"pos2", JVal::number(lp2->num + s->cachedLength));
+              } else {
+                evOps.push_back(jop({{u"pos1", JVal::number(position)}, {u"pos2", JVal::number(position + s->cachedLength)},
+                                     {u"props", pv}, {u"type", JVal::number(2)}}));
+              }
+            } else if (op == 0) {
+              evOps.push_back(jop({{u"pos1", JVal::number(position)}, {u"seg", segJson(s)}, {u"type", JVal::number(0)}}));
+            } else {
+              JVal* last = evOps.empty() ? nullptr : &evOps.back();
+              const JVal* lp1 = last ? obj_get(last->obj, u"pos1") : nullptr;
+              const JVal* lp2 = last ? obj_get(last->obj, u"pos2") : nullptr;
+              if (lp1 && lp1->t == JVal::Num && (int)lp1->num == position) {
+                obj_set(last->obj, u"pos2", JVal::number(lp2->num + s->cachedLength));
+              } else {
+                evOps.push_back(jop({{u"pos1", JVal::number(position)}, {u"pos2", JVal::number(position + s->cachedLength)},
+                                     {u"type", JVal::number(1)}}));
+              }
+            }
+          }
+          for (auto& o : evOps) ops.push_back(std::move(o));
+        };
+      struct Reset {
+        MergeTree& t;
+        ~Reset() { t.onDelta = nullptr; }
+      } reset{mt};
+      applyMsgCore(msg);
+      JVal stash = msg;
+      if (transform) {
+        obj_set(stash.obj, u"referenceSequenceNumber", JVal::number(seqN - 1));
+        if (ops.size() == 1) {
+          obj_set(stash.obj, u"contents", ops[0]);
+        } else {
+          JVal arr;
+          arr.t = JVal::Arr;
+          arr.arr = std::move(ops);
+          obj_set(stash.obj, u"contents", jop({{u"ops", arr}, {u"type", JVal::number(3)}}));
+        }
+      }
+      messagesSinceMSNChange.push_back(std::move(stash));
+      if (messagesSinceMSNChange.size() > 20) {  // "Do GC every once in a while"
+        const JVal* s20 = obj_get(messagesSinceMSNChange[20].obj, u"sequenceNumber");
+        if (s20 && s20->num < ms->num) processMinSequenceNumberChanged((int)ms->num);
+      }
+      return;
+    }
+  }
+  applyMsgCore(msg);
+}
+
+void Doc::applyMsgCore(const JVal& msg) {
   if (msg.t != JVal::Obj) throw OracleError(-8, "message is not an object");
   const JVal* cid = obj_get(msg.obj, u"clientId");
   if (!cid || cid->t != JVal::Str) fail_unsupported("message without string clientId");
@@ -1876,8 +1991,11 @@ std::vector<std::pair<std::string, std::string>> Doc::summarizeLegacy(const std:
   }
   if (length != segmentsTotalLength) fail_assert("0x05d", "emit: mismatch in segmentsTotalLength");
   if (count != total) fail_assert("0x05e", "emit: mismatch in totalSegmentCount");
-  if (!catchUpJson.empty()) {
-    JVal cu = json_parse(catchUpJson);
+  std::string tracked;
+  if (catchUpJson.empty() && catchUp) tracked = this->catchUpJson(seq);
+  const std::string& cuText = catchUpJson.empty() ? tracked : catchUpJson;
+  if (!cuText.empty()) {
+    JVal cu = json_parse(cuText);
     if (cu.t == JVal::Arr && !cu.arr.empty()) blobs.push_back({"catchupOps", json_stringify(cu)});
   }
   if (summaryJson) {

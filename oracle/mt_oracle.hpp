@@ -168,6 +168,9 @@ class MergeTree {
   void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
   void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
   void zamboniSegments();
+  // mergeTreeDeltaCallback (INSERT 0 / REMOVE 1 / ANNOTATE 2 with the annotate's props), fired after the
+  // op is applied and before its zamboni, only for non-empty delta segment lists
+  std::function<void(int, const std::vector<Seg*>&, const JObj*)> onDelta;
   // MergeTreeMaintenanceType.UNLINK observer (zamboni.ts:139-148)
   std::function<void(Seg*)> onUnlink;
   // getContainingSegment (mergeTree.ts:787-813) and getPosition (:1240) for PermutationVector
@@ -237,6 +240,7 @@ class Doc {
 
   // Client.applyMsg with a parsed ISequencedDocumentMessage
   void applyMsg(const JVal& msg);
+  void applyMsgCore(const JVal& msg);
   // remote delta op (already decoded)
   void applyRemoteDelta(const JVal& op, int clientShort, int refSeq, int seq);
   // binary record path (include/mtb.h mtb_op)
@@ -258,6 +262,12 @@ class Doc {
   std::vector<std::pair<std::string, std::string>> summarizeLegacy(const std::string& catchUpJson, std::string* summaryJson);
   // canonical segment dump used for engine parity (one JSON object per line)
   std::string dumpSegments();
+
+  // ---- SharedSegmentSequence catch-up messages (sequence.ts:680-748) for SnapshotLegacy summaries
+  bool catchUp = false;
+  std::vector<JVal> messagesSinceMSNChange;
+  void processMinSequenceNumberChanged(int minSeq);
+  std::string catchUpJson(int minSeq);
 
   // ---- PermutationVector (matrix/src/permutationvector.ts) when `perm` is set
   bool perm = false;

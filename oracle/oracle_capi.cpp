@@ -177,6 +177,8 @@ int orc_summarize_legacy(orc_doc* d, int msn, int seq, const char* catchup_json,
     *out = dupstr(s, len);
   });
 }
+// SharedSegmentSequence without newMergeTreeSnapshotFormat keeps messagesSinceMSNChange (sequence.ts:697)
+void orc_enable_catch_up(orc_doc* d) { d->doc.catchUp = true; }
 int orc_dump_segments(orc_doc* d, char** out, size_t* len) {
   return guard(d, [&] { *out = dupstr(d->doc.dumpSegments(), len); });
 }

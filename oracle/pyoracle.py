@@ -51,6 +51,7 @@ def lib():
         L.orc_checksum.restype = ctypes.c_uint64
         L.orc_checksum.argtypes = [vp]
         L.orc_load_v1.argtypes = [vp, cp, sz, cp]
+        L.orc_enable_catch_up.argtypes = [vp]
         L.orc_summarize_legacy.argtypes = [vp, i, i, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_matrix_create.restype = vp
         L.orc_matrix_create.argtypes = [i, i]
@@ -171,6 +172,10 @@ class OracleDoc:
         finally:
             self._L.orc_free(p)
         return json.loads(raw.decode("utf-8"))
+
+    def enable_catch_up(self):
+        """Track catch-up messages like a SharedString without the V1 snapshot option (sequence.ts:697-748)."""
+        self._L.orc_enable_catch_up(self._h)
 
     def summarize_legacy(self, msn=-1, seq=-1, catchup=None):
         """SnapshotLegacy summary (snapshotlegacy.ts): {"blobs": [[path, content]...], "summary": {...}}."""
