@@ -41,9 +41,10 @@ def _check(L, h, rc):
 class MergeTreeBatch:
     """A batch of independent merge-tree documents replayed together on one MI355X."""
 
-    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0, _flags=0):
+    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0, catch_up=False, _flags=0):
+        """catch_up: keep SharedSegmentSequence's catch-up messages (legacy summaries, MTB_BATCH_CATCHUP)."""
         self._L = _lib.lib()
-        opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, int(_flags))
+        opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, int(_flags) | (2 if catch_up else 0))
         h = ctypes.c_void_p()
         rc = self._L.mtb_batch_create(ctypes.byref(opts), ndocs, 1 << device, ctypes.byref(h))
         if rc != 0:

@@ -112,7 +112,7 @@ struct Lru {
   int32_t maxSeq;
 };
 
-struct DocState {     // 256 bytes
+struct DocState {     // 320 bytes
   // slice bases (elements) and capacities
   uint64_t op_base;
   uint64_t seg_base, blk_base, list_base, text_base, heap_base, aux_base, free_base;
@@ -133,8 +133,12 @@ struct DocState {     // 256 bytes
   uint64_t prof[7];     // MTB_PROFILE builds: s_memtime cycles per replay phase (see mtb_replay.hip)
   uint32_t flags;       // DSF_* (host-computed document properties)
   uint32_t cnt[5];      // MTB_PROFILE builds: event counters
+  // catch-up deltas (MTB_F_DELTA records): u32 entries [record, segment -> local position, length, props]
+  uint64_t delta_base;
+  uint32_t delta_cap, delta_used;  // entries
+  uint32_t pad2[12];
 };
-static_assert(sizeof(DocState) == 256, "DocState is copied as 64 dwords (mtb_rewind_kernel)");
+static_assert(sizeof(DocState) == 320, "DocState is copied as 80 dwords (mtb_rewind_kernel)");
 
 // Batch-global interned tables (read-only on the device).
 struct Tables {
@@ -144,6 +148,7 @@ struct Tables {
   const uint32_t* val_class; // matchProperties equivalence class of each value id
   const uint8_t* val_falsy;  // JS falsiness of each value id
   const uint32_t* key_rank;  // array-index keys: numeric value; other keys: MTB_NONE
+  uint32_t* delta;           // catch-up delta pool (per-document slices at DocState.delta_base, 4 words/entry)
 };
 
 // device error codes (DocState.err)
@@ -158,6 +163,7 @@ struct Tables {
 #define DERR_ASSERT_MSN 9  // 0x039 / 0x04e / 0x04f
 #define DERR_DEPTH 10
 #define DERR_SHAPE 11      // a block mixing segment and block children (never produced by the reference)
+#define DERR_CAP_DELTA 13  // catch-up delta slice exhausted
 #define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

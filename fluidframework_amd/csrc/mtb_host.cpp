@@ -224,6 +224,14 @@ struct HostDoc {
   uint64_t totalPayload = 0;
   // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
   bool loaded = false;
+  // SharedSegmentSequence.messagesSinceMSNChange (MTB_BATCH_CATCHUP, sequence.ts:697-748): stored
+  // messages; a lagging one is rewritten from the delta entries of its records (pending[first, +count))
+  struct CatchMsg {
+    hj::Value msg;
+    bool resolved = true;
+    uint32_t first = 0, count = 0;
+  };
+  std::vector<CatchMsg> catchup;
   // PermutationVector (matrix batches): segments carry handles; the handle table lives in the text arena
   bool perm = false;
   uint64_t totalSetcell = 0;
@@ -312,6 +320,7 @@ struct mtb_batch {
   DevBuf<uint32_t> dPSeg;
   DevBuf<FBlk> dPBlk;
   DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
+  DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
   bool matrix = false;              // MTB_BATCH_MATRIX: documents 2m / 2m+1 are matrix m's rows / cols
@@ -1155,6 +1164,8 @@ struct PhaseClock {
   }
 };
 
+void resolve_catch_up(mtb_batch* b, uint32_t i);
+
 void replay(mtb_batch* b, mtb_stats* out) {
   PhaseClock pc;
   if (!b->devInit) device_init(b);
@@ -1230,6 +1241,22 @@ void replay(mtb_batch* b, mtb_stats* out) {
       *out++ = o;
     }
   });
+  // catch-up delta slices: a record's delta has at most one entry per unit of its range
+  {
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      DocState& s = b->hst[i];
+      s.delta_base = tot;
+      s.delta_used = 0;
+      uint64_t cap = 0;
+      if (!s.err)
+        for (const mtb_op& o : b->docs[i].pending)
+          if (o.flags & MTB_F_DELTA) cap += o.type == MTB_OP_INSERT ? 1 : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1;
+      s.delta_cap = (uint32_t)cap;
+      tot += cap;
+    }
+    b->dDelta.ensure(4 * tot + 4);
+  }
   pc.mark("gather");
   scatter_u16(b, pay.get(), nPay, b->dText.p, payc);
   b->dOps.ensure(nOps + 1);
@@ -1244,6 +1271,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
   t.val_class = b->dValClass.p;
   t.val_falsy = b->dValFalsy.p;
   t.key_rank = b->dKeyRank.p;
+  t.delta = b->dDelta.p;
   b->residentLoad = anyLoad;
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
@@ -1264,6 +1292,12 @@ void replay(mtb_batch* b, mtb_stats* out) {
       const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
       if (e) b->hst[i].err = b->hst[i + 1].err = e;
     }
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    if (b->hst[i].err) continue;
+    bool open = false;
+    for (auto& m : b->docs[i].catchup) open |= !m.resolved;
+    if (open) resolve_catch_up(b, i);
+  }
   mtb_stats st{};
   st.kernel_ms = ms;
   int firstErr = 0;
@@ -1667,6 +1701,16 @@ void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std:
                 ",\"unreferencedBlobSize\":0}}";
 }
 
+// processMinSequenceNumberChanged (sequence.ts:737-748)
+void drop_catch_up(HostDoc& d, int64_t minSeq) {
+  size_t i = 0;
+  for (; i < d.catchup.size(); i++) {
+    const hj::Value* sq = member(d.catchup[i].msg, u"sequenceNumber");
+    if (sq && sq->n > (double)minSeq) break;
+  }
+  d.catchup.erase(d.catchup.begin(), d.catchup.begin() + (long)i);
+}
+
 // Client.applyMsg (client.ts:858-887) -> records appended to d
 void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
   {
@@ -1686,6 +1730,7 @@ void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
     const hj::Value* type = member(msg, u"type");
     const bool isOp = type && type->kind == hj::Value::kStr && type->s == u"op";
     const hj::Value* contents = member(msg, u"contents");
+    const size_t recFirst = d.pending.size();
     if (isOp) {
       if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
       if (longId == d.observer) {
@@ -1711,10 +1756,199 @@ void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
       recs.push_back(r);
     }
     recs.back().flags |= MTB_F_LAST;
+    if (isOp && (b->opts.flags & MTB_BATCH_CATCHUP) && !d.perm) {
+      // processMergeTreeMsg (sequence.ts:697-733)
+      HostDoc::CatchMsg cm;
+      cm.msg = msg;
+      cm.first = (uint32_t)recFirst;
+      cm.count = (uint32_t)recs.size();
+      if ((int64_t)base.ref_seq != (int64_t)base.seq - 1) {
+        cm.resolved = false;
+        for (mtb_op& r : recs) {
+          if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE))
+            raise(MTB_E_UNSUPPORTED, "unsupported: catch-up rewriting of a lagging rewrite annotate");
+          if (r.type == MTB_OP_INSERT || r.type == MTB_OP_REMOVE || r.type == MTB_OP_ANNOTATE) r.flags |= MTB_F_DELTA;
+        }
+      }
+      d.catchup.push_back(std::move(cm));
+      if (d.catchup.size() > 20) {  // "Do GC every once in a while"
+        const hj::Value* s20 = member(d.catchup[20].msg, u"sequenceNumber");
+        if (s20 && s20->n < (double)base.msn) drop_catch_up(d, (int64_t)base.msn);
+      }
+    }
     d.totalPayload += d.payload.size() - payloadBefore;
     d.pending.insert(d.pending.end(), recs.begin(), recs.end());
     d.totalOps += recs.size();
     d.lastSeq = base.seq;
+  }
+}
+
+// matchProperties (properties.ts:71-96) restated on parsed JSON values (JS semantics for the keys of
+// primitives: strings expose their indices, other primitives none)
+std::vector<U16> js_keys_of(const hj::Value* v) {
+  std::vector<U16> k;
+  if (!v) return k;
+  if (v->kind == hj::Value::kObj) for (auto& m : v->members) k.push_back(m.first);
+  else if (v->kind == hj::Value::kArr) for (size_t i = 0; i < v->items.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
+  else if (v->kind == hj::Value::kStr) for (size_t i = 0; i < v->s.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
+  return k;
+}
+bool js_get_of(const hj::Value* v, const U16& key, hj::Value& tmp, const hj::Value*& out) {
+  out = nullptr;
+  if (!v) return false;
+  if (v->kind == hj::Value::kObj) { out = v->find(key.c_str()); return out != nullptr; }
+  uint32_t idx;
+  if (!hj::array_index(key, &idx)) return false;
+  if (v->kind == hj::Value::kArr && idx < v->items.size()) { out = &v->items[idx]; return true; }
+  if (v->kind == hj::Value::kStr && idx < v->s.size()) { tmp.kind = hj::Value::kStr; tmp.s = U16(1, v->s[idx]); out = &tmp; return true; }
+  return false;
+}
+bool js_strict_eq(const hj::Value* a, const hj::Value* b) {
+  if (!a || !b) return a == b;
+  if (a->kind != b->kind) return false;
+  switch (a->kind) {
+    case hj::Value::kNull: case hj::Value::kUndef: return true;
+    case hj::Value::kBool: return a->b == b->b;
+    case hj::Value::kNum: return a->n == b->n;
+    case hj::Value::kStr: return a->s == b->s;
+    default: return a == b;  // object identity
+  }
+}
+bool js_match_props(const hj::Value* a, const hj::Value* b) {
+  if ((!a || !a->truthy()) && (!b || !b->truthy())) return true;
+  const auto ka = js_keys_of(a), kb = js_keys_of(b);
+  if (ka.size() != kb.size()) return false;
+  for (auto& k : ka) {
+    hj::Value ta, tb;
+    const hj::Value *av = nullptr, *bv = nullptr;
+    if (!js_get_of(b, k, tb, bv) || !bv || bv->kind == hj::Value::kUndef) return false;
+    js_get_of(a, k, ta, av);
+    if (bv->kind == hj::Value::kObj || bv->kind == hj::Value::kArr || bv->kind == hj::Value::kNull) {
+      if (!js_match_props(av, bv)) return false;
+    } else if (!js_strict_eq(bv, av)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// Rewrite the lagging catch-up messages of this replay from their records' delta entries:
+// SharedSegmentSequence.createOpsFromDelta (sequence.ts:120-172) per delta event, the message then
+// stored with referenceSequenceNumber = seq - 1 and the ops (a GROUP unless exactly one) as contents.
+void resolve_catch_up(mtb_batch* b, uint32_t i) {
+  HostDoc& d = b->docs[i];
+  const DocState& s = b->hst[i];
+  std::vector<uint32_t> ent(4 * (size_t)s.delta_used);
+  HIPCHK(hipMemcpy(ent.data(), b->dDelta.p + 4 * s.delta_base, ent.size() * 4, hipMemcpyDeviceToHost));
+  d.cached = false;
+  download_doc(b, i);
+  std::unordered_map<uint32_t, std::vector<uint32_t>> byRec;
+  for (uint32_t e = 0; e < s.delta_used; e++) byRec[ent[4 * e]].push_back(e);
+  for (auto& m : d.catchup) {
+    if (m.resolved) continue;
+    std::vector<std::string> ops;
+    for (uint32_t k = m.first; k < m.first + m.count && k < d.pending.size(); k++) {
+      const mtb_op& r = d.pending[k];
+      auto it = byRec.find(k);
+      if (it == byRec.end()) continue;  // no delta segments: no event
+      struct Ev { int pos1, pos2; std::string props; hj::Value pv; bool hasPos2; std::string json; };
+      std::vector<Ev> ev;
+      for (uint32_t e : it->second) {
+        const int position = (int)ent[4 * e + 1];
+        const int len = (int)ent[4 * e + 2];
+        const uint32_t ph = ent[4 * e + 3];
+        if (r.type == MTB_OP_INSERT) {
+          std::string seg;
+          if (r.flags & MTB_F_MARKER) {
+            seg = "{\"marker\":{";
+            if (r.pos2 != 0xFFFFFFFFu) seg += "\"refType\":" + std::to_string(r.pos2);
+            seg += "}";
+            if (r.props) { seg += ",\"props\":"; props_json(b, seg, props_of(b, d, ph)); }
+            seg += "}";
+          } else {
+            U16 text(reinterpret_cast<const char16_t*>(d.payload.data() + r.payload), r.pos2);
+            if (r.props) {
+              seg = "{\"text\":";
+              hj::quote(seg, text);
+              seg += ",\"props\":";
+              props_json(b, seg, props_of(b, d, ph));
+              seg += "}";
+            } else {
+              hj::quote(seg, text);
+            }
+          }
+          Ev x{};
+          x.json = "{\"pos1\":" + std::to_string(position) + ",\"seg\":" + seg + ",\"type\":0}";
+          ev.push_back(std::move(x));
+        } else if (r.type == MTB_OP_REMOVE) {
+          if (!ev.empty() && ev.back().pos1 == position) {
+            ev.back().pos2 += len;
+          } else {
+            Ev x{};
+            x.pos1 = position;
+            x.pos2 = position + len;
+            ev.push_back(std::move(x));
+          }
+        } else {  // ANNOTATE: props[key] = segment.properties?.[key] ?? null for the op's keys
+          const uint32_t* opl = b->in.pool.data() + b->in.pidx[2 * r.props];
+          const PropView sv = props_of(b, d, ph);
+          std::string pj = "{";
+          for (uint32_t q = 0; q < opl[0]; q++) {
+            const uint32_t key = opl[1 + 2 * q];
+            if (q) pj += ',';
+            hj::quote(pj, b->in.keys[key]);
+            pj += ':';
+            std::string val = "null";
+            for (uint32_t z = 0; z < sv.n(); z++)
+              if (sv.p[1 + 2 * z] == key) val = b->in.valJson[sv.p[2 + 2 * z]];
+            pj += val;
+          }
+          pj += "}";
+          hj::Value pv = hj::parse(pj.data(), pj.size());
+          if (!ev.empty() && ev.back().hasPos2 && ev.back().pos2 == position && js_match_props(&ev.back().pv, &pv)) {
+            ev.back().pos2 += len;
+          } else {
+            Ev x{};
+            x.pos1 = position;
+            x.pos2 = position + len;
+            x.hasPos2 = true;
+            x.props = pj;
+            x.pv = std::move(pv);
+            ev.push_back(std::move(x));
+          }
+        }
+      }
+      for (auto& x : ev) {
+        if (r.type == MTB_OP_INSERT) ops.push_back(x.json);
+        else if (r.type == MTB_OP_REMOVE)
+          ops.push_back("{\"pos1\":" + std::to_string(x.pos1) + ",\"pos2\":" + std::to_string(x.pos2) + ",\"type\":1}");
+        else
+          ops.push_back("{\"pos1\":" + std::to_string(x.pos1) + ",\"pos2\":" + std::to_string(x.pos2) + ",\"props\":" +
+                        x.props + ",\"type\":2}");
+      }
+    }
+    std::string contents;
+    if (ops.size() == 1) {
+      contents = ops[0];
+    } else {
+      contents = "{\"ops\":[";
+      for (size_t q = 0; q < ops.size(); q++) {
+        if (q) contents += ',';
+        contents += ops[q];
+      }
+      contents += "],\"type\":3}";
+    }
+    const hj::Value* sq = member(m.msg, u"sequenceNumber");
+    for (auto& mem : m.msg.members) {
+      if (mem.first == u"referenceSequenceNumber") {
+        mem.second = hj::Value();
+        mem.second.kind = hj::Value::kNum;
+        mem.second.n = sq->n - 1;
+      } else if (mem.first == u"contents") {
+        mem.second = hj::parse(contents.data(), contents.size());
+      }
+    }
+    m.resolved = true;
   }
 }
 
@@ -1821,8 +2055,23 @@ void summarize_legacy(mtb_batch* b, uint32_t i, const std::string& catchUp, std:
   const Chunk c1 = take(chunkSize, 0);
   blobs.push_back({"header", chunkText(c1, true)});
   if (c1.count < n) blobs.push_back({"body", chunkText(take(total, c1.count), false)});
-  if (!catchUp.empty()) {
-    hj::Value cu = hj::parse(catchUp.data(), catchUp.size());
+  std::string tracked;
+  if (catchUp.empty() && (b->opts.flags & MTB_BATCH_CATCHUP)) {
+    // SharedSegmentSequence.summarizeCore (sequence.ts:676-692)
+    HostDoc& dm = b->docs[i];
+    drop_catch_up(dm, seq);
+    tracked = "[";
+    for (size_t k = 0; k < dm.catchup.size(); k++) {
+      for (auto& mem : dm.catchup[k].msg.members)
+        if (mem.first == u"minimumSequenceNumber") mem.second.n = seq;
+      if (k) tracked += ',';
+      tracked += hj::dump(dm.catchup[k].msg);
+    }
+    tracked += "]";
+  }
+  const std::string& cuText = catchUp.empty() ? tracked : catchUp;
+  if (!cuText.empty()) {
+    hj::Value cu = hj::parse(cuText.data(), cuText.size());
     if (cu.kind != hj::Value::kArr) raise(MTB_E_PARSE, "catch-up messages must be a JSON array");
     if (!cu.items.empty()) blobs.push_back({"catchupOps", hj::dump(cu)});
   }
@@ -2107,6 +2356,7 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
     t.val_class = b->dValClass.p;
     t.val_falsy = b->dValFalsy.p;
     t.key_rank = b->dKeyRank.p;
+    t.delta = b->dDelta.p;
     HIPCHK(hipEventRecord(b->ev0, b->stream));
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,

@@ -193,6 +193,9 @@ struct Eng {
   bool sp_internal;
   int pending_fix;
   int ld_pos;                   // insertSegments' advancing insert position within a LOADSEG batch
+  uint32_t cur_k;               // index of the record being applied (catch-up delta entries name it)
+  bool delta_on;                // the record asks for its delta ranges (MTB_F_DELTA)
+  uint32_t delta_used;          // entries written in this document's delta slice
   static constexpr bool isPerm = MODE == MODE_MATRIX;  // matrix batches hold PermutationVectors only
   int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
@@ -1213,6 +1216,56 @@ struct Eng {
     return h;
   }
 
+  // ------------------------------------------------------------------ catch-up deltas
+  // SequenceDeltaEvent ranges (sequenceDelta.ts:43-56) for SharedSegmentSequence's rewriting of lagging
+  // messages (sequence.ts:697-733): one entry per delta segment, in tree order: [record, segment id ->
+  // local position after the op, cachedLength, property set after the op].
+  __device__ __forceinline__ uint32_t* dslice() const { return UP(sh->tab.delta) + ds->delta_base * 4; }
+  __device__ __forceinline__ void delta_emit(bool sel, uint32_t sid, uint32_t len, uint32_t props) {
+    const unsigned long long m = __ballot(sel);
+    if (!m) return;
+    const uint32_t n = (uint32_t)__popcll(m);
+    if (delta_used + n > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+    if (sel) {
+      uint32_t* e = dslice() + 4 * (delta_used + rank_below(m));
+      e[0] = cur_k;
+      e[1] = sid;
+      e[2] = len;
+      e[3] = props;
+    }
+    delta_used += n;
+    wsync();
+  }
+  // getPosition (mergeTree.ts:1240) of the segments named by entries [from, delta_used): the local
+  // lengths left of the segment in its block and left of each ancestor in theirs
+  __device__ __forceinline__ void delta_positions(uint32_t from) {
+    uint32_t* const dl = dslice();
+    for (uint32_t i = from; i < delta_used; i++) {
+      const uint32_t sid = U(dl[4 * i + 1]);
+      uint32_t child = MTB_LEAF | sid;
+      uint32_t b = U(segp[sid]);
+      int pos = 0;
+      while (b != MTB_NONE) {
+        const uint32_t* rec = bw(b);
+        uint32_t id = MTB_NONE, ln = 0, rs = 0;
+        if (lane < MTB_MAXCH) {
+          id = rec[F_ID * 8 + lane];
+          ln = rec[F_LEN * 8 + lane];
+          rs = rec[F_RSEQ * 8 + lane];
+        }
+        const uint32_t cnt = U(rec[FB_HDR]);
+        const uint32_t par = U(rec[FB_HDR + 1]);
+        const int j = first_set(__ballot((uint32_t)lane < cnt && id == child));
+        const int ol = lane < j ? child_olen(id, (int)ln, (int)rs) : 0;
+        pos += csum8(ol);
+        child = b;
+        b = par;
+      }
+      if (lane == 0) dl[4 * i + 1] = (uint32_t)pos;
+      wsync();
+    }
+  }
+
   // ------------------------------------------------------------------ nodeMap (remove / annotate)
   // The segments of one leaf-level block (depth d) touched by [start, end), all lanes at once (the
   // boundaries were split beforehand, so each segment is wholly in or out of the range).  `pos` is the
@@ -1261,6 +1314,7 @@ struct Eng {
       const int dsum = csum8(dl);
       if (lane == 0) sh->acc[d] += dsum;
       wsync();
+      if (COLD(delta_on)) delta_emit(fresh, id & ~MTB_LEAF, (uint32_t)len, props);
       // overlapping removes (already removed): append C to removedClientIds (copy-on-write list) and an
       // OVERLAP entry on every ancestor list (no observer-length change)
       unsigned long long om = __ballot(visit && rseq >= 0);
@@ -1299,6 +1353,7 @@ struct Eng {
         am &= ~__ballot(mine);
         wsync();
       }
+      if (COLD(delta_on)) delta_emit(visit, id & ~MTB_LEAF, (uint32_t)len, lane < count ? V.f[F_PROPS][lane] : 0u);
     }
     // addToLRUSet for the first visited segment (the block's needsScour then becomes true)
     const int t = first_set(vm);
@@ -2032,6 +2087,8 @@ struct Eng {
     memo_old = MTB_NONE;
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)(int16_t)o.client;
+    if constexpr (MODE == MODE_REPLAY) delta_on = (o.flags & MTB_F_DELTA) != 0;
+    else delta_on = false;
     if constexpr (MODE == MODE_LOAD) {
       apply_loadseg(o, S, C);
       return;
@@ -2073,6 +2130,12 @@ struct Eng {
           }
           settle();
           if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (COLD(delta_on)) {
+            const uint32_t from = delta_used;
+            delta_emit(lane == 0, sid, (uint32_t)len, o.props ? (MTB_GPROPS | UP(sh->tab.pidx)[2 * o.props + 1]) : 0u);
+            delta_positions(from);
+            if (bad()) return;
+          }
           PROF_ADD(PH_INSERT, t0);
         }
         zamboni_p();
@@ -2090,7 +2153,12 @@ struct Eng {
         PROF_ADD(PH_BOUNDARY, t0);
         if (bad()) return;
         t0 = PROF_T();
+        const uint32_t dfrom = delta_used;
         node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
+        if (COLD(delta_on)) {
+          if (bad()) return;
+          delta_positions(dfrom);
+        }
         PROF_ADD(PH_NODEMAP, t0);
         zamboni_p();
         break;
@@ -2167,6 +2235,9 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
   e.struct_changed = false;
   e.pending_fix = -1;
   e.ld_pos = 0;
+  e.delta_on = false;
+  e.delta_used = ds->delta_used;
+  e.cur_k = 0;
   e.sp_internal = false;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
@@ -2210,6 +2281,7 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
       if constexpr (MODE == MODE_LOAD) {
         if (cur.type != MTB_OP_LOADSEG) break;  // the summary body precedes every op
       }
+      e.cur_k = k;
       if constexpr (MODE == MODE_MATRIX) {
         if (cur.type == MTB_OP_SETCELL) {
           e.setcell(cur, par);
@@ -2244,6 +2316,7 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
     ds->text_used = e.text_used;
     ds->heap_cnt = e.heap_cnt;
     ds->aux_used = e.aux_used;
+    ds->delta_used = e.delta_used;
     ds->n_mod += e.n_mod;
     ds->ops_applied += e.ops_applied;
     ds->text_bytes += e.text_bytes;
@@ -2317,6 +2390,7 @@ extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pri
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pristine + i);
   uint32_t* dst = reinterpret_cast<uint32_t*>(docs + i);
   dst[l] = src[l];
+  if (l < 16) dst[64 + l] = src[64 + l];
   const uint64_t bb = pristine[i].blk_base, sb = pristine[i].seg_base;
   const uint32_t* ps = reinterpret_cast<const uint32_t*>(pblk + i);
   uint32_t* bd = reinterpret_cast<uint32_t*>(blks + bb);

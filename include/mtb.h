@@ -48,7 +48,8 @@ enum {
   MTB_F_MARKER = 0x02,  /* insert: Marker segment, pos2 = refType (0xFFFFFFFF = undefined) */
   MTB_F_REWRITE = 0x04, /* annotate: combiningOp {name:"rewrite"} */
   MTB_F_SEGOBJ = 0x08,  /* insert: seg given as {text, props?} object (props id may be 0) */
-  MTB_F_PERMSEG = 0x40  /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
+  MTB_F_PERMSEG = 0x40, /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
+  MTB_F_DELTA = 0x80    /* record the op's delta ranges (catch-up rewriting, MTB_BATCH_CATCHUP) */
 };
 typedef struct mtb_op {
   uint8_t type;
@@ -71,6 +72,9 @@ typedef struct mtb_options {
 } mtb_options;
 
 #define MTB_BATCH_MATRIX 1 /* mtb_options.flags: documents 2m / 2m+1 are matrix m's rows / cols PermutationVectors */
+#define MTB_BATCH_CATCHUP 2 /* mtb_options.flags: keep SharedSegmentSequence.messagesSinceMSNChange per document
+                               (sequence.ts:697-748), lagging messages rewritten from their deltas, for
+                               mtb_summarize_legacy's catch-up blob */
 
 typedef struct mtb_stats {
   uint64_t ops_applied;     /* delta ops applied (each GROUP member counts once) */

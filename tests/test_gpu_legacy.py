@@ -75,3 +75,68 @@ def test_synthetic_logs_legacy_summary_with_catch_up(new_mode):
         assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy blobs differ"
         assert gs == osum["summary"], f"doc {i}: summary tree differs"
         assert any(p == "catchupOps" for p, _ in gb) == bool(tails[i])
+
+
+@pytest.mark.parametrize("chunk", [0, 300])
+def test_reference_logs_legacy_catch_up_rewriting(chunk):
+    """MTB_BATCH_CATCHUP: the engine keeps messagesSinceMSNChange and rewrites lagging messages from the
+    kernel's delta entries; the legacy summary (header/body + catchupOps) equals the oracle's, whose
+    rewriting replays to the golden final text (tests/test_oracle.py)."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    fx = replay_fixtures()
+    B = MergeTreeBatch(len(fx), chunk_size=chunk, catch_up=True)
+    oracles = []
+    for i, (_, d) in enumerate(fx):
+        B[i].insertTextLocal(0, d["initialText"])
+        B[i].startOrUpdateCollaboration("A")
+        o = OracleDoc(chunk_size=chunk)
+        o.insert_text_local(0, d["initialText"])
+        o.start_collab("A")
+        o.enable_catch_up()
+        oracles.append(o)
+    ngroups = len(fx[0][1]["groups"])
+    for g in range(ngroups):
+        for i, (_, d) in enumerate(fx):
+            for m in d["groups"][g]["msgs"]:
+                B[i].applyMsg(msg_from_compact(m))
+                oracles[i].apply_msg(msg_from_compact(m))
+        if g % 16 == 15:
+            B.flush()
+            for i, (name, _) in enumerate(fx):
+                gb, gs = B.summarize_legacy(i)
+                osum = oracles[i].summarize_legacy()
+                assert [list(x) for x in gb] == osum["blobs"], f"{name} group {g}: legacy + catch-up blobs differ"
+                assert gs == osum["summary"], f"{name} group {g}"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_synthetic_logs_catch_up_rewriting(new_mode):
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    from pyloggen import LogBatch, make_cfg
+    from helpers import records_to_msgs
+    cfg = make_cfg(seed=123 + int(new_mode), n_ops=1000, new_length_calc=new_mode)
+    lb = LogBatch(cfg, 0, 16)
+    props = lb.props_json()
+    B = MergeTreeBatch(lb.n, new_length_calc=new_mode, catch_up=True)
+    oracles = []
+    for i in range(lb.n):
+        tb = lb.doc_text_bytes(i)
+        il = lb.docs[i].initial_len
+        B[i].insertTextLocal(0, tb[: il * 2].decode("utf-16-le"))
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, tb[: il * 2].decode("utf-16-le"))
+        o.start_collab("obs")
+        o.enable_catch_up()
+        for m in records_to_msgs(lb.doc_ops_bytes(i), lb.docs[i].n_ops, tb, props, lb.client_ids(i)):
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    for i in range(lb.n):
+        gb, gs = B.summarize_legacy(i)
+        osum = oracles[i].summarize_legacy()
+        assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy + catch-up blobs differ"
+        assert any(p == "catchupOps" for p, _ in gb)

@@ -228,3 +228,19 @@ def test_matrix_messages_pack_per_vector():
         assert all(x[1] & 0x40 for x in vec if x[0] == 0)  # MTB_F_PERMSEG
     with pytest.raises(MergeTreeError, match="mtb_matrix"):
         B.init_doc(0, "", "x")
+
+
+def test_catch_up_tracking_flags_lagging_records():
+    """MTB_BATCH_CATCHUP: records of messages with refSeq != seq - 1 ask the kernel for their deltas
+    (MTB_F_DELTA) so processMergeTreeMsg's rewriting (sequence.ts:697-733) can be done after replay."""
+    import struct
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1, catch_up=True)
+    B[0].insertTextLocal(0, "abcdef")
+    B[0].startOrUpdateCollaboration("A")
+    base = {"clientId": "B", "minimumSequenceNumber": 0, "type": "op"}
+    B[0].applyMsg(dict(base, sequenceNumber=1, referenceSequenceNumber=0, contents={"type": 0, "pos1": 1, "seg": "x"}))
+    B[0].applyMsg(dict(base, sequenceNumber=2, referenceSequenceNumber=0, contents={"type": 1, "pos1": 0, "pos2": 2}))
+    ops, n, _ = B.export_pending(0)
+    flags = [struct.unpack_from("<BB", ops, 32 * k)[1] for k in range(n)]
+    assert not flags[0] & 0x80 and flags[1] & 0x80
