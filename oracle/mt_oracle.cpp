@@ -1809,8 +1809,10 @@ void Doc::enablePermutation() {
   perm = true;
   // onMaintenance (permutationvector.ts:418-441): handles of unlinked segments back to the free list
   mt.onUnlink = [this](Seg* s) {
-    if (s->perm && s->start >= 1)
+    if (s->perm && s->start >= 1) {
+      if (onHandlesRecycled) onHandlesRecycled(s->start, s->cachedLength);  // clear, then free
       for (int i = 0; i < s->cachedLength; i++) freeHandle(s->start + i);
+    }
   };
 }
 int Doc::allocateHandle() {
@@ -1889,9 +1891,162 @@ void MatrixDoc::applyMsg(const JVal& msg) {
     cellsDropped++;
     return;
   }
-  rows.getAllocatedHandle(ar);
-  cols.getAllocatedHandle(ac);
+  const int rh = rows.getAllocatedHandle(ar);
+  const int ch = cols.getAllocatedHandle(ac);
+  // no pending local write for an observer (matrix.ts:682): cells.setCell(rowHandle, colHandle, value)
+  const JVal* v = obj_get(contents->obj, u"value");
+  std::optional<std::string> val;
+  if (v && !v->isUndef()) val = json_stringify(*v);
+  cells.setCell((uint32_t)rh, (uint32_t)ch, std::move(val));
   cellsSet++;
+}
+
+// ---------------------------------------------------------------- SparseArray2D (sparsearray2d.ts)
+namespace {
+uint32_t interlace8(uint32_t i) {  // x8ToInterlacedX16 (sparsearray2d.ts:8-14)
+  uint32_t j = i;
+  j = (j | (j << 4)) & 0x0f0f;
+  j = (j | (j << 2)) & 0x3333;
+  j = (j | (j << 1)) & 0x5555;
+  return j;
+}
+uint32_t interlaceBitsX16(uint32_t x) { return (interlace8((x >> 8) & 0xff) << 16) | interlace8(x & 0xff); }
+uint32_t r0ToMorton16(uint32_t row) { return interlaceBitsX16(row) << 1; }
+uint32_t c0ToMorton16(uint32_t col) { return interlaceBitsX16(col); }
+uint32_t morton2x16(uint32_t row, uint32_t col) { return r0ToMorton16(row) | c0ToMorton16(col); }
+inline uint32_t byte0(uint32_t x) { return x >> 24; }
+inline uint32_t byte1(uint32_t x) { return (x >> 16) & 0xff; }
+inline uint32_t byte2(uint32_t x) { return (x >> 8) & 0xff; }
+inline uint32_t byte3(uint32_t x) { return x & 0xff; }
+template <class C>
+C& getLevel(std::unique_ptr<C>& slot) {  // getLevel (:226-231): new Array(256).fill(undefined)
+  if (!slot) slot.reset(new C());
+  return *slot;
+}
+// the 16 keys of a 16x16 tile on one row (forEachKeyInRow :110-114) / col (forEachKeyInCol :116-120)
+template <class F> void keysInRow(uint32_t rowBits, F&& f) { for (uint32_t c = 0; c < 16; c++) f(rowBits | c0ToMorton16(c)); }
+template <class F> void keysInCol(uint32_t colBits, F&& f) { for (uint32_t r = 0; r < 16; r++) f(r0ToMorton16(r) | colBits); }
+}  // namespace
+
+void SparseArray2D::setCell(uint32_t row, uint32_t col, std::optional<std::string> value) {  // :93-103
+  const uint32_t keyHi = morton2x16(row >> 16, col >> 16);
+  const uint32_t keyLo = morton2x16(row & 0xffff, col & 0xffff);
+  if (keyHi >= rootLength) rootLength = (uint64_t)keyHi + 1;  // the JS array grows with holes
+  L0& l0 = getLevel(root[keyHi]);
+  L1& l1 = getLevel(l0[byte0(keyLo)]);
+  L2& l2 = getLevel(l1[byte1(keyLo)]);
+  L3& l3 = getLevel(l2[byte2(keyLo)]);
+  l3[byte3(keyLo)] = std::move(value);
+}
+const std::optional<std::string>* SparseArray2D::getCell(uint32_t row, uint32_t col) const {  // :68-88
+  const uint32_t keyHi = morton2x16(row >> 16, col >> 16);
+  auto it = root.find(keyHi);
+  if (it == root.end() || !it->second) return nullptr;
+  const uint32_t keyLo = morton2x16(row & 0xffff, col & 0xffff);
+  const auto& l1 = (*it->second)[byte0(keyLo)];
+  if (!l1) return nullptr;
+  const auto& l2 = (*l1)[byte1(keyLo)];
+  if (!l2) return nullptr;
+  const auto& l3 = (*l2)[byte2(keyLo)];
+  if (!l3) return nullptr;
+  return &(*l3)[byte3(keyLo)];
+}
+void SparseArray2D::clearRows(uint32_t rowStart, uint32_t rowCount) {  // :150-174
+  for (uint64_t row = rowStart; row < (uint64_t)rowStart + rowCount; row++) {
+    const uint32_t rowHi = r0ToMorton16((uint32_t)(row >> 16));
+    const uint32_t rowLo = r0ToMorton16((uint32_t)row & 0xffff);
+    // the reference scans colHi 0..0xffff; only existing root entries matter
+    for (auto& [keyHi, lvl0] : root) {
+      if (!lvl0 || ((keyHi & 0xAAAAAAAAu) != rowHi)) continue;
+      L0& l0 = *lvl0;
+      keysInRow(byte0(rowLo), [&](uint32_t k1) {
+        if (!l0[k1]) return;
+        L1& l1 = *l0[k1];
+        keysInRow(byte1(rowLo), [&](uint32_t k2) {
+          if (!l1[k2]) return;
+          L2& l2 = *l1[k2];
+          keysInRow(byte2(rowLo), [&](uint32_t k3) {
+            if (!l2[k3]) return;
+            L3& l3 = *l2[k3];
+            keysInRow(byte3(rowLo), [&](uint32_t k4) { l3[k4].reset(); });
+          });
+        });
+      });
+    }
+  }
+}
+void SparseArray2D::clearCols(uint32_t colStart, uint32_t colCount) {  // :198-224
+  for (uint64_t col = colStart; col < (uint64_t)colStart + colCount; col++) {
+    const uint32_t colHi = c0ToMorton16((uint32_t)(col >> 16));
+    const uint32_t colLo = c0ToMorton16((uint32_t)col & 0xffff);
+    for (auto& [keyHi, lvl0] : root) {
+      if (!lvl0 || ((keyHi & 0x55555555u) != colHi)) continue;
+      L0& l0 = *lvl0;
+      keysInCol(byte0(colLo), [&](uint32_t k1) {
+        if (!l0[k1]) return;
+        L1& l1 = *l0[k1];
+        keysInCol(byte1(colLo), [&](uint32_t k2) {
+          if (!l1[k2]) return;
+          L2& l2 = *l1[k2];
+          keysInCol(byte2(colLo), [&](uint32_t k3) {
+            if (!l2[k3]) return;
+            L3& l3 = *l2[k3];
+            keysInCol(byte3(colLo), [&](uint32_t k4) { l3[k4].reset(); });
+          });
+        });
+      });
+    }
+  }
+}
+std::string SparseArray2D::snapshotJson() const {  // JSON.stringify(root): holes and undefined -> null
+  std::string o = "[";
+  auto lvl = [&](auto& self, const auto& arr, auto leafTag) -> void {
+    (void)leafTag;
+    o += '[';
+    for (size_t i = 0; i < 256; i++) {
+      if (i) o += ',';
+      using E = std::decay_t<decltype(arr[i])>;
+      if constexpr (std::is_same_v<E, std::optional<std::string>>) {
+        o += arr[i] ? *arr[i] : std::string("null");
+      } else {
+        if (arr[i]) self(self, *arr[i], 0);
+        else o += "null";
+      }
+    }
+    o += ']';
+  };
+  for (uint64_t k = 0; k < rootLength; k++) {
+    if (k) o += ',';
+    auto it = root.find((uint32_t)k);
+    if (it != root.end() && it->second) lvl(lvl, *it->second, 0);
+    else o += "null";
+  }
+  return o + "]";
+}
+
+std::vector<std::pair<std::string, std::string>> MatrixDoc::summarize(std::string* summaryJson) {
+  std::string rj, cj;
+  auto rb = rows.summarizeV1(&rj);
+  auto cb = cols.summarizeV1(&cj);
+  const std::string cellsBlob = "[" + cells.snapshotJson() + ",[null]]";  // [cells.snapshot(), pending.snapshot()]
+  std::vector<std::pair<std::string, std::string>> blobs;
+  for (auto& x : rb) blobs.push_back({"rows/" + x.first, x.second});
+  for (auto& x : cb) blobs.push_back({"cols/" + x.first, x.second});
+  blobs.push_back({"cells", cellsBlob});
+  if (summaryJson) {
+    // SummaryTreeBuilder (summaryUtils.ts:138-198): addWithStats merges the vectors' stats, addBlob counts cells
+    const JVal r = json_parse(rj.data(), rj.size()), c = json_parse(cj.data(), cj.size());
+    auto stat = [](const JVal& v, const char16_t* k) { return (uint64_t)obj_get(obj_get(v.obj, u"stats")->obj, k)->num; };
+    std::string cq;
+    json_stringify_to(cq, JVal::string(utf8_to_u16(cellsBlob.data(), cellsBlob.size())));
+    uint64_t bytes = stat(r, u"totalBlobSize") + stat(c, u"totalBlobSize") + cellsBlob.size();  // UTF-8 bytes (getBlobSize)
+    *summaryJson = "{\"summary\":{\"type\":1,\"tree\":{\"rows\":" + json_stringify(*obj_get(r.obj, u"summary")) +
+                   ",\"cols\":" + json_stringify(*obj_get(c.obj, u"summary")) + ",\"cells\":{\"type\":2,\"content\":" + cq +
+                   "}}},\"stats\":{\"treeNodeCount\":" + std::to_string(1 + stat(r, u"treeNodeCount") + stat(c, u"treeNodeCount")) +
+                   ",\"blobNodeCount\":" + std::to_string(1 + stat(r, u"blobNodeCount") + stat(c, u"blobNodeCount")) +
+                   ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(bytes) + ",\"unreferencedBlobSize\":0}}";
+  }
+  return blobs;
 }
 
 // ---------------------------------------------------------------- SnapshotLegacy (snapshotlegacy.ts)

@@ -10,6 +10,7 @@
 // (MT = packages/dds/merge-tree/src).
 #pragma once
 #include <cstdint>
+#include <array>
 #include <deque>
 #include <functional>
 #include <map>
@@ -280,6 +281,27 @@ class Doc {
   int getAllocatedHandle(int pos);
   std::string handleTableJson() const;
   void enablePermutation();
+  // PermutationVector.handlesRecycledCallback (permutationvector.ts:418-441): handles about to be freed
+  std::function<void(int start, int count)> onHandlesRecycled;
+};
+
+// SparseArray2D (matrix/src/sparsearray2d.ts): cells keyed by Morton-interleaved (row, col) handles in a
+// root array indexed by the high 16 bits of both and four 256-entry levels for the low bits.  Values are
+// kept as their JSON text (nullopt = undefined).
+struct SparseArray2D {
+  using Leaf = std::array<std::optional<std::string>, 256>;
+  template <class C> using Lvl = std::array<std::unique_ptr<C>, 256>;
+  using L3 = Leaf;
+  using L2 = Lvl<L3>;
+  using L1 = Lvl<L2>;
+  using L0 = Lvl<L1>;
+  std::map<uint32_t, std::unique_ptr<L0>> root;  // sparse JS array `root`
+  uint64_t rootLength = 1;                       // `[undefined]`: length 1
+  void setCell(uint32_t row, uint32_t col, std::optional<std::string> value);
+  const std::optional<std::string>* getCell(uint32_t row, uint32_t col) const;
+  void clearRows(uint32_t rowStart, uint32_t rowCount);
+  void clearCols(uint32_t colStart, uint32_t colCount);
+  std::string snapshotJson() const;  // JSON.stringify(snapshot())
 };
 
 // SharedMatrix observer over two PermutationVectors (matrix/src/matrix.ts:636-697); the cell store
@@ -290,6 +312,9 @@ struct MatrixDoc {
   MatrixDoc(Doc& r, Doc& c) : rows(r), cols(c) {
     rows.enablePermutation();
     cols.enablePermutation();
+    // onRowHandlesRecycled / onColHandlesRecycled (matrix.ts:721-733)
+    rows.onHandlesRecycled = [this](int h, int n) { cells.clearRows((uint32_t)h, (uint32_t)n); };
+    cols.onHandlesRecycled = [this](int h, int n) { cells.clearCols((uint32_t)h, (uint32_t)n); };
   }
   void startOrUpdateCollaboration(const std::string& id, int minSeq, int curSeq) {
     rows.startOrUpdateCollaboration(id, minSeq, curSeq);
@@ -297,6 +322,9 @@ struct MatrixDoc {
   }
   void applyMsg(const JVal& msg);
   uint64_t cellsSet = 0, cellsDropped = 0;
+  SparseArray2D cells;  // matrix.ts:96 (the observer's `pending` array stays empty)
+  // SharedMatrix.summarizeCore (matrix.ts:449-463): {rows, cols: PermutationVector.summarize, cells}
+  std::vector<std::pair<std::string, std::string>> summarize(std::string* summaryJson);
 };
 
 uint64_t fnv1a64(const std::string& s);

@@ -72,6 +72,49 @@ int orc_matrix_apply_msg_json(orc_matrix* m, const char* json, size_t len) {
   return rc;
 }
 
+// SharedMatrix.summarizeCore (matrix.ts:449-463): {"blobs": [[path, content]...], "summary": ISummaryTreeWithStats}
+int orc_matrix_summarize(orc_matrix* m, char** out, size_t* len) {
+  int rc = guard(&m->rows, [&] {
+    std::string summary;
+    auto blobs = m->m.summarize(&summary);
+    JVal arr;
+    arr.t = JVal::Arr;
+    for (auto& b : blobs) {
+      JVal pair;
+      pair.t = JVal::Arr;
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.first)));
+      pair.arr.push_back(JVal::string(utf8_to_u16(b.second)));
+      arr.arr.push_back(pair);
+    }
+    std::string s = "{\"blobs\":" + json_stringify(arr) + ",\"summary\":" + summary + "}";
+    *out = dupstr(s, len);
+  });
+  if (rc) m->err = m->rows.err;
+  return rc;
+}
+// cells.getCell(rowHandle, colHandle) (sparsearray2d.ts:68-88): JSON text, "" when undefined
+int orc_matrix_get_cell_by_handle(orc_matrix* m, uint32_t rh, uint32_t ch, char** out, size_t* len) {
+  const std::optional<std::string>* v = m->m.cells.getCell(rh, ch);
+  *out = dupstr(v && *v ? **v : std::string(), len);
+  return 0;
+}
+
+// SparseArray2D on its own (sparsearray2d.spec.ts cases)
+SparseArray2D* orc_sa2d_create() { return new SparseArray2D(); }
+void orc_sa2d_destroy(SparseArray2D* a) { delete a; }
+void orc_sa2d_set(SparseArray2D* a, uint32_t r, uint32_t c, const char* json) {
+  a->setCell(r, c, json ? std::optional<std::string>(json) : std::nullopt);
+}
+int orc_sa2d_get(SparseArray2D* a, uint32_t r, uint32_t c, char* buf, size_t cap) {  // -1 undefined, else length
+  const std::optional<std::string>* v = a->getCell(r, c);
+  if (!v || !*v) return -1;
+  snprintf(buf, cap, "%s", (*v)->c_str());
+  return (int)(*v)->size();
+}
+void orc_sa2d_clear_rows(SparseArray2D* a, uint32_t s, uint32_t n) { a->clearRows(s, n); }
+void orc_sa2d_clear_cols(SparseArray2D* a, uint32_t s, uint32_t n) { a->clearCols(s, n); }
+char* orc_sa2d_snapshot(SparseArray2D* a, size_t* len) { return dupstr(a->snapshotJson(), len); }
+
 orc_doc* orc_create(int new_length_calc, int chunk_size, int verify) {
   Options o;
   o.newLengthCalc = new_length_calc != 0;

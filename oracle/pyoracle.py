@@ -62,8 +62,55 @@ def lib():
         L.orc_matrix_last_error.argtypes = [vp]
         L.orc_matrix_start_collab.argtypes = [vp, cp, i, i]
         L.orc_matrix_apply_msg_json.argtypes = [vp, cp, sz]
+        L.orc_matrix_summarize.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
+        L.orc_matrix_get_cell_by_handle.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(sz)]
+        u32 = ctypes.c_uint32
+        L.orc_sa2d_create.restype = vp
+        L.orc_sa2d_destroy.argtypes = [vp]
+        L.orc_sa2d_set.argtypes = [vp, u32, u32, cp]
+        L.orc_sa2d_get.argtypes = [vp, u32, u32, ctypes.c_char_p, sz]
+        L.orc_sa2d_clear_rows.argtypes = [vp, u32, u32]
+        L.orc_sa2d_clear_cols.argtypes = [vp, u32, u32]
+        L.orc_sa2d_snapshot.restype = vp
+        L.orc_sa2d_snapshot.argtypes = [vp, ctypes.POINTER(sz)]
         _LIB = L
     return _LIB
+
+
+class OracleSparseArray2D:
+    """SparseArray2D (matrix/src/sparsearray2d.ts) of the oracle; values are JSON texts (None = undefined)."""
+
+    def __init__(self):
+        self._L = lib()
+        self._h = self._L.orc_sa2d_create()
+        self._buf = ctypes.create_string_buffer(4096)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orc_sa2d_destroy(self._h)
+            self._h = None
+
+    def set_cell(self, r, c, value_json):
+        self._L.orc_sa2d_set(self._h, r, c, None if value_json is None else value_json.encode())
+
+    def get_cell(self, r, c):
+        n = self._L.orc_sa2d_get(self._h, r, c, self._buf, len(self._buf))
+        return None if n < 0 else self._buf.value.decode()
+
+    def clear_rows(self, start, count):
+        self._L.orc_sa2d_clear_rows(self._h, start, count)
+
+    def clear_cols(self, start, count):
+        self._L.orc_sa2d_clear_cols(self._h, start, count)
+
+    def snapshot(self):
+        n = ctypes.c_size_t()
+        p = self._L.orc_sa2d_snapshot(self._h, ctypes.byref(n))
+        try:
+            return ctypes.string_at(p, n.value).decode()
+        finally:
+            self._L.orc_free(p)
 
 
 class OracleError(RuntimeError):
@@ -256,3 +303,21 @@ class OracleMatrix:
     def apply_msg(self, msg):
         raw = msg if isinstance(msg, (bytes, bytearray)) else json.dumps(msg).encode()
         self._chk(self._L.orc_matrix_apply_msg_json(self._h, raw, len(raw)))
+
+    def _take(self, fn, *args):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(fn(self._h, *args, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return ctypes.string_at(p, n.value).decode("utf-8")
+        finally:
+            self._L.orc_free(p)
+
+    def summarize(self):
+        """SharedMatrix summary (matrix.ts:449-463): {"blobs": [[path, content]...], "summary": {...}}."""
+        return json.loads(self._take(self._L.orc_matrix_summarize))
+
+    def cell_by_handle(self, row_handle, col_handle):
+        """JSON text of cells.getCell(rowHandle, colHandle), or None when undefined."""
+        s = self._take(self._L.orc_matrix_get_cell_by_handle, row_handle, col_handle)
+        return s or None

@@ -253,3 +253,94 @@ def test_catch_up_messages_replay_to_the_final_text(idx):
         assert m["referenceSequenceNumber"] == m["sequenceNumber"] - 1
         r.apply_msg(m)
     assert r.get_text() == d["groups"][-1]["resultText"], name
+
+
+# ---------------------------------------------------------------- SharedMatrix cells (SparseArray2D)
+def _sa2d_fill(a, r0, c0, nr, nc):  # matrix/src/test/utils.ts fill: value = row * rowCount + col
+    for r in range(r0, r0 + nr):
+        for c in range(c0, c0 + nc):
+            a.set_cell(r, c, str(r * nr + c))
+
+
+def _sa2d_extract(a, r0, c0, nr, nc):
+    return [[a.get_cell(r, c) for c in range(c0, c0 + nc)] for r in range(r0, r0 + nr)]
+
+
+def test_sparse_array_2d_read_write_corners():
+    """sparsearray2d.spec.ts "read/write top-left / bottom-right 256x256" (64x64 here: same tiles)."""
+    from pyoracle import OracleSparseArray2D
+    a = OracleSparseArray2D()
+    for r0 in (0, 0xFFFFFF00):
+        _sa2d_fill(a, r0, r0, 64, 64)
+        assert _sa2d_extract(a, r0, r0, 64, 64) == [[str(r * 64 + c) for c in range(r0, r0 + 64)]
+                                                    for r in range(r0, r0 + 64)]
+    assert a.get_cell(0, 0xFFFFFF00) is None and a.get_cell(5, 300) is None
+
+
+def _clear_cases():
+    cases = [(0, 0, 1, 1, 0, 1), (0, 0, 256, 256, 127, 2)]
+    cases += [(0, 0, 16, 16, i, 1) for i in range(16)]
+    s = 0xFFFFFFF0
+    cases += [(s, s, 16, 16, i, 1) for i in range(s, s + 16)]
+    return cases
+
+
+@pytest.mark.parametrize("rows", [True, False])
+def test_sparse_array_2d_clear_rows_cols(rows):
+    """sparsearray2d.spec.ts "clear row/cols": clearing equals setting the cleared cells to undefined."""
+    from pyoracle import OracleSparseArray2D
+    for (r0, c0, nr, nc, cs, cn) in _clear_cases():
+        if nr == 256:
+            nr = nc = 160  # straddles the 127/128 discontinuity, fewer cells
+        actual, expected = OracleSparseArray2D(), OracleSparseArray2D()
+        _sa2d_fill(actual, r0, c0, nr, nc)
+        _sa2d_fill(expected, r0, c0, nr, nc)
+        if rows:
+            actual.clear_rows(cs, cn)
+            for r in range(cs, cs + cn):
+                for c in range(c0, c0 + nc):
+                    expected.set_cell(r, c, None)
+        else:
+            actual.clear_cols(cs, cn)
+            for r in range(r0, r0 + nr):
+                for c in range(cs, cs + cn):
+                    expected.set_cell(r, c, None)
+        assert _sa2d_extract(actual, r0, c0, nr, nc) == _sa2d_extract(expected, r0, c0, nr, nc)
+
+
+def test_sparse_array_2d_snapshot_layout():
+    """snapshot() is the root array itself: JSON.stringify turns holes and undefined into null; levels are
+    256-entry arrays created on first write and never removed (clears only reset leaves)."""
+    import json
+    from pyoracle import OracleSparseArray2D
+    a = OracleSparseArray2D()
+    assert a.snapshot() == "[null]"
+    a.set_cell(1, 2, '"x"')  # keyLo = row bits odd, col bits even = 0b110 -> leaf index 6
+    snap = json.loads(a.snapshot())
+    assert len(snap) == 1 and len(snap[0]) == 256 and snap[0][0][0][0][6] == "x"
+    a.clear_rows(1, 1)
+    assert json.loads(a.snapshot())[0][0][0][0] == [None] * 256
+    a.set_cell(0x10000, 0, "1")  # keyHi = morton(1, 0) = 2: the root grows to length 3 with a hole
+    snap = json.loads(a.snapshot())
+    assert len(snap) == 3 and snap[1] is None and snap[2][0][0][0][0] == 1
+
+
+def test_matrix_cells_follow_handles():
+    """SharedMatrix observer cells (matrix.ts:668-690): set at (rowHandle, colHandle) when both positions
+    survive; recycled handles clear their row/col before reuse (matrix.ts:721-733)."""
+    import json
+    from helpers import make_matrix_log
+    from pyoracle import OracleMatrix
+    o = OracleMatrix()
+    o.start_collab("obs")
+    for m in make_matrix_log(11, 600, n_clients=3, lag=8):
+        o.apply_msg(m)
+    s = o.summarize()
+    paths = [p for p, _ in s["blobs"]]
+    assert paths[-1] == "cells" and "rows/handleTable" in paths and "cols/handleTable" in paths
+    cells, pending = json.loads(s["blobs"][-1][1])
+    assert pending == [None]
+    st = s["summary"]["stats"]
+    assert st["treeNodeCount"] == 5 and st["blobNodeCount"] == len(paths)
+    assert st["totalBlobSize"] == sum(len(c.encode()) for _, c in s["blobs"])
+    assert list(s["summary"]["summary"]["tree"]) == ["rows", "cols", "cells"]
