@@ -320,7 +320,8 @@ MTB_BATCH_MATRIX = 1
 
 class MatrixBatch(MergeTreeBatch):
     """A batch of SharedMatrix observers (matrix.ts): matrix m is the PermutationVector documents 2m (rows)
-    and 2m+1 (cols).  Vector ops and setCell handle allocation replay on the GPU; cell values are not kept."""
+    and 2m+1 (cols).  Vector ops and setCell handle allocation replay on the GPU; the kernel's cell events
+    (setCell handles, recycled handles) are replayed on the host into each matrix's SparseArray2D."""
 
     def __init__(self, nmatrices, new_length_calc=False, chunk_size=0, device=0):
         super().__init__(2 * nmatrices, new_length_calc=new_length_calc, chunk_size=chunk_size, device=device,
@@ -335,6 +336,31 @@ class MatrixBatch(MergeTreeBatch):
 
     def init_matrix(self, m, observer_long_id, min_seq=0, cur_seq=0):
         self._chk(self._L.mtb_matrix_init(self._h, m, observer_long_id.encode(), min_seq, cur_seq))
+
+    def intern_value(self, value_json):
+        """Id of a setCell value (JSON text) for SETCELL records packed by the caller (0 = undefined)."""
+        raw = value_json.encode()
+        out = ctypes.c_uint32()
+        self._chk(self._L.mtb_matrix_intern_value(self._h, raw, len(raw), ctypes.byref(out)))
+        return out.value
+
+    def matrix_summarize(self, m):
+        """SharedMatrix.summarizeCore (matrix.ts:449): (blobs [(path, content)], ISummaryTreeWithStats)."""
+        self._ensure_flushed()
+        lst = _lib.MtbBlobList()
+        self._chk(self._L.mtb_matrix_summarize(self._h, m, ctypes.byref(lst)))
+        return _blob_list(self._L, lst)
+
+    def get_cell(self, m, row, col):
+        """SharedMatrix.getCell (matrix.ts:173): the value's JSON text, or None when undefined."""
+        self._ensure_flushed()
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_matrix_get_cell(self._h, m, row, col, buf, len(buf), ctypes.byref(n)))
+        if n.value >= len(buf):
+            buf = ctypes.create_string_buffer(n.value + 1)
+            self._chk(self._L.mtb_matrix_get_cell(self._h, m, row, col, buf, len(buf), ctypes.byref(n)))
+        return buf.value.decode("utf-8") if n.value else None
 
     def apply_matrix_msg(self, m, msg):
         s = msg if isinstance(msg, (bytes, bytearray)) else (msg.encode() if isinstance(msg, str) else json.dumps(msg).encode())
@@ -365,5 +391,11 @@ class SharedMatrix:
         return 2 * self._m + 1
 
     def summarize(self):
-        """{"rows": (blobs, summary), "cols": (blobs, summary)} of the two PermutationVectors."""
-        return {"rows": self._b.summarize_v1(self.rows_doc), "cols": self._b.summarize_v1(self.cols_doc)}
+        """SharedMatrix.summarizeCore (matrix.ts:449-463): (blobs, ISummaryTreeWithStats) with the rows / cols
+        PermutationVector summaries and the cells blob."""
+        return self._b.matrix_summarize(self._m)
+
+    def getCell(self, row, col):
+        """matrix.ts:173: the cell's value (parsed JSON), or None when undefined."""
+        v = self._b.get_cell(self._m, row, col)
+        return None if v is None else json.loads(v)

@@ -163,7 +163,9 @@ struct Tables {
 #define DERR_ASSERT_MSN 9  // 0x039 / 0x04e / 0x04f
 #define DERR_DEPTH 10
 #define DERR_SHAPE 11      // a block mixing segment and block children (never produced by the reference)
-#define DERR_CAP_DELTA 13  // catch-up delta slice exhausted
+#define DERR_CAP_DELTA 13  // catch-up delta / matrix cell-event slice exhausted
+#define MTB_CELL_SET 1     // matrix cell event: this vector's handle for a setCell record
+#define MTB_CELL_CLEAR 2   // matrix cell event: handles [start, start + count) recycled by zamboni
 #define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

@@ -209,6 +209,84 @@ struct LoadImage {
   uint32_t root = 0;
 };
 
+// ------------------------------------------------------------------ SharedMatrix cells
+// SparseArray2D (matrix/src/sparsearray2d.ts) as the host keeps it for a matrix batch: every (row, col)
+// handle pair ever written, with its current value id (0 = undefined).  The Morton-keyed tile levels
+// the reference allocates on a write (getLevel, :226-231) are exactly the prefixes of the written keys,
+// so the snapshot JSON is rebuilt from the sorted keys.  Written from the kernel's cell events.
+struct CellStore {
+  std::unordered_map<uint64_t, uint32_t> cells;  // (row << 32 | col) -> value id
+  std::unordered_map<uint32_t, std::vector<uint32_t>> rowCols, colRows;
+  static uint32_t spread(uint32_t x) {  // interlaceBitsX16: the low 16 bits onto the even positions
+    x &= 0xffff;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+  }
+  static uint32_t morton(uint32_t r, uint32_t c) { return (spread(r) << 1) | spread(c); }  // r0c0ToMorton2x16
+  void set(uint32_t r, uint32_t c, uint32_t v) {
+    auto [it, fresh] = cells.try_emplace(((uint64_t)r << 32) | c, v);
+    if (!fresh) {
+      it->second = v;
+      return;
+    }
+    rowCols[r].push_back(c);
+    colRows[c].push_back(r);
+  }
+  void clearRow(uint32_t r) {  // clearRows(r, 1) (:150-174): leaves only, tiles stay
+    auto it = rowCols.find(r);
+    if (it != rowCols.end())
+      for (uint32_t c : it->second) cells[((uint64_t)r << 32) | c] = 0;
+  }
+  void clearCol(uint32_t c) {
+    auto it = colRows.find(c);
+    if (it != colRows.end())
+      for (uint32_t r : it->second) cells[((uint64_t)r << 32) | c] = 0;
+  }
+  // JSON.stringify(snapshot()): the root array (holes -> null) of 256-entry levels
+  std::string snapshot_json(const std::vector<std::string>& vals) const {
+    std::vector<std::pair<uint64_t, uint32_t>> keys;  // (keyHi << 32 | keyLo, value id)
+    keys.reserve(cells.size());
+    for (auto& [k, v] : cells) {
+      const uint32_t r = (uint32_t)(k >> 32), c = (uint32_t)k;
+      keys.push_back({((uint64_t)morton(r >> 16, c >> 16) << 32) | morton(r, c), v});
+    }
+    std::sort(keys.begin(), keys.end());
+    std::string o = "[";
+    size_t i = 0;
+    const uint64_t rootLen = keys.empty() ? 1 : (keys.back().first >> 32) + 1;
+    // level `lv` (0..3) of the tile whose key prefix is `pre`: 256 entries, byte `lv` of keyLo
+    auto level = [&](auto& self, int lv, uint64_t pre) -> void {
+      o += '[';
+      for (uint32_t e = 0; e < 256; e++) {
+        if (e) o += ',';
+        const int shift = 24 - 8 * lv;
+        const uint64_t want = pre | ((uint64_t)e << shift);
+        const uint64_t mask = ~((1ull << shift) - 1);
+        if (i < keys.size() && (keys[i].first & mask) == want) {
+          if (lv == 3) {
+            o += keys[i].second ? vals[keys[i].second] : std::string("null");
+            i++;
+          } else {
+            self(self, lv + 1, want);
+          }
+        } else {
+          o += "null";
+        }
+      }
+      o += ']';
+    };
+    for (uint64_t hi = 0; hi < rootLen; hi++) {
+      if (hi) o += ',';
+      if (i < keys.size() && (keys[i].first >> 32) == hi) level(level, 0, hi << 32);
+      else o += "null";
+    }
+    return o + "]";
+  }
+};
+
 // ------------------------------------------------------------------ host mirror of a document
 struct HostDoc {
   std::vector<std::string> longIds;
@@ -235,6 +313,7 @@ struct HostDoc {
   // PermutationVector (matrix batches): segments carry handles; the handle table lives in the text arena
   bool perm = false;
   uint64_t totalSetcell = 0;
+  std::unique_ptr<CellStore> cells;  // rows vector of a matrix: the matrix's cells (matrix.ts:96)
   LoadImage img;
   // device mirror
   DocState st{};
@@ -324,6 +403,8 @@ struct mtb_batch {
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
   bool matrix = false;              // MTB_BATCH_MATRIX: documents 2m / 2m+1 are matrix m's rows / cols
+  std::vector<std::string> cellVals{"null"};                 // setCell values (JSON text), id 0 = undefined
+  std::unordered_map<std::string, uint32_t> cellValIds;
   // batched moves: chunk tables and host->device staging
   DevBuf<uint64_t> dMvSrc, dMvDst;
   DevBuf<uint32_t> dMvLen, dStageW;
@@ -1165,6 +1246,7 @@ struct PhaseClock {
 };
 
 void resolve_catch_up(mtb_batch* b, uint32_t i);
+void apply_cell_events(mtb_batch* b, uint32_t matrix);
 
 void replay(mtb_batch* b, mtb_stats* out) {
   PhaseClock pc;
@@ -1249,9 +1331,14 @@ void replay(mtb_batch* b, mtb_stats* out) {
       s.delta_base = tot;
       s.delta_used = 0;
       uint64_t cap = 0;
-      if (!s.err)
+      if (!s.err && b->matrix) {
+        // cell events: one per setCell, one per segment unlinked with handles (live segments plus at most
+        // three created per record)
+        cap = s.seg_cap + 4ull * b->docs[i].pending.size() + 1;
+      } else if (!s.err) {
         for (const mtb_op& o : b->docs[i].pending)
           if (o.flags & MTB_F_DELTA) cap += o.type == MTB_OP_INSERT ? 1 : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1;
+      }
       s.delta_cap = (uint32_t)cap;
       tot += cap;
     }
@@ -1292,6 +1379,9 @@ void replay(mtb_batch* b, mtb_stats* out) {
       const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
       if (e) b->hst[i].err = b->hst[i + 1].err = e;
     }
+  if (b->matrix)
+    for (uint32_t i = 0; i + 1 < b->ndocs; i += 2)
+      if (!b->hst[i].err) apply_cell_events(b, i / 2);
   for (uint32_t i = 0; i < b->ndocs; i++) {
     if (b->hst[i].err) continue;
     bool open = false;
@@ -1832,6 +1922,53 @@ bool js_match_props(const hj::Value* a, const hj::Value* b) {
   return true;
 }
 
+// Replay one matrix's cell events of this replay into its CellStore.  Both vectors' record streams hold
+// every setCell; a clear logged at record k of either stream happened after the setCells before k and
+// before the next one, and clears commute with each other, so events are merged by setCell ordinal.
+void apply_cell_events(mtb_batch* b, uint32_t m) {
+  HostDoc& R = b->docs[2 * m];
+  if (!R.cells) R.cells.reset(new CellStore());
+  struct Ev { uint32_t epoch, kind, a, n; };
+  std::vector<Ev> ev[2];
+  std::vector<uint32_t> setVal;
+  for (int v = 0; v < 2; v++) {
+    const DocState& s = b->hst[2 * m + v];
+    const std::vector<mtb_op>& recs = b->docs[2 * m + v].pending;
+    std::vector<uint32_t> ent(4 * (size_t)s.delta_used);
+    if (!ent.empty())
+      HIPCHK(hipMemcpy(ent.data(), b->dDelta.p + 4 * s.delta_base, ent.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ordinal(recs.size() + 1, 0);  // setCells before record k
+    for (size_t k = 0; k < recs.size(); k++) {
+      ordinal[k + 1] = ordinal[k] + (recs[k].type == MTB_OP_SETCELL);
+      if (v == 0 && recs[k].type == MTB_OP_SETCELL) setVal.push_back(recs[k].props);
+    }
+    for (uint32_t e = 0; e < s.delta_used; e++) {
+      const uint32_t k = ent[4 * e], kind = ent[4 * e + 1];
+      if (k >= recs.size()) raise(MTB_E_ASSERT, "cell event names no record");
+      ev[v].push_back({ordinal[k], kind, ent[4 * e + 2], ent[4 * e + 3]});
+    }
+  }
+  CellStore& cs = *R.cells;
+  size_t p[2] = {0, 0};
+  for (uint32_t j = 0;; j++) {
+    uint32_t h[2] = {0, 0};
+    bool have[2] = {false, false};
+    for (int v = 0; v < 2; v++)
+      for (; p[v] < ev[v].size() && ev[v][p[v]].epoch == j; p[v]++) {
+        const Ev& x = ev[v][p[v]];
+        if (x.kind == MTB_CELL_CLEAR) {
+          for (uint32_t q = 0; q < x.n; q++) v == 0 ? cs.clearRow(x.a + q) : cs.clearCol(x.a + q);
+        } else {  // the setCell with ordinal j: its record's events follow the clears logged before it
+          h[v] = x.a;
+          have[v] = true;
+        }
+      }
+    if (have[0] != have[1]) raise(MTB_E_ASSERT, "setCell allocated in one vector only");
+    if (have[0]) cs.set(h[0], h[1], setVal[j]);
+    if (p[0] == ev[0].size() && p[1] == ev[1].size()) break;
+  }
+}
+
 // Rewrite the lagging catch-up messages of this replay from their records' delta entries:
 // SharedSegmentSequence.createOpsFromDelta (sequence.ts:120-172) per delta event, the message then
 // stored with referenceSequenceNumber = seq - 1 and the ops (a GROUP unless exactly one) as contents.
@@ -2224,6 +2361,12 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json, size_t len)
   });
 }
 
+uint32_t intern_cell_value(mtb_batch* b, const std::string& json) {
+  auto [it, fresh] = b->cellValIds.try_emplace(json, (uint32_t)b->cellVals.size());
+  if (fresh) b->cellVals.push_back(json);
+  return it->second;
+}
+
 // SharedMatrix.processCore (matrix.ts:636-697): a vector op goes to its PermutationVector's applyMsg
 // (with that vector's updateSeqNumbers); a remote setCell becomes a SETCELL record in both vectors
 // (adjusted, exchanged and allocated on the GPU); a local setCell is an ack with no vector effect.
@@ -2258,6 +2401,8 @@ int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json, s
     base.ref_seq = u32field(msg, u"referenceSequenceNumber", "referenceSequenceNumber");
     base.msn = u32field(msg, u"minimumSequenceNumber", "minimumSequenceNumber");
     const uint32_t row = u32field(*contents, u"row", "row"), col = u32field(*contents, u"col", "col");
+    // the cell value (opaque JSON, matrix.ts:684), interned batch-wide; absent = undefined (id 0)
+    if (const hj::Value* v = member(*contents, u"value")) base.props = intern_cell_value(b, hj::dump(*v));
     mtb_op r = base, c = base;
     r.client = R.client(longId);  // getOrAddShortClientId in adjustPosition (client.ts:1070)
     r.pos1 = row;
@@ -2566,3 +2711,97 @@ void mtb_blob_list_free(mtb_blob_list* l) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ SharedMatrix cells and summary
+namespace {
+// PermutationVector.getMaybeHandle (permutationvector.ts:200-207, handlecache.ts): the handle stored
+// at local position `pos` of vector document i (start + offset; HandleUnallocated when none).
+uint32_t vector_handle_at(mtb_batch* b, uint32_t i, uint32_t pos) {
+  download_doc(b, i);
+  const HostDoc& d = b->docs[i];
+  uint32_t p = pos, found = MTB_NONE;
+  auto visit = [&](auto& self, uint32_t bi) -> bool {  // segments in order; true once pos is reached
+    const Blk& B = d.blks[bi];
+    for (int k = 0; k < B.count; k++) {
+      const uint32_t c = B.child[k];
+      if (!(c & MTB_LEAF)) {
+        if (self(self, c)) return true;
+        continue;
+      }
+      const Seg& g = d.segs[c & ~MTB_LEAF];
+      const uint32_t len = g.rseq < 0 ? (uint32_t)g.len : 0u;  // local view: removed segments are empty
+      if (p < len) {
+        found = g.text == MTB_HANDLE_UNALLOC ? MTB_HANDLE_UNALLOC : g.text + p;
+        return true;
+      }
+      p -= len;
+    }
+    return false;
+  };
+  if (!visit(visit, b->hst[i].root)) raise(MTB_E_ARG, "0x027 position out of range");  // ensureRange (matrix.ts:189)
+  return found;
+}
+}  // namespace
+
+int mtb_matrix_intern_value(mtb_batch* b, const char* json, size_t len, uint32_t* id_out) {
+  return guarded(b, [&] {
+    if (!json || !id_out) raise(MTB_E_ARG, "null argument");
+    hj::Value v = hj::parse(json, len);
+    *id_out = intern_cell_value(b, hj::dump(v));
+  });
+}
+
+int mtb_matrix_get_cell(mtb_batch* b, uint32_t matrix, uint32_t row, uint32_t col, char* buf, size_t cap, size_t* len_out) {
+  return guarded(b, [&] {
+    if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
+    if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    if (b->hst[2 * matrix].err) raise(derr_code(b->hst[2 * matrix].err), derr_text(b->hst[2 * matrix].err));
+    std::string v;
+    const uint32_t rh = vector_handle_at(b, 2 * matrix, row);
+    const uint32_t ch = vector_handle_at(b, 2 * matrix + 1, col);  // bounds-checked even for an unallocated row
+    const HostDoc& R = b->docs[2 * matrix];
+    if (rh != MTB_HANDLE_UNALLOC && ch != MTB_HANDLE_UNALLOC && R.cells) {
+      auto it = R.cells->cells.find(((uint64_t)rh << 32) | ch);
+      if (it != R.cells->cells.end() && it->second) v = b->cellVals[it->second];
+    }
+    if (len_out) *len_out = v.size();
+    if (buf && cap) snprintf(buf, cap, "%s", v.c_str());
+  });
+}
+
+// SharedMatrix.summarizeCore (matrix.ts:449-463) through SummaryTreeBuilder (summaryUtils.ts:138-198):
+// addWithStats(rows), addWithStats(cols) (PermutationVector.summarize), addBlob(cells)
+int mtb_matrix_summarize(mtb_batch* b, uint32_t matrix, mtb_blob_list* out) {
+  return guarded(b, [&] {
+    if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
+    if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    if (!out) raise(MTB_E_ARG, "null output");
+    std::vector<std::pair<std::string, std::string>> all, vb[2];
+    std::string vs[2];
+    for (int v = 0; v < 2; v++) summarize(b, 2 * matrix + v, vb[v], vs[v]);
+    const HostDoc& R = b->docs[2 * matrix];
+    const std::string cells = "[" + (R.cells ? R.cells->snapshot_json(b->cellVals) : std::string("[null]")) + ",[null]]";
+    for (int v = 0; v < 2; v++)
+      for (auto& x : vb[v]) all.push_back({(v ? "cols/" : "rows/") + x.first, x.second});
+    all.push_back({"cells", cells});
+    uint64_t st[3] = {1, 1, utf8_byte_length(cells)};  // treeNodeCount, blobNodeCount, totalBlobSize
+    std::string tree = "{";
+    for (int v = 0; v < 2; v++) {
+      const hj::Value sj = hj::parse(vs[v].data(), vs[v].size());
+      const hj::Value* stats = member(sj, u"stats");
+      st[0] += (uint64_t)member(*stats, u"treeNodeCount")->n;
+      st[1] += (uint64_t)member(*stats, u"blobNodeCount")->n;
+      st[2] += (uint64_t)member(*stats, u"totalBlobSize")->n;
+      tree += v ? ",\"cols\":" : "\"rows\":";
+      tree += hj::dump(*member(sj, u"summary"));
+    }
+    tree += ",\"cells\":{\"type\":2,\"content\":";
+    hj::quote(tree, hj::from_utf8(cells));
+    tree += "}}";
+    const std::string summary = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":" +
+                                std::to_string(st[0]) + ",\"blobNodeCount\":" + std::to_string(st[1]) +
+                                ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(st[2]) +
+                                ",\"unreferencedBlobSize\":0}}";
+    fill_blob_list(all, summary, out);
+  });
+}

@@ -1868,6 +1868,7 @@ struct Eng {
       m &= m - 1;
       const uint32_t st = rlu(start, t);
       const int n = rl(len, t);
+      cell_event(MTB_CELL_CLEAR, st, (uint32_t)n);  // handlesRecycledCallback before the free
       if (lane == 0) {
         uint32_t head = ht[1];
         for (int i = 0; i < n; i++) {
@@ -1957,30 +1958,46 @@ struct Eng {
   }
   // getAllocatedHandle (permutationvector.ts:183-207) at local position pos: nothing when the position
   // already has a handle, else walkSegments(pos, pos + 1, splitRange) isolates it and it gets one
-  __device__ __forceinline__ void allocated_handle(int pos, int Cl) {
+  __device__ __forceinline__ int allocated_handle(int pos, int Cl) {  // the handle, or -1 on failure
     view_clear();
     int j, off, lp;
     int d = find_seg(pos, curSeq, Cl, j, off, lp);
-    if (d < 0 || bad()) { fail(DERR_HANDLE); return; }
-    if ((int)U(sh->v[d].f[F_TEXT][j]) >= 1) return;  // start + offset is valid
+    if (d < 0 || bad()) { fail(DERR_HANDLE); return -1; }
+    const int st = (int)U(sh->v[d].f[F_TEXT][j]);
+    if (st >= 1) return st + off;  // start + offset is valid
     walk(pos, curSeq, Cl, -2, false, 0);  // ensureIntervalBoundary(pos) and (pos + 1), local view
     settle();
-    if (bad()) return;
+    if (bad()) return -1;
     view_clear();
     walk(pos + 1, curSeq, Cl, -2, false, 0);
     settle();
-    if (bad()) return;
+    if (bad()) return -1;
     view_clear();
     d = find_seg(pos, curSeq, Cl, j, off, lp);
-    if (d < 0 || bad() || off != 0 || (int)U(sh->v[d].f[F_LEN][j]) != 1) { fail(DERR_HANDLE); return; }
+    if (d < 0 || bad() || off != 0 || (int)U(sh->v[d].f[F_LEN][j]) != 1) { fail(DERR_HANDLE); return -1; }
     const uint32_t h = handle_alloc();
-    if (bad()) return;
+    if (bad()) return -1;
     if (lane == 0) {
       sh->v[d].f[F_TEXT][j] = h;
       blk[sh->v[d].b].f[F_TEXT][j] = h;
     }
     n_mod += 1;
     wsync();
+    return (int)h;
+  }
+  // SharedMatrix cell events in the document's delta slice, one 4-word entry each: [record, kind,
+  // handle or first recycled handle, count].  The host replays them, with the setCell values, into the
+  // matrix's SparseArray2D (matrix.ts:668-690 sets, :721-733 clears of recycled handles).
+  __device__ __forceinline__ void cell_event(uint32_t kind, uint32_t a, uint32_t n) {
+    if (delta_used + 1 > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+    if (lane == 0) {
+      uint32_t* e = dslice() + 4 * delta_used;
+      e[0] = cur_k;
+      e[1] = kind;
+      e[2] = a;
+      e[3] = n;
+    }
+    delta_used += 1;
   }
   // SharedMatrix setCell (matrix.ts:668-676) on this wave's vector: adjust, exchange with the partner
   // wave (the other vector of the same matrix) through LDS, allocate when both positions survive.
@@ -1990,7 +2007,10 @@ struct Eng {
     if (lane == 0) xch[par * 2 + wv] = adj;
     __syncthreads();
     const int other = U(xch[par * 2 + (wv ^ 1)]);
-    if (!err && adj >= 0 && other >= 0) allocated_handle(adj, (int)o.pos2);
+    if (!err && adj >= 0 && other >= 0) {
+      const int h = allocated_handle(adj, (int)o.pos2);
+      if (h >= 0 && !err) cell_event(MTB_CELL_SET, (uint32_t)h, 1);
+    }
   }
 
   // zamboniSegments (zamboni.ts:19-60)

@@ -61,5 +61,11 @@ export declare class MatrixBatch extends MergeTreeBatch {
 export declare class SharedMatrix {
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   applyMsg(msg: ISequencedDocumentMessage | string): void;
+  /** SharedMatrix.summarizeCore (matrix.ts:449): rows / cols PermutationVector summaries and the cells blob. */
+  summarize(): { blobs: [string, string][]; summary: unknown };
+  /** SharedMatrix.getCell (matrix.ts:173) in the observer's view. */
+  getCell(row: number, col: number): unknown;
+  readonly rowCount: number;
+  readonly colCount: number;
   summarizeVectors(): { rows: { blobs: [string, string][]; summary: unknown }; cols: { blobs: [string, string][]; summary: unknown } };
 }

@@ -221,7 +221,7 @@ class Client {
 /**
  * A batch of SharedMatrix observers (matrix.ts): matrix m is the PermutationVector documents 2m (rows)
  * and 2m+1 (cols).  Row/col ops and setCell handle allocation replay on the GPU (one workgroup per
- * matrix); cell values are not kept.
+ * matrix); the kernel's cell events are replayed on the host into each matrix's SparseArray2D.
  */
 class MatrixBatch extends MergeTreeBatch {
   constructor(nmatrices, options = {}) {
@@ -249,6 +249,24 @@ class SharedMatrix {
     native.matrixApplyMsg(this.batch.handle, this.m, typeof msg === "string" ? msg : JSON.stringify(msg));
     this.batch.dirty = true;
   }
+
+  /** SharedMatrix.summarizeCore (matrix.ts:449-463): rows / cols PermutationVector summaries + cells blob. */
+  summarize() {
+    this.batch.ensureFlushed();
+    const r = native.matrixSummarize(this.batch.handle, this.m);
+    return { blobs: r.blobs, summary: JSON.parse(r.summary) };
+  }
+
+  /** SharedMatrix.getCell(row, col) (matrix.ts:173-189) in the observer's view. */
+  getCell(row, col) {
+    this.batch.ensureFlushed();
+    const v = native.matrixGetCell(this.batch.handle, this.m, row, col);
+    return v === undefined ? undefined : JSON.parse(v);
+  }
+
+  get rowCount() { this.batch.ensureFlushed(); return native.getLength(this.batch.handle, 2 * this.m); }
+
+  get colCount() { this.batch.ensureFlushed(); return native.getLength(this.batch.handle, 2 * this.m + 1); }
 
   /** PermutationVector.summarize (permutationvector.ts:310) of rows and cols. */
   summarizeVectors() {

@@ -475,6 +475,7 @@ static napi_value js_checksum(napi_env env, napi_callback_info info) {
 }
 
 /* summarizeV1(h, doc, msn, seq) -> {blobs: [[path, content]...], summary: JSON text}   client.ts:966 */
+static napi_value blob_list_object(napi_env env, mtb_blob_list* lp);
 static napi_value js_summarize_v1(napi_env env, napi_callback_info info) {
   napi_value argv[4];
   if (!get_args(env, info, 4, argv)) return NULL;
@@ -486,6 +487,49 @@ static napi_value js_summarize_v1(napi_env env, napi_callback_info info) {
   memset(&l, 0, sizeof l);
   int rc = mtb_summarize_v1(b, doc, msn, seq, &l);
   if (rc) return throw_rc(env, b, rc);
+  return blob_list_object(env, &l);
+}
+
+/* matrixSummarize(h, matrix) -> {blobs, summary}                        matrix.ts:449-463 */
+static napi_value js_matrix_summarize(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t m;
+  if (!b || !get_u32(env, argv[1], &m)) return NULL;
+  mtb_blob_list l;
+  memset(&l, 0, sizeof l);
+  int rc = mtb_matrix_summarize(b, m, &l);
+  if (rc) return throw_rc(env, b, rc);
+  return blob_list_object(env, &l);
+}
+
+/* matrixGetCell(h, matrix, row, col) -> JSON text | undefined           matrix.ts:173-189 */
+static napi_value js_matrix_get_cell(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t m, r, c;
+  if (!b || !get_u32(env, argv[1], &m) || !get_u32(env, argv[2], &r) || !get_u32(env, argv[3], &c)) return NULL;
+  size_t n = 0;
+  int rc = mtb_matrix_get_cell(b, m, r, c, NULL, 0, &n);
+  if (rc) return throw_rc(env, b, rc);
+  if (n == 0) return undef(env);
+  char* buf = (char*)malloc(n + 1);
+  rc = mtb_matrix_get_cell(b, m, r, c, buf, n + 1, &n);
+  if (rc) {
+    free(buf);
+    return throw_rc(env, b, rc);
+  }
+  napi_value v;
+  napi_create_string_utf8(env, buf, n, &v);
+  free(buf);
+  return v;
+}
+
+/* {blobs: [[path, content]...], summary: JSON text}; frees the list */
+static napi_value blob_list_object(napi_env env, mtb_blob_list* lp) {
+  mtb_blob_list l = *lp;
   napi_value o, arr, sum;
   napi_create_object(env, &o);
   napi_create_array_with_length(env, l.count, &arr);
@@ -501,7 +545,7 @@ static napi_value js_summarize_v1(napi_env env, napi_callback_info info) {
   napi_create_string_utf8(env, l.summary_json, l.summary_json_len, &sum);
   napi_set_named_property(env, o, "blobs", arr);
   napi_set_named_property(env, o, "summary", sum);
-  mtb_blob_list_free(&l);
+  mtb_blob_list_free(lp);
   return o;
 }
 
@@ -556,6 +600,7 @@ static napi_value init(napi_env env, napi_value exports) {
   } fns[] = {
       {"create", js_create},           {"docInit", js_doc_init},       {"loadV1", js_load_v1},
       {"matrixInit", js_matrix_init},  {"matrixApplyMsg", js_matrix_apply_msg},
+      {"matrixSummarize", js_matrix_summarize}, {"matrixGetCell", js_matrix_get_cell},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

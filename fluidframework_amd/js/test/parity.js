@@ -44,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg"];
+    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -119,6 +119,18 @@ async function gpuChecks() {
   const v0 = mb.matrix(0).summarizeVectors(), v1 = mb.matrix(1).summarizeVectors();
   assert.deepStrictEqual(v0, v1);
   assert.strictEqual(v0.rows.blobs[v0.rows.blobs.length - 1][0], "handleTable");
+  // SharedMatrix.summarize (rows, cols, cells) against the oracle's, when the harness passes it
+  const s0 = mb.matrix(0).summarize();
+  assert.deepStrictEqual(s0, mb.matrix(1).summarize());
+  assert.strictEqual(s0.blobs[s0.blobs.length - 1][0], "cells");
+  const expect = process.env.MTB_JS_MATRIX_EXPECT;
+  if (expect) {
+    const e = JSON.parse(fs.readFileSync(expect, "utf8"));
+    assert.deepStrictEqual(s0.blobs, e.blobs, "matrix summary blobs vs oracle");
+    assert.deepStrictEqual(s0.summary, e.summary, "matrix summary tree vs oracle");
+    for (const [r, c, v] of e.cells)
+      assert.deepStrictEqual(mb.matrix(0).getCell(r, c), v === null ? undefined : JSON.parse(v), `getCell(${r}, ${c})`);
+  }
   console.log("js gpu matrix ok");
   const ref = new MergeTreeBatch(1);
   await ref.client(0).load(undefined, storageOf(snapshotBlobs("withMarkers")));

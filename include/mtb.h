@@ -154,11 +154,22 @@ int mtb_intern_props(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* 
  * Matrix m owns documents 2m (rows) and 2m+1 (cols), each a PermutationVector observer: remote
  * insert/remove of rows/cols are merge-tree ops on that vector; a remote setCell adjusts (row, col)
  * into the observer's view (adjustPosition, permutationvector.ts:209) and allocates storage handles
- * (getAllocatedHandle, :183) on the GPU.  The cell values (SparseArray2D) are not kept.  mtb_summarize_v1
- * and mtb_dump_segments on a vector document give PermutationVector.summarize (:310): blobs
- * "segments/header", "segments/body_i", "handleTable". */
+ * (getAllocatedHandle, :183) on the GPU; the kernel logs each setCell's handles and each zamboni handle
+ * recycling, which the host replays into the matrix's SparseArray2D (matrix.ts:96, :684, :721-733).
+ * mtb_summarize_v1 and mtb_dump_segments on a vector document give PermutationVector.summarize (:310):
+ * blobs "segments/header", "segments/body_i", "handleTable". */
 int mtb_matrix_init(mtb_batch* b, uint32_t matrix, const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq);
 int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json_utf8, size_t len);
+/* Intern a setCell value (JSON text) for records packed by the caller (mtb_append_ops): the SETCELL
+ * record's `props` field carries the id (0 = undefined). */
+int mtb_matrix_intern_value(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* id_out);
+/* SharedMatrix.summarizeCore (matrix.ts:449-463): blobs "rows/segments/header", ..., "rows/handleTable",
+ * "cols/...", "cells" (JSON [cells.snapshot(), pending.snapshot()]) and the ISummaryTreeWithStats. */
+int mtb_matrix_summarize(mtb_batch* b, uint32_t matrix, mtb_blob_list* out);
+/* SharedMatrix.getCell(row, col) (matrix.ts:173-189) in the observer's view: the value's JSON text, or
+ * *len_out = 0 when the cell is undefined or a position has no handle. */
+int mtb_matrix_get_cell(mtb_batch* b, uint32_t matrix, uint32_t row, uint32_t col, char* buf, size_t cap,
+                        size_t* len_out);
 
 /* Replay every pending op of every document on the GPU(s).  Blocking. */
 int mtb_replay(mtb_batch* b, mtb_stats* out);

@@ -99,6 +99,28 @@ int orc_matrix_get_cell_by_handle(orc_matrix* m, uint32_t rh, uint32_t ch, char*
   return 0;
 }
 
+// SharedMatrix.getCell(row, col) (matrix.ts:173-189): local positions -> handles -> cells; "" = undefined
+int orc_matrix_get_cell(orc_matrix* m, uint32_t row, uint32_t col, char** out, size_t* len) {
+  int rc = guard(&m->rows, [&] {
+    auto handleAt = [](Doc& d, int pos) {
+      int off = 0;
+      Seg* s = d.mt.containingSegment(pos, d.mt.window.currentSeq, d.mt.window.clientId, &off);
+      if (!s) throw OracleError(-1, "0x027 position out of range");
+      return s->start >= 1 ? s->start + off : HandleUnallocated;
+    };
+    const int rh = handleAt(m->rows.doc, (int)row);
+    const int ch = handleAt(m->cols.doc, (int)col);
+    std::string v;
+    if (rh != HandleUnallocated && ch != HandleUnallocated) {
+      const std::optional<std::string>* c = m->m.cells.getCell((uint32_t)rh, (uint32_t)ch);
+      if (c && *c) v = **c;
+    }
+    *out = dupstr(v, len);
+  });
+  if (rc) m->err = m->rows.err;
+  return rc;
+}
+
 // SparseArray2D on its own (sparsearray2d.spec.ts cases)
 SparseArray2D* orc_sa2d_create() { return new SparseArray2D(); }
 void orc_sa2d_destroy(SparseArray2D* a) { delete a; }

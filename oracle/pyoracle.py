@@ -63,6 +63,8 @@ def lib():
         L.orc_matrix_start_collab.argtypes = [vp, cp, i, i]
         L.orc_matrix_apply_msg_json.argtypes = [vp, cp, sz]
         L.orc_matrix_summarize.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
+        L.orc_matrix_get_cell.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(sz)]
         L.orc_matrix_get_cell_by_handle.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                                     ctypes.POINTER(sz)]
         u32 = ctypes.c_uint32
@@ -316,6 +318,10 @@ class OracleMatrix:
     def summarize(self):
         """SharedMatrix summary (matrix.ts:449-463): {"blobs": [[path, content]...], "summary": {...}}."""
         return json.loads(self._take(self._L.orc_matrix_summarize))
+
+    def get_cell(self, row, col):
+        """JSON text of SharedMatrix.getCell(row, col) in the observer's view, or None when undefined."""
+        return self._take(self._L.orc_matrix_get_cell, row, col) or None
 
     def cell_by_handle(self, row_handle, col_handle):
         """JSON text of cells.getCell(rowHandle, colHandle), or None when undefined."""

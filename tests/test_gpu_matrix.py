@@ -15,7 +15,12 @@ from helpers import first_diff, make_matrix_log
 pytestmark = pytest.mark.gpu
 
 
-def _check(B, m, o, what):
+def _check(B, m, o, what, cells=True):
+    if cells:  # SharedMatrix.summarize: rows / cols PermutationVector summaries + the cells blob
+        gb, gs = B.matrix_summarize(m)
+        osum = o.summarize()
+        assert [list(x) for x in gb] == osum["blobs"], f"{what}: matrix summary blobs differ"
+        assert gs == osum["summary"], f"{what}: matrix summary tree differs"
     for name, doc, od in (("rows", 2 * m, o.rows), ("cols", 2 * m + 1, o.cols)):
         gd, odd = B.dump_segments(doc), od.dump_segments()
         assert gd == odd, f"{what} {name}: dump differs: {first_diff(gd, odd)}"
@@ -53,6 +58,11 @@ def test_generated_matrix_logs_match_oracle(new_mode):
     B.flush()
     for i, (o, _) in enumerate(oracles):
         _check(B, i, o, f"matrix {i}")
+        # getCell over the whole observer view (matrix.ts:173-189)
+        nr, nc = o.rows.get_length(), o.cols.get_length()
+        for r in range(0, nr, max(1, nr // 12)):
+            for c in range(0, nc, max(1, nc // 12)):
+                assert B.get_cell(i, r, c) == o.get_cell(r, c), f"matrix {i} cell ({r}, {c})"
 
 
 def test_rewind_restores_handle_tables():
@@ -73,6 +83,7 @@ def test_rewind_restores_handle_tables():
     B.rewind()
     B.replay_resident()
     assert (B.dump_segments(0), B.dump_segments(1)) == first
+    _check(B, 0, o, "matrix after rewind")
 
 
 @pytest.mark.parametrize("new_mode", [False, True])

@@ -39,8 +39,25 @@ def test_js_package_cpu():
 
 @needs_node
 @pytest.mark.gpu
-def test_js_package_replays_reference_logs_on_gpu():
-    out = _node()
+def test_js_package_replays_reference_logs_on_gpu(tmp_path):
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import OracleMatrix
+    o = OracleMatrix()
+    o.start_collab("obs")
+    for m in json.load(open(os.path.join(JS, "test", "matrix_log.json"))):
+        o.apply_msg(m)
+    exp = o.summarize()
+    nr, nc = o.rows.get_length(), o.cols.get_length()
+    exp["cells"] = [[r, c, o.get_cell(r, c)] for r in range(nr) for c in range(nc)]
+    path = tmp_path / "matrix_expect.json"
+    path.write_text(json.dumps(exp))
+    os.environ["MTB_JS_MATRIX_EXPECT"] = str(path)
+    try:
+        out = _node()
+    finally:
+        del os.environ["MTB_JS_MATRIX_EXPECT"]
     assert "js gpu parity ok" in out
     assert "js gpu load ok" in out
     assert "js gpu matrix ok" in out
