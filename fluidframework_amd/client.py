@@ -139,8 +139,10 @@ class MergeTreeBatch:
     def replay(self):
         """Replay every pending op of every document (blocking).  Returns the stats dict."""
         st = _lib.MtbStats()
-        self._chk(self._L.mtb_replay(self._h, ctypes.byref(st)))
-        self._dirty = False
+        rc = self._L.mtb_replay(self._h, ctypes.byref(st))
+        if rc not in (-1, -2, -3):  # the records were replayed (a document error is reported once, sticky)
+            self._dirty = False
+        self._chk(rc)
         self.last_stats = {f: getattr(st, f) for f, _ in _lib.MtbStats._fields_}
         return self.last_stats
 

@@ -1250,6 +1250,11 @@ void apply_cell_events(mtb_batch* b, uint32_t matrix);
 
 void replay(mtb_batch* b, mtb_stats* out) {
   PhaseClock pc;
+  // documents that failed in an earlier replay stay failed (sticky) and are counted in the stats, but
+  // only a failure of this replay is reported as the call's error (the reference throws once, from
+  // the applyMsg that failed)
+  std::vector<uint8_t> failedBefore(b->ndocs);
+  for (uint32_t i = 0; i < b->ndocs && i < b->hst.size(); i++) failedBefore[i] = b->hst[i].err != 0;
   if (!b->devInit) device_init(b);
   pc.mark("device_init");
   upload_tables(b);
@@ -1403,7 +1408,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
     st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
     if (s.err) {
       st.errors++;
-      if (!firstErr) { firstErr = s.err; errDoc = i; }
+      if (!firstErr && !failedBefore[i]) { firstErr = s.err; errDoc = i; }
     }
   }
   if (getenv("MTB_PROFILE_OUT")) {  // MTB_PROFILE builds: per-phase device cycles and events per op, summed over documents

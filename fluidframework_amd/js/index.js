@@ -57,7 +57,14 @@ class MergeTreeBatch {
   /** Replay every pending op of every document (blocking).  Returns the replay statistics. */
   flush() {
     this.checkIdle();
-    this.lastStats = native.replay(this.handle);
+    try {
+      this.lastStats = native.replay(this.handle);
+    } catch (e) {
+      // a document's failure is thrown once (the reference throws from that applyMsg); the other
+      // documents' records were replayed
+      if (![-1, -2, -3].includes(e.code)) this.dirty = false;  // not MTB_E_ARG / NODEV / HIP
+      throw e;
+    }
     this.dirty = false;
     return this.lastStats;
   }
