@@ -222,6 +222,20 @@ class MergeTreeBatch:
         self._chk(self._L.mtb_doc_checksum(self._h, doc, ctypes.byref(out)))
         return out.value
 
+    def map_range(self, doc, start=0, end=-1, ref_seq=-1, long_client_id=None, limit=0):
+        """mapRange / nodeMap (mergeTree.ts:2456, 2531) over [start, end) in the (ref_seq, client) view
+        (defaults: currentSeq, the observer = the local view): [{"pos", "start", "end", "segment"}...]."""
+        self._ensure_flushed()
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_map_range(self._h, doc, start, end, ref_seq,
+                                        None if long_client_id is None else long_client_id.encode(), limit,
+                                        ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return json.loads(ctypes.string_at(p, n.value).decode("utf-8"))
+        finally:
+            self._L.mtb_free(p)
+
     def summarize_legacy(self, doc, msn=-1, seq=-1, catchup=None):
         """SnapshotLegacy summary (snapshotlegacy.ts): (blobs, ISummaryTreeWithStats); `catchup` is the list of
         messages above the MSN (SharedSegmentSequence.messagesSinceMSNChange)."""
@@ -297,6 +311,33 @@ class Client:
 
     def getText(self):
         return self._b.text(self._doc)
+
+    def getContainingSegment(self, pos, sequenceArgs=None):
+        """client.ts:1065: {"segment": dict | None, "offset": int | None} in the local view, or in the
+        view of sequenceArgs = {"referenceSequenceNumber", "clientId"} (a remote message's perspective)."""
+        ref, cid = (-1, None) if sequenceArgs is None else (sequenceArgs["referenceSequenceNumber"], sequenceArgs["clientId"])
+        hit = self._b.map_range(self._doc, pos, pos + 1, ref, cid, limit=1)
+        return {"segment": hit[0]["segment"], "offset": hit[0]["start"]} if hit else {"segment": None, "offset": None}
+
+    def getPropertiesAtPosition(self, pos):
+        """client.ts:1101: the properties of the segment at pos (local view), or None."""
+        seg = self.getContainingSegment(pos)["segment"]
+        return None if seg is None else seg.get("properties")
+
+    def walkSegments(self, handler, start=None, end=None, accum=None):
+        """client.ts:286 (mapRange in the local view): handler(segment, pos, refSeq, clientId, start, end,
+        accum) per visited segment; returning False stops the walk.  splitRange is not supported."""
+        cur = self.getCurrentSeq()
+        for e in self._b.map_range(self._doc, start or 0, -1 if end is None else end):
+            if handler(e["segment"], e["pos"], cur, 0, e["start"], e["end"], accum) is False:
+                break
+
+    def getClientId(self):
+        """client.ts:1126: the observer's short id."""
+        return 0
+
+    def getLongClientId(self, shortClientId):
+        return self._b.client_long_id(self._doc, shortClientId)
 
     def getLength(self):
         return self._b.length(self._doc)

@@ -2810,3 +2810,108 @@ int mtb_matrix_summarize(mtb_batch* b, uint32_t matrix, mtb_blob_list* out) {
     fill_blob_list(all, summary, out);
   });
 }
+
+// ------------------------------------------------------------------ segment queries (Client reads)
+namespace {
+// nodeLength of a leaf (mergeTree.ts:916-1004) in the (refSeq R, client C) view; -1 = undefined.
+// C == the observer is the local view (localNetLength, :613-634).  The observer engine holds no
+// unacked segments, so seq / removedSeq are never UnassignedSequenceNumber here.
+int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int minSeq, std::vector<int>& rc) {
+  const bool removed = seg_removed(g);
+  if (C == 0) {
+    if (!removed) return g.len;
+    return newMode ? 0 : (g.rseq > minSeq ? 0 : -1);
+  }
+  bool cRemoved = false;
+  if (removed) {
+    rc_list(d, g, rc);
+    cRemoved = std::find(rc.begin(), rc.end(), C) != rc.end();
+  }
+  if (newMode) {
+    if (removed && g.rseq <= minSeq) return -1;
+    if (removed && (g.rseq <= R || cRemoved)) return 0;
+    return (g.seq <= R || g.client == C) ? g.len : 0;
+  }
+  if (removed && g.rseq <= R) return -1;
+  if (g.client == C || g.seq <= R) return removed ? (cRemoved ? 0 : g.len) : g.len;
+  return removed ? -1 : 0;
+}
+}  // namespace
+
+// MergeTree.mapRange / nodeMap (mergeTree.ts:2456-2474, 2531-2582) over [start, end) in a perspective:
+// Client.walkSegments (client.ts:286, the local view), getContainingSegment (:1065, mergeTree.ts:787-813)
+// and getPropertiesAtPosition (client.ts:1101) are views of it.  Output: a JSON array of
+// {"pos", "start", "end", "segment"} per visited leaf (start / end relative to the segment, as the
+// reference's handler receives them), at most `limit` entries (0 = all).
+int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq, const char* long_client_id,
+                  uint32_t limit, char** out, size_t* out_len) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!out) raise(MTB_E_ARG, "null output");
+    if (b->hst[doc].err) raise(derr_code(b->hst[doc].err), derr_text(b->hst[doc].err));
+    download_doc(b, doc);
+    const DocState& s = b->hst[doc];
+    const bool newMode = b->opts.new_length_calc != 0;
+    const int R = ref_seq < 0 ? (int)s.cur_seq : (int)ref_seq;
+    int C = 0;
+    if (long_client_id) {  // getClientSequenceArgsForMessage: a client not seen yet owns nothing
+      auto it = d.shortOf.find(long_client_id);
+      C = it == d.shortOf.end() ? -3 : it->second;
+    }
+    std::vector<FlatSeg> fl;
+    flatten(d, s.root, fl, false);
+    std::vector<int> rc;
+    int64_t total = 0;
+    std::vector<int> lens(fl.size());
+    for (size_t k = 0; k < fl.size(); k++) {
+      lens[k] = leaf_length(d, d.segs[fl[k].id], R, C, newMode, (int)s.min_seq, rc);
+      if (lens[k] > 0) total += lens[k];
+    }
+    const int64_t endPos = end < 0 ? total : end;
+    std::string o = "[";
+    uint32_t n = 0;
+    int64_t pos = 0;
+    if (endPos != start)
+      for (size_t k = 0; k < fl.size() && pos < endPos; k++) {
+        const int len = lens[k];
+        if (len <= 0) continue;  // undefined or zero: Skip
+        const int64_t next = pos + len;
+        if (start >= next) {
+          pos = next;
+          continue;
+        }
+        const Seg& g = d.segs[fl[k].id];
+        if (n) o += ',';
+        o += "{\"pos\":" + std::to_string(pos) + ",\"start\":" + std::to_string(start - pos) + ",\"end\":" +
+             std::to_string(endPos - pos) + ",\"segment\":{\"type\":";
+        if (d.perm) {
+          o += "\"PermutationSegment\",\"start\":" + std::to_string(g.text == MTB_HANDLE_UNALLOC ? INT32_MIN : (int64_t)g.text);
+        } else if (is_marker(g)) {
+          const uint32_t rt = g.text & ~MTB_MARKER;
+          o += "\"Marker\",\"refType\":" + (rt == 0 ? std::string("null") : std::to_string(rt - 1));
+        } else {
+          o += "\"TextSegment\",\"text\":";
+          hj::quote(o, reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len);
+        }
+        o += ",\"cachedLength\":" + std::to_string(g.len) + ",\"seq\":" + std::to_string(g.seq) +
+             ",\"clientId\":" + std::to_string(g.client);
+        if (seg_removed(g)) {
+          o += ",\"removedSeq\":" + std::to_string(g.rseq) + ",\"removedClientIds\":[";
+          rc_list(d, g, rc);
+          for (size_t q = 0; q < rc.size(); q++) o += (q ? "," : "") + std::to_string(rc[q]);
+          o += "]";
+        }
+        PropView pv = props_of(b, d, g.props);
+        if (g.props && pv.n() > 0) {
+          o += ",\"properties\":";
+          props_json(b, o, pv);
+        }
+        o += "}}";
+        pos = next;
+        if (++n == limit) break;
+      }
+    o += "]";
+    *out = dup(o);
+    if (out_len) *out_len = o.size();
+  });
+}

@@ -38,6 +38,19 @@ export declare class MergeTreeBatch {
   rewind(): void;
   replayResident(): ReplayStats;
 }
+/** A segment as the read queries return it (short client ids). */
+export interface SegmentInfo {
+  type: "TextSegment" | "Marker" | "PermutationSegment";
+  text?: string;
+  refType?: number | null;
+  start?: number;
+  cachedLength: number;
+  seq: number;
+  clientId: number;
+  removedSeq?: number;
+  removedClientIds?: number[];
+  properties?: Record<string, unknown>;
+}
 export declare class Client {
   insertTextLocal(pos: number, text: string): void;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
@@ -49,6 +62,12 @@ export declare class Client {
   getCurrentSeq(): number;
   getCollabWindow(): { clientId: number; collaborating: boolean; minSeq: number; currentSeq: number };
   getLongClientId(shortClientId: number): string;
+  getClientId(): number;
+  getContainingSegment(pos: number, sequenceArgs?: { referenceSequenceNumber: number; clientId: string }):
+    { segment: SegmentInfo | undefined; offset: number | undefined };
+  getPropertiesAtPosition(pos: number): Record<string, unknown> | undefined;
+  walkSegments<T>(handler: (segment: SegmentInfo, pos: number, refSeq: number, clientId: number, start: number,
+                            end: number, accum?: T) => boolean | void, start?: number, end?: number, accum?: T): void;
   summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }): unknown;
 }
 export declare const TestClient: typeof Client;

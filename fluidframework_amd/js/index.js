@@ -209,6 +209,41 @@ class Client {
     return { clientId: 0, collaborating: true, minSeq, currentSeq };
   }
 
+  /**
+   * Client.getContainingSegment (client.ts:1065, mergeTree.ts:787-813): {segment, offset} in the local
+   * view, or in the view of `sequenceArgs` = {referenceSequenceNumber, clientId} (a remote message's).
+   * Segments are plain objects {type, text | refType | start, cachedLength, seq, clientId,
+   * removedSeq?, removedClientIds?, properties?} with short client ids.
+   */
+  getContainingSegment(pos, sequenceArgs) {
+    this.batch.ensureFlushed();
+    const ref = sequenceArgs ? sequenceArgs.referenceSequenceNumber : -1;
+    const id = sequenceArgs ? sequenceArgs.clientId : null;
+    const hit = JSON.parse(native.mapRange(this.batch.handle, this.doc, pos, pos + 1, ref, id, 1));
+    return hit.length ? { segment: hit[0].segment, offset: hit[0].start } : { segment: undefined, offset: undefined };
+  }
+
+  /** Client.getPropertiesAtPosition (client.ts:1101). */
+  getPropertiesAtPosition(pos) {
+    const { segment } = this.getContainingSegment(pos);
+    return segment ? segment.properties : undefined;
+  }
+
+  /**
+   * Client.walkSegments (client.ts:286): mapRange in the local view; handler(segment, pos, refSeq,
+   * clientId, start, end, accum) returning false stops the walk.  splitRange is not supported.
+   */
+  walkSegments(handler, start, end, accum, splitRange = false) {
+    if (splitRange) throw unsupported("walkSegments with splitRange on the observer engine");
+    this.batch.ensureFlushed();
+    const cur = this.getCurrentSeq();
+    const hits = JSON.parse(native.mapRange(this.batch.handle, this.doc, start || 0, end === undefined ? -1 : end, -1, null, 0));
+    for (const h of hits) if (handler(h.segment, h.pos, cur, 0, h.start, h.end, accum) === false) break;
+  }
+
+  /** Client.getClientId (client.ts:1126): the observer's short id. */
+  getClientId() { return 0; }
+
   /** Client.getLongClientId (client.ts:682). */
   getLongClientId(shortClientId) { return native.clientLongId(this.batch.handle, this.doc, shortClientId); }
 

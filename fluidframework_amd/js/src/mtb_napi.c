@@ -457,6 +457,35 @@ static napi_value js_dump_segments(napi_env env, napi_callback_info info) {
   return s;
 }
 
+/* mapRange(h, doc, start, end, refSeq, longClientId | null, limit) -> JSON text   mergeTree.ts:2456 */
+static napi_value js_map_range(napi_env env, napi_callback_info info) {
+  napi_value argv[7];
+  if (!get_args(env, info, 7, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc, limit;
+  int64_t start, end, ref;
+  if (!b || !get_u32(env, argv[1], &doc) || !get_i64(env, argv[2], &start) || !get_i64(env, argv[3], &end) ||
+      !get_i64(env, argv[4], &ref) || !get_u32(env, argv[6], &limit))
+    return NULL;
+  napi_valuetype t;
+  napi_typeof(env, argv[5], &t);
+  char* id = NULL;
+  if (t == napi_string) {
+    id = get_utf8(env, argv[5], NULL);
+    if (!id) return NULL;
+  }
+  char* out = NULL;
+  size_t n = 0;
+  int rc = mtb_map_range(b, doc, start, end, ref, id, limit, &out, &n);
+  free(id);
+  if (rc) return throw_rc(env, b, rc);
+  napi_value s;
+  napi_status ok = napi_create_string_utf8(env, out, n, &s);
+  mtb_free(out);
+  CHECK_NAPI(env, ok);
+  return s;
+}
+
 /* checksum(h, doc) -> 16-digit hex string */
 static napi_value js_checksum(napi_env env, napi_callback_info info) {
   napi_value argv[2];
@@ -606,6 +635,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"replay", js_replay},           {"replayAsync", js_replay_async},
       {"getText", js_get_text},        {"getLength", js_get_length},
       {"getSeq", js_get_seq},          {"dumpSegments", js_dump_segments},
+      {"mapRange", js_map_range},
       {"checksum", js_checksum},       {"summarizeV1", js_summarize_v1},
       {"rewind", js_rewind},           {"replayResident", js_replay_resident},
       {"clientLongId", js_client_long_id},

@@ -44,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell"];
+    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell", "mapRange"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -98,6 +98,19 @@ async function gpuChecks() {
   assert.ok(s.summary.tree.header);
   assert.strictEqual(c0.getLength(), c0.getText().length);
   assert.strictEqual(c0.getCurrentSeq(), fx[0].log.groups[ngroups - 1].msgs.slice(-1)[0][1]);
+  // segment queries: walkSegments covers the text in order; getContainingSegment agrees with it
+  fx.forEach((_, i) => {
+    const c = batch.client(i);
+    let text = "";
+    const walked = [];
+    c.walkSegments((seg, pos) => { text += seg.text || ""; walked.push([pos, seg]); });
+    assert.strictEqual(text, c.getText());
+    for (const [pos, seg] of walked.slice(0, 40)) {
+      const hit = c.getContainingSegment(pos);
+      assert.deepStrictEqual([hit.segment, hit.offset], [seg, 0]);
+      assert.deepStrictEqual(c.getPropertiesAtPosition(pos), seg.properties);
+    }
+  });
   console.log(`js gpu parity ok: ${checked} text checkpoints over ${fx.length} reference logs`);
   // Client.load: every document's summary loads into a fresh batch and summarizes back to the same bytes
   const loaded = new MergeTreeBatch(fx.length);

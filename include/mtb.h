@@ -181,6 +181,14 @@ int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq
 int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len);
 /* Per-document state checksum (FNV-1a 64 over the canonical dump). */
 int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out);
+/* MergeTree.mapRange / nodeMap (mergeTree.ts:2456-2474, 2531-2582) over [start, end) (end < 0: to the end)
+ * in the view of (ref_seq, long_client_id) (ref_seq < 0: currentSeq; long_client_id NULL: the observer,
+ * i.e. the local view).  Serves Client.walkSegments (client.ts:286), getContainingSegment (:1065) and
+ * getPropertiesAtPosition (:1101).  *out = JSON array of {"pos", "start", "end", "segment": {"type",
+ * "text" | "refType" | "start", "cachedLength", "seq", "clientId", "removedSeq"?, "removedClientIds"?,
+ * "properties"?}} (short client ids), at most `limit` entries (0 = all); free with mtb_free. */
+int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq,
+                  const char* long_client_id, uint32_t limit, char** out, size_t* out_len);
 /* Client.summarize with newMergeTreeSnapshotFormat: if `msn`/`seq` >= 0 first runs
  * updateSeqNumbers(msn, seq) (client.ts:979).  long_client_ids may be NULL (use registered ids). */
 int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,

@@ -1783,6 +1783,13 @@ Seg* MergeTree::containingSegment(int pos, int refSeq, int clientId, int* offset
   if (offset) *offset = off;
   return found;
 }
+void MergeTree::mapRange(int refSeq, int clientId, int start, int end, const std::function<bool(Seg*, int, int, int)>& f) {
+  if (end < 0) {
+    const int l = blockLength(root, refSeq, clientId);
+    end = l == UNDEF_LEN ? 0 : l;
+  }
+  nodeMap(refSeq, clientId, [&](Seg* s, int pos, int st, int en) { return f(s, pos, st, en); }, [](Block*) {}, start, end);
+}
 void MergeTree::mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f) {
   const int end = blockLength(root, refSeq, clientId);
   nodeMap(

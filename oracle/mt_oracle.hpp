@@ -180,6 +180,8 @@ class MergeTree {
   void boundary(int pos, int refSeq, int clientId) { ensureIntervalBoundary(pos, refSeq, clientId); }
   // mapRange(action, refSeq, clientId) over the whole tree (mergeTree.ts mapRange -> nodeMap)
   void mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f);
+  // mapRange (mergeTree.ts:2456-2474) over [start, end) (end < 0: the whole (refSeq, clientId) length)
+  void mapRange(int refSeq, int clientId, int start, int end, const std::function<bool(Seg*, int, int, int)>& f);
 
   // text / walks
   u16str getText();

@@ -72,6 +72,53 @@ int orc_matrix_apply_msg_json(orc_matrix* m, const char* json, size_t len) {
   return rc;
 }
 
+// Client.walkSegments / getContainingSegment / getPropertiesAtPosition through mapRange (same JSON as the
+// engine's mtb_map_range): [{"pos","start","end","segment":{...}}...]
+int orc_map_range(orc_doc* d, int start, int end, int ref_seq, const char* long_id, unsigned limit, char** out, size_t* len) {
+  return guard(d, [&] {
+    Doc& doc = d->doc;
+    MergeTree& t = doc.mt;
+    const int R = ref_seq < 0 ? t.window.currentSeq : ref_seq;
+    int C = t.window.clientId;
+    if (long_id) {
+      auto it = doc.longToShort.find(long_id);
+      C = it == doc.longToShort.end() ? -3 : it->second;
+    }
+    std::string o = "[";
+    unsigned n = 0;
+    t.mapRange(R, C, start, end, [&](Seg* s, int pos, int st, int en) {
+      if (n) o += ',';
+      o += "{\"pos\":" + std::to_string(pos) + ",\"start\":" + std::to_string(st) + ",\"end\":" + std::to_string(en) +
+           ",\"segment\":{\"type\":";
+      if (s->perm) {
+        o += "\"PermutationSegment\",\"start\":" + std::to_string(s->start);
+      } else if (s->isMarker) {
+        o += "\"Marker\",\"refType\":" + (s->refType < 0 ? std::string("null") : std::to_string(s->refType));
+      } else {
+        o += "\"TextSegment\",\"text\":";
+        json_stringify_to(o, JVal::string(s->text));
+      }
+      o += ",\"cachedLength\":" + std::to_string(s->cachedLength) + ",\"seq\":" + std::to_string(s->seq) +
+           ",\"clientId\":" + std::to_string(s->clientId);
+      if (s->removed) {
+        o += ",\"removedSeq\":" + std::to_string(s->removedSeq) + ",\"removedClientIds\":[";
+        for (size_t q = 0; q < s->removedClientIds.size(); q++) o += (q ? "," : "") + std::to_string(s->removedClientIds[q]);
+        o += "]";
+      }
+      if (s->props && !s->props->empty()) {
+        JVal pv;
+        pv.t = JVal::Obj;
+        pv.obj = *s->props;
+        o += ",\"properties\":" + json_stringify(pv);
+      }
+      o += "}}";
+      return ++n != limit;
+    });
+    o += "]";
+    *out = dupstr(o, len);
+  });
+}
+
 // SharedMatrix.summarizeCore (matrix.ts:449-463): {"blobs": [[path, content]...], "summary": ISummaryTreeWithStats}
 int orc_matrix_summarize(orc_matrix* m, char** out, size_t* len) {
   int rc = guard(&m->rows, [&] {

@@ -68,6 +68,7 @@ def lib():
         L.orc_matrix_get_cell_by_handle.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                                     ctypes.POINTER(sz)]
         u32 = ctypes.c_uint32
+        L.orc_map_range.argtypes = [vp, i, i, i, cp, ctypes.c_uint, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.orc_sa2d_create.restype = vp
         L.orc_sa2d_destroy.argtypes = [vp]
         L.orc_sa2d_set.argtypes = [vp, u32, u32, cp]
@@ -188,6 +189,18 @@ class OracleDoc:
         finally:
             self._L.orc_free(p)
         return raw.decode("utf-16-le", "surrogatepass")
+
+    def map_range(self, start=0, end=-1, ref_seq=-1, long_client_id=None, limit=0):
+        """mapRange over [start, end) in the (ref_seq, client) view: [{"pos","start","end","segment"}...]."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_map_range(self._h, start, end, ref_seq,
+                                        None if long_client_id is None else long_client_id.encode(), limit,
+                                        ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return json.loads(ctypes.string_at(p, n.value).decode("utf-8"))
+        finally:
+            self._L.orc_free(p)
 
     def get_length(self):
         return self._L.orc_get_length(self._h)

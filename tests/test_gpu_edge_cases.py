@@ -146,3 +146,46 @@ def test_ragged_batch_edge_cases_match_oracle(new_mode):
         assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: summary blobs"
         assert gs == osum["summary"], f"doc {i}: summary tree"
     assert B.text(bad) == "ok"  # the state before the failing op (blockInsert throws before mutating)
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_segment_queries_match_oracle(new_mode):
+    """Client.getContainingSegment (local view and remote perspectives), getPropertiesAtPosition and
+    walkSegments (client.ts:286, 1065, 1101) read the engine's state; the oracle answers the same queries
+    through its own nodeMap over partial lengths (mergeTree.ts:2531)."""
+    import random as _r
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    msgs = _gen(21, 800, 6, 96, ["insert", "insert", "remove", "annotate", "marker"], new_mode)
+    B = MergeTreeBatch(1, new_length_calc=new_mode)
+    B[0].insertTextLocal(0, "seed text\nwith a newline")
+    B[0].startOrUpdateCollaboration("obs")
+    o = OracleDoc(new_length_calc=new_mode)
+    o.insert_text_local(0, "seed text\nwith a newline")
+    o.start_collab("obs")
+    rng = _r.Random(5)
+    for k, m in enumerate(msgs):
+        B[0].applyMsg(m)
+        o.apply_msg(m)
+        if k % 200 != 199:
+            continue
+        assert B.map_range(0) == o.map_range(), f"walk after {k + 1}"
+        n = o.get_length()
+        for pos in rng.sample(range(n), min(n, 40)):
+            assert B.map_range(0, pos, pos + 1, limit=1) == o.map_range(pos, pos + 1, limit=1), f"pos {pos}"
+            seg = B[0].getContainingSegment(pos)
+            assert seg["segment"] is not None and 0 <= seg["offset"] < seg["segment"]["cachedLength"]
+        # remote perspectives: each client at a lagging refSeq inside the collab window (a sequenced op's
+        # refSeq is never below the MSN; below it the partial lengths have folded the history away)
+        cur, msn = o.current_seq, o.min_seq
+        for cid in ["c0", "c1", "c5", "never-seen"]:
+            ref = rng.randint(msn, cur)
+            assert B.map_range(0, 0, -1, ref, cid) == o.map_range(0, -1, ref, cid), f"{cid}@{ref}"
+            rl = len(o.map_range(0, -1, ref, cid))
+            if rl:
+                assert B.map_range(0, 3, 40, ref, cid) == o.map_range(3, 40, ref, cid)
+    props = [B[0].getPropertiesAtPosition(p) for p in range(0, o.get_length(), 7)]
+    assert props == [(o.map_range(p, p + 1, limit=1)[0]["segment"].get("properties")) for p in range(0, o.get_length(), 7)]
+    seen = []
+    B[0].walkSegments(lambda s, pos, *_: seen.append((pos, s["cachedLength"])) or len(seen) < 50, 5, 400)
+    assert seen == [(e["pos"], e["segment"]["cachedLength"]) for e in o.map_range(5, 400)][:50]
