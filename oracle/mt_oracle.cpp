@@ -2031,6 +2031,60 @@ std::string SparseArray2D::snapshotJson() const {  // JSON.stringify(root): hole
   return o + "]";
 }
 
+SparseArray2D SparseArray2D::load(const JVal& data) {
+  SparseArray2D a;
+  if (data.t != JVal::Arr) throw OracleError(-8, "cells snapshot is not an array");
+  a.rootLength = data.arr.size();
+  auto level = [](auto& self, const JVal& v, auto& out) -> void {
+    using C = std::decay_t<decltype(out)>;
+    if (v.t != JVal::Arr) throw OracleError(-8, "cells level is not an array");
+    for (size_t i = 0; i < v.arr.size() && i < 256; i++) {
+      const JVal& e = v.arr[i];
+      if constexpr (std::is_same_v<C, Leaf>) {
+        if (e.t != JVal::Null && !e.isUndef()) out[i] = json_stringify(e);
+      } else {
+        if (e.t == JVal::Null || e.isUndef()) continue;
+        using Child = typename std::decay_t<decltype(*out[i])>;
+        out[i].reset(new Child());
+        self(self, e, *out[i]);
+      }
+    }
+  };
+  for (size_t k = 0; k < data.arr.size(); k++) {
+    const JVal& e = data.arr[k];
+    if (e.t == JVal::Null || e.isUndef()) continue;
+    auto& l0 = a.root[(uint32_t)k];
+    l0.reset(new L0());
+    level(level, e, *l0);
+  }
+  return a;
+}
+
+void MatrixDoc::load(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId) {
+  auto findBlob = [&](const std::string& id) -> const std::string& {
+    for (auto& b : blobs)
+      if (b.first == id) return b.second;
+    throw OracleError(-1, "missing blob " + id);
+  };
+  for (int v = 0; v < 2; v++) {
+    Doc& d = v ? cols : rows;
+    const std::string pre = v ? "cols/" : "rows/";
+    const JVal ht = json_parse(findBlob(pre + "handleTable"));  // HandleTable.load (handletable.ts:88-90)
+    if (ht.t != JVal::Arr || ht.arr.empty()) throw OracleError(-8, "bad handleTable blob");
+    d.handles.clear();
+    for (auto& h : ht.arr) d.handles.push_back(h.t == JVal::Num ? (int64_t)h.num : 0);
+    std::vector<std::pair<std::string, std::string>> seg;
+    for (auto& b : blobs)
+      if (b.first.rfind(pre + "segments/", 0) == 0) seg.push_back({b.first.substr(pre.size() + 9), b.second});
+    d.loadV1(seg, observerId);
+  }
+  const JVal cd = json_parse(findBlob("cells"));  // [cells.snapshot(), pending.snapshot()]
+  if (cd.t != JVal::Arr || cd.arr.size() < 2) throw OracleError(-8, "bad cells blob");
+  cells = SparseArray2D::load(cd.arr[0]);
+  const SparseArray2D pend = SparseArray2D::load(cd.arr[1]);
+  if (pend.snapshotJson() != "[null]") throw OracleError(-6, "unsupported: pending local cell writes in a summary");
+}
+
 std::vector<std::pair<std::string, std::string>> MatrixDoc::summarize(std::string* summaryJson) {
   std::string rj, cj;
   auto rb = rows.summarizeV1(&rj);

@@ -304,6 +304,7 @@ struct SparseArray2D {
   void clearRows(uint32_t rowStart, uint32_t rowCount);
   void clearCols(uint32_t colStart, uint32_t colCount);
   std::string snapshotJson() const;  // JSON.stringify(snapshot())
+  static SparseArray2D load(const JVal& data);  // SparseArray2D.load (nullToUndefined over the arrays)
 };
 
 // SharedMatrix observer over two PermutationVectors (matrix/src/matrix.ts:636-697); the cell store
@@ -327,6 +328,9 @@ struct MatrixDoc {
   SparseArray2D cells;  // matrix.ts:96 (the observer's `pending` array stays empty)
   // SharedMatrix.summarizeCore (matrix.ts:449-463): {rows, cols: PermutationVector.summarize, cells}
   std::vector<std::pair<std::string, std::string>> summarize(std::string* summaryJson);
+  // SharedMatrix.loadCore (matrix.ts:611-634): rows / cols PermutationVector.load (handle table, then
+  // the SnapshotV1 segments, permutationvector.ts:327-345) and the cells blob
+  void load(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId);
 };
 
 uint64_t fnv1a64(const std::string& s);

@@ -139,6 +139,17 @@ int orc_matrix_summarize(orc_matrix* m, char** out, size_t* len) {
   if (rc) m->err = m->rows.err;
   return rc;
 }
+// SharedMatrix.loadCore (matrix.ts:611-634): blobs = JSON [[path, content]...]
+int orc_matrix_load(orc_matrix* m, const char* blobs_json, size_t len, const char* observer) {
+  int rc = guard(&m->rows, [&] {
+    const JVal a = json_parse(blobs_json, len);
+    std::vector<std::pair<std::string, std::string>> blobs;
+    for (auto& p : a.arr) blobs.push_back({u16_to_utf8(p.arr[0].str), u16_to_utf8(p.arr[1].str)});
+    m->m.load(blobs, observer ? observer : "snapshot");
+  });
+  if (rc) m->err = m->rows.err;
+  return rc;
+}
 // cells.getCell(rowHandle, colHandle) (sparsearray2d.ts:68-88): JSON text, "" when undefined
 int orc_matrix_get_cell_by_handle(orc_matrix* m, uint32_t rh, uint32_t ch, char** out, size_t* len) {
   const std::optional<std::string>* v = m->m.cells.getCell(rh, ch);

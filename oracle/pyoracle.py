@@ -62,6 +62,7 @@ def lib():
         L.orc_matrix_last_error.argtypes = [vp]
         L.orc_matrix_start_collab.argtypes = [vp, cp, i, i]
         L.orc_matrix_apply_msg_json.argtypes = [vp, cp, sz]
+        L.orc_matrix_load.argtypes = [vp, cp, sz, cp]
         L.orc_matrix_summarize.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_matrix_get_cell.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(sz)]
@@ -327,6 +328,11 @@ class OracleMatrix:
             return ctypes.string_at(p, n.value).decode("utf-8")
         finally:
             self._L.orc_free(p)
+
+    def load(self, blobs, observer="snapshot"):
+        """SharedMatrix.loadCore (matrix.ts:611-634) from [(path, content)...] as summarize() gives them."""
+        raw = json.dumps([list(b) for b in blobs]).encode()
+        self._chk(self._L.orc_matrix_load(self._h, raw, len(raw), observer.encode()))
 
     def summarize(self):
         """SharedMatrix summary (matrix.ts:449-463): {"blobs": [[path, content]...], "summary": {...}}."""
