@@ -19,7 +19,7 @@ ERRORS = {0: "MTB_OK", -1: "MTB_E_ARG", -2: "MTB_E_NODEV", -3: "MTB_E_HIP", -4: 
 # every entry point declared in include/mtb.h
 EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free", "mtb_doc_init",
            "mtb_doc_load_v1", "mtb_docs_load_v1", "mtb_matrix_init", "mtb_matrix_apply_msg_json",
-           "mtb_matrix_intern_value", "mtb_matrix_summarize", "mtb_matrix_get_cell",
+           "mtb_matrix_intern_value", "mtb_matrix_summarize", "mtb_matrix_get_cell", "mtb_matrix_load",
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
@@ -78,6 +78,7 @@ def lib():
                                    ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_char_p), u32]
     L.mtb_matrix_init.argtypes = [vp, u32, ctypes.c_char_p, u32, u32]
     L.mtb_matrix_apply_msg_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    L.mtb_matrix_load.argtypes = [vp, u32, vp, u32, ctypes.c_char_p]
     L.mtb_matrix_intern_value.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(u32)]
     L.mtb_matrix_get_cell.argtypes = [vp, u32, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.mtb_apply_msg_json.argtypes = [vp, u32, ctypes.c_char_p, sz]

@@ -100,8 +100,8 @@ class MergeTreeBatch:
         buf = ctypes.create_string_buffer(raw, max(2, len(raw)))
         self._chk(self._L.mtb_doc_init(self._h, doc, buf, len(raw) // 2, observer_long_id.encode(), min_seq, cur_seq))
 
-    def load_v1(self, doc, blobs, observer_long_id="snapshot"):
-        """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""
+    @staticmethod
+    def _blob_array(blobs):
         pairs = [(p.encode(), c.encode("utf-8") if isinstance(c, str) else bytes(c)) for p, c in blobs]
         arr = (_lib.MtbBlob * max(1, len(pairs)))()
         keep = []
@@ -111,7 +111,12 @@ class MergeTreeBatch:
             arr[i].path = p
             arr[i].content = ctypes.cast(buf, ctypes.c_void_p)
             arr[i].content_len = len(c)
-        self._chk(self._L.mtb_doc_load_v1(self._h, doc, arr, len(pairs), observer_long_id.encode()))
+        return arr, len(pairs), keep
+
+    def load_v1(self, doc, blobs, observer_long_id="snapshot"):
+        """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""
+        arr, n, _keep = self._blob_array(blobs)
+        self._chk(self._L.mtb_doc_load_v1(self._h, doc, arr, n, observer_long_id.encode()))
         self._dirty = True
 
     def load_v1_many(self, docs, summaries, observer_long_ids, threads=16):
@@ -380,6 +385,12 @@ class MatrixBatch(MergeTreeBatch):
     def init_matrix(self, m, observer_long_id, min_seq=0, cur_seq=0):
         self._chk(self._L.mtb_matrix_init(self._h, m, observer_long_id.encode(), min_seq, cur_seq))
 
+    def load_matrix(self, m, blobs, observer_long_id="snapshot"):
+        """SharedMatrix.loadCore (matrix.ts:611) from [(path, content), ...] as matrix_summarize gives them."""
+        arr, n, _keep = self._blob_array(blobs)
+        self._chk(self._L.mtb_matrix_load(self._h, m, arr, n, observer_long_id.encode()))
+        self._dirty = True
+
     def intern_value(self, value_json):
         """Id of a setCell value (JSON text) for SETCELL records packed by the caller (0 = undefined)."""
         raw = value_json.encode()
@@ -424,6 +435,11 @@ class SharedMatrix:
 
     def applyMsg(self, msg):
         self._b.apply_matrix_msg(self._m, msg)
+
+    def load(self, storage, clientId=None):
+        """SharedMatrix.loadCore (matrix.ts:611-634): `storage` maps blob path -> content (dict or pairs)."""
+        blobs = list(storage.items()) if isinstance(storage, dict) else list(storage)
+        self._b.load_matrix(self._m, blobs, clientId if clientId is not None else "snapshot")
 
     @property
     def rows_doc(self):

@@ -217,6 +217,7 @@ struct LoadImage {
 struct CellStore {
   std::unordered_map<uint64_t, uint32_t> cells;  // (row << 32 | col) -> value id
   std::unordered_map<uint32_t, std::vector<uint32_t>> rowCols, colRows;
+  uint64_t rootLen = 1;  // the root array's JS length (`[undefined]`, grown by writes or a load)
   static uint32_t spread(uint32_t x) {  // interlaceBitsX16: the low 16 bits onto the even positions
     x &= 0xffff;
     x = (x | (x << 8)) & 0x00ff00ffu;
@@ -227,6 +228,7 @@ struct CellStore {
   }
   static uint32_t morton(uint32_t r, uint32_t c) { return (spread(r) << 1) | spread(c); }  // r0c0ToMorton2x16
   void set(uint32_t r, uint32_t c, uint32_t v) {
+    rootLen = std::max<uint64_t>(rootLen, (uint64_t)morton(r >> 16, c >> 16) + 1);
     auto [it, fresh] = cells.try_emplace(((uint64_t)r << 32) | c, v);
     if (!fresh) {
       it->second = v;
@@ -256,7 +258,7 @@ struct CellStore {
     std::sort(keys.begin(), keys.end());
     std::string o = "[";
     size_t i = 0;
-    const uint64_t rootLen = keys.empty() ? 1 : (keys.back().first >> 32) + 1;
+
     // level `lv` (0..3) of the tile whose key prefix is `pre`: 256 entries, byte `lv` of keyLo
     auto level = [&](auto& self, int lv, uint64_t pre) -> void {
       o += '[';
@@ -556,7 +558,12 @@ LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<u
   const hj::Value& js = mergeInfo ? *member(spec, u"json") : spec;
   const hj::Value* props = nullptr;
   const U16* text = nullptr;
-  if (js.kind == hj::Value::kStr) {
+  if (d.perm) {  // PermutationSegment.fromJSONObject([length, start]) (permutationvector.ts:45-48)
+    if (js.kind != hj::Value::kArr || js.items.size() < 2 || js.items[0].kind != hj::Value::kNum)
+      raise(MTB_E_PARSE, "Unrecognized PermutationSegment spec");
+    g.len = (uint32_t)js.items[0].n;
+    g.text = js.items[1].kind == hj::Value::kNum ? (uint32_t)(int32_t)js.items[1].n : MTB_HANDLE_UNALLOC;
+  } else if (js.kind == hj::Value::kStr) {
     text = &js.s;
   } else if (js.kind == hj::Value::kObj && member(js, u"text")) {
     const hj::Value* tv = member(js, u"text");
@@ -756,18 +763,18 @@ void resolve_load_props(mtb_batch* b, HostDoc& d) {
 // Client.load of one SnapshotV1 summary into the fresh document d (client.ts:1007 -> SnapshotLoader,
 // snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in parallel.
 void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
-              PropsCache* pc) {
-  if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: summary load into a matrix batch (PermutationVector.load)");
+              PropsCache* pc, const std::string& prefix = std::string()) {
+  if (b->matrix && !d.perm) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_load");
   if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
   if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
   if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
   auto blob = [&](const std::string& path) -> hj::Value {
     for (uint32_t i = 0; i < nblobs; i++)
-      if (blobs[i].path && path == blobs[i].path) {
+      if (blobs[i].path && prefix + path == blobs[i].path) {
         if (!blobs[i].content && blobs[i].content_len) raise(MTB_E_ARG, "null blob content");
         return hj::parse(blobs[i].content ? blobs[i].content : "", blobs[i].content_len);
       }
-    raise(MTB_E_ARG, "summary blob not found: " + path);
+    raise(MTB_E_ARG, "summary blob not found: " + prefix + path);
   };
   // loadHeader (snapshotLoader.ts:133-167)
   const hj::Value header = blob("header");
@@ -804,6 +811,8 @@ void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, 
       if (cs && cs->kind == hj::Value::kArr)
         for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload, pc));
     }
+  if (d.perm && !body.empty())
+    raise(MTB_E_UNSUPPORTED, "unsupported: PermutationVector summary with body chunks (more than chunkSize rows/cols)");
   build_load_image(d, hdr);
   // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
   // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
@@ -931,7 +940,7 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
 // caps_for plus what a loaded summary already occupies (header segments, blocks, lists, aux words)
 Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
   Caps c = caps_for(n, payload, d.initText.size());
-  if (d.perm) c.text = (uint32_t)(2 * (d.totalSetcell + 4) + 64);  // the handle table (u32 words)
+  if (d.perm) c.text = (uint32_t)(2 * (d.totalSetcell + d.initText.size() / 2 + 4) + 64);  // the handle table (u32 words)
   if (d.loaded) {
     c.seg += (uint32_t)d.img.segp.size();
     c.blk += (uint32_t)d.img.blks.size() + (uint32_t)d.img.segp.size() / 4;
@@ -1045,6 +1054,7 @@ void device_init(mtb_batch* b) {
       recs.insert(recs.end(), im.aux.begin(), im.aux.end());
       txtc.add(texts.size(), s.text_base, d.initText.size());
       texts.insert(texts.end(), d.initText.begin(), d.initText.end());
+      if (d.perm) s.flags |= DSF_PERM;  // a loaded PermutationVector: initText is its handle table
       d.onDevice = true;
       continue;
     }
@@ -1268,7 +1278,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
       const DocState& s = b->hst[i];
       Caps need = doc_caps(d, d.totalOps, d.totalPayload + s.text_used);
       if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap ||
-          (d.perm && 2 * (d.totalSetcell + 4) > s.text_cap)) {
+          (d.perm && 2 * (d.totalSetcell + d.initText.size() / 2 + 4) > s.text_cap)) {
         want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
         grow = true;
       } else {
@@ -2913,5 +2923,98 @@ int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_
     o += "]";
     *out = dup(o);
     if (out_len) *out_len = o.size();
+  });
+}
+
+// ------------------------------------------------------------------ SharedMatrix load
+namespace {
+uint32_t compact_even(uint32_t x) {  // inverse of CellStore::spread: the even bits, packed
+  x &= 0x55555555u;
+  x = (x | (x >> 1)) & 0x33333333u;
+  x = (x | (x >> 2)) & 0x0f0f0f0fu;
+  x = (x | (x >> 4)) & 0x00ff00ffu;
+  x = (x | (x >> 8)) & 0x0000ffffu;
+  return x;
+}
+// SparseArray2D.load (sparsearray2d.ts:233-236) into a CellStore: every non-null leaf becomes a written
+// key; a 256-leaf tile whose leaves are all null keeps its place through one written-undefined key
+void load_cells(mtb_batch* b, CellStore& cs, const hj::Value& root) {
+  if (root.kind != hj::Value::kArr) raise(MTB_E_PARSE, "cells snapshot is not an array");
+  cs.rootLen = std::max<uint64_t>(1, root.items.size());
+  for (size_t hi = 0; hi < root.items.size(); hi++) {
+    const hj::Value& l0 = root.items[hi];
+    if (l0.kind == hj::Value::kNull) continue;
+    auto key = [&](uint32_t lo, uint32_t v) {
+      const uint32_t khi = (uint32_t)hi;
+      const uint32_t r = compact_even(lo >> 1) | (compact_even(khi >> 1) << 16);
+      const uint32_t c = compact_even(lo) | (compact_even(khi) << 16);
+      cs.set(r, c, v);
+    };
+    // levels 0..2 hold arrays, level 3 values; a level array with no children cannot be represented
+    auto walk = [&](auto& self, const hj::Value& a, int lv, uint32_t pre) -> void {
+      if (a.kind != hj::Value::kArr) raise(MTB_E_PARSE, "cells level is not an array");
+      bool any = false;
+      for (size_t e = 0; e < a.items.size() && e < 256; e++) {
+        const hj::Value& x = a.items[e];
+        if (x.kind == hj::Value::kNull) continue;
+        const uint32_t k = pre | ((uint32_t)e << (24 - 8 * lv));
+        if (lv == 3) key(k, intern_cell_value(b, hj::dump(x)));
+        else self(self, x, lv + 1, k);
+        any = true;
+      }
+      if (!any) {
+        if (lv < 3) raise(MTB_E_UNSUPPORTED, "unsupported: an empty SparseArray2D level above the leaves");
+        key(pre, 0);
+      }
+    };
+    walk(walk, l0, 0, 0);
+  }
+}
+}  // namespace
+
+// SharedMatrix.loadCore (matrix.ts:611-634): rows / cols PermutationVector.load (permutationvector.ts:
+// 327-345: HandleTable.load of "handleTable", then Client.load of "segments/...") and SparseArray2D.load
+// of "cells"; blob paths as mtb_matrix_summarize writes them.
+int mtb_matrix_load(mtb_batch* b, uint32_t matrix, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
+  return guarded(b, [&] {
+    if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
+    if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    if (!observer_long_id) raise(MTB_E_ARG, "observer long client id required");
+    if (nblobs && !blobs) raise(MTB_E_ARG, "null blob array");
+    for (int v = 0; v < 2; v++) {
+      const HostDoc& d = b->docs[2 * matrix + v];
+      if (d.inited || d.onDevice) raise(MTB_E_ARG, "matrix already initialised");
+    }
+    auto blob = [&](const std::string& path) -> hj::Value {
+      for (uint32_t i = 0; i < nblobs; i++)
+        if (blobs[i].path && path == blobs[i].path) return hj::parse(blobs[i].content ? blobs[i].content : "", blobs[i].content_len);
+      raise(MTB_E_ARG, "summary blob not found: " + path);
+    };
+    HostDoc fresh[2];
+    for (int v = 0; v < 2; v++) {
+      HostDoc& d = fresh[v];
+      d.perm = true;
+      const std::string pre = v ? "cols/" : "rows/";
+      const hj::Value ht = blob(pre + "handleTable");
+      if (ht.kind != hj::Value::kArr || ht.items.empty()) raise(MTB_E_PARSE, "bad handleTable blob");
+      load_one(b, d, blobs, nblobs, observer_long_id, nullptr, pre + "segments/");
+      d.initText.clear();  // the text arena of a PermutationVector holds its handle table: u32 [length, handles]
+      auto word = [&](uint32_t w) {
+        d.initText.push_back((uint16_t)(w & 0xFFFF));
+        d.initText.push_back((uint16_t)(w >> 16));
+      };
+      word((uint32_t)ht.items.size());
+      for (auto& h : ht.items) word(h.kind == hj::Value::kNum ? (uint32_t)(int64_t)h.n : 0u);
+      resolve_load_props(b, d);
+    }
+    const hj::Value cd = blob("cells");
+    if (cd.kind != hj::Value::kArr || cd.items.size() < 2) raise(MTB_E_PARSE, "bad cells blob");
+    std::unique_ptr<CellStore> cs(new CellStore());
+    load_cells(b, *cs, cd.items[0]);
+    const hj::Value& pend = cd.items[1];  // the observer's pending local writes must be empty
+    if (pend.kind != hj::Value::kArr || pend.items.size() != 1 || pend.items[0].kind != hj::Value::kNull)
+      raise(MTB_E_UNSUPPORTED, "unsupported: pending local cell writes in a summary");
+    fresh[0].cells = std::move(cs);
+    for (int v = 0; v < 2; v++) b->docs[2 * matrix + v] = std::move(fresh[v]);
   });
 }

@@ -80,6 +80,9 @@ export declare class MatrixBatch extends MergeTreeBatch {
 export declare class SharedMatrix {
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   applyMsg(msg: ISequencedDocumentMessage | string): void;
+  /** SharedMatrix.loadCore (matrix.ts:611) of a summary written by summarize(). */
+  load(runtime: { clientId?: string } | undefined,
+       storage: { readBlob(path: string): Promise<ArrayBufferLike | Uint8Array | string> }): Promise<void>;
   /** SharedMatrix.summarizeCore (matrix.ts:449): rows / cols PermutationVector summaries and the cells blob. */
   summarize(): { blobs: [string, string][]; summary: unknown };
   /** SharedMatrix.getCell (matrix.ts:173) in the observer's view. */

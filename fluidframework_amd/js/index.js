@@ -292,6 +292,27 @@ class SharedMatrix {
     this.batch.dirty = true;
   }
 
+  /**
+   * SharedMatrix.loadCore (matrix.ts:611-634) into a fresh slot: `storage.readBlob(path)` gives the blobs
+   * summarize() wrote ("rows/handleTable", "rows/segments/header" and its body chunks, "cols/...",
+   * "cells"); `runtime.clientId` becomes the observer id ("snapshot" when absent).
+   */
+  async load(runtime, storage) {
+    const text = (x) => (typeof x === "string" ? x : Buffer.from(x instanceof ArrayBuffer ? new Uint8Array(x) : x).toString("utf8"));
+    const blobs = [];
+    for (const v of ["rows", "cols"]) {
+      blobs.push([`${v}/handleTable`, text(await storage.readBlob(`${v}/handleTable`))]);
+      const header = text(await storage.readBlob(`${v}/segments/header`));
+      blobs.push([`${v}/segments/header`, header]);
+      const md = JSON.parse(header).headerMetadata;
+      const ids = md && Array.isArray(md.orderedChunkMetadata) ? md.orderedChunkMetadata.slice(1).map((c) => c.id) : [];
+      for (const id of ids) blobs.push([`${v}/segments/${id}`, text(await storage.readBlob(`${v}/segments/${id}`))]);
+    }
+    blobs.push(["cells", text(await storage.readBlob("cells"))]);
+    native.matrixLoad(this.batch.handle, this.m, blobs, runtime && runtime.clientId !== undefined ? runtime.clientId : "snapshot");
+    this.batch.dirty = true;
+  }
+
   /** SharedMatrix.summarizeCore (matrix.ts:449-463): rows / cols PermutationVector summaries + cells blob. */
   summarize() {
     this.batch.ensureFlushed();

@@ -181,7 +181,11 @@ static napi_value js_doc_init(napi_env env, napi_callback_info info) {
 }
 
 /* loadV1(h, doc, [[path, content], ...], observerLongId)               client.ts:1007, snapshotLoader.ts:41 */
-static napi_value js_load_v1(napi_env env, napi_callback_info info) {
+static napi_value load_blobs(napi_env env, napi_callback_info info, int matrix);
+static napi_value js_load_v1(napi_env env, napi_callback_info info) { return load_blobs(env, info, 0); }
+/* matrixLoad(h, matrix, [[path, content], ...], observerLongId)          matrix.ts:611-634 */
+static napi_value js_matrix_load(napi_env env, napi_callback_info info) { return load_blobs(env, info, 1); }
+static napi_value load_blobs(napi_env env, napi_callback_info info, int matrix) {
   napi_value argv[4];
   if (!get_args(env, info, 4, argv)) return NULL;
   mtb_batch* b = get_batch(env, argv[0]);
@@ -211,7 +215,7 @@ static napi_value js_load_v1(napi_env env, napi_callback_info info) {
   int rc = 0;
   if (ok) {
     id = get_utf8(env, argv[3], NULL);
-    if (id) rc = mtb_doc_load_v1(b, doc, blobs, n, id);
+    if (id) rc = matrix ? mtb_matrix_load(b, doc, blobs, n, id) : mtb_doc_load_v1(b, doc, blobs, n, id);
     else ok = 0;
   }
   for (uint32_t i = 0; i < n; i++) {
@@ -630,6 +634,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"create", js_create},           {"docInit", js_doc_init},       {"loadV1", js_load_v1},
       {"matrixInit", js_matrix_init},  {"matrixApplyMsg", js_matrix_apply_msg},
       {"matrixSummarize", js_matrix_summarize}, {"matrixGetCell", js_matrix_get_cell},
+      {"matrixLoad", js_matrix_load},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

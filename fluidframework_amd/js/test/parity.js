@@ -44,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell", "mapRange"];
+    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell", "mapRange", "matrixLoad"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -144,6 +144,15 @@ async function gpuChecks() {
     for (const [r, c, v] of e.cells)
       assert.deepStrictEqual(mb.matrix(0).getCell(r, c), v === null ? undefined : JSON.parse(v), `getCell(${r}, ${c})`);
   }
+  // SharedMatrix.load of that summary: the same summary back, the same cells by position
+  const lm = new MatrixBatch(1);
+  const store = new Map(s0.blobs);
+  await lm.matrix(0).load({ clientId: "obs" }, { readBlob: async (p) => store.get(p) });
+  assert.deepStrictEqual(lm.matrix(0).summarize().blobs, s0.blobs);
+  assert.strictEqual(lm.matrix(0).rowCount, mb.matrix(0).rowCount);
+  for (let r = 0; r < mb.matrix(0).rowCount; r += 3)
+    for (let c = 0; c < mb.matrix(0).colCount; c += 3)
+      assert.deepStrictEqual(lm.matrix(0).getCell(r, c), mb.matrix(0).getCell(r, c));
   console.log("js gpu matrix ok");
   const ref = new MergeTreeBatch(1);
   await ref.client(0).load(undefined, storageOf(snapshotBlobs("withMarkers")));

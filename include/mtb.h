@@ -163,6 +163,11 @@ int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json_ut
 /* Intern a setCell value (JSON text) for records packed by the caller (mtb_append_ops): the SETCELL
  * record's `props` field carries the id (0 = undefined). */
 int mtb_matrix_intern_value(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* id_out);
+/* SharedMatrix.loadCore (matrix.ts:611-634) of a matrix slot that is still fresh (instead of
+ * mtb_matrix_init): blobs as mtb_matrix_summarize writes them ("rows/handleTable", "rows/segments/header",
+ * "cols/...", "cells"); the observer id becomes both vectors' client id.  PermutationVector summaries
+ * with body chunks and summaries holding pending local cell writes are MTB_E_UNSUPPORTED. */
+int mtb_matrix_load(mtb_batch* b, uint32_t matrix, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id);
 /* SharedMatrix.summarizeCore (matrix.ts:449-463): blobs "rows/segments/header", ..., "rows/handleTable",
  * "cols/...", "cells" (JSON [cells.snapshot(), pending.snapshot()]) and the ISummaryTreeWithStats. */
 int mtb_matrix_summarize(mtb_batch* b, uint32_t matrix, mtb_blob_list* out);

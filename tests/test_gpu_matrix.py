@@ -104,3 +104,38 @@ def test_generated_matrix_records_match_oracle_checksums(new_mode):
     assert st["errors"] == 0
     bad = [(i, v) for i in range(lb.n) for v in (0, 1) if B.checksum(2 * i + v) != lb.mats[i].checksum[v]]
     assert not bad, f"{len(bad)} vectors differ, first {bad[:4]}"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_matrix_load_mid_stream_then_continue(new_mode):
+    """SharedMatrix.loadCore (matrix.ts:611-634) on the engine: an oracle summary taken mid-stream is loaded
+    (rows / cols handle tables + segments, cells) and the rest of the log replayed; summaries and getCell
+    equal the oracle that loaded the same summary."""
+    from fluidframework_amd import MatrixBatch
+    from pyoracle import OracleMatrix
+    n = 12
+    B = MatrixBatch(n, new_length_calc=new_mode)
+    oracles = []
+    for i in range(n):
+        msgs = make_matrix_log(700 + 3 * i + int(new_mode), 600 + 20 * i, n_clients=2 + i % 4, lag=3 + 2 * (i % 6),
+                               new_mode=new_mode)
+        src = OracleMatrix(new_length_calc=new_mode)
+        src.start_collab("obs")
+        half = len(msgs) // 2
+        for m in msgs[:half]:
+            src.apply_msg(m)
+        blobs = src.summarize()["blobs"]
+        o = OracleMatrix(new_length_calc=new_mode)
+        o.load(blobs, "obs")
+        B[i].load(blobs, "obs")
+        for m in msgs[half:]:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    for i, o in enumerate(oracles):
+        _check(B, i, o, f"loaded matrix {i}")
+        nr, nc = o.rows.get_length(), o.cols.get_length()
+        for r in range(0, nr, max(1, nr // 10)):
+            for c in range(0, nc, max(1, nc // 10)):
+                assert B.get_cell(i, r, c) == o.get_cell(r, c), f"matrix {i} cell ({r}, {c})"
