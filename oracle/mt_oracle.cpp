@@ -329,6 +329,13 @@ Seg* MergeTree::splitAt(Seg* s, int pos) {
   r->removedSeq = s->removedSeq;
   r->seq = s->seq;
   r->clientId = s->clientId;
+  r->localSeq = s->localSeq;
+  r->localRemovedSeq = s->localRemovedSeq;
+  for (SegGroup* g : s->groups) {  // segmentGroups.copyTo (mergeTreeNodes.ts:239-245)
+    g->segments.push_back(r);
+    r->groups.push_back(g);
+  }
+  if (s->hasPropManager && s->props) r->pendingKeys = s->pendingKeys;  // PropertiesManager.copyTo
   counters.segsTouched += 2;  // split: left half modified + right half created
   return r;
 }
@@ -474,9 +481,10 @@ void MergeTree::ensureIntervalBoundary(int pos, int refSeq, int clientId) {
 }
 
 // blockInsert (mergeTree.ts:1594-1685), single segment
-void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg) {
+void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg, int localSeq, SegGroup** group) {
   if (seg->cachedLength > 0) {
     seg->seq = seq;
+    seg->localSeq = localSeq;
     seg->clientId = clientId;
     InsertCtx ctx;
     ctx.insertMode = true;
@@ -487,7 +495,8 @@ void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg
     // saveIfLocal (mergeTree.ts:1617-1637)
     if (window.collaborating) {
       if (seg->seq == UnassignedSeq && clientId == window.clientId) {
-        fail_unsupported("local pending segment");
+        SegGroup* g = addToPendingList(seg, group ? *group : nullptr, localSeq);
+        if (group) *group = g;
       } else if (seg->seq > window.minSeq) {
         addToLRUSet(seg, seg->seq);
       }
@@ -499,7 +508,9 @@ void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg
 // insertSegments (mergeTree.ts:1397-1427)
 void MergeTree::insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
   ensureIntervalBoundary(pos, refSeq, clientId);
-  blockInsert(pos, refSeq, clientId, seq, seg);
+  const int localSeq = seq == UnassignedSeq ? ++window.localSeq : INT32_MIN;  // mergeTree.ts:1407-1408
+  SegGroup* group = nullptr;
+  blockInsert(pos, refSeq, clientId, seq, seg, localSeq, &group);
   if (onDelta && seg->parent && seg->cachedLength > 0) onDelta(0, {seg}, nullptr);
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
@@ -564,6 +575,69 @@ void MergeTree::nodeUpdateLengthNewStructure(Block* b, bool recur) {
 }
 
 // blockUpdateLength (mergeTree.ts:2436-2454)
+// addToPendingList (mergeTree.ts:1324-1357): one group per local op, enqueued on each of its segments
+SegGroup* MergeTree::addToPendingList(Seg* s, SegGroup* g, int localSeq) {
+  if (!g) {
+    groupPool.emplace_back(new SegGroup());
+    g = groupPool.back().get();
+    g->localSeq = localSeq;
+    g->refSeq = window.currentSeq;
+    pendingSegments.push_back(g);
+  }
+  g->segments.push_back(s);
+  s->groups.push_back(g);
+  return g;
+}
+
+// ackPendingSegment (mergeTree.ts:1283-1322) with BaseSegment.ack (mergeTreeNodes.ts:439-480)
+void MergeTree::ackPendingSegment(int opType, const JObj* props, int seq) {
+  SegGroup* g = nullptr;
+  if (!pendingSegments.empty()) {
+    g = pendingSegments.front();
+    pendingSegments.pop_front();
+  }
+  std::vector<Block*> nodesToUpdate;
+  bool overwrite = false;
+  if (g) {
+    for (Seg* s : g->segments) {
+      if (s->groups.empty() || s->groups.front() != g) fail_assert("0x043", "On ack, unexpected segmentGroup!");
+      s->groups.pop_front();
+      bool overlapping = false;
+      switch (opType) {
+        case 2:  // PropertiesManager.ackPendingProperties (segmentPropertiesManager.ts:31-58)
+          if (!s->hasPropManager) fail_assert("0x044", "On annotate ack, missing segment property manager!");
+          if (props)
+            for (auto& kv : *props) {
+              auto it = s->pendingKeys.find(kv.first);
+              if (it == s->pendingKeys.end()) continue;
+              if (it->second <= 0) fail_assert("0x05c", "Trying to update more annotate props than do exist!");
+              if (--it->second == 0) s->pendingKeys.erase(it);
+            }
+          break;
+        case 0:
+          if (s->seq != UnassignedSeq) fail_assert("0x045", "On insert, seq number already assigned!");
+          s->seq = seq;
+          s->localSeq = INT32_MIN;
+          break;
+        case 1:
+          if (!s->removed) fail_assert("0x046", "On remove ack, missing removal info!");
+          s->localRemovedSeq = INT32_MIN;
+          if (s->removedSeq == UnassignedSeq) s->removedSeq = seq;
+          else overlapping = true;
+          break;
+        default:
+          throw OracleError(-8, "unrecognized operation type in ack");
+      }
+      overwrite = overlapping || overwrite;
+      addToLRUSet(s, seq);
+      if (std::find(nodesToUpdate.begin(), nodesToUpdate.end(), s->parent) == nodesToUpdate.end())
+        nodesToUpdate.push_back(s->parent);
+    }
+    for (Block* b : nodesToUpdate) blockUpdatePathLengths(b, seq, window.clientId, overwrite);
+  }
+  zamboniSegments();
+}
+
 void MergeTree::blockUpdateLength(Block* b, int seq, int clientId) {
   blockUpdate(b);
   if (window.collaborating && seq != UnassignedSeq && seq != TreeMaintenanceSeq) {
@@ -583,6 +657,9 @@ void MergeTree::blockUpdatePathLengths(Block* b, int seq, int clientId, bool new
 
 // ---------------------------------------------------------------- partial lengths construction
 void MergeTree::plInsertSegment(PartialLengths& pl, Seg* s, bool removal) {  // partialLengths.ts:444-541
+  // an unacked insert / removal goes to unsequencedRecords, which only local-perspective queries with a
+  // localSeq need (computeLocalPartials); the observer-side restatement does not keep them
+  if ((!removal && s->seq == UnassignedSeq) || (removal && s->removedSeq == UnassignedSeq)) return;
   int seq = s->seq;
   int segLen = s->cachedLength;
   int clientId = s->clientId;
@@ -776,21 +853,29 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
   std::vector<Seg*> removed;  // removedSegments (mergeTree.ts:1973): fresh removals only
+  const int localSeq = seq == UnassignedSeq ? ++window.localSeq : INT32_MIN;  // mergeTree.ts:1973-1974
+  SegGroup* group = nullptr;
   auto markRemoved = [&](Seg* s, int, int, int) -> bool {
     if (!s->removed) removed.push_back(s);
     if (s->removed) {
       overwrite = true;
-      if (s->removedSeq == UnassignedSeq) fail_unsupported("local pending remove");
-      s->removedClientIds.push_back(clientId);
+      if (s->removedSeq == UnassignedSeq) {
+        // removed locally, but someone else removed it first: they go to the head (mergeTree.ts:1980-1988)
+        s->removedClientIds.insert(s->removedClientIds.begin(), clientId);
+        s->removedSeq = seq;
+      } else {
+        s->removedClientIds.push_back(clientId);
+      }
     } else {
       s->removed = true;
       s->removedClientIds = {clientId};
       s->removedSeq = seq;
+      s->localRemovedSeq = localSeq;
     }
     counters.segsTouched += 1;
     if (window.collaborating) {
-      if (s->removedSeq == UnassignedSeq && clientId == window.clientId) fail_unsupported("local pending remove");
-      addToLRUSet(s, seq);
+      if (s->removedSeq == UnassignedSeq && clientId == window.clientId) group = addToPendingList(s, group, localSeq);
+      else addToLRUSet(s, seq);
     }
     return true;
   };
@@ -803,21 +888,30 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
 
-// PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) for a sequenced remote op or a
-// non-collaborating local op (no pending local state), combined with BaseSegment.addProperties.
-static void applyProps(Seg* s, const JObj& newProps, bool rewrite) {
+// PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) combined with
+// BaseSegment.addProperties: a local op (seq Unassigned) while collaborating counts its keys as pending;
+// a sequenced remote op leaves the keys with pending local updates alone (shouldModifyKey).  Local
+// rewrites (pendingRewriteCount) are not restated.
+static void applyProps(Seg* s, const JObj& newProps, bool rewrite, int seq = UniversalSeq, bool collaborating = false) {
   s->hasPropManager = true;
   if (!s->props) s->props = JObj();
   JObj& old = *s->props;
+  auto shouldModify = [&](const u16str& k) {
+    return seq == UnassignedSeq || seq == UniversalSeq || s->pendingKeys.find(k) == s->pendingKeys.end();
+  };
   if (rewrite) {
     std::vector<u16str> keys;
     for (auto& kv : old) keys.push_back(kv.first);
     for (auto& k : keys) {
       const JVal* nv = obj_get(newProps, k);
-      if (js_falsy(nv)) obj_del(old, k);
+      if (js_falsy(nv) && shouldModify(k)) obj_del(old, k);
     }
   }
   for (auto& kv : newProps) {
+    if (collaborating) {
+      if (seq == UnassignedSeq) s->pendingKeys[kv.first]++;
+      else if (!shouldModify(kv.first)) continue;
+    }
     if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
   }
@@ -828,13 +922,16 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
   std::vector<Seg*> annotated;
+  const int localSeq = seq == UnassignedSeq ? ++window.localSeq : INT32_MIN;  // mergeTree.ts:1909-1910
+  SegGroup* group = nullptr;
+  if (seq == UnassignedSeq && rewrite) fail_unsupported("local rewrite annotate");
   auto annotate = [&](Seg* s, int, int, int) -> bool {
     annotated.push_back(s);
-    applyProps(s, props, rewrite);
+    applyProps(s, props, rewrite, seq, window.collaborating);
     counters.segsTouched += 1;
     if (window.collaborating) {
-      if (seq == UnassignedSeq) fail_unsupported("local pending annotate");
-      addToLRUSet(s, seq);
+      if (seq == UnassignedSeq) group = addToPendingList(s, group, localSeq);
+      else addToLRUSet(s, seq);
     }
     return true;
   };
@@ -880,7 +977,10 @@ void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {  // zamboni.t
     Node* c = node->children[k];
     if (c->leaf) {
       Seg* s = static_cast<Seg*>(c);
-      if (s->removed) {
+      if (!s->groups.empty()) {  // a segment with pending local ops stays as it is
+        hold.push_back(s);
+        prev = nullptr;
+      } else if (s->removed) {
         if (s->removedSeq > window.minSeq) {
           hold.push_back(s);
         } else {
@@ -1275,14 +1375,19 @@ void Doc::applyMsgCore(const JVal& msg) {
     const JVal* contents = obj_get(msg.obj, u"contents");
     if (!contents || contents->t != JVal::Obj) throw OracleError(-8, "op without contents");
     if (longClientId && longId == *longClientId) {
-      // ackPendingSegment with no pending segment groups: one zamboni per member (mergeTree.ts:1283-1321)
+      // Client.ackPendingSegment (client.ts:641-662): one MergeTree.ackPendingSegment per member op
+      auto ackOne = [&](const JVal& op) {
+        const JVal* t = obj_get(op.obj, u"type");
+        const JVal* pr = obj_get(op.obj, u"props");
+        mt.ackPendingSegment(t && t->t == JVal::Num ? (int)t->num : -1, pr && pr->t == JVal::Obj ? &pr->obj : nullptr, seq);
+      };
       const JVal* t = obj_get(contents->obj, u"type");
       if (t && t->t == JVal::Num && (int)t->num == 3) {
         const JVal* ops = obj_get(contents->obj, u"ops");
         if (ops && ops->t == JVal::Arr)
-          for (size_t i = 0; i < ops->arr.size(); i++) mt.zamboniSegments();
+          for (auto& m : ops->arr) ackOne(m);
       } else {
-        mt.zamboniSegments();
+        ackOne(*contents);
       }
     } else {
       applyRemoteDelta(*contents, client, refSeq, seq);
@@ -1348,6 +1453,44 @@ void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::ve
       break;
   }
   if (r.flags & 0x01) updateSeqNumbers((int)r.msn, (int)r.seq);
+}
+
+// ---------------------------------------------------------------- a live client's local ops
+// insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:196-247) through applyInsertOp /
+// applyRemoveRangeOp / applyAnnotateRangeOp with the local client's (currentSeq, clientId) and
+// UnassignedSequenceNumber; getValidOpRange (client.ts:527-592) bounds-checks the local positions.
+static void validLocalRange(int start, int end, int len, bool insert) {
+  if (start < 0 || start > len || (!insert && (end < start || end > len)))
+    throw OracleError(-1, "RangeOutOfBounds");
+}
+std::string Doc::insertLocalOp(int pos, const JVal& segSpec) {
+  if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
+  validLocalRange(pos, pos, mt.length(), true);
+  Seg* s = makeSegFromSpec(mt, segSpec);
+  if (s->cachedLength <= 0) return "";
+  mt.insertSegments(pos, s, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
+  JVal op;
+  op.t = JVal::Obj;
+  op.obj.push_back({u"pos1", JVal::number(pos)});
+  op.obj.push_back({u"seg", segSpec});
+  op.obj.push_back({u"type", JVal::number(0)});
+  return json_stringify(op);
+}
+std::string Doc::removeLocalOp(int start, int end) {
+  if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
+  validLocalRange(start, end, mt.length(), false);
+  mt.markRangeRemoved(start, end, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
+  return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"type\":1}";
+}
+std::string Doc::annotateLocalOp(int start, int end, const JObj& props) {
+  if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
+  validLocalRange(start, end, mt.length(), false);
+  mt.annotateRange(start, end, props, false, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
+  JVal pv;
+  pv.t = JVal::Obj;
+  pv.obj = props;
+  return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"props\":" + json_stringify(pv) +
+         ",\"type\":2}";
 }
 
 // ---------------------------------------------------------------- local (detached) edits

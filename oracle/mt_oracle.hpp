@@ -58,7 +58,20 @@ struct Seg : Node {
   std::vector<int> removedClientIds;
   std::optional<JObj> props;       // properties (undefined when nullopt)
   bool hasPropManager = false;     // propertyManager !== undefined
+  // local (unacked) state of a live client (mergeTreeNodes.ts:367-440): localSeq / localRemovedSeq
+  // (kNoLocalSeq = undefined), the queue of pending segment groups, PropertiesManager.pendingKeyUpdateCount
+  int localSeq = INT32_MIN;
+  int localRemovedSeq = INT32_MIN;
+  std::deque<struct SegGroup*> groups;
+  std::map<u16str, int> pendingKeys;
   Seg() : Node(true) {}
+};
+
+// SegmentGroup (mergeTreeNodes.ts:292-300): the segments of one local op awaiting its ack
+struct SegGroup {
+  std::vector<Seg*> segments;
+  int localSeq = INT32_MIN;
+  int refSeq = 0;
 };
 
 // PartialSequenceLength entry (MT/partialLengths.ts:105-140)
@@ -82,6 +95,7 @@ struct CollabWindow {  // MT/mergeTreeNodes.ts:656-673
   bool collaborating = false;
   int minSeq = 0;
   int currentSeq = 0;
+  int localSeq = 0;
 };
 
 // PartialSequenceLengths (MT/partialLengths.ts:239-850), remote-perspective part only.
@@ -168,6 +182,11 @@ class MergeTree {
   void reloadFromSegments(const std::vector<Seg*>& segs);
   void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
   void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
+  // pendingSegments (mergeTree.ts:532) and ackPendingSegment (:1283-1322) for one acked delta op
+  // (type INSERT 0 / REMOVE 1 / ANNOTATE 2, its props for ANNOTATE)
+  std::deque<std::unique_ptr<SegGroup>> groupPool;
+  std::deque<SegGroup*> pendingSegments;
+  void ackPendingSegment(int opType, const JObj* props, int seq);
   void zamboniSegments();
   // mergeTreeDeltaCallback (INSERT 0 / REMOVE 1 / ANNOTATE 2 with the annotate's props), fired after the
   // op is applied and before its zamboni, only for non-empty delta segment lists
@@ -201,7 +220,8 @@ class MergeTree {
   Changes leafAction(InsertCtx& ctx, Seg* s, int pos);
   Seg* splitAt(Seg* s, int pos);
   void ensureIntervalBoundary(int pos, int refSeq, int clientId);
-  void blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg);
+  void blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg, int localSeq = INT32_MIN,
+                   SegGroup** group = nullptr);
   bool continuePredicate(Block* b);
   Block* split(Block* b);
   void updateRoot(Block* splitNode);
@@ -209,6 +229,7 @@ class MergeTree {
   void blockUpdateLength(Block* b, int seq, int clientId);
   void blockUpdatePathLengths(Block* b, int seq, int clientId, bool newStructure);
   void addToLRUSet(Seg* s, int seq);
+  SegGroup* addToPendingList(Seg* s, SegGroup* g, int localSeq);  // mergeTree.ts:1324-1357
   void scourNode(Block* node, std::vector<Node*>& hold);
   void packParent(Block* parent);
   template <class Leaf, class Post>
@@ -235,6 +256,12 @@ class Doc {
   void startOrUpdateCollaboration(const std::string& id, int minSeq, int curSeq);
   void updateSeqNumbers(int min, int seq);
 
+  // a live client's local ops while collaborating (client.ts:196-247 insertSegmentLocal /
+  // removeRangeLocal / annotateRangeLocal): applied at (currentSeq, own id, UnassignedSequenceNumber)
+  // and returned as the IMergeTreeOp JSON to submit; acked by applyMsg of the sequenced message
+  std::string insertLocalOp(int pos, const JVal& segSpec);
+  std::string removeLocalOp(int start, int end);
+  std::string annotateLocalOp(int start, int end, const JObj& props);
   // local, non-collaborating edits (detached documents; used for the V1 snapshot fixtures)
   void insertTextLocal(int pos, const u16str& text, const std::optional<JObj>& props);
   void insertMarkerLocal(int pos, int refType, const std::optional<JObj>& props);

@@ -221,6 +221,20 @@ int orc_annotate_local(orc_doc* d, int start, int end, const char* props_json) {
 int orc_remove_local(orc_doc* d, int start, int end) {
   return guard(d, [&] { d->doc.removeRangeLocal(start, end); });
 }
+// a live client's local ops (client.ts:196-247): the op JSON to submit ("" when nothing was inserted)
+int orc_local_insert(orc_doc* d, int pos, const char* seg_json, char** out, size_t* len) {
+  return guard(d, [&] { *out = dupstr(d->doc.insertLocalOp(pos, json_parse(seg_json, strlen(seg_json))), len); });
+}
+int orc_local_remove(orc_doc* d, int start, int end, char** out, size_t* len) {
+  return guard(d, [&] { *out = dupstr(d->doc.removeLocalOp(start, end), len); });
+}
+int orc_local_annotate(orc_doc* d, int start, int end, const char* props_json, char** out, size_t* len) {
+  return guard(d, [&] {
+    JVal v = json_parse(props_json, strlen(props_json));
+    *out = dupstr(d->doc.annotateLocalOp(start, end, v.t == JVal::Obj ? v.obj : JObj()), len);
+  });
+}
+int orc_pending_groups(orc_doc* d) { return (int)d->doc.mt.pendingSegments.size(); }
 int orc_start_collab(orc_doc* d, const char* long_id, int min_seq, int cur_seq) {
   return guard(d, [&] { d->doc.startOrUpdateCollaboration(long_id, min_seq, cur_seq); });
 }

@@ -69,6 +69,11 @@ def lib():
         L.orc_matrix_get_cell_by_handle.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p),
                                                     ctypes.POINTER(sz)]
         u32 = ctypes.c_uint32
+        pp = ctypes.POINTER(vp)
+        L.orc_local_insert.argtypes = [vp, i, cp, pp, ctypes.POINTER(sz)]
+        L.orc_local_remove.argtypes = [vp, i, i, pp, ctypes.POINTER(sz)]
+        L.orc_local_annotate.argtypes = [vp, i, i, cp, pp, ctypes.POINTER(sz)]
+        L.orc_pending_groups.argtypes = [vp]
         L.orc_map_range.argtypes = [vp, i, i, i, cp, ctypes.c_uint, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.orc_sa2d_create.restype = vp
         L.orc_sa2d_destroy.argtypes = [vp]
@@ -190,6 +195,29 @@ class OracleDoc:
         finally:
             self._L.orc_free(p)
         return raw.decode("utf-16-le", "surrogatepass")
+
+    # --- a live client's local ops (client.ts:196-247): return the op contents to submit ------
+    def _op(self, fn, *args):
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(fn(self._h, *args, ctypes.byref(p), ctypes.byref(n)))
+        try:
+            raw = ctypes.string_at(p, n.value).decode("utf-8")
+        finally:
+            self._L.orc_free(p)
+        return json.loads(raw) if raw else None
+
+    def insert_local_op(self, pos, seg):
+        return self._op(self._L.orc_local_insert, pos, json.dumps(seg).encode())
+
+    def remove_local_op(self, start, end):
+        return self._op(self._L.orc_local_remove, start, end)
+
+    def annotate_local_op(self, start, end, props):
+        return self._op(self._L.orc_local_annotate, start, end, json.dumps(props).encode())
+
+    def pending_groups(self):
+        return self._L.orc_pending_groups(self._h)
 
     def map_range(self, start=0, end=-1, ref_seq=-1, long_client_id=None, limit=0):
         """mapRange over [start, end) in the (ref_seq, client) view: [{"pos","start","end","segment"}...]."""

@@ -179,3 +179,81 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
         m.apply_msg(msg)
         msgs.append(msg)
     return msgs
+
+
+def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False):
+    """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
+    `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
+    client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
+    receives the sequenced stream with its own lag (its own ops come back as acks).  An observer receives
+    everything.  Returns (clients, observer, sequenced messages)."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed)
+    ids = [f"c{k}" for k in range(n_clients)]
+    clients = []
+    for cid in ids:
+        o = OracleDoc(new_length_calc=new_mode, verify=verify)
+        o.insert_text_local(0, initial)
+        o.start_collab(cid)
+        clients.append(o)
+    obs = OracleDoc(new_length_calc=new_mode, verify=verify)
+    obs.insert_text_local(0, initial)
+    obs.start_collab("obs")
+    queue, log, seen = [], [], [0] * n_clients
+    words = ["a", "bc", "def", "\n", "xyz" * 3, "\U0001F600"]
+
+    def local_op(c):
+        n = c.get_length()
+        r = rng.random()
+        if n == 0 or r < 0.5:
+            t = rng.choice(words)
+            seg = {"text": t, "props": {"k": rng.randint(0, 2)}} if rng.random() < 0.2 else t
+            return c.insert_local_op(rng.randint(0, n), seg)
+        a = rng.randrange(n)
+        b = min(n, a + rng.randint(1, 6))
+        if not annotate or r < 0.8:
+            return c.remove_local_op(a, b)
+        return c.annotate_local_op(a, b, {"k": rng.choice([1, 2, None]), "w": rng.randint(0, 1)})
+
+    def sequence(m):
+        cid, ref, op = queue.pop(0)
+        msn = min([c.current_seq for c in clients] + [q[1] for q in queue] + [ref])
+        msg = {"clientId": cid, "sequenceNumber": len(log) + 1, "referenceSequenceNumber": ref,
+               "minimumSequenceNumber": msn, "type": "op", "contents": op}
+        log.append(msg)
+
+    def deliver(k, upto):
+        while seen[k] < upto:
+            clients[k].apply_msg(log[seen[k]])
+            seen[k] += 1
+
+    for _ in range(n_rounds):
+        for k in rng.sample(range(n_clients), rng.randint(1, n_clients)):
+            for _ in range(rng.randint(1, 3)):
+                ref = clients[k].current_seq
+                op = local_op(clients[k])
+                if op is not None:
+                    queue.append((ids[k], ref, op))
+        for _ in range(rng.randint(0, len(queue))):
+            sequence(None)
+        for k in range(n_clients):
+            deliver(k, seen[k] + rng.randint(0, len(log) - seen[k]))
+    while queue:
+        sequence(None)
+    for k in range(n_clients):
+        deliver(k, len(log))
+    for m in log:
+        obs.apply_msg(m)
+    return clients, obs, log
+
+
+def chars_with_props(doc):
+    """(character, properties) per visible character of a document's local view (TestClientLogger.validate
+    compares text and the properties at every position)."""
+    out = []
+    for e in doc.map_range():
+        s = e["segment"]
+        t = s.get("text", "￼")
+        out.extend((ch, json.dumps(s.get("properties"), sort_keys=True)) for ch in t)
+    return out

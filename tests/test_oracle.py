@@ -371,3 +371,22 @@ def test_matrix_summary_load_round_trip(new_mode):
     assert (b.rows.get_length(), b.cols.get_length()) == (a.rows.get_length(), a.cols.get_length())
     nr, nc = a.rows.get_length(), a.cols.get_length()
     assert [b.get_cell(r, c) for r in range(nr) for c in range(nc)] == [a.get_cell(r, c) for r in range(nr) for c in range(nc)]
+
+
+# ---------------------------------------------------------------- a live client's local ops
+@pytest.mark.parametrize("new_mode", [False, True])
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_local_op_farm_converges(seed, new_mode):
+    """Local insert / remove / annotate with pending segment groups and acks (mergeTree.ts:1283-1357,
+    mergeTreeNodes.ts:439-480, segmentPropertiesManager.ts:60-157): every client, each with its own
+    local ops and lag, converges to the observer's text and properties once all ops are acked."""
+    from helpers import chars_with_props, run_local_farm
+    # verify: every length query cross-checks the block partial lengths against the leaf sum
+    clients, obs, log = run_local_farm(seed, n_clients=4, n_rounds=80, new_mode=new_mode, verify=True)
+    want = obs.get_text()
+    wp = chars_with_props(obs)
+    assert len(log) > 100
+    for k, c in enumerate(clients):
+        assert c.pending_groups() == 0, f"client {k} still has pending ops"
+        assert c.get_text() == want, f"client {k} text diverged"
+        assert chars_with_props(c) == wp, f"client {k} properties diverged"
