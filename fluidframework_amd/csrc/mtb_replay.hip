@@ -80,11 +80,18 @@ __device__ __forceinline__ int csum8(int v) { return rl(cscan8(v), 7); }
 // SGPRs, so they cost no VGPR and branches on them stay scalar.
 __device__ __forceinline__ int U(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint32_t U(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+// Pointers kept in LDS or picked by a condition lose their address space and compile to flat_load /
+// flat_store, which also count against lgkmcnt (every LDS wait then waits for them): GP() names the
+// global address space explicitly, UP() also makes the pointer uniform.
 template <class T>
-__device__ __forceinline__ T* UP(T* p) {
+using gptr = __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr<T> GP(T* p) { return (gptr<T>)p; }
+template <class T>
+__device__ __forceinline__ gptr<T> UP(T* p) {
   const uint64_t v = (uint64_t)p;
   const uint32_t lo = U((uint32_t)v), hi = U((uint32_t)(v >> 32));
-  return (T*)(((uint64_t)hi << 32) | lo);
+  return (gptr<T>)(((uint64_t)hi << 32) | lo);
 }
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t rank_below(unsigned long long m) {
@@ -1028,14 +1035,26 @@ struct Eng {
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
   __device__ __forceinline__ Lru hget(uint32_t k) const {
-    Lru x = heap_lds ? sh->heap[k] : UP(sh->gheap)[k];
+    Lru x;
+    if (heap_lds) {
+      x = sh->heap[k];
+    } else {
+      const auto g = UP(sh->gheap) + k;
+      x.seg = g->seg;
+      x.maxSeq = g->maxSeq;
+    }
     x.seg = U(x.seg);
     x.maxSeq = U(x.maxSeq);
     return x;
   }
   __device__ __forceinline__ void hset(uint32_t k, Lru v) {
-    if (heap_lds) sh->heap[k] = v;
-    else UP(sh->gheap)[k] = v;
+    if (heap_lds) {
+      sh->heap[k] = v;
+    } else {
+      const auto g = UP(sh->gheap) + k;
+      g->seg = v.seg;
+      g->maxSeq = v.maxSeq;
+    }
   }
   __device__ __forceinline__ void heap_spill() {  // LDS -> global slice
     for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) sh->gheap[i] = sh->heap[i];
@@ -1092,14 +1111,14 @@ struct Eng {
   }
 
   // ------------------------------------------------------------------ properties
-  __device__ __forceinline__ const uint32_t* props_ptr(uint32_t h) const {
-    return (h & MTB_GPROPS) ? (UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : (aux + h);
+  __device__ __forceinline__ gptr<const uint32_t> props_ptr(uint32_t h) const {
+    return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : GP((const uint32_t*)aux + h);
   }
   // matchProperties (properties.ts:71-96) on interned property sets
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
     if (a == b) return true;
-    const uint32_t* pa = a ? props_ptr(a) : nullptr;
-    const uint32_t* pb = b ? props_ptr(b) : nullptr;
+    const gptr<const uint32_t> pa = a ? props_ptr(a) : nullptr;
+    const gptr<const uint32_t> pb = b ? props_ptr(b) : nullptr;
     const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
     if (na != nb) return false;
     for (uint32_t i = 0; i < na; i++) {
@@ -1108,7 +1127,8 @@ struct Eng {
       for (uint32_t q = 0; q < nb; q++) {
         if (pb[1 + 2 * q] == k) {
           found = true;
-          if (sh->tab.val_class[pa[2 + 2 * i]] != sh->tab.val_class[pb[2 + 2 * q]]) return false;
+          const auto vcl = UP(sh->tab.val_class);
+          if (vcl[pa[2 + 2 * i]] != vcl[pb[2 + 2 * q]]) return false;
           break;
         }
       }
@@ -1124,11 +1144,11 @@ struct Eng {
     return props_apply_slow(old, opId, rewrite);
   }
   __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite) {
-    const uint32_t* op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * opId]);
+    const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * opId]);
     const uint32_t nop = U(op[0]);
     uint32_t n = 0;
     if (old) {
-      const uint32_t* po = props_ptr(old);
+      const auto po = props_ptr(old);
       n = U(po[0]);
       if (n > 64) n = 64;
       for (uint32_t i = lane; i < n; i += 64) {
@@ -1220,14 +1240,14 @@ struct Eng {
   // SequenceDeltaEvent ranges (sequenceDelta.ts:43-56) for SharedSegmentSequence's rewriting of lagging
   // messages (sequence.ts:697-733): one entry per delta segment, in tree order: [record, segment id ->
   // local position after the op, cachedLength, property set after the op].
-  __device__ __forceinline__ uint32_t* dslice() const { return UP(sh->tab.delta) + ds->delta_base * 4; }
+  __device__ __forceinline__ gptr<uint32_t> dslice() const { return UP(sh->tab.delta) + ds->delta_base * 4; }
   __device__ __forceinline__ void delta_emit(bool sel, uint32_t sid, uint32_t len, uint32_t props) {
     const unsigned long long m = __ballot(sel);
     if (!m) return;
     const uint32_t n = (uint32_t)__popcll(m);
     if (delta_used + n > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
     if (sel) {
-      uint32_t* e = dslice() + 4 * (delta_used + rank_below(m));
+      const auto e = dslice() + 4 * (delta_used + rank_below(m));
       e[0] = cur_k;
       e[1] = sid;
       e[2] = len;
@@ -1239,7 +1259,7 @@ struct Eng {
   // getPosition (mergeTree.ts:1240) of the segments named by entries [from, delta_used): the local
   // lengths left of the segment in its block and left of each ancestor in theirs
   __device__ __forceinline__ void delta_positions(uint32_t from) {
-    uint32_t* const dl = dslice();
+    const auto dl = dslice();
     for (uint32_t i = from; i < delta_used; i++) {
       const uint32_t sid = U(dl[4 * i + 1]);
       uint32_t child = MTB_LEAF | sid;
@@ -1456,7 +1476,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
   __device__ __forceinline__ void copy_text(uint32_t dst, uint32_t src, uint32_t n) {
-    uint16_t* const txt = UP(sh->gtext);
+    const auto txt = UP(sh->gtext);
     for (uint32_t i = lane; i < n; i += 64) txt[dst + i] = txt[src + i];
   }
   __device__ __forceinline__ void stage_rec(uint32_t b) {
@@ -1511,13 +1531,13 @@ struct Eng {
     g.n = 0;
     g.k0 = g.c0 = g.k1 = g.c1 = 0;
     if (h) {
-      const uint32_t* p = props_ptr(h);  // pools carry >= 4 words of tail padding
+      const auto p = props_ptr(h);  // pools carry >= 4 words of tail padding
       g.n = p[0];
       g.k0 = p[1];
       const uint32_t v0 = p[2];
       g.k1 = p[3];
       const uint32_t v1 = p[4];
-      const uint32_t* vc = UP(sh->tab.val_class);
+      const auto vc = UP(sh->tab.val_class);
       if (g.n >= 1) g.c0 = vc[v0];
       if (g.n >= 2) g.c1 = vc[v1];
     }
@@ -1859,10 +1879,10 @@ struct Eng {
   }
   // ------------------------------------------------------------------ PermutationVector handles
   // HandleTable (matrix/src/handletable.ts) in the text arena: u32 [length, handles[0..length)].
-  __device__ __forceinline__ uint32_t* htab() const { return reinterpret_cast<uint32_t*>(UP(sh->gtext)); }
+  __device__ __forceinline__ gptr<uint32_t> htab() const { return (gptr<uint32_t>)UP(sh->gtext); }
   // free(start + i) for every lane of `m` in lane order (handletable.ts:55-58)
   __device__ __forceinline__ void handles_free_lanes(unsigned long long m, uint32_t start, int len) {
-    uint32_t* ht = htab();
+    const auto ht = htab();
     while (m) {
       const int t = first_set(m);
       m &= m - 1;
@@ -1882,7 +1902,7 @@ struct Eng {
   }
   // allocate (handletable.ts:36-41): the free-list head, growing the table when it is exhausted
   __device__ __forceinline__ uint32_t handle_alloc() {
-    uint32_t* ht = htab();
+    const auto ht = htab();
     const uint32_t L = U(ht[0]);
     const uint32_t fr = U(ht[1]);
     const uint32_t next = fr < L ? U(ht[1 + fr]) : fr + 1;  // handles[free] ?? free + 1
@@ -1991,7 +2011,7 @@ struct Eng {
   __device__ __forceinline__ void cell_event(uint32_t kind, uint32_t a, uint32_t n) {
     if (delta_used + 1 > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
     if (lane == 0) {
-      uint32_t* e = dslice() + 4 * delta_used;
+      const auto e = dslice() + 4 * delta_used;
       e[0] = cur_k;
       e[1] = kind;
       e[2] = a;
