@@ -601,7 +601,7 @@ void MergeTree::ackPendingSegment(int opType, const JObj* props, int seq) {
   if (g) {
     for (Seg* s : g->segments) {
       if (s->groups.empty() || s->groups.front() != g) fail_assert("0x043", "On ack, unexpected segmentGroup!");
-      s->groups.pop_front();
+      s->groups.erase(s->groups.begin());
       bool overlapping = false;
       switch (opType) {
         case 2:  // PropertiesManager.ackPendingProperties (segmentPropertiesManager.ts:31-58)

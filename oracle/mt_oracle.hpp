@@ -62,7 +62,7 @@ struct Seg : Node {
   // (kNoLocalSeq = undefined), the queue of pending segment groups, PropertiesManager.pendingKeyUpdateCount
   int localSeq = INT32_MIN;
   int localRemovedSeq = INT32_MIN;
-  std::deque<struct SegGroup*> groups;
+  std::vector<struct SegGroup*> groups;  // a queue (front = oldest); a vector allocates nothing when empty
   std::map<u16str, int> pendingKeys;
   Seg() : Node(true) {}
 };
