@@ -13,6 +13,8 @@ export interface BatchOptions {
   mergeTreeUseNewLengthCalculations?: boolean;
   mergeTreeSnapshotChunkSize?: number;
   device?: number;
+  /** false: SnapshotLegacy summaries with tracked catch-up messages (the reference default); default true here */
+  newMergeTreeSnapshotFormat?: boolean;
 }
 export interface ISequencedDocumentMessage {
   clientId: string | null;
@@ -35,6 +37,7 @@ export declare class MergeTreeBatch {
   dumpSegments(doc: number): string;
   checksum(doc: number): string;
   summarizeV1(doc: number, msn?: number, seq?: number): { blobs: [string, string][]; summary: unknown };
+  summarizeLegacy(doc: number, msn?: number, seq?: number, catchUpMsgs?: unknown[]): { blobs: [string, string][]; summary: unknown };
   rewind(): void;
   replayResident(): ReplayStats;
 }
@@ -68,7 +71,8 @@ export declare class Client {
   getPropertiesAtPosition(pos: number): Record<string, unknown> | undefined;
   walkSegments<T>(handler: (segment: SegmentInfo, pos: number, refSeq: number, clientId: number, start: number,
                             end: number, accum?: T) => boolean | void, start?: number, end?: number, accum?: T): void;
-  summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }): unknown;
+  summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }, handle?: unknown,
+            serializer?: unknown, catchUpMsgs?: unknown[]): unknown;
 }
 export declare const TestClient: typeof Client;
 

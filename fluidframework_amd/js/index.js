@@ -29,6 +29,7 @@ function unsupported(what) {
 }
 
 const MTB_BATCH_MATRIX = 1;
+const MTB_BATCH_CATCHUP = 2;
 
 class MergeTreeBatch {
   /**
@@ -36,11 +37,18 @@ class MergeTreeBatch {
    * @param {object} [options] IMergeTreeOptions subset: mergeTreeUseNewLengthCalculations
    *   (mergeTree.ts:413), mergeTreeSnapshotChunkSize (snapshotV1.ts:37); plus `device` (GPU index)
    */
+  /**
+   * options: mergeTreeUseNewLengthCalculations, mergeTreeSnapshotChunkSize, device, and
+   * newMergeTreeSnapshotFormat (IMergeTreeOptions, mergeTree.ts:413): without it summaries use
+   * SnapshotLegacy and the batch keeps SharedSegmentSequence's catch-up messages (sequence.ts:697-748).
+   */
   constructor(ndocs, options = {}, _rawDocs = undefined, _flags = 0) {
     const n = _rawDocs === undefined ? ndocs : _rawDocs;
     this.ndocs = n;
+    this.v1 = options.newMergeTreeSnapshotFormat !== false;
+    const catchUp = !this.v1 && !(_flags & MTB_BATCH_MATRIX) ? MTB_BATCH_CATCHUP : 0;
     this.handle = native.create(n, options.mergeTreeUseNewLengthCalculations ? 1 : 0,
-      options.mergeTreeSnapshotChunkSize || 0, options.device || 0, _flags);
+      options.mergeTreeSnapshotChunkSize || 0, options.device || 0, _flags | catchUp);
     this.dirty = false;
     this.busy = false;
     this.lastStats = undefined;
@@ -117,6 +125,14 @@ class MergeTreeBatch {
   summarizeV1(doc, msn = -1, seq = -1) {
     this.ensureFlushed();
     const r = native.summarizeV1(this.handle, doc, msn, seq);
+    return { blobs: r.blobs, summary: JSON.parse(r.summary) };
+  }
+
+  /** SnapshotLegacy blobs (header / body / catchupOps) and the ISummaryTreeWithStats object. */
+  summarizeLegacy(doc, msn = -1, seq = -1, catchUpMsgs = undefined) {
+    this.ensureFlushed();
+    const r = native.summarizeLegacy(this.handle, doc, msn, seq,
+      catchUpMsgs === undefined ? null : JSON.stringify(catchUpMsgs));
     return { blobs: r.blobs, summary: JSON.parse(r.summary) };
   }
 
@@ -252,11 +268,13 @@ class Client {
    * `runtime.deltaManager.{minimumSequenceNumber,lastSequenceNumber}` (client.ts:979) are passed
    * through when given.
    */
-  summarize(runtime) {
+  summarize(runtime, handle, serializer, catchUpMsgs) {
     const dm = runtime && runtime.deltaManager;
     const msn = dm && dm.minimumSequenceNumber !== undefined ? dm.minimumSequenceNumber : -1;
     const seq = dm && dm.lastSequenceNumber !== undefined ? dm.lastSequenceNumber : -1;
-    return this.batch.summarizeV1(this.doc, msn, seq).summary;
+    if (this.batch.v1) return this.batch.summarizeV1(this.doc, msn, seq).summary;
+    // SnapshotLegacy (client.ts:999-1003); catchUpMsgs default to the messages the batch tracked
+    return this.batch.summarizeLegacy(this.doc, msn, seq, catchUpMsgs).summary;
   }
 }
 

@@ -523,6 +523,31 @@ static napi_value js_summarize_v1(napi_env env, napi_callback_info info) {
   return blob_list_object(env, &l);
 }
 
+/* summarizeLegacy(h, doc, msn, seq, catchupJson | null) -> {blobs, summary}   client.ts:999-1003,
+ * snapshotlegacy.ts:122-259; null catch-up = the messages the batch tracked (MTB_BATCH_CATCHUP) */
+static napi_value js_summarize_legacy(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc;
+  int64_t msn, seq;
+  if (!b || !get_u32(env, argv[1], &doc) || !get_i64(env, argv[2], &msn) || !get_i64(env, argv[3], &seq)) return NULL;
+  napi_valuetype t;
+  napi_typeof(env, argv[4], &t);
+  char* cu = NULL;
+  size_t cul = 0;
+  if (t == napi_string) {
+    cu = get_utf8(env, argv[4], &cul);
+    if (!cu) return NULL;
+  }
+  mtb_blob_list l;
+  memset(&l, 0, sizeof l);
+  int rc = mtb_summarize_legacy(b, doc, msn, seq, cu, cul, &l);
+  free(cu);
+  if (rc) return throw_rc(env, b, rc);
+  return blob_list_object(env, &l);
+}
+
 /* matrixSummarize(h, matrix) -> {blobs, summary}                        matrix.ts:449-463 */
 static napi_value js_matrix_summarize(napi_env env, napi_callback_info info) {
   napi_value argv[2];
@@ -634,7 +659,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"create", js_create},           {"docInit", js_doc_init},       {"loadV1", js_load_v1},
       {"matrixInit", js_matrix_init},  {"matrixApplyMsg", js_matrix_apply_msg},
       {"matrixSummarize", js_matrix_summarize}, {"matrixGetCell", js_matrix_get_cell},
-      {"matrixLoad", js_matrix_load},
+      {"matrixLoad", js_matrix_load},  {"summarizeLegacy", js_summarize_legacy},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

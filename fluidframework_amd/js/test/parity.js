@@ -44,7 +44,7 @@ function toMsg(m) {
 function cpuChecks() {
   const names = ["create", "docInit", "applyMsg", "appendOps", "addClient", "internProps", "replay", "replayAsync",
     "getText", "getLength", "getSeq", "dumpSegments", "checksum", "summarizeV1", "rewind", "replayResident",
-    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell", "mapRange", "matrixLoad"];
+    "clientLongId", "loadV1", "matrixInit", "matrixApplyMsg", "matrixSummarize", "matrixGetCell", "mapRange", "matrixLoad", "summarizeLegacy"];
   for (const n of names) assert.strictEqual(typeof native[n], "function", n);
   const fx = loadFixtures();
   assert.strictEqual(fx.length, 30);
@@ -111,6 +111,25 @@ async function gpuChecks() {
       assert.deepStrictEqual(c.getPropertiesAtPosition(pos), seg.properties);
     }
   });
+  // SnapshotLegacy with tracked catch-up messages (newMergeTreeSnapshotFormat false), against the oracle
+  const lexp = process.env.MTB_JS_LEGACY_EXPECT;
+  if (lexp) {
+    const e = JSON.parse(fs.readFileSync(lexp, "utf8"));
+    const lb = new MergeTreeBatch(fx.length, { newMergeTreeSnapshotFormat: false });
+    fx.forEach(({ log }, i) => {
+      lb.client(i).insertTextLocal(0, log.initialText);
+      lb.client(i).startOrUpdateCollaboration("A");
+      for (const grp of log.groups) for (const m of grp.msgs) lb.client(i).applyMsg(toMsg(m));
+    });
+    lb.flush();
+    fx.forEach(({ name }, i) => {
+      const got = lb.summarizeLegacy(i);
+      assert.deepStrictEqual(got.blobs, e[i].blobs, `${name}: legacy blobs`);
+      assert.deepStrictEqual(got.summary, e[i].summary, `${name}: legacy summary`);
+      assert.deepStrictEqual(lb.client(i).summarize(), e[i].summary, `${name}: Client.summarize`);
+    });
+    console.log("js gpu legacy ok");
+  }
   console.log(`js gpu parity ok: ${checked} text checkpoints over ${fx.length} reference logs`);
   // Client.load: every document's summary loads into a fresh batch and summarizes back to the same bytes
   const loaded = new MergeTreeBatch(fx.length);

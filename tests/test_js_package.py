@@ -53,11 +53,30 @@ def test_js_package_replays_reference_logs_on_gpu(tmp_path):
     exp["cells"] = [[r, c, o.get_cell(r, c)] for r in range(nr) for c in range(nc)]
     path = tmp_path / "matrix_expect.json"
     path.write_text(json.dumps(exp))
+    # SnapshotLegacy + tracked catch-up messages of the 30 reference logs (oracle, sequence.ts:697-748)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import msg_from_compact, replay_fixtures
+    from pyoracle import OracleDoc
+    legacy = []
+    for _, d in replay_fixtures():
+        o = OracleDoc()
+        o.insert_text_local(0, d["initialText"])
+        o.start_collab("A")
+        o.enable_catch_up()
+        for g in d["groups"]:
+            for m in g["msgs"]:
+                o.apply_msg(msg_from_compact(m))
+        legacy.append(o.summarize_legacy())
+    lpath = tmp_path / "legacy_expect.json"
+    lpath.write_text(json.dumps(legacy))
     os.environ["MTB_JS_MATRIX_EXPECT"] = str(path)
+    os.environ["MTB_JS_LEGACY_EXPECT"] = str(lpath)
     try:
         out = _node()
     finally:
         del os.environ["MTB_JS_MATRIX_EXPECT"]
+        del os.environ["MTB_JS_LEGACY_EXPECT"]
+    assert "js gpu legacy ok" in out
     assert "js gpu parity ok" in out
     assert "js gpu load ok" in out
     assert "js gpu matrix ok" in out
