@@ -99,6 +99,7 @@ class MergeTreeBatch:
         raw = initial_text.encode("utf-16-le", "surrogatepass")
         buf = ctypes.create_string_buffer(raw, max(2, len(raw)))
         self._chk(self._L.mtb_doc_init(self._h, doc, buf, len(raw) // 2, observer_long_id.encode(), min_seq, cur_seq))
+        self._dirty = True  # reads flush first: the document reaches the device with the next replay
 
     @staticmethod
     def _blob_array(blobs):
@@ -384,6 +385,7 @@ class MatrixBatch(MergeTreeBatch):
 
     def init_matrix(self, m, observer_long_id, min_seq=0, cur_seq=0):
         self._chk(self._L.mtb_matrix_init(self._h, m, observer_long_id.encode(), min_seq, cur_seq))
+        self._dirty = True
 
     def load_matrix(self, m, blobs, observer_long_id="snapshot"):
         """SharedMatrix.loadCore (matrix.ts:611) from [(path, content), ...] as matrix_summarize gives them."""

@@ -167,6 +167,7 @@ struct Tables {
 #define MTB_CELL_SET 1     // matrix cell event: this vector's handle for a setCell record
 #define MTB_CELL_CLEAR 2   // matrix cell event: handles [start, start + count) recycled by zamboni
 #define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
+#define DERR_HOST 14       // host-side post-processing of the document's replay failed (HostDoc::hostErr)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

@@ -299,6 +299,11 @@ struct HostDoc {
   uint32_t min0 = 0, cur0 = 0;
   std::vector<mtb_op> pending;
   std::vector<uint16_t> payload;  // payload of pending ops
+  // the records (and payload) of the last replay, consumed before its host post-processing runs so
+  // that a post-processing failure can never make a later replay apply them twice
+  std::vector<mtb_op> applied;
+  std::vector<uint16_t> appliedPayload;
+  std::string hostErr;            // message of a sticky host-side failure (DERR_HOST)
   int64_t lastSeq = 0;            // last appended message seq (host-side 0x038 check)
   uint64_t totalOps = 0;          // all records ever appended (capacity sizing)
   uint64_t totalPayload = 0;
@@ -414,7 +419,7 @@ struct mtb_batch {
   ~mtb_batch() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
-    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release();
+    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release();
     dMvSrc.release(); dMvDst.release(); dMvLen.release(); dStageW.release(); dStageH.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1126,9 +1131,10 @@ void upload_tables(mtb_batch* b) {
 }
 
 void download_doc(mtb_batch* b, uint32_t i) {
+  if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
   HostDoc& d = b->docs[i];
   if (d.cached) return;
-  if (!d.onDevice) raise(MTB_E_ARG, "document has not been replayed");
+  if (!d.onDevice || !b->devInit || i >= b->hst.size()) raise(MTB_E_ARG, "document has not been replayed");
   const DocState& s = b->hst[i];
   std::vector<FBlk> fb(s.blk_used);
   std::vector<uint32_t> segp(s.seg_used);
@@ -1184,6 +1190,7 @@ std::string derr_text(int e) {
     case DERR_ASSERT_SEQ: return "0x038 Incoming op sequence# < local collabWindow's currentSequence#";
     case DERR_ASSERT_MSN: return "0x04e/0x04f/0x039 minimum sequence number out of order";
     case DERR_DEPTH: return "tree depth limit exceeded";
+    case DERR_HOST: return "host post-processing of the replay failed";
     default: return "device error " + std::to_string(e);
   }
 }
@@ -1265,6 +1272,16 @@ void replay(mtb_batch* b, mtb_stats* out) {
   // the applyMsg that failed)
   std::vector<uint8_t> failedBefore(b->ndocs);
   for (uint32_t i = 0; i < b->ndocs && i < b->hst.size(); i++) failedBefore[i] = b->hst[i].err != 0;
+  // the matrix kernel's two waves meet at one barrier per SETCELL record: both vectors of a matrix must
+  // carry the same number of them (checked before anything runs)
+  if (b->matrix)
+    for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
+      size_t n[2] = {0, 0};
+      for (int v = 0; v < 2; v++)
+        for (const mtb_op& o : b->docs[i + v].pending) n[v] += o.type == MTB_OP_SETCELL;
+      if (n[0] != n[1])
+        raise(MTB_E_ARG, "matrix " + std::to_string(i / 2) + ": rows and cols vectors hold different numbers of SETCELL records");
+    }
   if (!b->devInit) device_init(b);
   pc.mark("device_init");
   upload_tables(b);
@@ -1394,25 +1411,48 @@ void replay(mtb_batch* b, mtb_stats* out) {
       const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
       if (e) b->hst[i].err = b->hst[i + 1].err = e;
     }
+  // the records are consumed now: whatever the host post-processing below does, they never run again
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    d.applied.clear();
+    d.appliedPayload.clear();
+    d.applied.swap(d.pending);
+    d.appliedPayload.swap(d.payload);
+    d.cached = false;
+  }
+  // host post-processing (cell events, catch-up rewriting): a failure is sticky for its document
+  auto post = [&](uint32_t i, auto&& f) {
+    try {
+      f();
+    } catch (const MtbError& e) {
+      b->hst[i].err = DERR_HOST;
+      b->docs[i].hostErr = e.msg;
+    } catch (const std::exception& e) {
+      b->hst[i].err = DERR_HOST;
+      b->docs[i].hostErr = e.what();
+    }
+  };
   if (b->matrix)
     for (uint32_t i = 0; i + 1 < b->ndocs; i += 2)
-      if (!b->hst[i].err) apply_cell_events(b, i / 2);
+      if (!b->hst[i].err) {
+        post(i, [&] { apply_cell_events(b, i / 2); });
+        if (b->hst[i].err) {
+          b->hst[i + 1].err = b->hst[i].err;
+          b->docs[i + 1].hostErr = b->docs[i].hostErr;
+        }
+      }
   for (uint32_t i = 0; i < b->ndocs; i++) {
     if (b->hst[i].err) continue;
     bool open = false;
     for (auto& m : b->docs[i].catchup) open |= !m.resolved;
-    if (open) resolve_catch_up(b, i);
+    if (open) post(i, [&] { resolve_catch_up(b, i); });
   }
   mtb_stats st{};
   st.kernel_ms = ms;
   int firstErr = 0;
   uint32_t errDoc = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
-    HostDoc& d = b->docs[i];
     DocState& s = b->hst[i];
-    d.pending.clear();
-    d.payload.clear();
-    d.cached = false;
     st.docs++;
     st.ops_applied += s.ops_applied;
     st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
@@ -1444,6 +1484,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
             (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mxo);
   }
   if (out) *out = st;
+  if (firstErr == DERR_HOST) raise(MTB_E_ARG, "document " + std::to_string(errDoc) + ": " + b->docs[errDoc].hostErr);
   if (firstErr)
     raise(derr_code(firstErr), "document " + std::to_string(errDoc) + " op " + std::to_string(b->hst[errDoc].err_op) + ": " +
                                    derr_text(firstErr));
@@ -1948,7 +1989,7 @@ void apply_cell_events(mtb_batch* b, uint32_t m) {
   std::vector<uint32_t> setVal;
   for (int v = 0; v < 2; v++) {
     const DocState& s = b->hst[2 * m + v];
-    const std::vector<mtb_op>& recs = b->docs[2 * m + v].pending;
+    const std::vector<mtb_op>& recs = b->docs[2 * m + v].applied;
     std::vector<uint32_t> ent(4 * (size_t)s.delta_used);
     if (!ent.empty())
       HIPCHK(hipMemcpy(ent.data(), b->dDelta.p + 4 * s.delta_base, ent.size() * 4, hipMemcpyDeviceToHost));
@@ -1999,8 +2040,8 @@ void resolve_catch_up(mtb_batch* b, uint32_t i) {
   for (auto& m : d.catchup) {
     if (m.resolved) continue;
     std::vector<std::string> ops;
-    for (uint32_t k = m.first; k < m.first + m.count && k < d.pending.size(); k++) {
-      const mtb_op& r = d.pending[k];
+    for (uint32_t k = m.first; k < m.first + m.count && k < d.applied.size(); k++) {
+      const mtb_op& r = d.applied[k];
       auto it = byRec.find(k);
       if (it == byRec.end()) continue;  // no delta segments: no event
       struct Ev { int pos1, pos2; std::string props; hj::Value pv; bool hasPos2; std::string json; };
@@ -2018,7 +2059,7 @@ void resolve_catch_up(mtb_batch* b, uint32_t i) {
             if (r.props) { seg += ",\"props\":"; props_json(b, seg, props_of(b, d, ph)); }
             seg += "}";
           } else {
-            U16 text(reinterpret_cast<const char16_t*>(d.payload.data() + r.payload), r.pos2);
+            U16 text(reinterpret_cast<const char16_t*>(d.appliedPayload.data() + r.payload), r.pos2);
             if (r.props) {
               seg = "{\"text\":";
               hj::quote(seg, text);
@@ -2462,9 +2503,13 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    if (n && !ops) raise(MTB_E_ARG, "null records");
+    if (payload_len && !payload) raise(MTB_E_ARG, "null payload");
+    // validate every record first, then commit records, payload and totals together (all or nothing)
     const uint32_t base = (uint32_t)d.payload.size();
-    d.payload.insert(d.payload.end(), payload, payload + payload_len);
-    d.totalPayload += payload_len;
+    std::vector<mtb_op> staged;
+    staged.reserve(n);
+    uint64_t setcells = 0;
     for (uint32_t k = 0; k < n; k++) {
       mtb_op o = ops[k];
       if (o.type > MTB_OP_ACK && !(b->matrix && o.type == MTB_OP_SETCELL)) raise(MTB_E_ARG, "bad record type");
@@ -2472,7 +2517,8 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
       if (!d.perm && (o.flags & MTB_F_PERMSEG)) raise(MTB_E_ARG, "MTB_F_PERMSEG outside a matrix batch");
       if (o.type == MTB_OP_SETCELL) {
         if (o.flags & MTB_F_LAST) raise(MTB_E_ARG, "SETCELL records never carry MTB_F_LAST");
-        d.totalSetcell++;
+        if (o.props >= b->cellVals.size()) raise(MTB_E_ARG, "SETCELL value id out of range (mtb_matrix_intern_value)");
+        setcells++;
       }
       if (o.type == MTB_OP_INSERT && !(o.flags & (MTB_F_MARKER | MTB_F_PERMSEG))) {
         if ((uint64_t)o.payload + o.pos2 > payload_len) raise(MTB_E_ARG, "record payload out of range");
@@ -2482,8 +2528,12 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
         raise(MTB_E_ARG, "record props id out of range");
       if (o.client >= d.longIds.size() && o.type != MTB_OP_NOOP)
         raise(MTB_E_ARG, "record client id not registered (mtb_add_client)");
-      d.pending.push_back(o);
+      staged.push_back(o);
     }
+    d.payload.insert(d.payload.end(), payload, payload + payload_len);
+    d.totalPayload += payload_len;
+    d.pending.insert(d.pending.end(), staged.begin(), staged.end());
+    d.totalSetcell += setcells;
     d.totalOps += n;
   });
 }
@@ -2545,8 +2595,8 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
 
 int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out) {
   return guarded(b, [&] {
-    download_doc(b, doc);
     HostDoc& d = docref(b, doc);
+    download_doc(b, doc);
     std::vector<FlatSeg> fl;
     flatten(d, b->hst[doc].root, fl, false);
     size_t n = 0;
@@ -2770,6 +2820,9 @@ int mtb_matrix_get_cell(mtb_batch* b, uint32_t matrix, uint32_t row, uint32_t co
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
+    if (!b->docs[2 * matrix].inited) raise(MTB_E_ARG, "mtb_matrix_init must be called first");
+    if (!b->devInit || !b->docs[2 * matrix].onDevice || !b->docs[2 * matrix + 1].onDevice)
+      raise(MTB_E_ARG, "matrix has not been replayed");
     if (b->hst[2 * matrix].err) raise(derr_code(b->hst[2 * matrix].err), derr_text(b->hst[2 * matrix].err));
     std::string v;
     const uint32_t rh = vector_handle_at(b, 2 * matrix, row);
@@ -2858,6 +2911,7 @@ int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (!out) raise(MTB_E_ARG, "null output");
+    if (!d.onDevice || !b->devInit) raise(MTB_E_ARG, "document has not been replayed");
     if (b->hst[doc].err) raise(derr_code(b->hst[doc].err), derr_text(b->hst[doc].err));
     download_doc(b, doc);
     const DocState& s = b->hst[doc];

@@ -98,6 +98,7 @@ class MergeTreeBatch {
   }
 
   internProps(props) {
+    this.checkIdle();
     return native.internProps(this.handle, typeof props === "string" ? props : JSON.stringify(props));
   }
 
@@ -108,7 +109,10 @@ class MergeTreeBatch {
     this.dirty = true;
   }
 
-  addClient(doc, longId) { native.addClient(this.handle, doc, longId); }
+  addClient(doc, longId) {
+    this.checkIdle();
+    native.addClient(this.handle, doc, longId);
+  }
 
   /** Canonical segment dump (parity read-out; one JSON line per segment). */
   dumpSegments(doc) {
@@ -137,9 +141,15 @@ class MergeTreeBatch {
   }
 
   /** Benchmark utilities: restore every document to its pre-replay state / replay resident records. */
-  rewind() { native.rewind(this.handle); }
+  rewind() {
+    this.checkIdle();
+    native.rewind(this.handle);
+  }
 
-  replayResident() { return native.replayResident(this.handle); }
+  replayResident() {
+    this.checkIdle();
+    return native.replayResident(this.handle);
+  }
 }
 
 /** One document slot with the reference Client / TestClient call shapes (observer path). */

@@ -244,3 +244,60 @@ def test_catch_up_tracking_flags_lagging_records():
     ops, n, _ = B.export_pending(0)
     flags = [struct.unpack_from("<BB", ops, 32 * k)[1] for k in range(n)]
     assert not flags[0] & 0x80 and flags[1] & 0x80
+
+
+def test_reads_of_bad_or_unreplayed_documents_fail_cleanly():
+    """Out-of-range documents and documents never replayed return MTB_E_ARG (no out-of-bounds reads)."""
+    import ctypes
+    from fluidframework_amd import MatrixBatch, MergeTreeBatch, _lib
+    L = _lib.lib()
+    B = MergeTreeBatch(2)
+    B.init_doc(0, "abc", "obs")
+    n = ctypes.c_size_t()
+    ln = ctypes.c_uint32()
+    for doc in (2, 10 ** 6):
+        assert L.mtb_get_text(B._h, doc, None, 0, ctypes.byref(n)) == -1
+        assert L.mtb_get_length(B._h, doc, ctypes.byref(ln)) == -1
+    assert L.mtb_get_text(B._h, 0, None, 0, ctypes.byref(n)) == -1  # not replayed yet
+    out, outn = ctypes.c_void_p(), ctypes.c_size_t()
+    assert L.mtb_map_range(B._h, 0, 0, -1, -1, None, 0, ctypes.byref(out), ctypes.byref(outn)) == -1
+    assert B._dirty  # a read through the Python shim flushes first
+    M = MatrixBatch(1)
+    M.init_matrix(0, "obs")
+    buf = ctypes.create_string_buffer(64)
+    assert L.mtb_matrix_get_cell(M._h, 0, 0, 0, buf, 64, ctypes.byref(n)) == -1
+    assert b"not been replayed" in L.mtb_last_error(M._h)
+
+
+def test_append_ops_is_all_or_nothing():
+    """A rejected mtb_append_ops leaves no record, payload or capacity count behind."""
+    import struct
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    B = MergeTreeBatch(1)
+    B.init_doc(0, "", "obs")
+    B.add_client(0, "c1")
+    good = struct.pack("<BBHIIIIIII", 0, 1, 1, 1, 0, 0, 0, 2, 0, 0)
+    bad = struct.pack("<BBHIIIIIII", 0, 1, 9, 2, 0, 0, 0, 1, 2, 0)  # client 9 not registered
+    with pytest.raises(MergeTreeError, match="not registered"):
+        B.append_records(0, good + bad, 2, "xyz".encode("utf-16-le"))
+    ops, n, payload = B.export_pending(0)
+    assert n == 0 and payload == b""
+    B.append_records(0, good, 1, "xy".encode("utf-16-le"))
+    ops, n, payload = B.export_pending(0)
+    assert n == 1 and payload == "xy".encode("utf-16-le")
+
+
+def test_matrix_setcell_records_are_validated():
+    import struct
+    from fluidframework_amd import MatrixBatch, MergeTreeError
+    M = MatrixBatch(1)
+    M.init_matrix(0, "obs")
+    for d in (0, 1):
+        M.add_client(d, "c1")
+    setcell = struct.pack("<BBHIIIIIII", 6, 0, 1, 1, 0, 0, 0, 0, 0, 7)  # value id 7 never interned
+    with pytest.raises(MergeTreeError, match="value id"):
+        M.append_records(0, setcell, 1, b"")
+    ok = struct.pack("<BBHIIIIIII", 6, 0, 1, 1, 0, 0, 0, 0, 0, 0)
+    M.append_records(0, ok, 1, b"")  # rows vector only: the cols vector lacks its SETCELL record
+    with pytest.raises(MergeTreeError, match="different numbers of SETCELL"):
+        M.replay()
