@@ -23,7 +23,7 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
-           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range"]
+           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests"]
 
 
 class MtbOptions(ctypes.Structure):
@@ -91,6 +91,7 @@ def lib():
     L.mtb_get_seq.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)]
     L.mtb_dump_segments.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.mtb_doc_checksum.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_uint64)]
+    L.mtb_doc_digests.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_uint64)]
     L.mtb_summarize_v1.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MtbBlobList)]
     L.mtb_summarize_legacy.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, sz,
                                        ctypes.POINTER(MtbBlobList)]

@@ -228,6 +228,15 @@ class MergeTreeBatch:
         self._chk(self._L.mtb_doc_checksum(self._h, doc, ctypes.byref(out)))
         return out.value
 
+    def digests(self, first=0, n=None):
+        """State digests v1 of documents [first, first + n) computed on the GPU by the last replay
+        (DESIGN.md "State digest"; the oracle's Doc::digest computes the same values)."""
+        self._ensure_flushed()
+        n = self.ndocs - first if n is None else n
+        arr = (ctypes.c_uint64 * max(1, n))()
+        self._chk(self._L.mtb_doc_digests(self._h, first, n, arr))
+        return list(arr[:n])
+
     def map_range(self, doc, start=0, end=-1, ref_seq=-1, long_client_id=None, limit=0):
         """mapRange / nodeMap (mergeTree.ts:2456, 2531) over [start, end) in the (ref_seq, client) view
         (defaults: currentSeq, the observer = the local view): [{"pos", "start", "end", "segment"}...]."""

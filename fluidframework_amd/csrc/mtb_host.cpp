@@ -44,10 +44,22 @@ hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, c
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables);
+hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState* docs, const FBlk* blks,
+                             const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint64_t* khash,
+                             const uint64_t* vhash, uint64_t* out);
 
 namespace {
 
 using hj::U16;
+
+uint64_t fnv_bytes(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
 
 struct MtbError {
   int code;
@@ -397,6 +409,9 @@ struct mtb_batch {
   DevBuf<uint32_t> dAux, dFree;
   DevBuf<uint32_t> dPool, dPidx, dValClass, dKeyRank;
   DevBuf<uint8_t> dValFalsy;
+  DevBuf<uint64_t> dKHash, dVHash;  // state digest: FNV-1a of each key's UTF-8 / each value's JSON text
+  DevBuf<uint64_t> dDigest;         // per document {digest, segments, observer length} of the last replay
+  std::vector<uint64_t> digests;
   std::vector<DocState> hst;
   double lastKernelMs = 0;
   // rewind support: state right after the first upload of every document's records
@@ -419,7 +434,7 @@ struct mtb_batch {
   ~mtb_batch() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
-    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release();
+    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release(); dKHash.release(); dVHash.release(); dDigest.release();
     dMvSrc.release(); dMvDst.release(); dMvLen.release(); dStageW.release(); dStageH.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1127,7 +1142,33 @@ void upload_tables(mtb_batch* b) {
   up(b->dValClass, in.valClass);
   up(b->dValFalsy, in.valFalsy);
   up(b->dKeyRank, in.keyRank);
+  // state digest hashes of every interned key and value (DESIGN.md "State digest")
+  std::vector<uint64_t> kh(in.keys.size()), vh(in.valJson.size());
+  for (size_t k = 0; k < kh.size(); k++) kh[k] = fnv_bytes(hj::to_utf8(in.keys[k].data(), in.keys[k].size()));
+  for (size_t v = 0; v < vh.size(); v++) vh[v] = fnv_bytes(in.valJson[v]);
+  up(b->dKHash, kh);
+  up(b->dVHash, vh);
   in.dirty = false;
+}
+
+// State digest v1 of every document (mtb_digest_kernel) after a replay: fills the stats' segments_final,
+// text_units_final and checksum (sum of the per-document digests mod 2^64) and keeps the per-document
+// values for mtb_doc_digests.
+void run_digest(mtb_batch* b, mtb_stats& st) {
+  b->dDigest.ensure(3ull * b->ndocs);
+  HIPCHK(mtb_launch_digest(b->stream, b->ndocs, b->dDocs.p, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p, b->dKHash.p,
+                           b->dVHash.p, b->dDigest.p));
+  b->digests.resize(3ull * b->ndocs);
+  HIPCHK(hipMemcpyAsync(b->digests.data(), b->dDigest.p, b->digests.size() * 8, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  st.segments_final = st.text_units_final = st.checksum = 0;
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    st.checksum += b->digests[3ull * i];
+    st.segments_final += b->digests[3ull * i + 1];
+    st.text_units_final += b->digests[3ull * i + 2];
+  }
+  // + 24 B per final segment record + 2 B per final text unit (the state write-back term)
+  st.bytes_alg += 24ull * st.segments_final + 2ull * st.text_units_final;
 }
 
 void download_doc(mtb_batch* b, uint32_t i) {
@@ -1461,6 +1502,7 @@ void replay(mtb_batch* b, mtb_stats* out) {
       if (!firstErr && !failedBefore[i]) { firstErr = s.err; errDoc = i; }
     }
   }
+  run_digest(b, st);
   if (getenv("MTB_PROFILE_OUT")) {  // MTB_PROFILE builds: per-phase device cycles and events per op, summed over documents
     double p[7] = {0, 0, 0, 0, 0, 0, 0}, c[5] = {0, 0, 0, 0, 0};
     for (uint32_t i = 0; i < b->ndocs; i++) {
@@ -2589,6 +2631,7 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
       st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
       if (s.err) st.errors++;
     }
+    run_digest(b, st);
     if (out) *out = st;
   });
 }
@@ -2638,6 +2681,15 @@ int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len) {
     std::string s = dump_doc(b, doc);
     *out = dup(s);
     if (out_len) *out_len = s.size();
+  });
+}
+
+int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out) {
+  return guarded(b, [&] {
+    if (!out && n) raise(MTB_E_ARG, "null output");
+    if ((uint64_t)first + n > b->ndocs) raise(MTB_E_ARG, "document range out of bounds");
+    if (b->digests.size() != 3ull * b->ndocs) raise(MTB_E_ARG, "no replay yet");
+    for (uint32_t k = 0; k < n; k++) out[k] = b->digests[3ull * (first + k)];
   });
 }
 

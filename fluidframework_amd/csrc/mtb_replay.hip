@@ -2419,6 +2419,189 @@ hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, c
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------- state digest v1
+// One wave per document folds the replayed state -- every segment in tree order with its tree path,
+// text (or marker / handle span), seq, client, removal info and properties -- into 64 bits
+// (DESIGN.md "State digest"; the checker restates the same definition over its own tree, Doc::digest).
+// Per document out[3d..3d+2] = {digest, segments in the tree, observer length}; a failed document or a
+// tree the walk cannot trust (depth > 16, a block id out of range, a text span outside the arena)
+// reports digest 0.
+namespace mtbk {
+__device__ __forceinline__ uint64_t dg_fmix(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+__device__ __forceinline__ uint64_t dg_mix(uint64_t h, uint64_t x) {
+  return dg_fmix(h ^ (x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2)));
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+}  // namespace mtbk
+
+#define MTB_DG_DEPTH 16
+extern "C" __global__ void __launch_bounds__(64)
+    mtb_digest_kernel(const DocState* __restrict__ docs, uint32_t ndocs, const FBlk* blks, const uint16_t* text,
+                      const uint32_t* aux, const uint32_t* pool, const uint64_t* khash, const uint64_t* vhash,
+                      uint64_t* out) {
+  __shared__ uint32_t ids[MTB_DG_DEPTH][MTB_MAXCH];
+  __shared__ int32_t cnt[MTB_DG_DEPTH], nxt[MTB_DG_DEPTH];
+  __shared__ uint32_t rec[64];
+  const uint32_t doc = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (doc >= ndocs) return;
+  const DocState& s = docs[doc];
+  const int32_t derr = s.err;
+  if (derr) {
+    if (lane < 3) out[3 * doc + lane] = 0;
+    return;
+  }
+  const FBlk* B = blks + s.blk_base;
+  const uint16_t* T = text + s.text_base;
+  const uint32_t* A = aux + s.aux_base;
+  const uint32_t blk_used = s.blk_used, text_cap = s.text_cap, aux_used = s.aux_used;
+  const bool perm = (s.flags & DSF_PERM) != 0;
+  const uint32_t root = s.root;
+  const int sg = lane >> 3, q = lane & 7;  // leaf blocks: lane (segment slot, part)
+  uint64_t acc = 0;
+  uint64_t nsegs = 0;
+  bool bad = root >= blk_used;
+  int d = 0;
+  uint32_t entered = 1;  // a block is entered once per walk: more entries than blocks is a corrupt tree
+  // fetch block b as depth d of the walk: children ids + count, the whole record into rec[]
+  auto enter = [&](uint32_t b, int dd) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B + b);
+    const uint32_t v = w[lane];
+    const uint32_t c = w[FB_HDR];
+    rec[lane] = v;
+    if (lane < MTB_MAXCH) ids[dd][lane] = v;
+    if (lane == 0) {
+      cnt[dd] = (int32_t)(c > MTB_MAXCH ? MTB_MAXCH : c);
+      nxt[dd] = 0;
+    }
+    __syncthreads();
+  };
+  if (!bad) enter(root, 0);
+  while (!bad) {
+    const int c = cnt[d], k = nxt[d];
+    if (k >= c) {
+      if (d == 0) break;
+      d--;
+      continue;
+    }
+    const uint32_t child = ids[d][k];
+    if (child & MTB_LEAF) {
+      // a leaf-level block (the one entered last): all its segments at once, 8 lanes per segment
+      uint64_t P = 0;
+      for (int l = 0; l < d; l++) P += (uint64_t)(nxt[l]) << (4 * l);  // nxt[l] = slot taken + 1
+      uint64_t t = 0;
+      bool kbad = false;
+      uint32_t len = 0, seq = 0, rseq = 0, cli = 0, rcx = 0, props = 0, txt = 0, id = MTB_NONE;
+      if (sg < c) {
+        id = rec[F_ID * 8 + sg];
+        len = rec[F_LEN * 8 + sg];
+        seq = rec[F_SEQ * 8 + sg];
+        rseq = rec[F_RSEQ * 8 + sg];
+        cli = rec[F_CLI * 8 + sg];
+        rcx = rec[F_RCX * 8 + sg];
+        props = rec[F_PROPS * 8 + sg];
+        txt = rec[F_TEXT * 8 + sg];
+        if (!(id & MTB_LEAF)) kbad = true;
+        if (!perm && !(txt & MTB_MARKER)) {
+          if ((uint64_t)txt + len > text_cap) kbad = true;
+          else
+            for (uint32_t j = (uint32_t)q; j < len; j += 8)
+              t += dg_fmix((((uint64_t)j << 16) | T[txt + j]) + 0x632BE59BD9B4E019ull);
+        }
+      }
+      t += shfl_xor64(t, 1);
+      t += shfl_xor64(t, 2);
+      t += shfl_xor64(t, 4);
+      if (sg < c && q == 0) {
+        uint64_t K = 0;
+        if (perm) {
+          K = 2;
+          t = dg_fmix(((uint64_t)txt << 32) | len);
+        } else if (txt & MTB_MARKER) {
+          K = 1;
+          t = dg_fmix(0x4D00000000ull | (txt & ~MTB_MARKER));
+        }
+        uint64_t Rc = 0;
+        if ((int32_t)rseq >= 0) {
+          Rc = dg_mix(1, (uint32_t)(int32_t)(int16_t)(cli >> 16));
+          if (rcx) {
+            const uint32_t n = rcx < aux_used ? A[rcx] : 0;
+            for (uint32_t i = 0; i < n && rcx + 1 + i < aux_used; i++) Rc += dg_mix(i + 2, A[rcx + 1 + i]);
+          }
+        }
+        uint64_t Ph = 0;
+        if (props) {
+          const uint32_t* ps = (props & MTB_GPROPS) ? pool + (props & ~MTB_GPROPS) : A + props;
+          const uint32_t n = ps[0];
+          for (uint32_t i = 0; i < n; i++) Ph += dg_mix(dg_mix(i + 1, khash[ps[1 + 2 * i]]), vhash[ps[2 + 2 * i]]);
+        }
+        uint64_t h = 0;
+        h = dg_mix(h, P + ((uint64_t)(sg + 1) << (4 * d)));
+        h = dg_mix(h, K);
+        h = dg_mix(h, t);
+        h = dg_mix(h, len);
+        h = dg_mix(h, seq);
+        h = dg_mix(h, (uint32_t)(int32_t)(int16_t)(cli & 0xFFFF));
+        h = dg_mix(h, rseq);
+        h = dg_mix(h, Rc);
+        h = dg_mix(h, Ph);
+        acc += dg_fmix(h + (nsegs + (uint64_t)sg + 1) * 0xD6E8FEB86659FD93ull);
+      }
+      if (__ballot(kbad)) bad = true;
+      nsegs += (uint64_t)c;
+      __syncthreads();
+      if (lane == 0) nxt[d] = c;
+      __syncthreads();
+      continue;
+    }
+    if (lane == 0) nxt[d] = k + 1;
+    __syncthreads();
+    if (d + 1 >= MTB_DG_DEPTH || child >= blk_used || ++entered > blk_used) {
+      bad = true;
+      break;
+    }
+    d++;
+    enter(child, d);
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) acc += shfl_xor64(acc, m);
+  if (lane == 0) {
+    uint64_t D = 0;
+    uint32_t len = 0;
+    if (!bad) {
+      len = (uint32_t)B[root].len;
+      D = 0x4D544231ull;
+      D = dg_mix(D, (uint32_t)s.min_seq);
+      D = dg_mix(D, (uint32_t)s.cur_seq);
+      D = dg_mix(D, len);
+      D = dg_mix(D, nsegs);
+      D = dg_mix(D, acc);
+    }
+    out[3 * doc] = D;
+    out[3 * doc + 1] = bad ? 0 : nsegs;
+    out[3 * doc + 2] = len;
+  }
+}
+
+hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState* docs, const FBlk* blks,
+                             const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint64_t* khash,
+                             const uint64_t* vhash, uint64_t* out) {
+  hipLaunchKernelGGL(mtb_digest_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, blks, text, aux, pool, khash,
+                     vhash, out);
+  return hipGetLastError();
+}
+
 // Rewind every document to its post-init state (benchmark / re-replay utility): restores the
 // DocState header, the root block and the initial segment's parent; ops and payload stay resident.
 extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, uint32_t* segp,

@@ -23,14 +23,25 @@ def shard_docs(total_docs: int, world: int, rank: int):
     return [g for g in range(total_docs) if fnv32(g) % world == rank]
 
 
-def reduce_counters(dist, device, elapsed: float, counters):
-    """MAX-reduce `elapsed` and SUM-reduce the integer `counters` over the process group.
+MASK64 = (1 << 64) - 1
 
+
+def _as_i64(x: int) -> int:
+    v = int(x) & MASK64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def reduce_counters(dist, device, elapsed: float, counters):
+    """MAX-reduce `elapsed` and SUM-reduce the integer `counters` (mod 2^64) over the process group.
+
+    The counters are unsigned 64-bit values: ops applied, errors, bytes and the per-rank checksum (the sum
+    of its documents' state digests mod 2^64), carried in int64 two's complement so that
+    one all-reduce (RCCL on the GPU box, gloo in the CPU tests) sums them with wrap-around.
     Returns (elapsed_max, [summed counters]).  `dist` is torch.distributed (already initialised).
     """
     import torch
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    c = torch.tensor([int(x) for x in counters], dtype=torch.int64, device=device)
+    c = torch.tensor([_as_i64(x) for x in counters], dtype=torch.int64, device=device)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
-    return float(t.item()), [int(x) for x in c.tolist()]
+    return float(t.item()), [int(x) & MASK64 for x in c.tolist()]

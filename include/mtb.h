@@ -79,10 +79,11 @@ typedef struct mtb_options {
 typedef struct mtb_stats {
   uint64_t ops_applied;     /* delta ops applied (each GROUP member counts once) */
   uint64_t docs;            /* documents replayed */
-  uint64_t segments_final;  /* live segments after replay */
-  uint64_t text_units_final;/* visible UTF-16 units after replay */
+  uint64_t segments_final;  /* segments in the documents' trees after replay (tombstones included) */
+  uint64_t text_units_final;/* observer-view length (Client.getLength) summed over documents */
   uint64_t bytes_alg;       /* algorithmic bytes */
-  uint64_t checksum;        /* xor-fold of per-document state checksums */
+  uint64_t checksum;        /* sum mod 2^64 of the per-document state digests (mtb_doc_digests); a
+                               SUM so that shards reduce with one all-reduce */
   uint64_t errors;          /* documents whose replay stopped on an error */
   double kernel_ms;         /* device time of the replay kernel(s) (HIP events) */
 } mtb_stats;
@@ -186,6 +187,9 @@ int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq
 int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len);
 /* Per-document state checksum (FNV-1a 64 over the canonical dump). */
 int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out);
+/* State digests v1 (DESIGN.md "State digest": the canonical dump's content folded into 64 bits on the
+ * GPU by every replay) of documents [first, first + n), from the last replay; 0 for a failed document. */
+int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out);
 /* MergeTree.mapRange / nodeMap (mergeTree.ts:2456-2474, 2531-2582) over [start, end) (end < 0: to the end)
  * in the view of (ref_seq, long_client_id) (ref_seq < 0: currentSeq; long_client_id NULL: the observer,
  * i.e. the local view).  Serves Client.walkSegments (client.ts:286), getContainingSegment (:1065) and

@@ -83,6 +83,7 @@ struct loggen_doc {
   uint32_t final_len;
   uint32_t final_segments;
   int32_t error;
+  uint64_t digest;        // oracle's final state digest v1 (Doc::digest, DESIGN.md "State digest")
 };
 
 }  // extern "C"
@@ -134,6 +135,7 @@ static int gen_one(const loggen_cfg& cfg, uint32_t docIndex, loggen_doc* out) {
     if (cfg.initial_len > 0)
       doc.insertTextLocal(0, u16str(reinterpret_cast<const char16_t*>(text.data()), text.size()), std::nullopt);
     doc.startOrUpdateCollaboration("obs", 0, 0);
+    doc.mt.counters = Counters{};  // count the sequenced ops only (the detached initial insert is not one)
     out->client_writer[0] = 0;
     std::vector<int> shortOf(K + 1, -1);
     std::vector<uint32_t> refSeq(K + 1, 0);
@@ -237,6 +239,7 @@ static int gen_one(const loggen_cfg& cfg, uint32_t docIndex, loggen_doc* out) {
   out->initial_len = (uint32_t)cfg.initial_len;
   std::string dump = doc.dumpSegments();
   out->checksum = fnv1a64(dump);
+  out->digest = doc.digest();
   out->ops_applied = doc.mt.counters.ops;
   out->segs_touched = doc.mt.counters.segsTouched;
   out->final_len = (uint32_t)doc.mt.length();

@@ -1831,6 +1831,87 @@ std::string Doc::dumpSegments() {
   return out;
 }
 
+// State digest v1 (DESIGN.md "State digest"): the canonical dump's content (tree paths, segment text /
+// marker / handle span, seq, client, removal info, properties) folded into 64 bits with a definition
+// that a GPU wave can evaluate over its own layout.  Checker-side restatement of the same definition.
+namespace {
+inline uint64_t dg_fmix(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+inline uint64_t dg_mix(uint64_t h, uint64_t x) { return dg_fmix(h ^ (x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2))); }
+}  // namespace
+
+uint64_t Doc::digest() {
+  uint64_t S = 0, nsegs = 0;
+  std::vector<int> path;
+  std::function<void(Block*)> rec = [&](Block* b) {
+    for (int i = 0; i < b->childCount; i++) {
+      path.push_back(i);
+      Node* c = b->children[i];
+      if (!c->leaf) {
+        rec(static_cast<Block*>(c));
+        path.pop_back();
+        continue;
+      }
+      const Seg* s = static_cast<const Seg*>(c);
+      uint64_t P = 0;
+      for (size_t l = 0; l < path.size() && l < 16; l++) P += (uint64_t)(path[l] + 1) << (4 * l);
+      uint64_t K, T = 0;
+      int len;
+      if (s->perm) {
+        K = 2;
+        len = s->cachedLength;
+        T = dg_fmix(((uint64_t)(uint32_t)s->start << 32) | (uint32_t)len);
+      } else if (s->isMarker) {
+        K = 1;
+        len = 1;
+        T = dg_fmix(0x4D00000000ull | (uint32_t)(s->refType + 1));
+      } else {
+        K = 0;
+        len = (int)s->text.size();
+        for (size_t j = 0; j < s->text.size(); j++) T += dg_fmix((((uint64_t)j << 16) | (uint16_t)s->text[j]) + 0x632BE59BD9B4E019ull);
+      }
+      uint64_t Rc = 0;
+      if (s->removed)
+        for (size_t q = 0; q < s->removedClientIds.size(); q++) Rc += dg_mix(q + 1, (uint32_t)(int32_t)s->removedClientIds[q]);
+      uint64_t Ph = 0;
+      if (s->props) {
+        uint64_t q = 0;
+        for (auto& kv : *s->props) {
+          if (kv.second.t == JVal::Undef) continue;  // JSON.stringify omits it
+          Ph += dg_mix(dg_mix(q + 1, fnv1a64(u16_to_utf8(kv.first))), fnv1a64(json_stringify(kv.second)));
+          q++;
+        }
+      }
+      uint64_t h = 0;
+      h = dg_mix(h, P);
+      h = dg_mix(h, K);
+      h = dg_mix(h, T);
+      h = dg_mix(h, (uint32_t)len);
+      h = dg_mix(h, (uint32_t)s->seq);
+      h = dg_mix(h, (uint32_t)s->clientId);
+      h = dg_mix(h, (uint32_t)(s->removed ? s->removedSeq : -1));
+      h = dg_mix(h, Rc);
+      h = dg_mix(h, Ph);
+      nsegs++;
+      S += dg_fmix(h + nsegs * 0xD6E8FEB86659FD93ull);
+      path.pop_back();
+    }
+  };
+  rec(mt.root);
+  uint64_t D = 0x4D544231ull;  // "MTB1"
+  D = dg_mix(D, (uint32_t)mt.window.minSeq);
+  D = dg_mix(D, (uint32_t)mt.window.currentSeq);
+  D = dg_mix(D, (uint32_t)mt.length());
+  D = dg_mix(D, nsegs);
+  return dg_mix(D, S);
+}
+
 // Client.load -> SnapshotLoader (snapshotLoader.ts:41-257) for SnapshotV1 chunks.
 void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId) {
   auto findBlob = [&](const std::string& id) -> const std::string& {

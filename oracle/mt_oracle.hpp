@@ -292,6 +292,8 @@ class Doc {
   std::vector<std::pair<std::string, std::string>> summarizeLegacy(const std::string& catchUpJson, std::string* summaryJson);
   // canonical segment dump used for engine parity (one JSON object per line)
   std::string dumpSegments();
+  // state digest v1 (DESIGN.md "State digest"): the dump's content folded into 64 bits
+  uint64_t digest();
 
   // ---- SharedSegmentSequence catch-up messages (sequence.ts:680-748) for SnapshotLegacy summaries
   bool catchUp = false;

@@ -50,6 +50,8 @@ def lib():
         L.orc_dump_segments.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_checksum.restype = ctypes.c_uint64
         L.orc_checksum.argtypes = [vp]
+        L.orc_digest.restype = ctypes.c_uint64
+        L.orc_digest.argtypes = [vp]
         L.orc_load_v1.argtypes = [vp, cp, sz, cp]
         L.orc_enable_catch_up.argtypes = [vp]
         L.orc_summarize_legacy.argtypes = [vp, i, i, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
@@ -292,6 +294,10 @@ class OracleDoc:
 
     def checksum(self):
         return self._L.orc_checksum(self._h)
+
+    def digest(self):
+        """State digest v1 (DESIGN.md "State digest"), as the engine's mtb_doc_digests computes it."""
+        return self._L.orc_digest(self._h)
 
     def load_v1(self, blobs, observer_id):
         """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""

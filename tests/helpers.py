@@ -257,3 +257,22 @@ def chars_with_props(doc):
         t = s.get("text", "￼")
         out.extend((ch, json.dumps(s.get("properties"), sort_keys=True)) for ch in t)
     return out
+
+
+def load_logbatch(B, lb, docs=None, props_interned=False):
+    """Queue generated logs (oracle/loggen.cpp) into engine batch B: document j of B gets log docs[j]
+    (default: log j).  The props table is interned first so its ids follow the generator's table."""
+    docs = list(range(lb.n)) if docs is None else list(docs)
+    if not props_interned:
+        props = lb.props_json()
+        ids = [B.intern_props(p) if p else 0 for p in props]
+        assert ids == list(range(len(props))), "props ids must follow the generator table"
+    for j, u in enumerate(docs):
+        tb = lb.doc_text_bytes(u)
+        il = lb.docs[u].initial_len
+        B.init_doc(j, tb[: il * 2].decode("utf-16-le"), "obs")
+        for cid in lb.client_ids(u)[1:]:
+            B.add_client(j, cid)
+        # payload offsets in the generated records index the doc's text arena (initial text first)
+        B.append_records(j, lb.doc_ops_bytes(u), lb.docs[u].n_ops, tb)
+    return docs

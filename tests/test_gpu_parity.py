@@ -11,6 +11,19 @@ from helpers import first_diff, msg_from_compact, replay_fixtures
 pytestmark = pytest.mark.gpu
 
 
+def expected_alg_bytes(lb, i):
+    """SURVEY 8(d) algorithmic bytes of document i, computed from the oracle's counters and the records."""
+    import struct
+    d = lb.docs[i]
+    ops = lb.doc_ops_bytes(i)
+    text_units = 0
+    for k in range(d.n_ops):
+        t, fl, _c, _s, _r, _m, _p1, p2, _pay, _pr = struct.unpack_from("<BBHIIIIIII", ops, 32 * k)
+        if t == 0 and not fl & 0x42:  # text inserts (not markers / PermutationSegments)
+            text_units += p2
+    return 32 * d.ops_applied + 2 * text_units + 24 * d.segs_touched + 24 * d.final_segments + 2 * d.final_len
+
+
 def _engine():
     from fluidframework_amd import MergeTreeBatch
     return MergeTreeBatch
@@ -62,6 +75,7 @@ def test_reference_replay_logs_segments_and_summary_match_oracle():
         o = _oracle_for_fixture(d)
         gd, od = B.dump_segments(i), o.dump_segments()
         assert gd == od, f"{name}: segment dump differs: {first_diff(gd, od)}"
+        assert B.digests(i, 1)[0] == o.digest(), f"{name}: state digest differs"
         gb, gs = B.summarize_v1(i)
         osum = o.summarize_v1()
         assert [list(x) for x in gb] == osum["blobs"], f"{name}: SnapshotV1 blobs differ"
@@ -89,6 +103,15 @@ def test_synthetic_logs_bit_exact(new_mode):
     st = B.replay()
     assert st["errors"] == 0
     assert st["ops_applied"] == sum(lb.docs[i].ops_applied for i in range(lb.n))
+    # state digests (GPU) == the oracle's, and the stats fold them
+    dg = B.digests()
+    assert dg == [lb.docs[i].digest for i in range(lb.n)]
+    assert st["checksum"] == sum(dg) % (1 << 64)
+    assert st["segments_final"] == sum(lb.docs[i].final_segments for i in range(lb.n))
+    assert st["text_units_final"] == sum(lb.docs[i].final_len for i in range(lb.n))
+    # roofline numerator: 32 B per op + 2 B per inserted text unit + 24 B per segment record
+    # the oracle creates or modifies, + the final state write-back -- every term from the oracle
+    assert st["bytes_alg"] == sum(expected_alg_bytes(lb, i) for i in range(lb.n))
     bad = [i for i in range(lb.n) if B.checksum(i) != lb.docs[i].checksum]
     if bad:
         from pyoracle import OracleDoc
