@@ -27,6 +27,12 @@
 // released lists go to a per-class free stack whose heads live in the slice's first 16 words.
 #define MTB_LCLASSES 16
 #define MTB_LIST_RESERVED 4  // WEnt entries (16 words) reserved for the heads
+// A window list keeps its entries in non-decreasing seq order, so the entries above a view's refSeq are
+// its tail.  The list capacity word (a power of two) carries this flag when the order is not known (lists
+// built by a summary load's body appends, or a rebuild whose seq window exceeds the sort's buckets):
+// such a list is scanned whole.
+#define MTB_LUNSORTED 0x80000000u
+#define MTB_SORT_BUCKETS 1024  // rebuild's counting sort: seq - minSeq - 1 in [0, 1024)
 
 // Internal record type (never accepted from mtb_append_ops): one body segment of a SnapshotV1 load,
 // appended by insertSegments(root length, [segs], UniversalSeq, client, seq) (snapshotLoader.ts:187-220).

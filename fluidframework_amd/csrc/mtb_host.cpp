@@ -752,6 +752,8 @@ void build_load_image(HostDoc& d, const std::vector<LoadSeg>& hdr) {
             e.ck |= (int32_t)((j - (ni - k)) << 20);
             im.lists.push_back(e);
           }
+        // window lists are kept in seq order (MTB_LUNSORTED clear): views read only their tail
+        std::stable_sort(im.lists.begin() + n.loff, im.lists.end(), [](const WEnt& a, const WEnt& b) { return a.seq < b.seq; });
         im.lists.resize(n.loff + cap, WEnt{});
       }
       for (size_t j = ni - k; j < ni; j++) {

@@ -336,41 +336,69 @@ struct Eng {
     }
     PROF_CNT(CN_VIEW, 1);
     const uint64_t tv0 = PROF_T();
-    uint32_t loff, lcnt, lcap0;
-    meta_of(d, loff, lcnt, lcap0);
+    uint32_t loff, lcnt, lcapw;
+    meta_of(d, loff, lcnt, lcapw);
+    // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength).  Entries at or
+    // below minSeq sit in the reference's minLength whatever refSeq is, so the scan threshold is
+    // max(refSeq, minSeq) (only a summary load's body inserts, at refSeq 0, ever see refSeq < minSeq).
+    const int Rl = R > minSeq ? R : minSeq;
+    const int Cm = C & 0xFFFF;
+    // A sorted list's entries above Rl are its tail: it is read backwards from the end, one or two
+    // 64-entry chunks in flight with the record (two when the op's view lags far behind the window),
+    // more only while every entry read is still above Rl.  An unsorted list is read whole, front first.
+    const bool sorted = !(lcapw & MTB_LUNSORTED);
+    const bool two = lcnt > 64 && (!sorted || curSeq - Rl > 56);
     const uint32_t* src = bw(b);
     const uint32_t w = src[lane];
     const uint32_t h = lane < 5 ? src[FB_HDR + lane] : 0u;
-    WEnt e0;
-    e0.seq = MTB_NOKEY;
-    e0.ck = 0;
-    e0.delta = 0;
-    if ((uint32_t)lane < lcnt) e0 = lst[loff + lane];
+    const uint32_t i0 = sorted ? lcnt - 1 - (uint32_t)lane : (uint32_t)lane;
+    const uint32_t i1 = sorted ? lcnt - 65 - (uint32_t)lane : 64u + (uint32_t)lane;
+    const bool v0 = (uint32_t)lane < lcnt;
+    const bool v1 = two && (uint32_t)lane + 64 < lcnt;
+    WEnt e0, e1;
+    e0.seq = e1.seq = MTB_NOKEY;
+    e0.ck = e1.ck = 0;
+    e0.delta = e1.delta = 0;
+    if (v0) e0 = lst[loff + i0];
+    if (v1) e1 = lst[loff + i1];
     if (lane < MTB_MAXCH) sh->corr[lane] = 0;
     (&V.f[0][0])[lane] = w;
     const int count = rl((int)h, 0);
     const uint32_t hpar = rlu(h, 1);
     const int hsc = rl((int)h, 3), hlen = rl((int)h, 4);
     wsync();
-    PROF_CNT(CN_ENTRIES, lcnt);
-    // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength).  Entries at or
-    // below minSeq sit in the reference's minLength whatever refSeq is, so the scan threshold is
-    // max(refSeq, minSeq) (only a summary load's body inserts, at refSeq 0, ever see refSeq < minSeq).
-    const int Rl = R > minSeq ? R : minSeq;
-    const int Cm = C & 0xFFFF;
-    if ((uint32_t)lane < lcnt && e0.seq > Rl) {
-      const int c = e0.ck & 0xFFFF, kind = (e0.ck >> 16) & 0xF;
-      if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e0.ck >> 20) & 7], e0.delta);
-    }
-    for (uint32_t base = 64; base < lcnt; base += 64) {
-      if (base + lane < lcnt) {
-        const WEnt e = lst[loff + base + lane];
-        if (e.seq > Rl) {
-          const int c = e.ck & 0xFFFF, kind = (e.ck >> 16) & 0xF;
-          if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
-        }
+    auto correct = [&](const WEnt& e, bool v) {
+      if (v && e.seq > Rl) {
+        const int c = e.ck & 0xFFFF, kind = (e.ck >> 16) & 0xF;
+        if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
+      }
+    };
+    correct(e0, v0);
+    correct(e1, v1);
+    uint32_t done = two ? 128u : 64u;  // entries fetched (from the end when sorted, from the front if not)
+    if (sorted) {
+      bool more = done < lcnt && __ballot((v0 && e0.seq <= Rl) || (v1 && e1.seq <= Rl)) == 0;
+      while (COLD(more)) {
+        const uint32_t i = lcnt - done - 1 - (uint32_t)lane;
+        const bool v = (uint32_t)lane < lcnt - done;
+        WEnt e;
+        e.seq = MTB_NOKEY;
+        if (v) e = lst[loff + i];
+        correct(e, v);
+        done += 64;
+        more = done < lcnt && __ballot(v && e.seq <= Rl) == 0;
+      }
+    } else {
+      for (; done < lcnt; done += 128) {
+        const uint32_t ia = done + (uint32_t)lane, ib = ia + 64;
+        WEnt ea, eb;
+        if (ia < lcnt) ea = lst[loff + ia];
+        if (ib < lcnt) eb = lst[loff + ib];
+        correct(ea, ia < lcnt);
+        correct(eb, ib < lcnt);
       }
     }
+    PROF_CNT(CN_ENTRIES, done < lcnt ? done : lcnt);
     wsync();
     if (lane < count) {
       const uint32_t id = V.f[F_ID][lane];
@@ -423,7 +451,8 @@ struct Eng {
     list_used += cap;
     return o;
   }
-  __device__ __forceinline__ void list_free(uint32_t off, uint32_t cap) {
+  __device__ __forceinline__ void list_free(uint32_t off, uint32_t capw) {
+    const uint32_t cap = capw & ~MTB_LUNSORTED;
     if (cap < 8 || (cap & (cap - 1))) return;
     const int c = list_class(cap);
     if (c >= MTB_LCLASSES) return;
@@ -490,7 +519,8 @@ struct Eng {
   }
   // Append (seqv, client, kind, delta) to the lists of the path blocks at depths [lo, hi), each entry
   // tagged with the slot the path takes at that depth.  One lane per depth; full lists are
-  // re-allocated afterwards, one at a time.
+  // re-allocated afterwards, one at a time.  A replay appends the current op's seq, never below any
+  // entry, so the lists stay sorted; a summary load's body appends any seq and marks them unsorted.
   __device__ __forceinline__ void append_levels(int lo, int hi, int seqv, int client, int kind, int delta) {
     if (hi <= lo) return;
     bool need = false;
@@ -508,7 +538,20 @@ struct Eng {
         lcnt = P.f[F_RSEQ][k];
         lcap = P.f[F_CLI][k];
       }
-      if (lcnt < lcap) {
+      if constexpr (MODE == MODE_LOAD) {
+        if (lcnt < (lcap & ~MTB_LUNSORTED) && !(lcap & MTB_LUNSORTED)) {
+          lcap |= MTB_LUNSORTED;
+          if (i == 0) {
+            sh->rmeta[2] = lcap;
+            blk[sh->path[0]].lcap = lcap;
+          } else {
+            const int k = sh->slot[i - 1];
+            sh->v[i - 1].f[F_CLI][k] = lcap;
+            blk[sh->path[i - 1]].f[F_CLI][k] = lcap;
+          }
+        }
+      }
+      if (lcnt < (lcap & ~MTB_LUNSORTED)) {
         WEnt e;
         e.seq = seqv;
         e.ck = WE_KEY(client, kind, sh->slot[i]);
@@ -537,6 +580,7 @@ struct Eng {
       uint32_t live, cap;
       const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
       if (bad()) return;
+      const uint32_t flag = (MODE == MODE_LOAD) ? MTB_LUNSORTED : (lcap & MTB_LUNSORTED);
       if (lane == 0) {
         WEnt e;
         e.seq = seqv;
@@ -544,7 +588,56 @@ struct Eng {
         e.delta = delta;
         e.pad = 0;
         lst[no + live] = e;
-        set_meta(d, no, live + 1, cap);
+        set_meta(d, no, live + 1, cap | flag);
+      }
+      wsync();
+    }
+  }
+  // Insert an overlapping remover's (removedSeq, client, OVERLAP, +len) entry into the lists of the path
+  // blocks at depths [lo, hi) at its seq position (removedSeq is older than the current op): the tail of
+  // entries above it moves up by one, chunk by chunk from the end.  Rare (overlapping removes).
+  __device__ __forceinline__ void insert_levels_sorted(int lo, int hi, int seqv, int client, int kind, int delta) {
+    for (int dd = lo; dd < hi && !err; dd++) {
+      uint32_t loff, lcnt, lcapw;
+      meta_of(dd, loff, lcnt, lcapw);
+      if (lcnt >= (lcapw & ~MTB_LUNSORTED)) {
+        uint32_t live, cap;
+        const uint32_t no = list_regrow(loff, lcnt, lcapw, 1, live, cap);
+        if (bad()) return;
+        lcapw = cap | (lcapw & MTB_LUNSORTED);
+        if (lane == 0) set_meta(dd, no, live, lcapw);
+        wsync();
+        loff = no;
+        lcnt = live;
+      }
+      uint32_t p = lcnt;
+      if (!(lcapw & MTB_LUNSORTED)) {
+        uint32_t top = lcnt;
+        while (top > 0) {
+          const uint32_t n = top < 64 ? top : 64u;
+          const uint32_t i = top - n + (uint32_t)lane;
+          const bool v = (uint32_t)lane < n;
+          WEnt e;
+          e.seq = MTB_NOKEY;
+          if (v) e = lst[loff + i];
+          const bool gt = v && e.seq > seqv;
+          const unsigned long long m = __ballot(gt);
+          if (gt) lst[loff + i + 1] = e;  // (sorted: the lanes above seqv are a suffix of the chunk)
+          wsync();
+          const uint32_t g = (uint32_t)__popcll(m);
+          p = top - g;
+          if (g < n) break;
+          top -= n;
+        }
+      }
+      if (lane == 0) {
+        WEnt e;
+        e.seq = seqv;
+        e.ck = WE_KEY(client, kind, sh->slot[dd]);
+        e.delta = delta;
+        e.pad = 0;
+        lst[loff + p] = e;
+        set_meta(dd, loff, lcnt + 1, lcapw);
       }
       wsync();
     }
@@ -696,9 +789,74 @@ struct Eng {
     }
     wsync();
     list_free(old_loff, old_lcap);
-    loff_out = no;
-    lcnt_out = wpos;
-    lcap_out = cap;
+    // Sort the new list by seq (a counting sort over seq - minSeq - 1 into a second list) so that views
+    // can read only its tail.  The 1024 16-bit bucket counters live in the scour union, which no caller
+    // holds live across a rebuild.  A seq window too wide for the buckets leaves the list unsorted.
+    const uint32_t T = wpos;
+    uint32_t outOff = no, outCap = cap | MTB_LUNSORTED;
+    if (T <= 1) {
+      outCap = cap;
+    } else if (T < 65536) {
+      uint32_t* hist = &sh->hold[0][0];
+      for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
+      wsync();
+      bool over = false;
+      for (uint32_t base = 0; base < T; base += 64) {
+        const uint32_t i = base + (uint32_t)lane;
+        if (i < T) {
+          const int bk = lst[no + i].seq - minSeq - 1;
+          if (bk < 0 || bk >= MTB_SORT_BUCKETS) over = true;
+          else atomicAdd(&hist[bk >> 1], 1u << ((bk & 1) * 16));
+        }
+      }
+      if (!__ballot(over)) {
+        wsync();
+        // exclusive scan of the counts: lane l owns buckets [16 l, 16 l + 16) = words [8 l, 8 l + 8)
+        uint32_t wv[8];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          wv[q] = hist[8 * lane + q];
+          tot += (wv[q] & 0xFFFF) + (wv[q] >> 16);
+        }
+        int incl = (int)tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += t;
+        }
+        uint32_t run = (uint32_t)incl - tot;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t c0 = run;
+          run += wv[q] & 0xFFFF;
+          hist[8 * lane + q] = c0 | (run << 16);
+          run += wv[q] >> 16;
+        }
+        wsync();
+        uint32_t cap2;
+        const uint32_t no2 = list_alloc(T + T / 2 + 4, cap2);
+        if (bad()) return;
+        for (uint32_t base = 0; base < T; base += 64) {
+          const uint32_t i = base + (uint32_t)lane;
+          if (i < T) {
+            const WEnt e = lst[no + i];
+            const int bk = e.seq - minSeq - 1;
+            const uint32_t sft = (uint32_t)(bk & 1) * 16;
+            const uint32_t old = atomicAdd(&hist[bk >> 1], 1u << sft);
+            lst[no2 + ((old >> sft) & 0xFFFF)] = e;
+          }
+        }
+        wsync();
+        list_free(no, cap);
+        outOff = no2;
+        outCap = cap2;
+      }
+      wsync();
+    }
+    loff_out = outOff;
+    lcnt_out = T;
+    lcap_out = outCap;
   }
 
   // ------------------------------------------------------------------ tree primitives
@@ -1354,7 +1512,7 @@ struct Eng {
           blk[b].f[F_RCX][t] = h;
         }
         wsync();
-        append_levels(0, d, rl(rseq, t), C, WK_OVERLAP, rl(len, t));
+        insert_levels_sorted(0, d, rl(rseq, t), C, WK_OVERLAP, rl(len, t));
         if (bad()) return 0;
       }
     } else {
@@ -1826,6 +1984,9 @@ struct Eng {
         const int base = nh / cc;
         int rem = nh % cc;
         int taken = 0;
+        // first every new block gets its children (the scour output in hold[] is consumed here) ...
+        uint32_t nbs = 0;  // lane q: new block q, its observer length, whether its children are blocks
+        int lens = 0, kbs = 0;
         for (int q = 0; q < cc; q++) {
           int n = base;
           if (rem > 0) {
@@ -1837,15 +1998,30 @@ struct Eng {
           const int len = place_children(nb, taken, n);
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
-          uint32_t a = 0, c2 = 0, e = 0;
-          if (__ballot(kblk)) {
-            rebuild(nb, 0, 0, a, c2, e);
-            if (bad()) return;
+          const int kb = __ballot(kblk) != 0;
+          if (lane == q) {
+            nbs = nb;
+            lens = len;
+            kbs = kb;
           }
           if (lane == 0) {
             blk[nb].parent = parent;
             blk[nb].index = (uint32_t)q;
             blk[nb].len = len;
+          }
+          wsync();
+          taken += n;
+        }
+        // ... then the lists of those whose children are blocks (rebuild uses the union as scratch)
+        for (int q = 0; q < cc; q++) {
+          const uint32_t nb = rlu(nbs, q);
+          uint32_t a = 0, c2 = 0, e = 0;
+          if (rl(kbs, q)) {
+            rebuild(nb, 0, 0, a, c2, e);
+            if (bad()) return;
+          }
+          const int len = rl(lens, q);
+          if (lane == 0) {
             FBlk& P = blk[parent];
             P.f[F_ID][q] = nb;
             P.f[F_LEN][q] = (uint32_t)len;
@@ -1857,7 +2033,6 @@ struct Eng {
             P.f[F_TEXT][q] = 0;
           }
           wsync();
-          taken += n;
         }
       }
       {
