@@ -142,7 +142,8 @@ struct DocState {     // 320 bytes
   // catch-up deltas (MTB_F_DELTA records): u32 entries [record, segment -> local position, length, props]
   uint64_t delta_base;
   uint32_t delta_cap, delta_used;  // entries
-  uint32_t pad2[12];
+  uint64_t prof2[4];    // MTB_PROFILE builds: more phases (prof[7 + i])
+  uint32_t cnt2[4];     // MTB_PROFILE builds: more event counters (cnt[5 + i])
 };
 static_assert(sizeof(DocState) == 320, "DocState is copied as 80 dwords (mtb_rewind_kernel)");
 

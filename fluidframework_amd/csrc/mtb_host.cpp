@@ -1506,16 +1506,19 @@ void replay(mtb_batch* b, mtb_stats* out) {
   }
   run_digest(b, st);
   if (getenv("MTB_PROFILE_OUT")) {  // MTB_PROFILE builds: per-phase device cycles and events per op, summed over documents
-    double p[7] = {0, 0, 0, 0, 0, 0, 0}, c[5] = {0, 0, 0, 0, 0};
+    double p[11] = {0}, c[9] = {0};
     for (uint32_t i = 0; i < b->ndocs; i++) {
       for (int k = 0; k < 7; k++) p[k] += (double)b->hst[i].prof[k];
+      for (int k = 0; k < 4; k++) p[7 + k] += (double)b->hst[i].prof2[k];
       for (int k = 0; k < 5; k++) c[k] += b->hst[i].cnt[k];
+      for (int k = 0; k < 4; k++) c[5 + k] += b->hst[i].cnt2[k];
     }
     const double n = (double)std::max<uint64_t>(1, st.ops_applied);
     fprintf(stderr, "mtb_profile cycles/op: boundary %.0f insert %.0f nodemap %.0f zamboni %.0f total %.0f | view %.0f scour %.0f (ops %llu)\n",
             p[0] / n, p[1] / n, p[2] / n, p[3] / n, p[4] / n, p[5] / n, p[6] / n, (unsigned long long)st.ops_applied);
-    fprintf(stderr, "mtb_profile events/op: scour %.3f pack %.3f rebuild %.3f view %.3f entries %.2f\n", c[0] / n, c[1] / n,
-            c[2] / n, c[3] / n, c[4] / n);
+    fprintf(stderr, "mtb_profile zamboni cycles/op: heap %.0f stage %.0f place %.0f pack %.0f\n", p[7] / n, p[8] / n, p[9] / n, p[10] / n);
+    fprintf(stderr, "mtb_profile events/op: scour %.3f pack %.3f rebuild %.3f view %.3f entries %.2f zcalls %.3f pops %.3f popskips %.3f psig %.3f\n",
+            c[0] / n, c[1] / n, c[2] / n, c[3] / n, c[4] / n, c[5] / n, c[6] / n, c[7] / n, c[8] / n);
     uint64_t mx[7] = {0, 0, 0, 0, 0, 0, 0}, mxo = 0;
     for (uint32_t i = 0; i < b->ndocs; i++) {
       const DocState& q = b->hst[i];

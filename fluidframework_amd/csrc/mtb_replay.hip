@@ -46,8 +46,10 @@ namespace mtbk {
 #define PROF_ADD(i, t0) ((void)(t0))
 #define PROF_CNT(i, n) ((void)0)
 #endif
-enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL = 4, PH_VIEW = 5, PH_SCOUR = 6, NPH = 7 };
-enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, NCN = 5, CN_SPLIT = 99, CN_GROW = 99, CN_ZRECORD = 99 };
+enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL = 4, PH_VIEW = 5, PH_SCOUR = 6, PH_HEAP = 7,
+       PH_STAGE = 8, PH_PLACE = 9, PH_PACK = 10, NPH = 11 };
+enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, CN_ZCALL = 5, CN_POP = 6, CN_PSKIP = 7, CN_PSIG = 8,
+       NCN = 9, CN_SPLIT = 99, CN_GROW = 99, CN_ZRECORD = 99 };
 
 #define MTB_LDS_HEAP 128
 #define MTB_VDEPTH 12  // depth of the LDS path cache; 4^12 segments per document is far beyond any input
@@ -196,6 +198,7 @@ struct Eng {
   uint32_t n_mod, ops_applied, text_bytes;  // this launch's counts (added to DocState at the end)
   bool heap_lds;                // LRU heap lives in LDS (spills to the global slice when it outgrows it)
   int walk_depth;               // depth of the leaf-level block reached by the last walk (-1: none)
+  uint32_t vmask;               // bit d: the LDS view of depth d may hold a fetched record (else it is empty)
   bool struct_changed;          // a block split / root growth happened since the last walk started
   bool sp_internal;
   int pending_fix;
@@ -252,6 +255,7 @@ struct Eng {
   }
   __device__ __forceinline__ void view_clear() {
     if (lane < MTB_VDEPTH) sh->v[lane].b = MTB_NONE;
+    vmask = 0;
     wsync();
   }
 
@@ -314,30 +318,55 @@ struct Eng {
       lcap = U(P.f[F_CLI][k]);
     }
   }
+  // Slot `lane` of a block, in registers (lanes < count): child id, its F_SEQ / F_RSEQ / F_CLI fields
+  // (segment: seq, removedSeq, client word; block: its list offset, count, capacity word) and the
+  // child's length in the op's (R, C) view (MTB_UNDEF: undefined).
+  struct Kid {
+    uint32_t id, seq, rseq, cli;
+    int rl;
+  };
   // Fetch block b (depth d of the current path) together with its window list, and compute its
-  // children's lengths in the (R, C) view.  Returns the child count.
-  __device__ __forceinline__ int load_view(int d, uint32_t b, int R, int C) {
+  // children's lengths in the (R, C) view.  Returns the child count; `k` receives slot `lane` in
+  // registers (the walk decides from them without reading the LDS view back).  The record is also
+  // stored as the LDS view of depth d for the op's later steps.  A caller that knows the block's list
+  // metadata (the walk: its parent's slot fields, in registers) passes it in.
+  __device__ __forceinline__ int load_view(int d, uint32_t b, int R, int C, Kid& k, bool haveMeta = false,
+                                           uint32_t mloff = 0, uint32_t mlcnt = 0, uint32_t mlcap = 0) {
     View& V = sh->v[d];
-    const uint32_t vb = U(V.b);
-    const int vrlv = U(V.rlv);
-    if (vb == b && vrlv) return U(V.count);
-    if (vb == b) {  // record still valid (e.g. after a segment split): recompute lengths from LDS
-      const int count = U(V.count);
-      bool segs = true;
-      if (lane < count) segs = (V.f[F_ID][lane] & MTB_LEAF) != 0;
-      if (__ballot(!segs) == 0) {
-        if (lane < count)
-          V.rl[lane] = seg_vis((int)V.f[F_LEN][lane], (int)V.f[F_SEQ][lane], (int)V.f[F_RSEQ][lane], V.f[F_CLI][lane],
-                               V.f[F_RCX][lane], R, C);
-        if (lane == 0) V.rlv = 1;
-        wsync();
-        return count;
+    k.id = MTB_NONE;
+    k.seq = k.rseq = k.cli = 0;
+    k.rl = 0;
+    if (vmask & (1u << d)) {
+      const uint32_t vb = U(V.b);
+      if (vb == b) {
+        const int count = U(V.count);
+        const int vrlv = U(V.rlv);
+        if (lane < count) {
+          k.id = V.f[F_ID][lane];
+          k.seq = V.f[F_SEQ][lane];
+          k.rseq = V.f[F_RSEQ][lane];
+          k.cli = V.f[F_CLI][lane];
+        }
+        if (vrlv) {
+          if (lane < count) k.rl = V.rl[lane];
+          return count;
+        }
+        // record still valid (e.g. after a segment split): recompute the leaves' lengths from LDS
+        if (__ballot(lane < count && !(k.id & MTB_LEAF)) == 0) {
+          if (lane < count) {
+            k.rl = seg_vis((int)V.f[F_LEN][lane], (int)k.seq, (int)k.rseq, k.cli, V.f[F_RCX][lane], R, C);
+            V.rl[lane] = k.rl;
+          }
+          if (lane == 0) V.rlv = 1;
+          wsync();
+          return count;
+        }
       }
     }
     PROF_CNT(CN_VIEW, 1);
     const uint64_t tv0 = PROF_T();
-    uint32_t loff, lcnt, lcapw;
-    meta_of(d, loff, lcnt, lcapw);
+    uint32_t loff = mloff, lcnt = mlcnt, lcapw = mlcap;
+    if (!haveMeta) meta_of(d, loff, lcnt, lcapw);
     // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength).  Entries at or
     // below minSeq sit in the reference's minLength whatever refSeq is, so the scan threshold is
     // max(refSeq, minSeq) (only a summary load's body inserts, at refSeq 0, ever see refSeq < minSeq).
@@ -349,8 +378,17 @@ struct Eng {
     const bool sorted = !(lcapw & MTB_LUNSORTED);
     const bool two = lcnt > 64 && (!sorted || curSeq - Rl > 56);
     const uint32_t* src = bw(b);
+    // the record twice: linear (lane i = dword i) for the LDS view, and slot-major on lanes 0..7
     const uint32_t w = src[lane];
     const uint32_t h = lane < 5 ? src[FB_HDR + lane] : 0u;
+    uint32_t flen = 0, frcx = 0;
+    if (lane < MTB_MAXCH) {
+      flen = src[F_LEN * 8 + lane];
+      k.seq = src[F_SEQ * 8 + lane];
+      k.rseq = src[F_RSEQ * 8 + lane];
+      k.cli = src[F_CLI * 8 + lane];
+      frcx = src[F_RCX * 8 + lane];
+    }
     const uint32_t i0 = sorted ? lcnt - 1 - (uint32_t)lane : (uint32_t)lane;
     const uint32_t i1 = sorted ? lcnt - 65 - (uint32_t)lane : 64u + (uint32_t)lane;
     const bool v0 = (uint32_t)lane < lcnt;
@@ -401,13 +439,9 @@ struct Eng {
     PROF_CNT(CN_ENTRIES, done < lcnt ? done : lcnt);
     wsync();
     if (lane < count) {
-      const uint32_t id = V.f[F_ID][lane];
-      int r;
-      if (id & MTB_LEAF)
-        r = seg_vis((int)V.f[F_LEN][lane], (int)V.f[F_SEQ][lane], (int)V.f[F_RSEQ][lane], V.f[F_CLI][lane], V.f[F_RCX][lane], R, C);
-      else
-        r = (int)V.f[F_LEN][lane] - sh->corr[lane];
-      V.rl[lane] = r;
+      k.id = w;
+      k.rl = (w & MTB_LEAF) ? seg_vis((int)flen, (int)k.seq, (int)k.rseq, k.cli, frcx, R, C) : (int)flen - sh->corr[lane];
+      V.rl[lane] = k.rl;
     }
     if (lane == 0) {
       V.b = b;
@@ -417,9 +451,14 @@ struct Eng {
       V.len = hlen;
       V.rlv = 1;
     }
+    vmask |= 1u << d;
     wsync();
     PROF_ADD(PH_VIEW, tv0);
     return count;
+  }
+  __device__ __forceinline__ int load_view(int d, uint32_t b, int R, int C) {
+    Kid k;
+    return load_view(d, b, R, C, k);
   }
 
   // ------------------------------------------------------------------ window lists
@@ -487,11 +526,13 @@ struct Eng {
     }
   }
   // Copy `cnt` entries at `off` into a fresh list with room for `extra` more, dropping entries at or
-  // below minSeq.  Returns the new offset; `live` receives the kept count and `cap` the capacity.
+  // below minSeq.  Returns the new offset; `live` receives
+  // the kept count, `cap` the capacity word: MTB_LUNSORTED unless the kept entries are in seq order
+  // (a list rebuilt unsorted becomes sorted again once its out-of-order entries fall below minSeq).
   __device__ __forceinline__ uint32_t list_regrow(uint32_t off, uint32_t cnt, uint32_t ocap, uint32_t extra, uint32_t& live,
                                                    uint32_t& cap) {
     PROF_CNT(CN_GROW, 1);
-    uint32_t n = 0;
+    uint32_t n = 0;  // kept entries (the capacity follows them, not the stale ones)
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
       const bool keep = i < cnt && lst[off + i].seq > minSeq;
@@ -500,6 +541,8 @@ struct Eng {
     const uint32_t no = list_alloc(2 * (n + extra), cap);
     if (bad()) return 0;
     uint32_t w = 0;
+    int carry = MTB_NOKEY;  // largest kept seq of the chunks before
+    bool unsorted = false;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
       WEnt e;
@@ -511,8 +554,21 @@ struct Eng {
       const unsigned long long m = __ballot(keep);
       if (keep) lst[no + w + rank_below(m)] = e;
       w += __popcll(m);
+      // order check: each kept entry against the largest kept seq before it (prefix max)
+      int pm = keep ? e.seq : MTB_NOKEY;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(pm, o, 64);
+        if (lane >= o) pm = max(pm, t);
+      }
+      int prev = __shfl_up(pm, 1, 64);
+      if (lane == 0) prev = MTB_NOKEY;
+      prev = max(prev, carry);
+      if (keep && e.seq < prev) unsorted = true;
+      carry = max(carry, rl(pm, 63));
     }
     live = w;
+    if (__ballot(unsorted)) cap |= MTB_LUNSORTED;
     wsync();
     list_free(off, ocap);
     return no;
@@ -580,7 +636,7 @@ struct Eng {
       uint32_t live, cap;
       const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
       if (bad()) return;
-      const uint32_t flag = (MODE == MODE_LOAD) ? MTB_LUNSORTED : (lcap & MTB_LUNSORTED);
+      const uint32_t flag = (MODE == MODE_LOAD) ? MTB_LUNSORTED : 0u;  // (cap carries the kept entries' order)
       if (lane == 0) {
         WEnt e;
         e.seq = seqv;
@@ -604,7 +660,7 @@ struct Eng {
         uint32_t live, cap;
         const uint32_t no = list_regrow(loff, lcnt, lcapw, 1, live, cap);
         if (bad()) return;
-        lcapw = cap | (lcapw & MTB_LUNSORTED);
+        lcapw = cap;
         if (lane == 0) set_meta(dd, no, live, lcapw);
         wsync();
         loff = no;
@@ -790,13 +846,13 @@ struct Eng {
     wsync();
     list_free(old_loff, old_lcap);
     // Sort the new list by seq (a counting sort over seq - minSeq - 1 into a second list) so that views
-    // can read only its tail.  The 1024 16-bit bucket counters live in the scour union, which no caller
+    // can read only its tail; lists of one chunk stay unsorted (list_regrow restores the order later).  The 1024 16-bit bucket counters live in the scour union, which no caller
     // holds live across a rebuild.  A seq window too wide for the buckets leaves the list unsorted.
     const uint32_t T = wpos;
     uint32_t outOff = no, outCap = cap | MTB_LUNSORTED;
     if (T <= 1) {
       outCap = cap;
-    } else if (T < 65536) {
+    } else if (T > 64 && T < 65536) {  // (a list of one chunk is read whole anyway: left unsorted)
       uint32_t* hist = &sh->hold[0][0];
       for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
       wsync();
@@ -1093,6 +1149,8 @@ struct Eng {
     uint32_t b = root;
     int p = pos;
     int d = 0;
+    bool haveMeta = false;  // the list metadata of block b (its parent's slot fields, read from registers)
+    uint32_t mo = 0, mc = 0, mk = 0;
     if (resume && walk_depth >= 0 && !struct_changed) {
       d = walk_depth;
       b = U(sh->path[d]);
@@ -1107,14 +1165,15 @@ struct Eng {
         sh->pp[d] = p;
       }
       wsync();
-      const int count = load_view(d, b, R, C);
+      Kid k;
+      const int count = load_view(d, b, R, C, k, haveMeta, mo, mc, mk);
       const View& V = sh->v[d];
       uint32_t cid = MTB_NONE;
       int clen = 0, cseq = 0;
       if (lane < count) {
-        cid = V.f[F_ID][lane];
-        clen = V.rl[lane];
-        cseq = (int)V.f[F_SEQ][lane];
+        cid = k.id;
+        clen = k.rl;
+        cseq = (int)k.seq;
       }
       const int def = (lane < count && clen > 0) ? clen : 0;
       const int incl = cscan8(def);
@@ -1131,6 +1190,10 @@ struct Eng {
         if (lane == 0) sh->slot[d] = j;
         wsync();
         if (!(cj & MTB_LEAF)) {
+          haveMeta = true;
+          mo = rlu(k.seq, j);
+          mc = rlu(k.rseq, j);
+          mk = rlu(k.cli, j);
           b = cj;
           p = pjj;
           d++;
@@ -1727,10 +1790,23 @@ struct Eng {
         const int rseq = (int)f[F_RSEQ];
         if (rseq >= 0) kind = rseq > minSeq ? 0 : 1;
         else if ((int)f[F_SEQ] <= minSeq) kind = 2;
-        if (kind == 2) {
-          if (hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0) last = UP(sh->gtext)[f[F_TEXT] + f[F_LEN] - 1];
-          g = psig_of(f[F_PROPS]);
-        }
+        if (kind == 2 && hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0)
+          last = UP(sh->gtext)[f[F_TEXT] + f[F_LEN] - 1];
+      }
+    }
+    // property signatures only where matchProperties can decide a merge: an acked segment whose left
+    // neighbour is also acked and carries a different property-set handle (equal handles match)
+    {
+      const bool k2 = s < count && kind == 2;
+      const int lk2 = dpp_shr_t<0x111>((int)k2);
+      const uint32_t lph = (uint32_t)dpp_shr_t<0x111>((int)f[F_PROPS]);
+      const int rk2 = dpp_shr_t<0x101>((int)k2);
+      const uint32_t rph = (uint32_t)dpp_shr_t<0x101>((int)f[F_PROPS]);
+      const bool needL = s > 0 && lk2 != 0 && lph != f[F_PROPS];
+      const bool needR = s < 7 && rk2 != 0 && rph != f[F_PROPS];
+      if (__ballot(k2 && (needL || needR))) {
+        PROF_CNT(CN_PSIG, 1);
+        if (k2) g = psig_of(f[F_PROPS]);
       }
     }
     int target = -1;  // per lane: lane it was appended into (-1 kept / dropped)
@@ -1960,27 +2036,26 @@ struct Eng {
       const uint32_t pparent = U(sh->zr.parent), pindex = U(sh->zr.index);
       const uint32_t kids = lane < pc ? sh->zr.f[F_ID][lane] : MTB_NONE;
       const uint32_t kloff = lane < pc ? sh->zr.f[F_SEQ][lane] : 0u, kcap = lane < pc ? sh->zr.f[F_CLI][lane] : 0u;
-      // P's own list metadata (its parent's slot, or the root header)
-      uint32_t ploff, pcap;
-      if (pparent == MTB_NONE) {
-        ploff = U(blk[parent].loff);
-        pcap = U(blk[parent].lcap);
-      } else {
-        ploff = U(blk[pparent].f[F_SEQ][pindex]);
-        pcap = U(blk[pparent].f[F_CLI][pindex]);
-      }
+      // P's own list metadata (its parent's slot, or the root header), in flight with the siblings
+      const uint32_t* pm = pparent == MTB_NONE ? &blk[parent].loff : &blk[pparent].f[F_SEQ][pindex];
+      const uint32_t ploff_v = pm[0], pcap_v = pparent == MTB_NONE ? pm[2] : pm[2 * MTB_MAXCH];
       stage_recs(pc, kids);
+      const uint32_t ploff = U(ploff_v), pcap = U(pcap_v);
       const int nh = scour(pc, 0);
       if (bad()) return;
-      for (int i = 0; i < pc; i++) {
-        free_blk(rlu(kids, i));
-        list_free(rlu(kloff, i), rlu(kcap, i));
-      }
       int cc = 0;
       if (nh > 0) {
         cc = nh / (MTB_MAXCH / 2);
         if (cc > MTB_MAXCH - 1) cc = MTB_MAXCH - 1;
         if (cc < 1) cc = 1;
+      }
+      // the new blocks reuse the siblings' records (block identity is not observable): no free-stack
+      // round trip; siblings beyond the new count go back to the free stack
+      for (int i = 0; i < pc; i++) {
+        if (i >= cc) free_blk(rlu(kids, i));
+        list_free(rlu(kloff, i), rlu(kcap, i));
+      }
+      if (nh > 0) {
         const int base = nh / cc;
         int rem = nh % cc;
         int taken = 0;
@@ -1993,7 +2068,7 @@ struct Eng {
             n++;
             rem--;
           }
-          const uint32_t nb = alloc_blk();
+          const uint32_t nb = q < pc ? rlu(kids, q) : alloc_blk();
           if (bad()) return;
           const int len = place_children(nb, taken, n);
           bool kblk = false;
@@ -2008,6 +2083,7 @@ struct Eng {
             blk[nb].parent = parent;
             blk[nb].index = (uint32_t)q;
             blk[nb].len = len;
+            blk[nb].scour = -1;  // a new block (makeBlock): needsScour undefined
           }
           wsync();
           taken += n;
@@ -2210,25 +2286,39 @@ struct Eng {
 
   // zamboniSegments (zamboni.ts:19-60)
   __device__ __forceinline__ void zamboni() {
+    PROF_CNT(CN_ZCALL, 1);
     for (int i = 0; i < 2 && !err; i++) {
       if (heap_cnt == 0) break;
       const Lru top = hget(1);
       if (top.maxSeq > minSeq) break;
+      PROF_CNT(CN_POP, 1);
+      uint64_t tz = PROF_T();
+      const uint32_t bp = segp[top.seg];  // in flight while the heap is fixed down
       heap_get();
-      const uint32_t b = U(segp[top.seg]);
-      if (b == MTB_NONE) continue;
+      PROF_ADD(PH_HEAP, tz);
+      tz = PROF_T();
+      const uint32_t b = U(bp);
+      if (b == MTB_NONE) { PROF_CNT(CN_PSKIP, 1); PROF_ADD(PH_STAGE, tz); continue; }
       stage_recs(1, b);
-      if (U(sh->pr[0].scour) == 0) continue;
+      const int sc = U(sh->pr[0].scour);
+      PROF_ADD(PH_STAGE, tz);
+      if (sc == 0) { PROF_CNT(CN_PSKIP, 1); continue; }
       const int count = U(sh->pr[0].count);
       const uint32_t parent = U(sh->pr[0].parent);
       const int nh = scour(1, 0);
       if (bad()) return;
+      tz = PROF_T();
       if (lane == 0) blk[b].scour = 0;
       wsync();
       // nh == count: nothing was dropped or appended, the record is unchanged
       if (nh < count) {
         place_children(b, 0, nh);
+        PROF_ADD(PH_PLACE, tz);
+        tz = PROF_T();
         if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);
+        PROF_ADD(PH_PACK, tz);
+      } else {
+        PROF_ADD(PH_PLACE, tz);
       }
     }
   }
@@ -2447,6 +2537,7 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
   const uint32_t n = ds->n_ops;
   uint32_t errk = n;  // MODE_MATRIX: index after the record that failed
   e.walk_depth = -1;
+  e.vmask = 0;
   e.struct_changed = false;
   e.pending_fix = -1;
   e.ld_pos = 0;
@@ -2536,8 +2627,14 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
     ds->ops_applied += e.ops_applied;
     ds->text_bytes += e.text_bytes;
 #ifdef MTB_PROFILE
-    for (int i = 0; i < NPH; i++) ds->prof[i] += e.prof[i];
-    for (int i = 0; i < NCN; i++) ds->cnt[i] += e.evc[i];
+    for (int i = 0; i < NPH; i++) {
+      if (i < 7) ds->prof[i] += e.prof[i];
+      else ds->prof2[i - 7] += e.prof[i];
+    }
+    for (int i = 0; i < NCN; i++) {
+      if (i < 5) ds->cnt[i] += e.evc[i];
+      else ds->cnt2[i - 5] += e.evc[i];
+    }
 #endif
     if (e.err && !ds->err) {
       ds->err = e.err;
