@@ -23,7 +23,8 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
-           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests"]
+           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
+           "mtb_summarize_v1_many", "mtb_blob_list_fnv"]
 
 
 class MtbOptions(ctypes.Structure):
@@ -96,6 +97,9 @@ def lib():
     L.mtb_summarize_legacy.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, sz,
                                        ctypes.POINTER(MtbBlobList)]
     L.mtb_blob_list_free.argtypes = [ctypes.POINTER(MtbBlobList)]
+    L.mtb_blob_list_fnv.argtypes = [ctypes.POINTER(MtbBlobList), ctypes.POINTER(ctypes.c_uint64)]
+    L.mtb_summarize_v1_many.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.c_int64, ctypes.c_int64, u32,
+                                        ctypes.POINTER(MtbBlobList)]
     L.mtb_matrix_summarize.argtypes = [vp, u32, ctypes.POINTER(MtbBlobList)]
     L.mtb_rewind.argtypes = [vp]
     L.mtb_map_range.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, u32,

@@ -274,6 +274,27 @@ class MergeTreeBatch:
         return blobs, summary
 
 
+    def summarize_v1_many(self, docs, msn=-1, seq=-1, threads=16, fingerprints=False):
+        """mtb_summarize_v1_many: the SnapshotV1 summaries of many documents (one replay, one bulk download,
+        host threads).  Returns [(blobs, summary)] per document, or with fingerprints=True the FNV-1a 64 of
+        each blob list (mtb_blob_list_fnv) without copying the summaries out."""
+        self._ensure_flushed()
+        n = len(docs)
+        lists = (_lib.MtbBlobList * max(1, n))()
+        ids = (ctypes.c_uint32 * max(1, n))(*docs)
+        self._chk(self._L.mtb_summarize_v1_many(self._h, n, ids, msn, seq, threads, lists))
+        out = []
+        for k in range(n):
+            if fingerprints:
+                h = ctypes.c_uint64()
+                self._L.mtb_blob_list_fnv(ctypes.byref(lists[k]), ctypes.byref(h))
+                self._L.mtb_blob_list_free(ctypes.byref(lists[k]))
+                out.append(h.value)
+            else:
+                out.append(_blob_list(self._L, lists[k]))
+        return out
+
+
 def _blob_list(L, lst):
     try:
         blobs = [(lst.blobs[i].path.decode(), ctypes.string_at(lst.blobs[i].content, lst.blobs[i].content_len).decode("utf-8"))

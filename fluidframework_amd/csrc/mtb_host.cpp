@@ -1173,22 +1173,9 @@ void run_digest(mtb_batch* b, mtb_stats& st) {
   st.bytes_alg += 24ull * st.segments_final + 2ull * st.text_units_final;
 }
 
-void download_doc(mtb_batch* b, uint32_t i) {
-  if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
-  HostDoc& d = b->docs[i];
-  if (d.cached) return;
-  if (!d.onDevice || !b->devInit || i >= b->hst.size()) raise(MTB_E_ARG, "document has not been replayed");
-  const DocState& s = b->hst[i];
-  std::vector<FBlk> fb(s.blk_used);
-  std::vector<uint32_t> segp(s.seg_used);
-  d.text.resize(s.text_used);
-  d.aux.resize(s.aux_used);
-  if (s.seg_used) HIPCHK(hipMemcpyAsync(segp.data(), b->dSegs.p + s.seg_base, s.seg_used * 4, hipMemcpyDeviceToHost, b->stream));
-  if (s.blk_used) HIPCHK(hipMemcpyAsync(fb.data(), b->dBlks.p + s.blk_base, s.blk_used * sizeof(FBlk), hipMemcpyDeviceToHost, b->stream));
-  if (s.text_used) HIPCHK(hipMemcpyAsync(d.text.data(), b->dText.p + s.text_base, s.text_used * 2, hipMemcpyDeviceToHost, b->stream));
-  if (s.aux_used) HIPCHK(hipMemcpyAsync(d.aux.data(), b->dAux.p + s.aux_base, s.aux_used * 4, hipMemcpyDeviceToHost, b->stream));
-  HIPCHK(hipStreamSynchronize(b->stream));
-  // host views: blocks from the records, segments from their parent's slot (hot fields live inline)
+// Host views of a document from its downloaded slices: blocks from the records, segments from their
+// parent's slot (hot fields live inline).
+void populate_doc(HostDoc& d, const DocState& s, const FBlk* fb, const uint32_t* segp) {
   d.blks.assign(s.blk_used, Blk{});
   d.segs.assign(s.seg_used, Seg{});
   for (uint32_t k = 0; k < s.seg_used; k++) d.segs[k].parent = MTB_NONE;
@@ -1219,6 +1206,71 @@ void download_doc(mtb_batch* b, uint32_t i) {
     }
   }
   d.cached = true;
+}
+
+void download_doc(mtb_batch* b, uint32_t i) {
+  if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
+  HostDoc& d = b->docs[i];
+  if (d.cached) return;
+  if (!d.onDevice || !b->devInit || i >= b->hst.size()) raise(MTB_E_ARG, "document has not been replayed");
+  const DocState& s = b->hst[i];
+  std::vector<FBlk> fb(s.blk_used);
+  std::vector<uint32_t> segp(s.seg_used);
+  d.text.resize(s.text_used);
+  d.aux.resize(s.aux_used);
+  if (s.seg_used) HIPCHK(hipMemcpyAsync(segp.data(), b->dSegs.p + s.seg_base, s.seg_used * 4, hipMemcpyDeviceToHost, b->stream));
+  if (s.blk_used) HIPCHK(hipMemcpyAsync(fb.data(), b->dBlks.p + s.blk_base, s.blk_used * sizeof(FBlk), hipMemcpyDeviceToHost, b->stream));
+  if (s.text_used) HIPCHK(hipMemcpyAsync(d.text.data(), b->dText.p + s.text_base, s.text_used * 2, hipMemcpyDeviceToHost, b->stream));
+  if (s.aux_used) HIPCHK(hipMemcpyAsync(d.aux.data(), b->dAux.p + s.aux_base, s.aux_used * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  populate_doc(d, s, fb.data(), segp.data());
+}
+
+// download_doc for many documents at once: every listed document's used slices are gathered on the
+// device into one staging buffer per element width (one kernel per pool), copied with two transfers,
+// and the host views are built on host threads.
+void download_docs(mtb_batch* b, const std::vector<uint32_t>& docs) {
+  std::vector<uint32_t> todo;
+  for (uint32_t i : docs) {
+    if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
+    if (b->docs[i].cached) continue;
+    if (!b->docs[i].onDevice || !b->devInit || i >= b->hst.size()) raise(MTB_E_ARG, "document has not been replayed");
+    todo.push_back(i);
+  }
+  if (todo.empty()) return;
+  const uint64_t bw = sizeof(FBlk) / 4;
+  Chunks seg, blk, aux, txt;
+  std::vector<uint64_t> oSeg(todo.size()), oBlk(todo.size()), oAux(todo.size()), oTxt(todo.size());
+  uint64_t nw = 0, nh = 0;
+  for (size_t k = 0; k < todo.size(); k++) {
+    const DocState& s = b->hst[todo[k]];
+    oSeg[k] = nw; seg.add(s.seg_base, nw, s.seg_used); nw += s.seg_used;
+    oBlk[k] = nw; blk.add(s.blk_base * bw, nw, (uint64_t)s.blk_used * bw); nw += (uint64_t)s.blk_used * bw;
+    oAux[k] = nw; aux.add(s.aux_base, nw, s.aux_used); nw += s.aux_used;
+    oTxt[k] = nh; txt.add(s.text_base, nh, s.text_used); nh += s.text_used;
+  }
+  DevBuf<uint32_t> dw;
+  DevBuf<uint16_t> dh;
+  dw.ensure(nw + 1);
+  dh.ensure(nh + 1);
+  move_words(b, b->dSegs.p, dw.p, seg);
+  move_words(b, b->dBlks.p, dw.p, blk);
+  move_words(b, b->dAux.p, dw.p, aux);
+  move_u16(b, b->dText.p, dh.p, txt);
+  std::vector<uint32_t> hw(nw + 1);
+  std::vector<uint16_t> hh(nh + 1);
+  if (nw) HIPCHK(hipMemcpyAsync(hw.data(), dw.p, nw * 4, hipMemcpyDeviceToHost, b->stream));
+  if (nh) HIPCHK(hipMemcpyAsync(hh.data(), dh.p, nh * 2, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  dw.release();
+  dh.release();
+  parallel_docs((uint32_t)todo.size(), [&](uint32_t k) {
+    HostDoc& d = b->docs[todo[k]];
+    const DocState& s = b->hst[todo[k]];
+    d.text.assign(hh.begin() + (long)oTxt[k], hh.begin() + (long)(oTxt[k] + s.text_used));
+    d.aux.assign(hw.begin() + (long)oAux[k], hw.begin() + (long)(oAux[k] + s.aux_used));
+    populate_doc(d, s, reinterpret_cast<const FBlk*>(hw.data() + oBlk[k]), hw.data() + oSeg[k]);
+  });
 }
 
 std::string derr_text(int e) {
@@ -2773,6 +2825,55 @@ int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_b
   });
 }
 
+// Client.summarize (SnapshotV1) of many documents: one replay for the optional updateSeqNumbers, one
+// bulk download of every listed document, and the summaries serialized on `threads` host threads.
+int mtb_summarize_v1_many(mtb_batch* b, uint32_t n, const uint32_t* docs, int64_t msn, int64_t seq, uint32_t threads,
+                          mtb_blob_list* out) {
+  return guarded(b, [&] {
+    if (n && (!docs || !out)) raise(MTB_E_ARG, "null argument");
+    std::vector<uint32_t> list(docs, docs + n);
+    for (uint32_t i : list) docref(b, i);
+    if (msn >= 0 && seq >= 0) {  // updateSeqNumbers(deltaManager.MSN, lastSequenceNumber) (client.ts:979)
+      for (uint32_t i : list) {
+        mtb_op r{};
+        r.type = MTB_OP_NOOP;
+        r.flags = MTB_F_LAST;
+        r.seq = (uint32_t)seq;
+        r.msn = (uint32_t)msn;
+        b->docs[i].pending.push_back(r);
+        b->docs[i].totalOps++;
+      }
+      replay(b, nullptr);
+    }
+    download_docs(b, list);
+    std::vector<std::string> errs(n);
+    std::atomic<uint32_t> next{0};
+    auto work = [&] {
+      for (uint32_t k = next++; k < n; k = next++) {
+        try {
+          std::vector<std::pair<std::string, std::string>> blobs;
+          std::string summary;
+          summarize(b, list[k], blobs, summary);
+          fill_blob_list(blobs, summary, &out[k]);
+        } catch (const MtbError& e) {
+          errs[k] = e.msg;
+          out[k] = mtb_blob_list{};
+        } catch (const std::exception& e) {
+          errs[k] = e.what();
+          out[k] = mtb_blob_list{};
+        }
+      }
+    };
+    const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, n));
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
+    work();
+    for (auto& t : ts) t.join();
+    for (uint32_t k = 0; k < n; k++)
+      if (!errs[k].empty()) raise(MTB_E_ARG, "document " + std::to_string(list[k]) + ": " + errs[k]);
+  });
+}
+
 int mtb_export_pending(mtb_batch* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out, uint16_t* payload,
                        size_t pcap, size_t* plen_out) {
   return guarded(b, [&] {
@@ -2817,6 +2918,29 @@ int mtb_client_long_id(mtb_batch* b, uint32_t doc, uint32_t short_id, char* buf,
       memcpy(buf, s.c_str(), s.size() + 1);
     }
   });
+}
+
+// FNV-1a 64 over a blob list: for each blob its path, a 0 byte, its content, a 0 byte; then the summary
+// JSON (the same definition as the checker's summary hash, oracle/loggen.cpp)
+int mtb_blob_list_fnv(const mtb_blob_list* l, uint64_t* out) {
+  if (!l || !out) return MTB_E_ARG;
+  uint64_t h = 1469598103934665603ull;
+  auto add = [&](const char* p, size_t n) {
+    for (size_t i = 0; i < n; i++) {
+      h ^= (unsigned char)p[i];
+      h *= 1099511628211ull;
+    }
+  };
+  const char z = 0;
+  for (uint32_t k = 0; k < l->count; k++) {
+    add(l->blobs[k].path, strlen(l->blobs[k].path));
+    add(&z, 1);
+    add(l->blobs[k].content, l->blobs[k].content_len);
+    add(&z, 1);
+  }
+  if (l->summary_json) add(l->summary_json, l->summary_json_len);
+  *out = h;
+  return MTB_OK;
 }
 
 void mtb_blob_list_free(mtb_blob_list* l) {

@@ -737,12 +737,14 @@ struct Eng {
     int ne = 0, nov = 0;
     int slen = 0, sseq = 0, srseq = -1;
     uint32_t scli = 0, srcx = 0;
+    bool sv = false;  // lane (k, s) holds a segment
     if (kblk) {
       const uint32_t* c = bw(ck);
       const int ccount = (int)c[FB_HDR];
       if (s < ccount) {
         const uint32_t sid = c[F_ID * 8 + s];
         if (sid & MTB_LEAF) {
+          sv = true;
           slen = (int)c[F_LEN * 8 + s];
           sseq = (int)c[F_SEQ * 8 + s];
           srseq = (int)c[F_RSEQ * 8 + s];
@@ -765,6 +767,22 @@ struct Eng {
     const int lincl = cscan8((int)lc);
     const int ltotal = rl(lincl, 7);
     const int lexcl = lincl - (int)lc;
+    // the parent of leaf blocks (splits and packs below the leaf level): only derived entries, written
+    // sorted straight from registers
+    if (ltotal == 0 && __ballot(nov > 0) == 0) {
+      bool ha, hb;
+      WEnt ea, eb;
+      derived2(sv, k, slen, sseq, srseq, scli, ha, ea, hb, eb);
+      uint32_t no, cnt, cap;
+      if (write_sorted2(ha, ea, hb, eb, no, cnt, cap)) {
+        if (bad()) return;
+        list_free(old_loff, old_lcap);
+        loff_out = no;
+        lcnt_out = cnt;
+        lcap_out = cap;
+        return;
+      }
+    }
     int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
     for (int q = 0; q < MTB_MAXCH; q++) {
@@ -1019,7 +1037,7 @@ struct Eng {
   }
   // Split every full block on the path, from depth d upwards.  Written as a state machine with a
   // single list-rebuild site (the halves of an internal split, the new root, the parent).
-  __device__ __forceinline__ void fix_overflow_slow(int d) {
+  __device__ __noinline__ void fix_overflow_slow(int d) {
     int level = d;
     int phase = 0;  // 0 split `level` | 1 rebuild left half | 2 rebuild right half | 3 link | 4 parent done | 5 root done
     uint32_t b = MTB_NONE, nb = MTB_NONE;
@@ -2027,8 +2045,110 @@ struct Eng {
     }
     wsync();
   }
+  // A new window list holding the entries ea (lanes with ha) and eb (lanes with hb), at most two per
+  // lane, in seq order: a counting sort over seq - minSeq - 1 in the scour union (no caller holds it live
+  // here), straight from registers.  Returns false, having written nothing, if a seq falls outside the
+  // buckets.
+  __device__ __forceinline__ bool write_sorted2(bool ha, const WEnt& ea, bool hb, const WEnt& eb, uint32_t& no_out,
+                                                uint32_t& cnt_out, uint32_t& cap_out) {
+    const int ba = ea.seq - minSeq - 1, bb = eb.seq - minSeq - 1;
+    if (__ballot((ha && (ba < 0 || ba >= MTB_SORT_BUCKETS)) || (hb && (bb < 0 || bb >= MTB_SORT_BUCKETS)))) return false;
+    const uint32_t T = (uint32_t)(__popcll(__ballot(ha)) + __popcll(__ballot(hb)));
+    uint32_t* hist = &sh->hold[0][0];
+    wsync();
+    for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
+    wsync();
+    if (ha) atomicAdd(&hist[ba >> 1], 1u << ((ba & 1) * 16));
+    if (hb) atomicAdd(&hist[bb >> 1], 1u << ((bb & 1) * 16));
+    wsync();
+    uint32_t tot = 0;
+    for (int k = 0; k < 8; k++) {
+      const uint32_t w = hist[8 * lane + k];
+      tot += (w & 0xFFFF) + (w >> 16);
+    }
+    int incl = (int)tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    uint32_t run = (uint32_t)incl - tot;
+    for (int k = 0; k < 8; k++) {  // (the words are read again: keeps register pressure low)
+      const uint32_t w = hist[8 * lane + k];
+      const uint32_t c0 = run;
+      run += w & 0xFFFF;
+      hist[8 * lane + k] = c0 | (run << 16);
+      run += w >> 16;
+    }
+    wsync();
+    uint32_t cap;
+    const uint32_t no = list_alloc(T + T / 2 + 4, cap);
+    if (bad()) return true;
+    if (ha) {
+      const uint32_t sft = (uint32_t)(ba & 1) * 16;
+      lst[no + ((atomicAdd(&hist[ba >> 1], 1u << sft) >> sft) & 0xFFFF)] = ea;
+    }
+    if (hb) {
+      const uint32_t sft = (uint32_t)(bb & 1) * 16;
+      lst[no + ((atomicAdd(&hist[bb >> 1], 1u << sft) >> sft) & 0xFFFF)] = eb;
+    }
+    wsync();
+    no_out = no;
+    cnt_out = T;
+    cap_out = cap;
+    return true;
+  }
+  // Derived window-list entries of a segment (the combine semantics of partialLengths.ts:256 that
+  // rebuild() applies to the segments of its leaf-block children): insert (seq, client, +len) above
+  // minSeq, removal (removedSeq, removedClientIds[0], -len) above minSeq, tagged with the slot k of the
+  // block that holds the segment.
+  __device__ __forceinline__ void derived2(bool valid, int k, int len, int sq, int rs, uint32_t cl, bool& ha, WEnt& ea,
+                                           bool& hb, WEnt& eb) const {
+    ha = valid && sq > minSeq;
+    hb = valid && rs >= 0 && rs > minSeq;
+    ea.seq = sq;
+    ea.ck = WE_KEY(cli_client(cl), WK_MAIN, k);
+    ea.delta = len;
+    ea.pad = 0;
+    eb.seq = rs;
+    eb.ck = WE_KEY(cli_rc0(cl), WK_MAIN, k);
+    eb.delta = -len;
+    eb.pad = 0;
+  }
+  // The parent's list after packParent spread leaf children over new blocks: the derived entries of the
+  // kept segments still in hold[.][0, nh) -- segment i went to new block q(i) (`base` children each, the
+  // first `rem` one more) -- instead of rebuild() re-reading the records just written.  Returns false,
+  // having changed nothing, when a segment has overlapping removers or the seq window is too wide for
+  // the sort (the caller then runs rebuild()).
+  __device__ __forceinline__ bool rebuild_from_hold(int nh, int base, int rem, uint32_t old_loff, uint32_t old_lcap,
+                                                    uint32_t& loff_out, uint32_t& lcnt_out, uint32_t& lcap_out) {
+    int len = 0, sq = 0, rs = -1;
+    uint32_t cl = 0, rx = 0;
+    if (lane < nh) {
+      len = (int)sh->hold[F_LEN][lane];
+      sq = (int)sh->hold[F_SEQ][lane];
+      rs = (int)sh->hold[F_RSEQ][lane];
+      cl = sh->hold[F_CLI][lane];
+      rx = sh->hold[F_RCX][lane];
+    }
+    const int big = rem * (base + 1);
+    const int q = lane < big ? lane / (base + 1) : rem + (lane - big) / (base > 0 ? base : 1);
+    bool ha, hb;
+    WEnt ea, eb;
+    derived2(lane < nh, q, len, sq, rs, cl, ha, ea, hb, eb);
+    if (__ballot(hb && rx != 0)) return false;
+    uint32_t no, cnt, cap;
+    if (!write_sorted2(ha, ea, hb, eb, no, cnt, cap)) return false;
+    if (bad()) return true;
+    PROF_CNT(CN_REBUILD, 1);
+    list_free(old_loff, old_lcap);
+    loff_out = no;
+    lcnt_out = cnt;
+    lcap_out = cap;
+    return true;
+  }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
-  __device__ __forceinline__ void pack_parent(uint32_t parent) {
+  __device__ __noinline__ void pack_parent(uint32_t parent) {
     while (!err) {
       PROF_CNT(CN_PACK, 1);
       stage_rec(parent);
@@ -2043,7 +2163,8 @@ struct Eng {
       const uint32_t ploff = U(ploff_v), pcap = U(pcap_v);
       const int nh = scour(pc, 0);
       if (bad()) return;
-      int cc = 0;
+      int cc = 0, base = 0, rem0 = 0;
+      bool leafcase = true;  // the new blocks' children are segments
       if (nh > 0) {
         cc = nh / (MTB_MAXCH / 2);
         if (cc > MTB_MAXCH - 1) cc = MTB_MAXCH - 1;
@@ -2056,8 +2177,9 @@ struct Eng {
         list_free(rlu(kloff, i), rlu(kcap, i));
       }
       if (nh > 0) {
-        const int base = nh / cc;
-        int rem = nh % cc;
+        base = nh / cc;
+        rem0 = nh % cc;
+        int rem = rem0;
         int taken = 0;
         // first every new block gets its children (the scour output in hold[] is consumed here) ...
         uint32_t nbs = 0;  // lane q: new block q, its observer length, whether its children are blocks
@@ -2074,6 +2196,7 @@ struct Eng {
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
           const int kb = __ballot(kblk) != 0;
+          if (kb) leafcase = false;
           if (lane == q) {
             nbs = nb;
             lens = len;
@@ -2118,7 +2241,7 @@ struct Eng {
       if (lane == 0) blk[parent].count = (uint32_t)cc;
       wsync();
       uint32_t a, c2, e;
-      rebuild(parent, ploff, pcap, a, c2, e);
+      if (!(leafcase && nh > 0 && rebuild_from_hold(nh, base, rem0, ploff, pcap, a, c2, e))) rebuild(parent, ploff, pcap, a, c2, e);
       if (bad()) return;
       store_meta_of(parent, pparent, pindex, a, c2, e);
       if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {

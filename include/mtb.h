@@ -203,6 +203,15 @@ int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_
 int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,
                      mtb_blob_list* out);
 void mtb_blob_list_free(mtb_blob_list* l);
+/* mtb_summarize_v1 for n documents at once (out[k] for docs[k]; free each with mtb_blob_list_free): one
+ * replay for the optional updateSeqNumbers(msn, seq), one bulk download of the documents' slices and the
+ * summaries serialized on `threads` host threads.  No reference counterpart (the reference summarizes
+ * one channel at a time); each blob list equals what mtb_summarize_v1 returns for that document. */
+int mtb_summarize_v1_many(mtb_batch* b, uint32_t n, const uint32_t* docs, int64_t msn, int64_t seq, uint32_t threads,
+                          mtb_blob_list* out);
+/* FNV-1a 64 over a blob list (each blob's path, 0, content, 0; then the summary JSON): a compact
+ * fingerprint for comparing many summaries with a checker without copying them out. */
+int mtb_blob_list_fnv(const mtb_blob_list* l, uint64_t* out);
 /* Client.summarize without newMergeTreeSnapshotFormat (client.ts:999-1003, snapshotlegacy.ts:122-259):
  * "header" / "body" chunks of the segments at the MSN, plus a "catchupOps" blob holding
  * `catchup_json` (a JSON array of the messages above the MSN that the caller keeps, as

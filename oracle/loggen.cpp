@@ -84,6 +84,8 @@ struct loggen_doc {
   uint32_t final_segments;
   int32_t error;
   uint64_t digest;        // oracle's final state digest v1 (Doc::digest, DESIGN.md "State digest")
+  uint64_t summary_fnv;   // FNV-1a 64 of the final SnapshotV1 summary (each blob's path, 0, content, 0; then
+                          // the ISummaryTreeWithStats JSON), the engine's mtb_blob_list_fnv definition
 };
 
 }  // extern "C"
@@ -240,6 +242,24 @@ static int gen_one(const loggen_cfg& cfg, uint32_t docIndex, loggen_doc* out) {
   std::string dump = doc.dumpSegments();
   out->checksum = fnv1a64(dump);
   out->digest = doc.digest();
+  {
+    std::string summary;
+    const auto blobs = doc.summarizeV1(&summary);
+    uint64_t h = 1469598103934665603ull;
+    auto add = [&](const std::string& x, bool zero) {
+      for (unsigned char c : x) {
+        h ^= c;
+        h *= 1099511628211ull;
+      }
+      if (zero) h *= 1099511628211ull;  // (FNV-1a of a 0 byte: xor 0, multiply)
+    };
+    for (auto& bl : blobs) {
+      add(bl.first, true);
+      add(bl.second, true);
+    }
+    add(summary, false);
+    out->summary_fnv = h;
+  }
   out->ops_applied = doc.mt.counters.ops;
   out->segs_touched = doc.mt.counters.segsTouched;
   out->final_len = (uint32_t)doc.mt.length();

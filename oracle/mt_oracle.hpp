@@ -202,6 +202,9 @@ class MergeTree {
   // mapRange (mergeTree.ts:2456-2474) over [start, end) (end < 0: the whole (refSeq, clientId) length)
   void mapRange(int refSeq, int clientId, int start, int end, const std::function<bool(Seg*, int, int, int)>& f);
 
+  // packParent(root) as the reference's zamboni tests call it directly (mergeTree.zamboni.spec.ts)
+  void packParentRoot() { packParent(root); }
+
   // text / walks
   u16str getText();
   template <class F> void walkAllSegments(F&& f);

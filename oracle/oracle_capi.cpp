@@ -321,6 +321,13 @@ int orc_dump_segments(orc_doc* d, char** out, size_t* len) {
 }
 uint64_t orc_checksum(orc_doc* d) { return fnv1a64(d->doc.dumpSegments()); }
 uint64_t orc_digest(orc_doc* d) { return d->doc.digest(); }
+// direct zamboniSegments / packParent(root) calls (the reference's zamboni tests, mergeTree.zamboni.spec.ts)
+int orc_zamboni(orc_doc* d) {
+  return guard(d, [&] { d->doc.mt.zamboniSegments(); });
+}
+int orc_pack_parent_root(orc_doc* d) {
+  return guard(d, [&] { d->doc.mt.packParentRoot(); });
+}
 // Client.load of a SnapshotV1 summary: blobs_json = [[path, content], ...] (as orc_summarize_v1 returns)
 int orc_load_v1(orc_doc* d, const char* blobs_json, size_t len, const char* observer_id) {
   return guard(d, [&] {

@@ -23,7 +23,8 @@ class LoggenDoc(ctypes.Structure):
                 ("client_writer", ctypes.c_uint16 * 256), ("n_short", ctypes.c_uint32),
                 ("checksum", ctypes.c_uint64), ("ops_applied", ctypes.c_uint64),
                 ("segs_touched", ctypes.c_uint64), ("final_len", ctypes.c_uint32),
-                ("final_segments", ctypes.c_uint32), ("error", ctypes.c_int32), ("digest", ctypes.c_uint64)]
+                ("final_segments", ctypes.c_uint32), ("error", ctypes.c_int32), ("digest", ctypes.c_uint64),
+                ("summary_fnv", ctypes.c_uint64)]
 
 
 class LoggenMatrix(ctypes.Structure):

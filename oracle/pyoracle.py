@@ -52,6 +52,8 @@ def lib():
         L.orc_checksum.argtypes = [vp]
         L.orc_digest.restype = ctypes.c_uint64
         L.orc_digest.argtypes = [vp]
+        L.orc_zamboni.argtypes = [vp]
+        L.orc_pack_parent_root.argtypes = [vp]
         L.orc_load_v1.argtypes = [vp, cp, sz, cp]
         L.orc_enable_catch_up.argtypes = [vp]
         L.orc_summarize_legacy.argtypes = [vp, i, i, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
@@ -294,6 +296,14 @@ class OracleDoc:
 
     def checksum(self):
         return self._L.orc_checksum(self._h)
+
+    def zamboni(self):
+        """zamboniSegments(mergeTree) called directly (mergeTree.zamboni.spec.ts)."""
+        self._chk(self._L.orc_zamboni(self._h))
+
+    def pack_parent_root(self):
+        """packParent(mergeTree.root) called directly (mergeTree.zamboni.spec.ts)."""
+        self._chk(self._L.orc_pack_parent_root(self._h))
 
     def digest(self):
         """State digest v1 (DESIGN.md "State digest"), as the engine's mtb_doc_digests computes it."""

@@ -86,7 +86,8 @@ def test_cfg5_annotate_heavy_strings(new_mode):
 
 
 def test_cfg2_slice_full_length_logs():
-    """configs[1] slice: 64 documents x 10,000 messages (the bench's per-document length), 8 clients."""
+    """configs[1] slice: 64 documents x 10,000 messages (the bench's per-document length), 8 clients; the
+    north star's SnapshotV1 summaries of every document byte-equal to the oracle's (batched summarize)."""
     from pyloggen import LogBatch, make_cfg
     cfg = make_cfg(seed=202, n_ops=10000)
     lb = LogBatch(cfg, 0, 64)
@@ -94,3 +95,9 @@ def test_cfg2_slice_full_length_logs():
     docs = load_logbatch(B, lb)
     st = B.replay()
     _check(B, lb, docs, st)
+    fps = B.summarize_v1_many(list(range(lb.n)), threads=8, fingerprints=True)
+    bad = [j for j in range(lb.n) if fps[j] != lb.docs[j].summary_fnv]
+    assert not bad, f"{len(bad)}/{lb.n} SnapshotV1 summaries differ from the oracle's (first: {bad[:5]})"
+    full = B.summarize_v1_many([3, 17], threads=2)
+    assert [list(map(list, full[0][0])), full[0][1]] == [list(map(list, B.summarize_v1(3)[0])), B.summarize_v1(3)[1]]
+    assert full[1][0] == B.summarize_v1(17)[0]
