@@ -10,7 +10,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", "mtb_replay.hip"), os.path.join(HERE, "csrc", "mtb_host.cpp")]
+SRCS = [os.path.join(HERE, "csrc", "mtb_replay.hip"), os.path.join(HERE, "csrc", "mtb_host.cpp"),
+        os.path.join(HERE, "csrc", "mtb_multi.cpp")]
 OUT = os.path.join(HERE, "libmtb.so")
 NAPI_SRC = os.path.join(HERE, "js", "src", "mtb_napi.c")
 NAPI_OUT = os.path.join(HERE, "js", "mtb_napi.node")

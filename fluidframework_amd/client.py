@@ -39,14 +39,16 @@ def _check(L, h, rc):
 
 
 class MergeTreeBatch:
-    """A batch of independent merge-tree documents replayed together on one MI355X."""
+    """A batch of independent merge-tree documents replayed together on one MI355X, or spread over several
+    (`devices`: documents by hash, each device replaying its share at the same time)."""
 
-    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0, catch_up=False, _flags=0):
+    def __init__(self, ndocs, new_length_calc=False, chunk_size=0, device=0, catch_up=False, _flags=0, devices=None):
         """catch_up: keep SharedSegmentSequence's catch-up messages (legacy summaries, MTB_BATCH_CATCHUP)."""
         self._L = _lib.lib()
         opts = _lib.MtbOptions(int(bool(new_length_calc)), int(chunk_size), 64, int(_flags) | (2 if catch_up else 0))
         h = ctypes.c_void_p()
-        rc = self._L.mtb_batch_create(ctypes.byref(opts), ndocs, 1 << device, ctypes.byref(h))
+        mask = sum(1 << d for d in devices) if devices else 1 << device
+        rc = self._L.mtb_batch_create(ctypes.byref(opts), ndocs, mask, ctypes.byref(h))
         if rc != 0:
             raise MergeTreeError(rc, "mtb_batch_create failed")
         self._h = h

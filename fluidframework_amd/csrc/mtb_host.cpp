@@ -26,6 +26,7 @@
 
 #include "../../include/mtb.h"
 #include "hjson.hpp"
+#include "mtb_dev.h"
 #include "mtb_device.h"
 
 // defined in mtb_replay.hip
@@ -389,7 +390,7 @@ struct Chunks {
 
 }  // namespace
 
-struct mtb_batch {
+struct mtb_dev {
   mtb_options opts{};
   uint32_t ndocs = 0;
   int device = 0;
@@ -431,7 +432,7 @@ struct mtb_batch {
   DevBuf<uint64_t> dMvSrc, dMvDst;
   DevBuf<uint32_t> dMvLen, dStageW;
   DevBuf<uint16_t> dStageH;
-  ~mtb_batch() {
+  ~mtb_dev() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
     dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release(); dKHash.release(); dVHash.release(); dDigest.release();
@@ -445,8 +446,11 @@ struct mtb_batch {
 namespace {
 
 template <class F>
-int guarded(mtb_batch* b, F&& f) {
+int guarded(mtb_dev* b, F&& f) {
   if (!b) return MTB_E_ARG;
+  // HIP's current device is per host thread: a batch driven from several threads (the multi-device
+  // front end replays its shards in parallel) selects its device on every entry
+  if (b->stream) (void)hipSetDevice(b->device);
   try {
     f();
     return MTB_OK;
@@ -462,7 +466,7 @@ int guarded(mtb_batch* b, F&& f) {
   }
 }
 
-HostDoc& docref(mtb_batch* b, uint32_t doc) {
+HostDoc& docref(mtb_dev* b, uint32_t doc) {
   if (doc >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
   return b->docs[doc];
 }
@@ -484,7 +488,7 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel) {
 }
 
 // One delta op -> record (client.ts:489-524 insert, :430 remove, :457 annotate)
-void pack_delta(mtb_batch* b, HostDoc& d, const hj::Value& op, mtb_op base, std::vector<mtb_op>& out) {
+void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::vector<mtb_op>& out) {
   const hj::Value* t = member(op, u"type");
   const int type = t && t->kind == hj::Value::kNum ? (int)t->n : -1;
   mtb_op r = base;
@@ -572,7 +576,7 @@ struct PropsCache {
   std::unordered_map<std::string, uint32_t> ids;
 };
 
-LoadSeg load_spec(mtb_batch* b, HostDoc& d, const hj::Value& spec, std::vector<uint16_t>& sink, PropsCache* pc) {
+LoadSeg load_spec(mtb_dev* b, HostDoc& d, const hj::Value& spec, std::vector<uint16_t>& sink, PropsCache* pc) {
   LoadSeg g;
   const bool mergeInfo = spec.kind == hj::Value::kObj && member(spec, u"json");
   const hj::Value& js = mergeInfo ? *member(spec, u"json") : spec;
@@ -776,7 +780,7 @@ void build_load_image(HostDoc& d, const std::vector<LoadSeg>& hdr) {
 }
 
 // Header segments' props ids -> global property-set handles (after every parallel load has interned).
-void resolve_load_props(mtb_batch* b, HostDoc& d) {
+void resolve_load_props(mtb_dev* b, HostDoc& d) {
   for (FBlk& f : d.img.blks)
     for (uint32_t k = 0; k < f.count; k++)
       if ((f.f[F_ID][k] & MTB_LEAF) && f.f[F_PROPS][k]) f.f[F_PROPS][k] = MTB_GPROPS | b->in.pidx[2 * f.f[F_PROPS][k] + 1];
@@ -784,7 +788,7 @@ void resolve_load_props(mtb_batch* b, HostDoc& d) {
 
 // Client.load of one SnapshotV1 summary into the fresh document d (client.ts:1007 -> SnapshotLoader,
 // snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in parallel.
-void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
+void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
               PropsCache* pc, const std::string& prefix = std::string()) {
   if (b->matrix && !d.perm) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_load");
   if (d.inited || d.onDevice) raise(MTB_E_ARG, "document already initialised");
@@ -873,7 +877,7 @@ void load_one(mtb_batch* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, 
 }
 
 // ------------------------------------------------------------------ device management
-void ensure_stream(mtb_batch* b) {
+void ensure_stream(mtb_dev* b) {
   if (b->stream) return;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) raise(MTB_E_NODEV, "no HIP device available (the engine has no CPU fallback)");
@@ -883,7 +887,7 @@ void ensure_stream(mtb_batch* b) {
   HIPCHK(hipEventCreate(&b->ev1));
 }
 
-void upload_chunks(mtb_batch* b, const Chunks& c) {
+void upload_chunks(mtb_dev* b, const Chunks& c) {
   b->dMvSrc.ensure(c.src.size());
   b->dMvDst.ensure(c.dst.size());
   b->dMvLen.ensure(c.len.size());
@@ -892,33 +896,33 @@ void upload_chunks(mtb_batch* b, const Chunks& c) {
   HIPCHK(hipMemcpyAsync(b->dMvLen.p, c.len.data(), c.len.size() * 4, hipMemcpyHostToDevice, b->stream));
 }
 // device words -> device words
-void move_words(mtb_batch* b, const void* src, void* dst, const Chunks& c) {
+void move_words(mtb_dev* b, const void* src, void* dst, const Chunks& c) {
   if (c.len.empty()) return;
   upload_chunks(b, c);
   HIPCHK(mtb_launch_move_words(b->stream, (const uint32_t*)src, b->dMvSrc.p, (uint32_t*)dst, b->dMvDst.p, b->dMvLen.p,
                                (uint32_t)c.len.size()));
   HIPCHK(hipStreamSynchronize(b->stream));
 }
-void move_u16(mtb_batch* b, const uint16_t* src, uint16_t* dst, const Chunks& c) {
+void move_u16(mtb_dev* b, const uint16_t* src, uint16_t* dst, const Chunks& c) {
   if (c.len.empty()) return;
   upload_chunks(b, c);
   HIPCHK(mtb_launch_move_u16(b->stream, src, b->dMvSrc.p, dst, b->dMvDst.p, b->dMvLen.p, (uint32_t)c.len.size()));
   HIPCHK(hipStreamSynchronize(b->stream));
 }
 // host words -> device (via one staging upload)
-void scatter_words(mtb_batch* b, const std::vector<uint32_t>& host, void* dst, const Chunks& c) {
+void scatter_words(mtb_dev* b, const std::vector<uint32_t>& host, void* dst, const Chunks& c) {
   if (c.len.empty()) return;
   b->dStageW.ensure(host.size());
   HIPCHK(hipMemcpyAsync(b->dStageW.p, host.data(), host.size() * 4, hipMemcpyHostToDevice, b->stream));
   move_words(b, b->dStageW.p, dst, c);
 }
-void scatter_u16(mtb_batch* b, const uint16_t* host, size_t n, uint16_t* dst, const Chunks& c) {
+void scatter_u16(mtb_dev* b, const uint16_t* host, size_t n, uint16_t* dst, const Chunks& c) {
   if (c.len.empty()) return;
   b->dStageH.ensure(n);
   HIPCHK(hipMemcpyAsync(b->dStageH.p, host, n * 2, hipMemcpyHostToDevice, b->stream));
   move_u16(b, b->dStageH.p, dst, c);
 }
-void scatter_u16(mtb_batch* b, const std::vector<uint16_t>& host, uint16_t* dst, const Chunks& c) {
+void scatter_u16(mtb_dev* b, const std::vector<uint16_t>& host, uint16_t* dst, const Chunks& c) {
   scatter_u16(b, host.data(), host.size(), dst, c);
 }
 // f(i) for every document i, on up to 16 host threads (documents are independent)
@@ -977,7 +981,7 @@ bool fits(const DocState& s, const Caps& c) {
 }
 
 // (Re)lay out every document's slices so that each holds at least `want[i]`, copying live state.
-void layout(mtb_batch* b, const std::vector<Caps>& want) {
+void layout(mtb_dev* b, const std::vector<Caps>& want) {
   b->haveRewind = false;  // slice bases move: the pristine snapshot is no longer valid
   std::vector<DocState> ns = b->hst;
   uint64_t seg = 0, blk = 0, lst = 0, txt = 0, hp = 0, ax = 0;
@@ -1035,7 +1039,7 @@ void layout(mtb_batch* b, const std::vector<Caps>& want) {
   b->hst = ns;
 }
 
-void device_init(mtb_batch* b) {
+void device_init(mtb_dev* b) {
   ensure_stream(b);
   b->hst.assign(b->ndocs, DocState{});
   std::vector<Caps> want(b->ndocs);
@@ -1131,7 +1135,7 @@ void device_init(mtb_batch* b) {
   b->devInit = true;
 }
 
-void upload_tables(mtb_batch* b) {
+void upload_tables(mtb_dev* b) {
   Interner& in = b->in;
   if (!in.dirty && b->dPool.p) return;
   auto up = [&](auto& buf, const auto& vec) {
@@ -1156,7 +1160,7 @@ void upload_tables(mtb_batch* b) {
 // State digest v1 of every document (mtb_digest_kernel) after a replay: fills the stats' segments_final,
 // text_units_final and checksum (sum of the per-document digests mod 2^64) and keeps the per-document
 // values for mtb_doc_digests.
-void run_digest(mtb_batch* b, mtb_stats& st) {
+void run_digest(mtb_dev* b, mtb_stats& st) {
   b->dDigest.ensure(3ull * b->ndocs);
   HIPCHK(mtb_launch_digest(b->stream, b->ndocs, b->dDocs.p, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p, b->dKHash.p,
                            b->dVHash.p, b->dDigest.p));
@@ -1208,7 +1212,7 @@ void populate_doc(HostDoc& d, const DocState& s, const FBlk* fb, const uint32_t*
   d.cached = true;
 }
 
-void download_doc(mtb_batch* b, uint32_t i) {
+void download_doc(mtb_dev* b, uint32_t i) {
   if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
   HostDoc& d = b->docs[i];
   if (d.cached) return;
@@ -1229,7 +1233,7 @@ void download_doc(mtb_batch* b, uint32_t i) {
 // download_doc for many documents at once: every listed document's used slices are gathered on the
 // device into one staging buffer per element width (one kernel per pool), copied with two transfers,
 // and the host views are built on host threads.
-void download_docs(mtb_batch* b, const std::vector<uint32_t>& docs) {
+void download_docs(mtb_dev* b, const std::vector<uint32_t>& docs) {
   std::vector<uint32_t> todo;
   for (uint32_t i : docs) {
     if (i >= b->ndocs) raise(MTB_E_ARG, "document index out of range");
@@ -1297,7 +1301,7 @@ int derr_code(int e) {
 }
 
 // Snapshot the freshly initialised documents (before their first replay) for mtb_rewind.
-void capture_pristine(mtb_batch* b) {
+void capture_pristine(mtb_dev* b) {
   b->hPristine = b->hst;
   b->dPristine.ensure(b->ndocs);
   b->dPSeg.ensure(b->ndocs);
@@ -1357,10 +1361,10 @@ struct PhaseClock {
   }
 };
 
-void resolve_catch_up(mtb_batch* b, uint32_t i);
-void apply_cell_events(mtb_batch* b, uint32_t matrix);
+void resolve_catch_up(mtb_dev* b, uint32_t i);
+void apply_cell_events(mtb_dev* b, uint32_t matrix);
 
-void replay(mtb_batch* b, mtb_stats* out) {
+void replay(mtb_dev* b, mtb_stats* out) {
   PhaseClock pc;
   // documents that failed in an earlier replay stay failed (sticky) and are counted in the stats, but
   // only a failure of this replay is reported as the call's error (the reference throws once, from
@@ -1630,14 +1634,14 @@ struct PropView {
   const uint32_t* p = nullptr;  // [n, (k, v)*n]
   uint32_t n() const { return p ? p[0] : 0; }
 };
-PropView props_of(mtb_batch* b, const HostDoc& d, uint32_t h) {
+PropView props_of(mtb_dev* b, const HostDoc& d, uint32_t h) {
   PropView v;
   if (!h) return v;
   if (h & MTB_GPROPS) v.p = b->in.pool.data() + (h & ~MTB_GPROPS);
   else v.p = d.aux.data() + h;
   return v;
 }
-void props_json(mtb_batch* b, std::string& o, PropView v) {
+void props_json(mtb_dev* b, std::string& o, PropView v) {
   o += '{';
   for (uint32_t i = 0; i < v.n(); i++) {
     if (i) o += ',';
@@ -1647,7 +1651,7 @@ void props_json(mtb_batch* b, std::string& o, PropView v) {
   }
   o += '}';
 }
-bool props_match(mtb_batch* b, PropView a, PropView c) {
+bool props_match(mtb_dev* b, PropView a, PropView c) {
   if (a.n() != c.n()) return false;
   for (uint32_t i = 0; i < a.n(); i++) {
     bool found = false;
@@ -1684,7 +1688,7 @@ std::string handle_table_json(const HostDoc& d) {
   return o + "]";
 }
 
-std::string dump_doc(mtb_batch* b, uint32_t i) {
+std::string dump_doc(mtb_dev* b, uint32_t i) {
   download_doc(b, i);
   const HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
@@ -1758,7 +1762,7 @@ uint64_t utf8_byte_length(const std::string& utf8) {
 }
 
 // SnapshotV1.extractSync + emit (snapshotV1.ts:122-312) over the downloaded document.
-void summarize(mtb_batch* b, uint32_t i, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
+void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
   download_doc(b, i);
   const HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
@@ -1957,7 +1961,7 @@ void drop_catch_up(HostDoc& d, int64_t minSeq) {
 }
 
 // Client.applyMsg (client.ts:858-887) -> records appended to d
-void apply_msg(mtb_batch* b, HostDoc& d, const hj::Value& msg) {
+void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
   {
     if (msg.kind != hj::Value::kObj) raise(MTB_E_PARSE, "message is not an object");
     const hj::Value* cid = member(msg, u"clientId");
@@ -2080,7 +2084,7 @@ bool js_match_props(const hj::Value* a, const hj::Value* b) {
 // Replay one matrix's cell events of this replay into its CellStore.  Both vectors' record streams hold
 // every setCell; a clear logged at record k of either stream happened after the setCells before k and
 // before the next one, and clears commute with each other, so events are merged by setCell ordinal.
-void apply_cell_events(mtb_batch* b, uint32_t m) {
+void apply_cell_events(mtb_dev* b, uint32_t m) {
   HostDoc& R = b->docs[2 * m];
   if (!R.cells) R.cells.reset(new CellStore());
   struct Ev { uint32_t epoch, kind, a, n; };
@@ -2127,7 +2131,7 @@ void apply_cell_events(mtb_batch* b, uint32_t m) {
 // Rewrite the lagging catch-up messages of this replay from their records' delta entries:
 // SharedSegmentSequence.createOpsFromDelta (sequence.ts:120-172) per delta event, the message then
 // stored with referenceSequenceNumber = seq - 1 and the ops (a GROUP unless exactly one) as contents.
-void resolve_catch_up(mtb_batch* b, uint32_t i) {
+void resolve_catch_up(mtb_dev* b, uint32_t i) {
   HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
   std::vector<uint32_t> ent(4 * (size_t)s.delta_used);
@@ -2248,7 +2252,7 @@ void resolve_catch_up(mtb_batch* b, uint32_t i) {
 // segment in the MSN view (inserted at or below the MSN, not removed at or below it), coalesced with
 // canAppend + matchProperties, split into "header" (first mergeTreeSnapshotChunkSize chars) and "body",
 // plus the catch-up messages blob (sequence.ts:680-692) when given.
-void summarize_legacy(mtb_batch* b, uint32_t i, const std::string& catchUp, std::vector<std::pair<std::string, std::string>>& blobs,
+void summarize_legacy(mtb_dev* b, uint32_t i, const std::string& catchUp, std::vector<std::pair<std::string, std::string>>& blobs,
                       std::string& summaryJson) {
   download_doc(b, i);
   const HostDoc& d = b->docs[i];
@@ -2394,9 +2398,9 @@ char* dup(const std::string& s) {
 // ====================================================================== C ABI
 extern "C" {
 
-int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_mask, mtb_batch** out) {
+int mtbx_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_mask, mtb_dev** out) {
   if (!out || ndocs == 0) return MTB_E_ARG;
-  auto* b = new mtb_batch();
+  auto* b = new mtb_dev();
   if (opts) b->opts = *opts;
   b->matrix = (b->opts.flags & MTB_BATCH_MATRIX) != 0;
   if (b->matrix && (ndocs & 1)) {
@@ -2412,11 +2416,11 @@ int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_ma
   return MTB_OK;
 }
 
-void mtb_batch_destroy(mtb_batch* b) { delete b; }
-const char* mtb_last_error(mtb_batch* b) { return b ? b->err.c_str() : "null batch"; }
+void mtbx_batch_destroy(mtb_dev* b) { delete b; }
+const char* mtbx_last_error(mtb_dev* b) { return b ? b->err.c_str() : "null batch"; }
 void mtb_free(void* p) { free(p); }
 
-int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_t n_units, const char* observer_long_id,
+int mtbx_doc_init(mtb_dev* b, uint32_t doc, const uint16_t* initial_text, size_t n_units, const char* observer_long_id,
                  uint32_t min_seq, uint32_t cur_seq) {
   return guarded(b, [&] {
     if (b->matrix) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_init");
@@ -2434,7 +2438,7 @@ int mtb_doc_init(mtb_batch* b, uint32_t doc, const uint16_t* initial_text, size_
 }
 
 // Client.load of a SnapshotV1 summary (client.ts:1007 -> SnapshotLoader.initialize, snapshotLoader.ts:41-257).
-int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
+int mtbx_doc_load_v1(mtb_dev* b, uint32_t doc, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     try {
@@ -2450,7 +2454,7 @@ int mtb_doc_load_v1(mtb_batch* b, uint32_t doc, const mtb_blob* blobs, uint32_t 
 // Many documents at once: blobs are parsed and headers rebuilt on `threads` host threads (the batch's
 // props table is shared under a lock).  On failure the first failing document's error is returned and
 // that document (and every other failing one) is left fresh; the others are loaded.
-int mtb_docs_load_v1(mtb_batch* b, uint32_t n, const uint32_t* docs, const mtb_blob* const* blobs,
+int mtbx_docs_load_v1(mtb_dev* b, uint32_t n, const uint32_t* docs, const mtb_blob* const* blobs,
                      const uint32_t* nblobs, const char* const* observer_long_ids, uint32_t threads) {
   return guarded(b, [&] {
     if (n && (!docs || !blobs || !nblobs || !observer_long_ids)) raise(MTB_E_ARG, "null argument");
@@ -2496,18 +2500,18 @@ int mtb_docs_load_v1(mtb_batch* b, uint32_t n, const uint32_t* docs, const mtb_b
   });
 }
 
-int mtb_add_client(mtb_batch* b, uint32_t doc, const char* long_id) {
+int mtbx_add_client(mtb_dev* b, uint32_t doc, const char* long_id) {
   return guarded(b, [&] { docref(b, doc).client(long_id ? long_id : ""); });
 }
 
-int mtb_intern_props(mtb_batch* b, const char* json, size_t len, uint32_t* id_out) {
+int mtbx_intern_props(mtb_dev* b, const char* json, size_t len, uint32_t* id_out) {
   return guarded(b, [&] {
     hj::Value v = hj::parse(json, len);
     *id_out = b->in.props(v);
   });
 }
 
-int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json, size_t len) {
+int mtbx_apply_msg_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
   return guarded(b, [&] {
     if (b->matrix) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_apply_msg_json");
     HostDoc& d = docref(b, doc);
@@ -2516,7 +2520,7 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json, size_t len)
   });
 }
 
-uint32_t intern_cell_value(mtb_batch* b, const std::string& json) {
+uint32_t intern_cell_value(mtb_dev* b, const std::string& json) {
   auto [it, fresh] = b->cellValIds.try_emplace(json, (uint32_t)b->cellVals.size());
   if (fresh) b->cellVals.push_back(json);
   return it->second;
@@ -2525,7 +2529,7 @@ uint32_t intern_cell_value(mtb_batch* b, const std::string& json) {
 // SharedMatrix.processCore (matrix.ts:636-697): a vector op goes to its PermutationVector's applyMsg
 // (with that vector's updateSeqNumbers); a remote setCell becomes a SETCELL record in both vectors
 // (adjusted, exchanged and allocated on the GPU); a local setCell is an ack with no vector effect.
-int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json, size_t len) {
+int mtbx_matrix_apply_msg_json(mtb_dev* b, uint32_t matrix, const char* json, size_t len) {
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
@@ -2576,7 +2580,7 @@ int mtb_matrix_apply_msg_json(mtb_batch* b, uint32_t matrix, const char* json, s
 
 // SharedMatrix observers (rows = document 2m, cols = 2m + 1) in a MTB_BATCH_MATRIX batch:
 // startOrUpdateCollaboration on both PermutationVectors (matrix.ts:102-118 construct them empty).
-int mtb_matrix_init(mtb_batch* b, uint32_t matrix, const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq) {
+int mtbx_matrix_init(mtb_dev* b, uint32_t matrix, const char* observer_long_id, uint32_t min_seq, uint32_t cur_seq) {
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
@@ -2598,7 +2602,7 @@ int mtb_matrix_init(mtb_batch* b, uint32_t matrix, const char* observer_long_id,
   });
 }
 
-int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, const uint16_t* payload, size_t payload_len) {
+int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, const uint16_t* payload, size_t payload_len) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
@@ -2637,11 +2641,11 @@ int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, co
   });
 }
 
-int mtb_replay(mtb_batch* b, mtb_stats* out) {
+int mtbx_replay(mtb_dev* b, mtb_stats* out) {
   return guarded(b, [&] { replay(b, out); });
 }
 
-int mtb_rewind(mtb_batch* b) {
+int mtbx_rewind(mtb_dev* b) {
   return guarded(b, [&] {
     if (!b->haveRewind) raise(MTB_E_ARG, "nothing to rewind: replay the batch first");
     for (auto& d : b->docs)
@@ -2656,7 +2660,7 @@ int mtb_rewind(mtb_batch* b) {
 }
 
 // Replay the records already resident on the device (after mtb_rewind); no host->device traffic.
-int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
+int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
   return guarded(b, [&] {
     if (!b->haveRewind) raise(MTB_E_ARG, "no resident records");
     Tables t;
@@ -2693,7 +2697,7 @@ int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
   });
 }
 
-int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out) {
+int mtbx_get_text(mtb_dev* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     download_doc(b, doc);
@@ -2711,7 +2715,7 @@ int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* 
   });
 }
 
-int mtb_get_length(mtb_batch* b, uint32_t doc, uint32_t* len_out) {
+int mtbx_get_length(mtb_dev* b, uint32_t doc, uint32_t* len_out) {
   return guarded(b, [&] {
     docref(b, doc);
     download_doc(b, doc);
@@ -2719,7 +2723,7 @@ int mtb_get_length(mtb_batch* b, uint32_t doc, uint32_t* len_out) {
   });
 }
 
-int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq) {
+int mtbx_get_seq(mtb_dev* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (d.onDevice) {
@@ -2732,7 +2736,7 @@ int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq
   });
 }
 
-int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len) {
+int mtbx_dump_segments(mtb_dev* b, uint32_t doc, char** out, size_t* out_len) {
   return guarded(b, [&] {
     docref(b, doc);
     std::string s = dump_doc(b, doc);
@@ -2741,7 +2745,7 @@ int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len) {
   });
 }
 
-int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out) {
+int mtbx_doc_digests(mtb_dev* b, uint32_t first, uint32_t n, uint64_t* out) {
   return guarded(b, [&] {
     if (!out && n) raise(MTB_E_ARG, "null output");
     if ((uint64_t)first + n > b->ndocs) raise(MTB_E_ARG, "document range out of bounds");
@@ -2750,7 +2754,7 @@ int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out) {
   });
 }
 
-int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out) {
+int mtbx_doc_checksum(mtb_dev* b, uint32_t doc, uint64_t* out) {
   return guarded(b, [&] {
     docref(b, doc);
     *out = fnv(dump_doc(b, doc));
@@ -2769,7 +2773,7 @@ void fill_blob_list(const std::vector<std::pair<std::string, std::string>>& blob
   out->summary_json = dup(summary);
   out->summary_json_len = summary.size();
 }
-void summary_catch_up(mtb_batch* b, HostDoc& d, int64_t msn, int64_t seq) {
+void summary_catch_up(mtb_dev* b, HostDoc& d, int64_t msn, int64_t seq) {
   if (msn >= 0 && seq >= 0) {  // Client.summarize: updateSeqNumbers(deltaManager.MSN, lastSequenceNumber)
     mtb_op r{};
     r.type = MTB_OP_NOOP;
@@ -2784,7 +2788,7 @@ void summary_catch_up(mtb_batch* b, HostDoc& d, int64_t msn, int64_t seq) {
 }  // namespace
 
 // Client.summarize without newMergeTreeSnapshotFormat (client.ts:999-1003)
-int mtb_summarize_legacy(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, const char* catchup_json, size_t catchup_len,
+int mtbx_summarize_legacy(mtb_dev* b, uint32_t doc, int64_t msn, int64_t seq, const char* catchup_json, size_t catchup_len,
                          mtb_blob_list* out) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
@@ -2797,7 +2801,7 @@ int mtb_summarize_legacy(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, c
   });
 }
 
-int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_blob_list* out) {
+int mtbx_summarize_v1(mtb_dev* b, uint32_t doc, int64_t msn, int64_t seq, mtb_blob_list* out) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (msn >= 0 && seq >= 0) {  // Client.summarize: updateSeqNumbers(deltaManager.MSN, lastSequenceNumber)
@@ -2827,7 +2831,7 @@ int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_b
 
 // Client.summarize (SnapshotV1) of many documents: one replay for the optional updateSeqNumbers, one
 // bulk download of every listed document, and the summaries serialized on `threads` host threads.
-int mtb_summarize_v1_many(mtb_batch* b, uint32_t n, const uint32_t* docs, int64_t msn, int64_t seq, uint32_t threads,
+int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t msn, int64_t seq, uint32_t threads,
                           mtb_blob_list* out) {
   return guarded(b, [&] {
     if (n && (!docs || !out)) raise(MTB_E_ARG, "null argument");
@@ -2874,7 +2878,7 @@ int mtb_summarize_v1_many(mtb_batch* b, uint32_t n, const uint32_t* docs, int64_
   });
 }
 
-int mtb_export_pending(mtb_batch* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out, uint16_t* payload,
+int mtbx_export_pending(mtb_dev* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out, uint16_t* payload,
                        size_t pcap, size_t* plen_out) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
@@ -2891,7 +2895,7 @@ int mtb_export_pending(mtb_batch* b, uint32_t doc, mtb_op* ops, uint32_t cap, ui
   });
 }
 
-int mtb_props_json(mtb_batch* b, uint32_t id, char* buf, size_t cap, size_t* len_out) {
+int mtbx_props_json(mtb_dev* b, uint32_t id, char* buf, size_t cap, size_t* len_out) {
   return guarded(b, [&] {
     for (auto& kv : b->in.propsByJson) {
       if (kv.second == id) {
@@ -2907,7 +2911,7 @@ int mtb_props_json(mtb_batch* b, uint32_t id, char* buf, size_t cap, size_t* len
   });
 }
 
-int mtb_client_long_id(mtb_batch* b, uint32_t doc, uint32_t short_id, char* buf, size_t cap, size_t* len_out) {
+int mtbx_client_long_id(mtb_dev* b, uint32_t doc, uint32_t short_id, char* buf, size_t cap, size_t* len_out) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (short_id >= d.longIds.size()) raise(MTB_E_ARG, "unknown short client id");
@@ -2962,7 +2966,7 @@ void mtb_blob_list_free(mtb_blob_list* l) {
 namespace {
 // PermutationVector.getMaybeHandle (permutationvector.ts:200-207, handlecache.ts): the handle stored
 // at local position `pos` of vector document i (start + offset; HandleUnallocated when none).
-uint32_t vector_handle_at(mtb_batch* b, uint32_t i, uint32_t pos) {
+uint32_t vector_handle_at(mtb_dev* b, uint32_t i, uint32_t pos) {
   download_doc(b, i);
   const HostDoc& d = b->docs[i];
   uint32_t p = pos, found = MTB_NONE;
@@ -2989,7 +2993,7 @@ uint32_t vector_handle_at(mtb_batch* b, uint32_t i, uint32_t pos) {
 }
 }  // namespace
 
-int mtb_matrix_intern_value(mtb_batch* b, const char* json, size_t len, uint32_t* id_out) {
+int mtbx_matrix_intern_value(mtb_dev* b, const char* json, size_t len, uint32_t* id_out) {
   return guarded(b, [&] {
     if (!json || !id_out) raise(MTB_E_ARG, "null argument");
     hj::Value v = hj::parse(json, len);
@@ -2997,7 +3001,7 @@ int mtb_matrix_intern_value(mtb_batch* b, const char* json, size_t len, uint32_t
   });
 }
 
-int mtb_matrix_get_cell(mtb_batch* b, uint32_t matrix, uint32_t row, uint32_t col, char* buf, size_t cap, size_t* len_out) {
+int mtbx_matrix_get_cell(mtb_dev* b, uint32_t matrix, uint32_t row, uint32_t col, char* buf, size_t cap, size_t* len_out) {
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
@@ -3020,7 +3024,7 @@ int mtb_matrix_get_cell(mtb_batch* b, uint32_t matrix, uint32_t row, uint32_t co
 
 // SharedMatrix.summarizeCore (matrix.ts:449-463) through SummaryTreeBuilder (summaryUtils.ts:138-198):
 // addWithStats(rows), addWithStats(cols) (PermutationVector.summarize), addBlob(cells)
-int mtb_matrix_summarize(mtb_batch* b, uint32_t matrix, mtb_blob_list* out) {
+int mtbx_matrix_summarize(mtb_dev* b, uint32_t matrix, mtb_blob_list* out) {
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");
@@ -3087,7 +3091,7 @@ int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int 
 // and getPropertiesAtPosition (client.ts:1101) are views of it.  Output: a JSON array of
 // {"pos", "start", "end", "segment"} per visited leaf (start / end relative to the segment, as the
 // reference's handler receives them), at most `limit` entries (0 = all).
-int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq, const char* long_client_id,
+int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq, const char* long_client_id,
                   uint32_t limit, char** out, size_t* out_len) {
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
@@ -3173,7 +3177,7 @@ uint32_t compact_even(uint32_t x) {  // inverse of CellStore::spread: the even b
 }
 // SparseArray2D.load (sparsearray2d.ts:233-236) into a CellStore: every non-null leaf becomes a written
 // key; a 256-leaf tile whose leaves are all null keeps its place through one written-undefined key
-void load_cells(mtb_batch* b, CellStore& cs, const hj::Value& root) {
+void load_cells(mtb_dev* b, CellStore& cs, const hj::Value& root) {
   if (root.kind != hj::Value::kArr) raise(MTB_E_PARSE, "cells snapshot is not an array");
   cs.rootLen = std::max<uint64_t>(1, root.items.size());
   for (size_t hi = 0; hi < root.items.size(); hi++) {
@@ -3210,7 +3214,7 @@ void load_cells(mtb_batch* b, CellStore& cs, const hj::Value& root) {
 // SharedMatrix.loadCore (matrix.ts:611-634): rows / cols PermutationVector.load (permutationvector.ts:
 // 327-345: HandleTable.load of "handleTable", then Client.load of "segments/...") and SparseArray2D.load
 // of "cells"; blob paths as mtb_matrix_summarize writes them.
-int mtb_matrix_load(mtb_batch* b, uint32_t matrix, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
+int mtbx_matrix_load(mtb_dev* b, uint32_t matrix, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id) {
   return guarded(b, [&] {
     if (!b->matrix) raise(MTB_E_ARG, "not a matrix batch (MTB_BATCH_MATRIX)");
     if (matrix >= b->ndocs / 2) raise(MTB_E_ARG, "matrix index out of range");

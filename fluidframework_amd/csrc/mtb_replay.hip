@@ -51,7 +51,8 @@ enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL 
 enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, CN_ZCALL = 5, CN_POP = 6, CN_PSKIP = 7, CN_PSIG = 8,
        NCN = 9, CN_SPLIT = 99, CN_GROW = 99, CN_ZRECORD = 99 };
 
-#define MTB_LDS_HEAP 128
+#define MTB_LDS_HEAP 128        // LRU heap entries kept in LDS by the batch kernels (more spill to HBM)
+#define MTB_LDS_HEAP_LONG 2048  // ... by the few-document kernel (long documents keep big heaps)
 #define MTB_VDEPTH 12  // depth of the LDS path cache; 4^12 segments per document is far beyond any input
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -87,6 +88,10 @@ __device__ __forceinline__ uint32_t U(uint32_t x) { return (uint32_t)__builtin_a
 // global address space explicitly, UP() also makes the pointer uniform.
 template <class T>
 using gptr = __attribute__((address_space(1))) T*;
+template <class T>
+using lptr = __attribute__((address_space(3))) T*;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <class T>
 __device__ __forceinline__ gptr<T> GP(T* p) { return (gptr<T>)p; }
 template <class T>
@@ -129,7 +134,8 @@ struct Rec {
   int32_t scour;
 };
 
-struct Scratch {  // LDS, one per wave
+template <int HEAPN>
+struct ScratchT {  // LDS, one per wave
   View v[MTB_VDEPTH];
   uint32_t path[MTB_VDEPTH];   // block at each depth of the current walk
   int32_t slot[MTB_VDEPTH];    // child slot taken at each depth
@@ -156,8 +162,11 @@ struct Scratch {  // LDS, one per wave
       uint32_t pv[64];
     };
   };
-  Lru heap[MTB_LDS_HEAP];      // LRU heap while it fits (index 0 unused)
+  alignas(16) Lru heap[HEAPN];  // LRU heap while it fits (index 0 unused; 16-byte child-pair reads)
 };
+
+using Scratch = ScratchT<MTB_LDS_HEAP>;
+using ScratchBig = ScratchT<MTB_LDS_HEAP_LONG>;
 
 // cold uniform state kept in LDS (frees scalar registers on the hot path)
 #define sp_lenL sh->sp[0]
@@ -179,14 +188,15 @@ struct Scratch {  // LDS, one per wave
 // the head of each document's records (mtb_load_kernel); MODE_MATRIX replays SharedMatrix vector pairs
 // with setCell handle allocation (mtb_matrix_kernel).  Each variant carries only its own code.
 enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2 };
-template <int MODE>
+template <int MODE, class SCR>
 struct Eng {
   DocState* ds;
   uint32_t* segp;  // parent block of each segment
   FBlk* blk;
   WEnt* lst;
   uint32_t* aux;
-  Scratch* sh;
+  SCR* sh;
+  static constexpr uint32_t lheap_n = sizeof(SCR::heap) / sizeof(Lru);  // LDS heap capacity
   int lane;
   // uniform document state (mirrors DocState)
   int minSeq, curSeq;
@@ -720,55 +730,87 @@ struct Eng {
   // each block child k, the entries of k's own list plus entries derived from k's segment children
   // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
   // where P's metadata lives.
+  // holdN > 0 (packParent spreading leaf children over new blocks): P's children are leaf blocks whose
+  // segments are the kept ones still in hold[.][0, holdN) -- segment i went to new block q(i), `hbase`
+  // children each, the first `hrem` one more -- so the derived entries come from there instead of
+  // re-reading the records just written (the records are read only if that shortcut cannot finish).
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out, int holdN = 0, int hbase = 0,
+                                         int hrem = 0) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
-    const uint32_t* src = bw(P);
-    const uint32_t w = src[lane];
-    const int count = U((int)src[FB_HDR]);
-    (&Z.f[0][0])[lane] = w;
-    wsync();
-    // lane (k, s): segment child s of block child k
-    const int k = lane >> 3, s = lane & 7;
-    uint32_t ck = MTB_NONE;
-    if (k < count) ck = Z.f[F_ID][k];
-    const bool kblk = k < count && !(ck & MTB_LEAF);
+    int count = 0;
+    int k = lane >> 3, s = lane & 7;  // lane (k, s): segment child s of block child k
+    bool kblk = false;
     int ne = 0, nov = 0;
     int slen = 0, sseq = 0, srseq = -1;
     uint32_t scli = 0, srcx = 0;
-    bool sv = false;  // lane (k, s) holds a segment
-    if (kblk) {
-      const uint32_t* c = bw(ck);
-      const int ccount = (int)c[FB_HDR];
-      if (s < ccount) {
-        const uint32_t sid = c[F_ID * 8 + s];
-        if (sid & MTB_LEAF) {
-          sv = true;
-          slen = (int)c[F_LEN * 8 + s];
-          sseq = (int)c[F_SEQ * 8 + s];
-          srseq = (int)c[F_RSEQ * 8 + s];
-          scli = c[F_CLI * 8 + s];
-          srcx = c[F_RCX * 8 + s];
-          if (sseq > minSeq) ne++;
-          if (srseq >= 0 && srseq > minSeq) {
-            ne++;
-            if (srcx) nov = (int)aux[srcx];
+    bool sv = false;  // the lane holds a segment
+    uint32_t lc = 0, lo = 0;
+    auto load_children = [&]() {
+      const uint32_t* src = bw(P);
+      const uint32_t w = src[lane];
+      count = U((int)src[FB_HDR]);
+      (&Z.f[0][0])[lane] = w;
+      wsync();
+      k = lane >> 3;
+      s = lane & 7;
+      uint32_t ck = MTB_NONE;
+      if (k < count) ck = Z.f[F_ID][k];
+      kblk = k < count && !(ck & MTB_LEAF);
+      ne = nov = 0;
+      slen = sseq = 0;
+      srseq = -1;
+      scli = srcx = 0;
+      sv = false;
+      if (kblk) {
+        const uint32_t* c = bw(ck);
+        const int ccount = (int)c[FB_HDR];
+        if (s < ccount) {
+          const uint32_t sid = c[F_ID * 8 + s];
+          if (sid & MTB_LEAF) {
+            sv = true;
+            slen = (int)c[F_LEN * 8 + s];
+            sseq = (int)c[F_SEQ * 8 + s];
+            srseq = (int)c[F_RSEQ * 8 + s];
+            scli = c[F_CLI * 8 + s];
+            srcx = c[F_RCX * 8 + s];
+            if (sseq > minSeq) ne++;
+            if (srseq >= 0 && srseq > minSeq) {
+              ne++;
+              if (srcx) nov = (int)aux[srcx];
+            }
           }
         }
       }
+      // the block children's own lists (metadata in P's slots), concatenated
+      lc = lo = 0;
+      if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
+        lo = Z.f[F_SEQ][lane];
+        lc = Z.f[F_RSEQ][lane];
+      }
+    };
+    if (holdN > 0) {
+      if (lane < holdN) {
+        sv = true;
+        slen = (int)sh->hold[F_LEN][lane];
+        sseq = (int)sh->hold[F_SEQ][lane];
+        srseq = (int)sh->hold[F_RSEQ][lane];
+        scli = sh->hold[F_CLI][lane];
+        srcx = sh->hold[F_RCX][lane];
+        if (srseq >= 0 && srseq > minSeq && srcx) nov = 1;  // (overlaps: the general path below)
+      }
+      const int big = hrem * (hbase + 1);
+      k = lane < big ? lane / (hbase + 1) : hrem + (lane - big) / (hbase > 0 ? hbase : 1);
+      wsync();
+    } else {
+      load_children();
     }
-    // the block children's own lists (metadata in P's slots), concatenated
-    uint32_t lc = 0, lo = 0;
-    if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
-      lo = Z.f[F_SEQ][lane];
-      lc = Z.f[F_RSEQ][lane];
-    }
-    const int lincl = cscan8((int)lc);
-    const int ltotal = rl(lincl, 7);
-    const int lexcl = lincl - (int)lc;
+    int lincl = cscan8((int)lc);
+    int ltotal = rl(lincl, 7);
     // the parent of leaf blocks (splits and packs below the leaf level): only derived entries, written
     // sorted straight from registers
+    bool reload = holdN > 0;  // hold[] shortcut that could not finish: the general path needs the records
     if (ltotal == 0 && __ballot(nov > 0) == 0) {
       bool ha, hb;
       WEnt ea, eb;
@@ -782,7 +824,15 @@ struct Eng {
         lcap_out = cap;
         return;
       }
+      reload = true;  // (rare: a seq window wider than the sort's buckets; fetching again keeps the
+                      // general path's values out of registers while the shortcut runs)
     }
+    if (reload) {
+      load_children();
+      lincl = cscan8((int)lc);
+      ltotal = rl(lincl, 7);
+    }
+    const int lexcl = lincl - (int)lc;
     int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
     for (int q = 0; q < MTB_MAXCH; q++) {
@@ -1037,7 +1087,7 @@ struct Eng {
   }
   // Split every full block on the path, from depth d upwards.  Written as a state machine with a
   // single list-rebuild site (the halves of an internal split, the new root, the parent).
-  __device__ __noinline__ void fix_overflow_slow(int d) {
+  __device__ __forceinline__ void fix_overflow_slow(int d) {
     int level = d;
     int phase = 0;  // 0 split `level` | 1 rebuild left half | 2 rebuild right half | 3 link | 4 parent done | 5 root done
     uint32_t b = MTB_NONE, nb = MTB_NONE;
@@ -1276,7 +1326,9 @@ struct Eng {
   __device__ __forceinline__ Lru hget(uint32_t k) const {
     Lru x;
     if (heap_lds) {
-      x = sh->heap[k];
+      const u32x2 y = *reinterpret_cast<const u32x2*>(&sh->heap[k]);
+      x.seg = y.x;
+      x.maxSeq = (int)y.y;
     } else {
       const auto g = UP(sh->gheap) + k;
       x.seg = g->seg;
@@ -1286,9 +1338,32 @@ struct Eng {
     x.maxSeq = U(x.maxSeq);
     return x;
   }
+  // children j and j + 1 (j even) with one round trip: a 16-byte LDS read, or two global loads in flight
+  __device__ __forceinline__ void hget2(uint32_t j, Lru& a, Lru& b) const {
+    if (heap_lds) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&sh->heap[j]);
+      a.seg = v.x;
+      a.maxSeq = (int)v.y;
+      b.seg = v.z;
+      b.maxSeq = (int)v.w;
+    } else {
+      const auto g = UP(sh->gheap) + j;
+      a.seg = g[0].seg;
+      a.maxSeq = g[0].maxSeq;
+      b.seg = g[1].seg;
+      b.maxSeq = g[1].maxSeq;
+    }
+    a.seg = U(a.seg);
+    a.maxSeq = U(a.maxSeq);
+    b.seg = U(b.seg);
+    b.maxSeq = U(b.maxSeq);
+  }
   __device__ __forceinline__ void hset(uint32_t k, Lru v) {
     if (heap_lds) {
-      sh->heap[k] = v;
+      u32x2 y;
+      y.x = v.seg;
+      y.y = (uint32_t)v.maxSeq;
+      *reinterpret_cast<u32x2*>(&sh->heap[k]) = y;
     } else {
       const auto g = UP(sh->gheap) + k;
       g->seg = v.seg;
@@ -1296,13 +1371,17 @@ struct Eng {
     }
   }
   __device__ __forceinline__ void heap_spill() {  // LDS -> global slice
-    for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) sh->gheap[i] = sh->heap[i];
+    for (uint32_t i = 1 + lane; i <= heap_cnt; i += 64) {
+      const u32x2 v = *reinterpret_cast<const u32x2*>(&sh->heap[i]);
+      sh->gheap[i].seg = v.x;
+      sh->gheap[i].maxSeq = (int)v.y;
+    }
     heap_lds = false;
     wsync();
   }
   __device__ __forceinline__ void heap_add(uint32_t s, int maxSeq) {
     if (heap_cnt + 1 >= ds->heap_cap) { fail(DERR_CAP_HEAP); return; }
-    if (COLD(heap_lds && heap_cnt + 1 >= MTB_LDS_HEAP)) heap_spill();
+    if (COLD(heap_lds && heap_cnt + 1 >= lheap_n)) heap_spill();
     uint32_t k = ++heap_cnt;
     Lru x;
     x.seg = s;
@@ -1321,16 +1400,14 @@ struct Eng {
     heap_cnt--;
     const uint32_t count = heap_cnt;
     uint32_t k = 1;
-    // fixDown with the last element placed at the root
+    // fixDown with the last element placed at the root (collections/heap.ts:50-64)
     while ((k << 1) <= count) {
       uint32_t j = k << 1;
-      Lru a = hget(j);
-      if (j < count) {
-        const Lru bb = hget(j + 1);
-        if (a.maxSeq - bb.maxSeq > 0) {
-          j++;
-          a = bb;
-        }
+      Lru a, bb;
+      hget2(j, a, bb);  // (j + 1 <= the old count: inside the heap's storage)
+      if (j < count && a.maxSeq - bb.maxSeq > 0) {
+        j++;
+        a = bb;
       }
       if (last.maxSeq - a.maxSeq <= 0) break;
       hset(k, a);
@@ -2047,13 +2124,36 @@ struct Eng {
   }
   // A new window list holding the entries ea (lanes with ha) and eb (lanes with hb), at most two per
   // lane, in seq order: a counting sort over seq - minSeq - 1 in the scour union (no caller holds it live
-  // here), straight from registers.  Returns false, having written nothing, if a seq falls outside the
-  // buckets.
+  // here), straight from registers; a list of one chunk is written unsorted (views read it whole).
+  // Returns false, having written nothing, if a seq falls outside the buckets.
   __device__ __forceinline__ bool write_sorted2(bool ha, const WEnt& ea, bool hb, const WEnt& eb, uint32_t& no_out,
                                                 uint32_t& cnt_out, uint32_t& cap_out) {
     const int ba = ea.seq - minSeq - 1, bb = eb.seq - minSeq - 1;
     if (__ballot((ha && (ba < 0 || ba >= MTB_SORT_BUCKETS)) || (hb && (bb < 0 || bb >= MTB_SORT_BUCKETS)))) return false;
-    const uint32_t T = (uint32_t)(__popcll(__ballot(ha)) + __popcll(__ballot(hb)));
+    const unsigned long long ma = __ballot(ha), mb = __ballot(hb);
+    const uint32_t T = (uint32_t)(__popcll(ma) + __popcll(mb));
+    if (T <= 64) {  // one chunk: read whole by every view anyway -- written as is, flagged unsorted
+      uint32_t cap;
+      const uint32_t no = list_alloc(T + T / 2 + 4, cap);
+      if (bad()) return true;
+      if (ha) {
+        WEnt& d = lst[no + rank_below(ma)];
+        d.seq = ea.seq;
+        d.ck = ea.ck;
+        d.delta = ea.delta;
+      }
+      if (hb) {
+        WEnt& d = lst[no + (uint32_t)__popcll(ma) + rank_below(mb)];
+        d.seq = eb.seq;
+        d.ck = eb.ck;
+        d.delta = eb.delta;
+      }
+      wsync();
+      no_out = no;
+      cnt_out = T;
+      cap_out = T > 1 ? cap | MTB_LUNSORTED : cap;
+      return true;
+    }
     uint32_t* hist = &sh->hold[0][0];
     wsync();
     for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
@@ -2084,13 +2184,19 @@ struct Eng {
     uint32_t cap;
     const uint32_t no = list_alloc(T + T / 2 + 4, cap);
     if (bad()) return true;
-    if (ha) {
+    if (ha) {  // (the pad word is never read)
       const uint32_t sft = (uint32_t)(ba & 1) * 16;
-      lst[no + ((atomicAdd(&hist[ba >> 1], 1u << sft) >> sft) & 0xFFFF)] = ea;
+      WEnt& d = lst[no + ((atomicAdd(&hist[ba >> 1], 1u << sft) >> sft) & 0xFFFF)];
+      d.seq = ea.seq;
+      d.ck = ea.ck;
+      d.delta = ea.delta;
     }
     if (hb) {
       const uint32_t sft = (uint32_t)(bb & 1) * 16;
-      lst[no + ((atomicAdd(&hist[bb >> 1], 1u << sft) >> sft) & 0xFFFF)] = eb;
+      WEnt& d = lst[no + ((atomicAdd(&hist[bb >> 1], 1u << sft) >> sft) & 0xFFFF)];
+      d.seq = eb.seq;
+      d.ck = eb.ck;
+      d.delta = eb.delta;
     }
     wsync();
     no_out = no;
@@ -2115,40 +2221,8 @@ struct Eng {
     eb.delta = -len;
     eb.pad = 0;
   }
-  // The parent's list after packParent spread leaf children over new blocks: the derived entries of the
-  // kept segments still in hold[.][0, nh) -- segment i went to new block q(i) (`base` children each, the
-  // first `rem` one more) -- instead of rebuild() re-reading the records just written.  Returns false,
-  // having changed nothing, when a segment has overlapping removers or the seq window is too wide for
-  // the sort (the caller then runs rebuild()).
-  __device__ __forceinline__ bool rebuild_from_hold(int nh, int base, int rem, uint32_t old_loff, uint32_t old_lcap,
-                                                    uint32_t& loff_out, uint32_t& lcnt_out, uint32_t& lcap_out) {
-    int len = 0, sq = 0, rs = -1;
-    uint32_t cl = 0, rx = 0;
-    if (lane < nh) {
-      len = (int)sh->hold[F_LEN][lane];
-      sq = (int)sh->hold[F_SEQ][lane];
-      rs = (int)sh->hold[F_RSEQ][lane];
-      cl = sh->hold[F_CLI][lane];
-      rx = sh->hold[F_RCX][lane];
-    }
-    const int big = rem * (base + 1);
-    const int q = lane < big ? lane / (base + 1) : rem + (lane - big) / (base > 0 ? base : 1);
-    bool ha, hb;
-    WEnt ea, eb;
-    derived2(lane < nh, q, len, sq, rs, cl, ha, ea, hb, eb);
-    if (__ballot(hb && rx != 0)) return false;
-    uint32_t no, cnt, cap;
-    if (!write_sorted2(ha, ea, hb, eb, no, cnt, cap)) return false;
-    if (bad()) return true;
-    PROF_CNT(CN_REBUILD, 1);
-    list_free(old_loff, old_lcap);
-    loff_out = no;
-    lcnt_out = cnt;
-    lcap_out = cap;
-    return true;
-  }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
-  __device__ __noinline__ void pack_parent(uint32_t parent) {
+  __device__ __forceinline__ void pack_parent(uint32_t parent) {
     while (!err) {
       PROF_CNT(CN_PACK, 1);
       stage_rec(parent);
@@ -2165,6 +2239,8 @@ struct Eng {
       if (bad()) return;
       int cc = 0, base = 0, rem0 = 0;
       bool leafcase = true;  // the new blocks' children are segments
+      uint32_t nbs = 0;      // lane q: new block q, its observer length, whether its children are blocks
+      int lens = 0, kbs = 0;
       if (nh > 0) {
         cc = nh / (MTB_MAXCH / 2);
         if (cc > MTB_MAXCH - 1) cc = MTB_MAXCH - 1;
@@ -2182,8 +2258,6 @@ struct Eng {
         int rem = rem0;
         int taken = 0;
         // first every new block gets its children (the scour output in hold[] is consumed here) ...
-        uint32_t nbs = 0;  // lane q: new block q, its observer length, whether its children are blocks
-        int lens = 0, kbs = 0;
         for (int q = 0; q < cc; q++) {
           int n = base;
           if (rem > 0) {
@@ -2211,28 +2285,6 @@ struct Eng {
           wsync();
           taken += n;
         }
-        // ... then the lists of those whose children are blocks (rebuild uses the union as scratch)
-        for (int q = 0; q < cc; q++) {
-          const uint32_t nb = rlu(nbs, q);
-          uint32_t a = 0, c2 = 0, e = 0;
-          if (rl(kbs, q)) {
-            rebuild(nb, 0, 0, a, c2, e);
-            if (bad()) return;
-          }
-          const int len = rl(lens, q);
-          if (lane == 0) {
-            FBlk& P = blk[parent];
-            P.f[F_ID][q] = nb;
-            P.f[F_LEN][q] = (uint32_t)len;
-            P.f[F_SEQ][q] = a;
-            P.f[F_RSEQ][q] = c2;
-            P.f[F_CLI][q] = e;
-            P.f[F_RCX][q] = 0;
-            P.f[F_PROPS][q] = 0;
-            P.f[F_TEXT][q] = 0;
-          }
-          wsync();
-        }
       }
       {
         const int fld = lane >> 3, s = lane & 7;
@@ -2240,9 +2292,32 @@ struct Eng {
       }
       if (lane == 0) blk[parent].count = (uint32_t)cc;
       wsync();
-      uint32_t a, c2, e;
-      if (!(leafcase && nh > 0 && rebuild_from_hold(nh, base, rem0, ploff, pcap, a, c2, e))) rebuild(parent, ploff, pcap, a, c2, e);
-      if (bad()) return;
+      // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
+      // site; rebuild uses the union as scratch, and P's leaf case takes its segments from hold[])
+      uint32_t a = 0, c2 = 0, e = 0;
+      for (int q = 0; q <= cc; q++) {
+        const bool isP = q == cc;
+        const uint32_t nb = isP ? parent : rlu(nbs, q);
+        a = c2 = e = 0;
+        if (isP || rl(kbs, q)) {
+          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e, isP && leafcase ? nh : 0, base, rem0);
+          if (bad()) return;
+        }
+        if (isP) break;
+        const int len = rl(lens, q);
+        if (lane == 0) {
+          FBlk& P = blk[parent];
+          P.f[F_ID][q] = nb;
+          P.f[F_LEN][q] = (uint32_t)len;
+          P.f[F_SEQ][q] = a;
+          P.f[F_RSEQ][q] = c2;
+          P.f[F_CLI][q] = e;
+          P.f[F_RCX][q] = 0;
+          P.f[F_PROPS][q] = 0;
+          P.f[F_TEXT][q] = 0;
+        }
+        wsync();
+      }
       store_meta_of(parent, pparent, pindex, a, c2, e);
       if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {
         parent = pparent;
@@ -2617,14 +2692,15 @@ using namespace mtbk;
 #ifndef MTB_WAVES_PER_SIMD
 #define MTB_WAVES_PER_SIMD 4
 #endif
-template <int MODE>
-__device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* xch, int wv, DocState* __restrict__ docs,
+template <int MODE, class SCR>
+__device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, int wv,
+                                           DocState* __restrict__ docs,
                                            uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
                                            uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                                            const Tables& tables) {
   if (doc >= ndocs) return;
   DocState* ds = &docs[doc];
-  Eng<MODE> e;
+  Eng<MODE, SCR> e;
   e.xch = xch;
   e.wv = wv;
   e.ds = ds;
@@ -2681,9 +2757,14 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
     sh.lfree[e.lane] = reinterpret_cast<const uint32_t*>(e.lst)[e.lane];
   }
   if (e.lane == 0) sh.path[0] = e.root;
-  e.heap_lds = e.heap_cnt + 1 < MTB_LDS_HEAP;
+  e.heap_lds = e.heap_cnt + 1 < e.lheap_n;
   if (e.heap_lds)
-    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) sh.heap[i] = gheap[i];
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) {
+      u32x2 v;
+      v.x = gheap[i].seg;
+      v.y = (uint32_t)gheap[i].maxSeq;
+      *reinterpret_cast<u32x2*>(&sh.heap[i]) = v;
+    }
   e.view_clear();
   __syncthreads();
   if (k < n) {
@@ -2731,7 +2812,11 @@ __device__ __forceinline__ void replay_doc(Scratch& sh, uint32_t doc, int32_t* x
     }
   }
   if (e.heap_lds)
-    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) gheap[i] = sh.heap[i];
+    for (uint32_t i = 1 + e.lane; i <= e.heap_cnt; i += 64) {
+      const u32x2 v = *reinterpret_cast<const u32x2*>(&sh.heap[i]);
+      gheap[i].seg = v.x;
+      gheap[i].maxSeq = (int)v.y;
+    }
   if (e.lane < MTB_LCLASSES) reinterpret_cast<uint32_t*>(e.lst)[e.lane] = sh.lfree[e.lane];
   __syncthreads();
   if (e.lane == 0) {
@@ -2773,6 +2858,15 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   __shared__ Scratch sh;
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+// The same engine for batches of few documents (at most a few per CU, e.g. BASELINE configs[3]'s single
+// long document): LDS is not what limits occupancy there, so the zamboni LRU heap keeps up to 2,047
+// entries in LDS instead of spilling to HBM past 127.
+extern "C" __global__ void __launch_bounds__(64, 1)
+    mtb_replay_few_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                          WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ ScratchBig sh;
+  replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
 // SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
@@ -2788,15 +2882,21 @@ extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
   __shared__ Scratch sh[2];
   __shared__ int32_t xch[4];
   const int wv = (int)(threadIdx.x >> 6);
-  replay_doc<MODE_MATRIX>(sh[wv], 2 * blockIdx.x + (uint32_t)wv, xch, wv, docs, ndocs, ops, segp, blks, lists, text,
-                          heap, aux, freel, tables);
+  replay_doc<MODE_MATRIX>(sh[wv], 2 * blockIdx.x + (uint32_t)wv, xch, wv, docs, ndocs, ops, segp, blks, lists, text, heap,
+                          aux, freel, tables);
 }
 
+// Up to MTB_FEW_DOCS documents (at most ~4 per CU) replay on the large-LDS-heap variant.
+#define MTB_FEW_DOCS 1024
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables) {
-  hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
-                     aux, freel, tables);
+  if (ndocs <= MTB_FEW_DOCS)
+    hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
+                       heap, aux, freel, tables);
+  else
+    hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
+                       aux, freel, tables);
   return hipGetLastError();
 }
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,

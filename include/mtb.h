@@ -114,6 +114,13 @@ enum {
   MTB_E_PARSE = -8        /* malformed JSON message */
 };
 
+/* device_mask: the HIP devices the batch spreads over (bit k = device k; 0 = device 0).  With several,
+ * documents are assigned by hash(document index) mod the device count (SharedMatrix batches: whole
+ * matrices), each device holds its own HBM pools and stream, and mtb_replay / mtb_rewind /
+ * mtb_replay_resident run every device at once (one host thread each), merging the statistics.  Props
+ * objects passed to mtb_intern_props get the same id on every device; a props object first met inside a
+ * message is interned by that document's device only (its id in mtb_export_pending records is that
+ * device's). */
 int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_mask, mtb_batch** out);
 void mtb_batch_destroy(mtb_batch* b);
 const char* mtb_last_error(mtb_batch* b);

@@ -101,3 +101,26 @@ def test_cfg2_slice_full_length_logs():
     full = B.summarize_v1_many([3, 17], threads=2)
     assert [list(map(list, full[0][0])), full[0][1]] == [list(map(list, B.summarize_v1(3)[0])), B.summarize_v1(3)[1]]
     assert full[1][0] == B.summarize_v1(17)[0]
+
+
+def test_multi_shard_batch_on_one_device(monkeypatch):
+    """The multi-device front end (mtb_multi.cpp) with 3 shards on device 0 (MTB_SHARDS_PER_DEVICE): the
+    shards replay at once from three host threads (three streams); every document's digest, the merged
+    stats and the batched summaries equal the oracle's, also after rewind + resident replay."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyloggen import LogBatch, make_cfg
+    cfg = make_cfg(seed=707, n_ops=1500)
+    lb = LogBatch(cfg, 0, 40)
+    monkeypatch.setenv("MTB_SHARDS_PER_DEVICE", "3")
+    B = MergeTreeBatch(lb.n)
+    monkeypatch.delenv("MTB_SHARDS_PER_DEVICE")
+    docs = load_logbatch(B, lb)
+    st = B.replay()
+    _check(B, lb, docs, st)
+    assert st["ops_applied"] == sum(d.ops_applied for d in lb.docs)
+    fps = B.summarize_v1_many(list(range(lb.n)), threads=6, fingerprints=True)
+    assert fps == [lb.docs[j].summary_fnv for j in range(lb.n)]
+    B.rewind()
+    st2 = B.replay_resident()
+    assert st2["checksum"] == st["checksum"] and st2["ops_applied"] == st["ops_applied"]
+    assert B.digests() == [lb.docs[j].digest for j in range(lb.n)]

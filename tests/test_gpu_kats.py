@@ -57,7 +57,9 @@ def test_passive_observer_race(new_mode):
 
 
 def _view_len(B, ref, client):
-    return sum(e["end"] - e["start"] for e in B.map_range(0, 0, -1, ref, client))
+    """The document's length in (ref, client)'s view: mapRange over all of it visits exactly the segments
+    with a non-zero length there (nodeMap, mergeTree.ts:2556-2558), each with its whole cachedLength."""
+    return sum(e["segment"]["cachedLength"] for e in B.map_range(0, 0, -1, ref, client))
 
 
 def _partial(msgs):
