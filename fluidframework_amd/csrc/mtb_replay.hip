@@ -730,108 +730,50 @@ struct Eng {
   // each block child k, the entries of k's own list plus entries derived from k's segment children
   // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
   // where P's metadata lives.
-  // holdN > 0 (packParent spreading leaf children over new blocks): P's children are leaf blocks whose
-  // segments are the kept ones still in hold[.][0, holdN) -- segment i went to new block q(i), `hbase`
-  // children each, the first `hrem` one more -- so the derived entries come from there instead of
-  // re-reading the records just written (the records are read only if that shortcut cannot finish).
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out, int holdN = 0, int hbase = 0,
-                                         int hrem = 0) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
-    int count = 0;
-    int k = lane >> 3, s = lane & 7;  // lane (k, s): segment child s of block child k
-    bool kblk = false;
+    const uint32_t* src = bw(P);
+    const uint32_t w = src[lane];
+    const int count = U((int)src[FB_HDR]);
+    (&Z.f[0][0])[lane] = w;
+    wsync();
+    // lane (k, s): segment child s of block child k
+    const int k = lane >> 3, s = lane & 7;
+    uint32_t ck = MTB_NONE;
+    if (k < count) ck = Z.f[F_ID][k];
+    const bool kblk = k < count && !(ck & MTB_LEAF);
     int ne = 0, nov = 0;
     int slen = 0, sseq = 0, srseq = -1;
     uint32_t scli = 0, srcx = 0;
-    bool sv = false;  // the lane holds a segment
-    uint32_t lc = 0, lo = 0;
-    auto load_children = [&]() {
-      const uint32_t* src = bw(P);
-      const uint32_t w = src[lane];
-      count = U((int)src[FB_HDR]);
-      (&Z.f[0][0])[lane] = w;
-      wsync();
-      k = lane >> 3;
-      s = lane & 7;
-      uint32_t ck = MTB_NONE;
-      if (k < count) ck = Z.f[F_ID][k];
-      kblk = k < count && !(ck & MTB_LEAF);
-      ne = nov = 0;
-      slen = sseq = 0;
-      srseq = -1;
-      scli = srcx = 0;
-      sv = false;
-      if (kblk) {
-        const uint32_t* c = bw(ck);
-        const int ccount = (int)c[FB_HDR];
-        if (s < ccount) {
-          const uint32_t sid = c[F_ID * 8 + s];
-          if (sid & MTB_LEAF) {
-            sv = true;
-            slen = (int)c[F_LEN * 8 + s];
-            sseq = (int)c[F_SEQ * 8 + s];
-            srseq = (int)c[F_RSEQ * 8 + s];
-            scli = c[F_CLI * 8 + s];
-            srcx = c[F_RCX * 8 + s];
-            if (sseq > minSeq) ne++;
-            if (srseq >= 0 && srseq > minSeq) {
-              ne++;
-              if (srcx) nov = (int)aux[srcx];
-            }
+    if (kblk) {
+      const uint32_t* c = bw(ck);
+      const int ccount = (int)c[FB_HDR];
+      if (s < ccount) {
+        const uint32_t sid = c[F_ID * 8 + s];
+        if (sid & MTB_LEAF) {
+          slen = (int)c[F_LEN * 8 + s];
+          sseq = (int)c[F_SEQ * 8 + s];
+          srseq = (int)c[F_RSEQ * 8 + s];
+          scli = c[F_CLI * 8 + s];
+          srcx = c[F_RCX * 8 + s];
+          if (sseq > minSeq) ne++;
+          if (srseq >= 0 && srseq > minSeq) {
+            ne++;
+            if (srcx) nov = (int)aux[srcx];
           }
         }
       }
-      // the block children's own lists (metadata in P's slots), concatenated
-      lc = lo = 0;
-      if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
-        lo = Z.f[F_SEQ][lane];
-        lc = Z.f[F_RSEQ][lane];
-      }
-    };
-    if (holdN > 0) {
-      if (lane < holdN) {
-        sv = true;
-        slen = (int)sh->hold[F_LEN][lane];
-        sseq = (int)sh->hold[F_SEQ][lane];
-        srseq = (int)sh->hold[F_RSEQ][lane];
-        scli = sh->hold[F_CLI][lane];
-        srcx = sh->hold[F_RCX][lane];
-        if (srseq >= 0 && srseq > minSeq && srcx) nov = 1;  // (overlaps: the general path below)
-      }
-      const int big = hrem * (hbase + 1);
-      k = lane < big ? lane / (hbase + 1) : hrem + (lane - big) / (hbase > 0 ? hbase : 1);
-      wsync();
-    } else {
-      load_children();
     }
-    int lincl = cscan8((int)lc);
-    int ltotal = rl(lincl, 7);
-    // the parent of leaf blocks (splits and packs below the leaf level): only derived entries, written
-    // sorted straight from registers
-    bool reload = holdN > 0;  // hold[] shortcut that could not finish: the general path needs the records
-    if (ltotal == 0 && __ballot(nov > 0) == 0) {
-      bool ha, hb;
-      WEnt ea, eb;
-      derived2(sv, k, slen, sseq, srseq, scli, ha, ea, hb, eb);
-      uint32_t no, cnt, cap;
-      if (write_sorted2(ha, ea, hb, eb, no, cnt, cap)) {
-        if (bad()) return;
-        list_free(old_loff, old_lcap);
-        loff_out = no;
-        lcnt_out = cnt;
-        lcap_out = cap;
-        return;
-      }
-      reload = true;  // (rare: a seq window wider than the sort's buckets; fetching again keeps the
-                      // general path's values out of registers while the shortcut runs)
+    // the block children's own lists (metadata in P's slots), concatenated
+    uint32_t lc = 0, lo = 0;
+    if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
+      lo = Z.f[F_SEQ][lane];
+      lc = Z.f[F_RSEQ][lane];
     }
-    if (reload) {
-      load_children();
-      lincl = cscan8((int)lc);
-      ltotal = rl(lincl, 7);
-    }
+    const int lincl = cscan8((int)lc);
+    const int ltotal = rl(lincl, 7);
     const int lexcl = lincl - (int)lc;
     int pre[MTB_MAXCH], off[MTB_MAXCH];
 #pragma unroll
@@ -2122,105 +2064,6 @@ struct Eng {
     }
     wsync();
   }
-  // A new window list holding the entries ea (lanes with ha) and eb (lanes with hb), at most two per
-  // lane, in seq order: a counting sort over seq - minSeq - 1 in the scour union (no caller holds it live
-  // here), straight from registers; a list of one chunk is written unsorted (views read it whole).
-  // Returns false, having written nothing, if a seq falls outside the buckets.
-  __device__ __forceinline__ bool write_sorted2(bool ha, const WEnt& ea, bool hb, const WEnt& eb, uint32_t& no_out,
-                                                uint32_t& cnt_out, uint32_t& cap_out) {
-    const int ba = ea.seq - minSeq - 1, bb = eb.seq - minSeq - 1;
-    if (__ballot((ha && (ba < 0 || ba >= MTB_SORT_BUCKETS)) || (hb && (bb < 0 || bb >= MTB_SORT_BUCKETS)))) return false;
-    const unsigned long long ma = __ballot(ha), mb = __ballot(hb);
-    const uint32_t T = (uint32_t)(__popcll(ma) + __popcll(mb));
-    if (T <= 64) {  // one chunk: read whole by every view anyway -- written as is, flagged unsorted
-      uint32_t cap;
-      const uint32_t no = list_alloc(T + T / 2 + 4, cap);
-      if (bad()) return true;
-      if (ha) {
-        WEnt& d = lst[no + rank_below(ma)];
-        d.seq = ea.seq;
-        d.ck = ea.ck;
-        d.delta = ea.delta;
-      }
-      if (hb) {
-        WEnt& d = lst[no + (uint32_t)__popcll(ma) + rank_below(mb)];
-        d.seq = eb.seq;
-        d.ck = eb.ck;
-        d.delta = eb.delta;
-      }
-      wsync();
-      no_out = no;
-      cnt_out = T;
-      cap_out = T > 1 ? cap | MTB_LUNSORTED : cap;
-      return true;
-    }
-    uint32_t* hist = &sh->hold[0][0];
-    wsync();
-    for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
-    wsync();
-    if (ha) atomicAdd(&hist[ba >> 1], 1u << ((ba & 1) * 16));
-    if (hb) atomicAdd(&hist[bb >> 1], 1u << ((bb & 1) * 16));
-    wsync();
-    uint32_t tot = 0;
-    for (int k = 0; k < 8; k++) {
-      const uint32_t w = hist[8 * lane + k];
-      tot += (w & 0xFFFF) + (w >> 16);
-    }
-    int incl = (int)tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    uint32_t run = (uint32_t)incl - tot;
-    for (int k = 0; k < 8; k++) {  // (the words are read again: keeps register pressure low)
-      const uint32_t w = hist[8 * lane + k];
-      const uint32_t c0 = run;
-      run += w & 0xFFFF;
-      hist[8 * lane + k] = c0 | (run << 16);
-      run += w >> 16;
-    }
-    wsync();
-    uint32_t cap;
-    const uint32_t no = list_alloc(T + T / 2 + 4, cap);
-    if (bad()) return true;
-    if (ha) {  // (the pad word is never read)
-      const uint32_t sft = (uint32_t)(ba & 1) * 16;
-      WEnt& d = lst[no + ((atomicAdd(&hist[ba >> 1], 1u << sft) >> sft) & 0xFFFF)];
-      d.seq = ea.seq;
-      d.ck = ea.ck;
-      d.delta = ea.delta;
-    }
-    if (hb) {
-      const uint32_t sft = (uint32_t)(bb & 1) * 16;
-      WEnt& d = lst[no + ((atomicAdd(&hist[bb >> 1], 1u << sft) >> sft) & 0xFFFF)];
-      d.seq = eb.seq;
-      d.ck = eb.ck;
-      d.delta = eb.delta;
-    }
-    wsync();
-    no_out = no;
-    cnt_out = T;
-    cap_out = cap;
-    return true;
-  }
-  // Derived window-list entries of a segment (the combine semantics of partialLengths.ts:256 that
-  // rebuild() applies to the segments of its leaf-block children): insert (seq, client, +len) above
-  // minSeq, removal (removedSeq, removedClientIds[0], -len) above minSeq, tagged with the slot k of the
-  // block that holds the segment.
-  __device__ __forceinline__ void derived2(bool valid, int k, int len, int sq, int rs, uint32_t cl, bool& ha, WEnt& ea,
-                                           bool& hb, WEnt& eb) const {
-    ha = valid && sq > minSeq;
-    hb = valid && rs >= 0 && rs > minSeq;
-    ea.seq = sq;
-    ea.ck = WE_KEY(cli_client(cl), WK_MAIN, k);
-    ea.delta = len;
-    ea.pad = 0;
-    eb.seq = rs;
-    eb.ck = WE_KEY(cli_rc0(cl), WK_MAIN, k);
-    eb.delta = -len;
-    eb.pad = 0;
-  }
   // packParent (zamboni.ts:63-120), iterative over the recursion to the grandparent
   __device__ __forceinline__ void pack_parent(uint32_t parent) {
     while (!err) {
@@ -2237,8 +2080,7 @@ struct Eng {
       const uint32_t ploff = U(ploff_v), pcap = U(pcap_v);
       const int nh = scour(pc, 0);
       if (bad()) return;
-      int cc = 0, base = 0, rem0 = 0;
-      bool leafcase = true;  // the new blocks' children are segments
+      int cc = 0;
       uint32_t nbs = 0;      // lane q: new block q, its observer length, whether its children are blocks
       int lens = 0, kbs = 0;
       if (nh > 0) {
@@ -2253,9 +2095,8 @@ struct Eng {
         list_free(rlu(kloff, i), rlu(kcap, i));
       }
       if (nh > 0) {
-        base = nh / cc;
-        rem0 = nh % cc;
-        int rem = rem0;
+        const int base = nh / cc;
+        int rem = nh % cc;
         int taken = 0;
         // first every new block gets its children (the scour output in hold[] is consumed here) ...
         for (int q = 0; q < cc; q++) {
@@ -2270,7 +2111,6 @@ struct Eng {
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
           const int kb = __ballot(kblk) != 0;
-          if (kb) leafcase = false;
           if (lane == q) {
             nbs = nb;
             lens = len;
@@ -2293,14 +2133,14 @@ struct Eng {
       if (lane == 0) blk[parent].count = (uint32_t)cc;
       wsync();
       // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
-      // site; rebuild uses the union as scratch, and P's leaf case takes its segments from hold[])
+      // site; rebuild uses the union as scratch)
       uint32_t a = 0, c2 = 0, e = 0;
       for (int q = 0; q <= cc; q++) {
         const bool isP = q == cc;
         const uint32_t nb = isP ? parent : rlu(nbs, q);
         a = c2 = e = 0;
         if (isP || rl(kbs, q)) {
-          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e, isP && leafcase ? nh : 0, base, rem0);
+          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e);
           if (bad()) return;
         }
         if (isP) break;
