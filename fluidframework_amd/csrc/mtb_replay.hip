@@ -1651,84 +1651,84 @@ struct Eng {
   // markRangeRemoved (mergeTree.ts:1960-2052) when `remove`, else annotateRange (mergeTree.ts:1895-1958).
   // Emulates depthFirstNodeWalk (mergeTreeNodeWalk.ts:35) with an explicit stack; block post-actions
   // (blockUpdateLength) become one flush of the accumulated observer-length delta per block into its
-  // parent's slot and list.
+  // parent's slot and list.  The walk's per-child loop (skip children of undefined / zero length or
+  // wholly before `start`, stop at the first one at or after `end`) is one scan over the block's slots:
+  // the next child descended into is the first slot at or after the cursor that overlaps the range.
   __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
     if (end == start) return;
-    int pos = 0;
     int d = 0;
-    bool exiting = false;
+    bool exiting = false;  // a leaf block reached `end`: every open block is only flushed from here on
+    walk_depth = -1;       // (pp[] holds the node_map block starts below)
     if (lane == 0) {
       sh->path[0] = root;
       sh->sidx[0] = 0;
       sh->acc[0] = 0;
+      sh->pp[0] = 0;
     }
     wsync();
     load_view(0, root, R, C);
     while (!err) {
       View& V = sh->v[d];
       const int count = U(V.count);
-      int idx = U(sh->sidx[d]);
-      if (!exiting && idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
-        // a block of segments: every touched segment at once
-        pos += map_leaf_block(d, pos, start, end, S, C, remove, opId, rewrite);
-        if (bad()) return;
-        if (pos >= end) exiting = true;
-        idx = count;
-        if (lane == 0) sh->sidx[d] = count;
-        wsync();
-      }
-      if (exiting || idx >= count) {
-        // post-order: flush this block's accumulated observer-length delta into its parent
-        const int a = U(sh->acc[d]);
-        if (a != 0) {
-          if (d > 0) {
-            const int L = d - 1;
-            const int k = U(sh->slot[L]);
+      const int bpos = U(sh->pp[d]);  // position of the block's start in the (R, C) view
+      const int idx = U(sh->sidx[d]);
+      if (!exiting) {
+        if (idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
+          // a block of segments: every touched segment at once
+          const int tot = map_leaf_block(d, bpos, start, end, S, C, remove, opId, rewrite);
+          if (bad()) return;
+          if (bpos + tot >= end) exiting = true;
+        } else {
+          int rlj = 0;
+          if (lane < count) rlj = V.rl[lane];
+          const int def = (lane < count && rlj > 0) ? rlj : 0;
+          const int sj = bpos + cscan8(def) - def;
+          const unsigned long long m = __ballot(lane >= idx && def > 0 && start < sj + def && sj < end);
+          if (m) {
+            const int j = first_set(m);
+            const uint32_t c = U(V.f[F_ID][j]);
+            if (c & MTB_LEAF) { fail(DERR_SHAPE); return; }
+            if (d + 1 >= MTB_VDEPTH) { fail(DERR_DEPTH); return; }
+            const int cpos = rl(sj, j);
             if (lane == 0) {
-              const int v = (int)sh->v[L].f[F_LEN][k] + a;
-              sh->v[L].f[F_LEN][k] = (uint32_t)v;
-              blk[sh->path[L]].f[F_LEN][k] = (uint32_t)v;
-              sh->acc[L] += a;
+              sh->sidx[d] = j + 1;
+              sh->slot[d] = j;
+              sh->path[d + 1] = c;
+              sh->sidx[d + 1] = 0;
+              sh->acc[d + 1] = 0;
+              sh->pp[d + 1] = cpos;
             }
             wsync();
-            append_levels(L, d, S, C, WK_MAIN, a);
+            d++;
+            load_view(d, c, R, C);
+            continue;
           }
+        }
+      }
+      // post-order: flush this block's accumulated observer-length delta into its parent
+      const int a = U(sh->acc[d]);
+      if (a != 0) {
+        if (d > 0) {
+          const int L = d - 1;
+          const int k = U(sh->slot[L]);
           if (lane == 0) {
-            const int v = sh->v[d].len + a;
-            sh->v[d].len = v;
-            blk[sh->path[d]].len = v;
+            const int v = (int)sh->v[L].f[F_LEN][k] + a;
+            sh->v[L].f[F_LEN][k] = (uint32_t)v;
+            blk[sh->path[L]].f[F_LEN][k] = (uint32_t)v;
+            sh->acc[L] += a;
           }
           wsync();
+          append_levels(L, d, S, C, WK_MAIN, a);
         }
-        if (d == 0) break;
-        d--;
-        continue;
+        if (lane == 0) {
+          const int v = sh->v[d].len + a;
+          sh->v[d].len = v;
+          blk[sh->path[d]].len = v;
+        }
+        wsync();
       }
-      if (lane == 0) sh->sidx[d] = idx + 1;
-      wsync();
-      if (end <= pos) {
-        exiting = true;
-        continue;
-      }
-      const int len = U(V.rl[idx]);
-      if (len == MTB_UNDEF || len == 0) continue;
-      const int nextPos = pos + len;
-      if (start >= nextPos) {
-        pos = nextPos;
-        continue;
-      }
-      const uint32_t c = U(V.f[F_ID][idx]);
-      if (c & MTB_LEAF) { fail(DERR_SHAPE); return; }
-      if (d + 1 >= MTB_VDEPTH) { fail(DERR_DEPTH); return; }
-      if (lane == 0) {
-        sh->slot[d] = idx;
-        sh->path[d + 1] = c;
-        sh->sidx[d + 1] = 0;
-        sh->acc[d + 1] = 0;
-      }
-      wsync();
-      d++;
-      load_view(d, c, R, C);
+      if (d == 0) break;
+      d--;
     }
   }
 
