@@ -316,10 +316,13 @@ class Client:
         self._initial = []
         self.longClientId = None
 
-    # detached local edits before collaboration (client.replay.spec.ts:27 insertTextLocal)
-    def insertTextLocal(self, pos, text):
+    # local edits: detached before collaboration (client.replay.spec.ts:27), afterwards a live client's
+    # pending ops (client.ts:196, see insertSegmentLocal)
+    def insertTextLocal(self, pos, text, props=None):
         if self.longClientId is not None:
-            raise MergeTreeError(-6, "unsupported: local ops while collaborating (observer engine)")
+            return self.insertSegmentLocal(pos, text if props is None else {"text": text, "props": props})
+        if props is not None:
+            raise MergeTreeError(-6, "unsupported: detached text with properties")
         cur = "".join(self._initial)
         self._initial = [cur[:pos] + text + cur[pos:]]
 
@@ -341,11 +344,27 @@ class Client:
         self.longClientId = longId
 
     def applyMsg(self, msg, local=False):
-        if local:
-            raise MergeTreeError(-6, "unsupported: local (ack) application on the observer engine")
+        """client.ts:858-887.  A message from this client's own id (`local`) acks its oldest pending op."""
         s = msg if isinstance(msg, (bytes, bytearray)) else (msg.encode() if isinstance(msg, str) else json.dumps(msg).encode())
         self._b._chk(self._b._L.mtb_apply_msg_json(self._b._h, self._doc, s, len(s)))
         self._b._dirty = True
+
+    # ---- a live client's own ops (client.ts:196-247): applied at the next replay, acked by applyMsg
+    def applyLocalOp(self, op):
+        """Queue the IMergeTreeOp `op` (dict or JSON) as this client's local op; returns it."""
+        s = op if isinstance(op, (bytes, bytearray)) else (op.encode() if isinstance(op, str) else json.dumps(op).encode())
+        self._b._chk(self._b._L.mtb_local_op_json(self._b._h, self._doc, s, len(s)))
+        self._b._dirty = True
+        return op
+
+    def insertSegmentLocal(self, pos, seg):
+        """insertSegmentLocal (client.ts:196): `seg` is an IJSONSegment (text, {"text", "props"} or
+        {"marker": {...}, "props"}); returns the IMergeTreeInsertMsg to send."""
+        return self.applyLocalOp({"pos1": pos, "seg": seg, "type": 0})
+
+    def removeRangeLocal(self, start, end):
+        """removeRangeLocal (client.ts:230): returns the IMergeTreeRemoveMsg to send."""
+        return self.applyLocalOp({"pos1": start, "pos2": end, "type": 1})
 
     def getText(self):
         return self._b.text(self._doc)

@@ -11,7 +11,7 @@
 //   heap   : Lru  (8 B)   zamboni LRU heap         (reference: Heap<LRUSegment>, collections/heap.ts)
 //   aux    : u32          property sets and overlapping-remove client lists
 //   freel  : u32          free-block stack
-// A DocState header (256 B) holds each document's slice bases, bump pointers and collab window.
+// A DocState header (384 B) holds each document's slice bases, bump pointers and collab window.
 #pragma once
 #include <stdint.h>
 
@@ -42,6 +42,18 @@
 #define MTB_OP_LOADSEG 5
 #define MTB_F_LDFIRST 0x10  // first segment of an insertSegments batch: ensureIntervalBoundary at the root length
 #define MTB_F_LDLAST 0x20   // last segment of the batch: zamboniSegments
+// Local ops of a live client (the document's own client, short id 0; client.ts:196-247): insert / remove
+// records carrying MTB_F_LOCAL are applied at (currentSeq, own id) with UnassignedSequenceNumber; an
+// MTB_OP_ACK record (the client's own sequenced op) has pos2 = the acked op's type.
+#define MTB_F_LOCAL 0x10
+// A pending (unacked) local insert / remove stores MTB_PEND + localSeq in the segment's F_SEQ / F_RSEQ:
+// larger than every sequence number, so every remote perspective sees it as "not yet" and breakTie orders
+// it after sequenced segments (UnassignedSequenceNumber -> Number.MAX_SAFE_INTEGER - 1, mergeTree.ts:1719).
+#define MTB_PEND 0x40000000
+// Pending segment groups (pendingSegments, mergeTree.ts:532; one SegmentGroup per local op that touched
+// segments): a FIFO directory of MTB_PEND_GROUPS entries [localSeq, member list offset, count, capacity]
+// in the aux arena; member lists (segment ids, group order) grow by doubling.
+#define MTB_PEND_GROUPS 64
 // PermutationVector documents (matrix/src/permutationvector.ts): segments carry a storage-handle start
 // in the F_TEXT field instead of a text offset; their handle table lives in the (otherwise unused) text
 // arena as u32 words [length, handles[0], handles[1], ...] (handletable.ts: handles[0] = free-list head).
@@ -144,8 +156,14 @@ struct DocState {     // 320 bytes
   uint32_t delta_cap, delta_used;  // entries
   uint64_t prof2[4];    // MTB_PROFILE builds: more phases (prof[7 + i])
   uint32_t cnt2[4];     // MTB_PROFILE builds: more event counters (cnt[5 + i])
+  // live client (local ops): collabWindow.localSeq and the pending segment-group FIFO
+  int32_t local_seq;
+  uint32_t pend_dir;    // aux offset of the group directory (0: none yet)
+  uint32_t pend_head;   // directory index of the oldest pending group
+  uint32_t pend_n;      // pending groups
+  uint32_t pad3[12];
 };
-static_assert(sizeof(DocState) == 320, "DocState is copied as 80 dwords (mtb_rewind_kernel)");
+static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
 // Batch-global interned tables (read-only on the device).
 struct Tables {
@@ -175,6 +193,11 @@ struct Tables {
 #define MTB_CELL_CLEAR 2   // matrix cell event: handles [start, start + count) recycled by zamboni
 #define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
 #define DERR_HOST 14       // host-side post-processing of the document's replay failed (HostDoc::hostErr)
+#define DERR_RANGE 15      // a local op outside the local view (getValidOpRange, client.ts:527-592)
+#define DERR_CAP_PEND 16   // more than MTB_PEND_GROUPS unacked local ops
+#define DERR_ACK_INSERT 17 // 0x045 "On insert, seq number already assigned!"
+#define DERR_ACK_REMOVE 18 // 0x046 "On remove ack, missing removal info!"
+#define DERR_LOCAL 19      // a local op the engine does not support (local annotate)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

@@ -38,7 +38,7 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              const uint32_t* psegp, FBlk* blks, const FBlk* pblk);
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                             Tables tables);
+                             Tables tables, int live);
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
@@ -425,6 +425,7 @@ struct mtb_dev {
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
+  bool live = false;                // a document of the batch has made local ops (mtb_local_op_json)
   bool matrix = false;              // MTB_BATCH_MATRIX: documents 2m / 2m+1 are matrix m's rows / cols
   std::vector<std::string> cellVals{"null"};                 // setCell values (JSON text), id 0 = undefined
   std::unordered_map<std::string, uint32_t> cellValIds;
@@ -1364,6 +1365,17 @@ struct PhaseClock {
 void resolve_catch_up(mtb_dev* b, uint32_t i);
 void apply_cell_events(mtb_dev* b, uint32_t matrix);
 
+// the batch's replay kernel: matrix pairs, live clients (local ops anywhere in the batch so far), or the
+// observer replay engine
+void launch_main(mtb_dev* b, const Tables& t) {
+  if (b->matrix)
+    HIPCHK(mtb_launch_matrix(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t));
+  else
+    HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t, b->live ? 1 : 0));
+}
+
 void replay(mtb_dev* b, mtb_stats* out) {
   PhaseClock pc;
   // documents that failed in an earlier replay stay failed (sticky) and are counted in the stats, but
@@ -1495,9 +1507,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
     HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                            b->dHeap.p, b->dAux.p, b->dFree.p, t));
-  HIPCHK((b->matrix ? mtb_launch_matrix : mtb_launch_replay)(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p,
-                                                            b->dBlks.p, b->dLists.p, b->dText.p, b->dHeap.p, b->dAux.p,
-                                                            b->dFree.p, t));
+  launch_main(b, t);
   HIPCHK(hipEventRecord(b->ev1, b->stream));
   HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
@@ -1628,6 +1638,9 @@ void flatten(const HostDoc& d, uint32_t root, std::vector<FlatSeg>& out, bool wi
 }
 
 bool seg_removed(const Seg& s) { return s.rseq >= 0; }
+// a live client's unacked insert / remove (F_SEQ / F_RSEQ = MTB_PEND + localSeq): UnassignedSequenceNumber
+bool seg_pending(int32_t seq) { return seq >= MTB_PEND; }
+int32_t seq_out(int32_t seq) { return seg_pending(seq) ? -1 : seq; }
 bool is_marker(const Seg& s) { return (s.text & MTB_MARKER) != 0; }
 
 struct PropView {
@@ -1724,7 +1737,7 @@ std::string dump_doc(mtb_dev* b, uint32_t i) {
       hj::quote(q, hj::from_utf8(d.longId(c)));
       return q;
     };
-    o += ',' + std::to_string(g.seq) + ',' + cl(g.client) + ',' + std::to_string(seg_removed(g) ? g.rseq : -1) + ",[";
+    o += ',' + std::to_string(seq_out(g.seq)) + ',' + cl(g.client) + ',' + std::to_string(seg_removed(g) ? seq_out(g.rseq) : -1) + ",[";
     rc_list(d, g, rc);
     for (size_t k = 0; k < rc.size(); k++) {
       if (k) o += ',';
@@ -1813,8 +1826,9 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
   std::vector<int> rc;
   for (auto& f : fl) {
     const Seg& g = d.segs[f.id];
+    if (seg_pending(g.seq)) continue;                         // seq === UnassignedSequenceNumber
     if (seg_removed(g) && g.rseq <= minSeq) continue;  // elided
-    if (g.seq <= minSeq && !seg_removed(g)) {
+    if (g.seq <= minSeq && (!seg_removed(g) || seg_pending(g.rseq))) {
       const bool marker = !perm && is_marker(g);
       if (perm) {  // PermutationSegment.canAppend: both unallocated, or contiguous handles
         if (prev && (prev->start == MTB_HANDLE_UNALLOC ? g.text == MTB_HANDLE_UNALLOC : g.text == prev->start + (uint32_t)prev->len)) {
@@ -1867,6 +1881,7 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
       hj::quote(o, hj::from_utf8(d.longId(g.client)));
     }
     if (seg_removed(g)) {
+      if (seg_pending(g.rseq)) raise(MTB_E_ASSERT, "0x065 invalid removed seq");
       rc_list(d, g, rc);
       o += ",\"removedSeq\":" + std::to_string(g.rseq) + ",\"removedClient\":";
       hj::quote(o, hj::from_utf8(d.longId(rc[0])));
@@ -1983,17 +1998,22 @@ void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
     if (isOp) {
       if (!contents || contents->kind != hj::Value::kObj) raise(MTB_E_PARSE, "op message without contents");
       if (longId == d.observer) {
-        // ack path with no pending local segments: one zamboni per member (client.ts:866, mergeTree.ts:1283)
-        const hj::Value* t = member(*contents, u"type");
-        size_t members = 1;
-        if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
-          const hj::Value* ops = member(*contents, u"ops");
-          members = ops && ops->kind == hj::Value::kArr ? ops->items.size() : 0;
-        }
-        for (size_t k = 0; k < members; k++) {
+        // the client's own op: Client.ackPendingSegment (client.ts:641-662), one MergeTree.ackPendingSegment
+        // (mergeTree.ts:1283-1322: the oldest pending group, then zamboni) per member; pos2 = its op type
+        auto ack = [&](const hj::Value& op) {
+          const hj::Value* t = member(op, u"type");
           mtb_op r = base;
           r.type = MTB_OP_ACK;
+          r.pos2 = t && t->kind == hj::Value::kNum ? (uint32_t)(int)t->n : 0xFFFFFFFFu;
           recs.push_back(r);
+        };
+        const hj::Value* t = member(*contents, u"type");
+        if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
+          const hj::Value* ops = member(*contents, u"ops");
+          if (ops && ops->kind == hj::Value::kArr)
+            for (auto& m : ops->items) ack(m);
+        } else {
+          ack(*contents);
         }
       } else {
         pack_delta(b, d, *contents, base, recs);
@@ -2520,6 +2540,39 @@ int mtbx_apply_msg_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) 
   });
 }
 
+// A live client's own op (client.ts:196-247 insertSegmentLocal / removeRangeLocal): the IMergeTreeOp it
+// sends, applied at the document's next replay in its own view with UnassignedSequenceNumber
+// (DESIGN.md section 10).  Local annotates are not supported.
+int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
+  return guarded(b, [&] {
+    if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: local ops on a matrix batch");
+    if (b->opts.flags & MTB_BATCH_CATCHUP) raise(MTB_E_UNSUPPORTED, "unsupported: local ops in a catch-up batch");
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    const hj::Value op = hj::parse(json, len);
+    if (op.kind != hj::Value::kObj) raise(MTB_E_PARSE, "op is not an object");
+    mtb_op base{};
+    base.flags = MTB_F_LOCAL;
+    std::vector<mtb_op> recs;
+    const size_t payloadBefore = d.payload.size();
+    try {
+      pack_delta(b, d, op, base, recs);
+      for (const mtb_op& r : recs) {
+        if (r.type == MTB_OP_ANNOTATE) raise(MTB_E_UNSUPPORTED, "unsupported: local annotate (pending property keys)");
+        if (r.type != MTB_OP_INSERT && r.type != MTB_OP_REMOVE) raise(MTB_E_ARG, "local op without an effect");
+        if (r.type == MTB_OP_INSERT && !(r.flags & MTB_F_MARKER) && r.pos2 == 0) raise(MTB_E_ARG, "empty local insert");
+      }
+    } catch (...) {
+      d.payload.resize(payloadBefore);
+      throw;
+    }
+    b->live = true;
+    d.totalPayload += d.payload.size() - payloadBefore;
+    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
+    d.totalOps += recs.size();
+  });
+}
+
 uint32_t intern_cell_value(mtb_dev* b, const std::string& json) {
   auto [it, fresh] = b->cellValIds.try_emplace(json, (uint32_t)b->cellVals.size());
   if (fresh) b->cellVals.push_back(json);
@@ -2618,6 +2671,7 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
       if (o.type > MTB_OP_ACK && !(b->matrix && o.type == MTB_OP_SETCELL)) raise(MTB_E_ARG, "bad record type");
       if (d.perm && o.type == MTB_OP_INSERT && !(o.flags & MTB_F_PERMSEG)) raise(MTB_E_ARG, "PermutationVector insert without MTB_F_PERMSEG");
       if (!d.perm && (o.flags & MTB_F_PERMSEG)) raise(MTB_E_ARG, "MTB_F_PERMSEG outside a matrix batch");
+      if (o.flags & (MTB_F_LOCAL | MTB_F_LDLAST)) raise(MTB_E_ARG, "record flags 0x10 / 0x20 are internal (local ops: mtb_local_op_json)");
       if (o.type == MTB_OP_SETCELL) {
         if (o.flags & MTB_F_LAST) raise(MTB_E_ARG, "SETCELL records never carry MTB_F_LAST");
         if (o.props >= b->cellVals.size()) raise(MTB_E_ARG, "SETCELL value id out of range (mtb_matrix_intern_value)");
@@ -2674,9 +2728,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
-    HIPCHK((b->matrix ? mtb_launch_matrix : mtb_launch_replay)(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p,
-                                                              b->dBlks.p, b->dLists.p, b->dText.p, b->dHeap.p, b->dAux.p,
-                                                              b->dFree.p, t));
+    launch_main(b, t);
     HIPCHK(hipEventRecord(b->ev1, b->stream));
     HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
@@ -3062,8 +3114,8 @@ int mtbx_matrix_summarize(mtb_dev* b, uint32_t matrix, mtb_blob_list* out) {
 // ------------------------------------------------------------------ segment queries (Client reads)
 namespace {
 // nodeLength of a leaf (mergeTree.ts:916-1004) in the (refSeq R, client C) view; -1 = undefined.
-// C == the observer is the local view (localNetLength, :613-634).  The observer engine holds no
-// unacked segments, so seq / removedSeq are never UnassignedSequenceNumber here.
+// C == the observer is the local view (localNetLength, :613-634).  A live client's unacked insert /
+// remove holds MTB_PEND + localSeq, above every refSeq (UnassignedSequenceNumber).
 int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int minSeq, std::vector<int>& rc) {
   const bool removed = seg_removed(g);
   if (C == 0) {
@@ -3082,7 +3134,7 @@ int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int 
   }
   if (removed && g.rseq <= R) return -1;
   if (g.client == C || g.seq <= R) return removed ? (cRemoved ? 0 : g.len) : g.len;
-  return removed ? -1 : 0;
+  return removed && !seg_pending(g.rseq) ? -1 : 0;
 }
 }  // namespace
 
@@ -3142,10 +3194,10 @@ int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t
           o += "\"TextSegment\",\"text\":";
           hj::quote(o, reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len);
         }
-        o += ",\"cachedLength\":" + std::to_string(g.len) + ",\"seq\":" + std::to_string(g.seq) +
+        o += ",\"cachedLength\":" + std::to_string(g.len) + ",\"seq\":" + std::to_string(seq_out(g.seq)) +
              ",\"clientId\":" + std::to_string(g.client);
         if (seg_removed(g)) {
-          o += ",\"removedSeq\":" + std::to_string(g.rseq) + ",\"removedClientIds\":[";
+          o += ",\"removedSeq\":" + std::to_string(seq_out(g.rseq)) + ",\"removedClientIds\":[";
           rc_list(d, g, rc);
           for (size_t q = 0; q < rc.size(); q++) o += (q ? "," : "") + std::to_string(rc[q]);
           o += "]";

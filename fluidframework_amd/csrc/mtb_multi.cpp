@@ -276,6 +276,9 @@ int mtb_intern_props(mtb_batch* b, const char* json_utf8, size_t len, uint32_t* 
 int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len) {
   DOC_CALL(doc, mtbx_apply_msg_json(d_, l_, json_utf8, len));
 }
+int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len) {
+  DOC_CALL(doc, mtbx_local_op_json(d_, l_, json_utf8, len));
+}
 
 int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, const uint16_t* payload, size_t payload_len) {
   DOC_CALL(doc, mtbx_append_ops(d_, l_, ops, n, payload, payload_len));

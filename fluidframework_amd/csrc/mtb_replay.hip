@@ -41,10 +41,19 @@ namespace mtbk {
 #define PROF_T() ((uint64_t)__builtin_amdgcn_s_memtime())
 #define PROF_ADD(i, t0) (prof[i] += PROF_T() - (t0))
 #define PROF_CNT(i, n) ((i) < NCN ? (void)(evc[(i) < NCN ? (i) : 0] += (n)) : (void)0)
+#ifdef MTB_PROFILE_PACK  // the heap / stage / place slots time packParent's staging, scour and placement instead
+#define PROF_ZADD(i, t0) ((void)(t0))
+#define PROF_PADD(i, t0) PROF_ADD(i, t0)
+#else
+#define PROF_ZADD(i, t0) PROF_ADD(i, t0)
+#define PROF_PADD(i, t0) ((void)(t0))
+#endif
 #else
 #define PROF_T() ((uint64_t)0)
 #define PROF_ADD(i, t0) ((void)(t0))
 #define PROF_CNT(i, n) ((void)0)
+#define PROF_ZADD(i, t0) ((void)(t0))
+#define PROF_PADD(i, t0) ((void)(t0))
 #endif
 enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL = 4, PH_VIEW = 5, PH_SCOUR = 6, PH_HEAP = 7,
        PH_STAGE = 8, PH_PLACE = 9, PH_PACK = 10, NPH = 11 };
@@ -148,7 +157,7 @@ struct ScratchT {  // LDS, one per wave
   uint32_t nseg[8];            // staged fields of a child being inserted
   uint32_t sp[8];              // split_block results: cachedLength and list metadata of both halves
   int32_t ins[4];              // the segment placed by the last insert walk: block, slot, depth, needsScour
-  uint32_t memo[2];            // per-op annotate memo: old props -> new props
+  uint32_t memo[3];            // per-op annotate memo: old props -> new props; [2] MODE_LIVE: overtaken blocks
   Tables tab;                  // batch-wide property tables
   Lru* gheap;                  // the document's global LRU heap slice
   uint32_t* gfree;             // free-block stack
@@ -186,8 +195,10 @@ using ScratchBig = ScratchT<MTB_LDS_HEAP_LONG>;
 
 // Engine variants: MODE_REPLAY (mtb_replay_kernel); MODE_LOAD applies only the LOADSEG records at
 // the head of each document's records (mtb_load_kernel); MODE_MATRIX replays SharedMatrix vector pairs
-// with setCell handle allocation (mtb_matrix_kernel).  Each variant carries only its own code.
-enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2 };
+// with setCell handle allocation (mtb_matrix_kernel); MODE_LIVE is MODE_REPLAY plus the local ops, acks and
+// pending segment groups of live clients (mtb_live_kernel).  Each variant carries
+// only its own code.
+enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3 };
 template <int MODE, class SCR>
 struct Eng {
   DocState* ds;
@@ -217,6 +228,10 @@ struct Eng {
   bool delta_on;                // the record asks for its delta ranges (MTB_F_DELTA)
   uint32_t delta_used;          // entries written in this document's delta slice
   static constexpr bool isPerm = MODE == MODE_MATRIX;  // matrix batches hold PermutationVectors only
+  static constexpr bool isLive = MODE == MODE_LIVE;    // local ops / acks of the document's own client (id 0)
+  int local_seq;                // MODE_LIVE: collabWindow.localSeq
+  uint32_t pend_dir, pend_head, pend_n;  // MODE_LIVE: pending segment-group FIFO (DocState)
+  bool grp_open;                // MODE_LIVE: the current local op already has its group
   int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
   uint64_t prof[NPH];
@@ -303,8 +318,14 @@ struct Eng {
       if (removed) return rc_has(cli_rc0(cli), rcx, C) ? 0 : len;
       return len;
     }
-    if (removed) return MTB_UNDEF;
+    if (removed && !(isLive && rseq >= MTB_PEND)) return MTB_UNDEF;  // (removedSeq !== Unassigned)
     return 0;
+  }
+  // nodeLength of a leaf in the op's perspective: the local client's own view (mergeTree.ts:917-921) or a
+  // remote one
+  __device__ __forceinline__ int leaf_len(int len, int seq, int rseq, uint32_t cli, uint32_t rcx, int R, int C) const {
+    if (isLive && C == 0) return local_len(len, rseq);
+    return seg_vis(len, seq, rseq, cli, rcx, R, C);
   }
   // observer-view length contribution of a child (blockUpdate: cachedLength = sum localNetLength ?? 0)
   __device__ __forceinline__ int child_olen(uint32_t id, int len, int rseq) const {
@@ -364,7 +385,7 @@ struct Eng {
         // record still valid (e.g. after a segment split): recompute the leaves' lengths from LDS
         if (__ballot(lane < count && !(k.id & MTB_LEAF)) == 0) {
           if (lane < count) {
-            k.rl = seg_vis((int)V.f[F_LEN][lane], (int)k.seq, (int)k.rseq, k.cli, V.f[F_RCX][lane], R, C);
+            k.rl = leaf_len((int)V.f[F_LEN][lane], (int)k.seq, (int)k.rseq, k.cli, V.f[F_RCX][lane], R, C);
             V.rl[lane] = k.rl;
           }
           if (lane == 0) V.rlv = 1;
@@ -377,6 +398,7 @@ struct Eng {
     const uint64_t tv0 = PROF_T();
     uint32_t loff = mloff, lcnt = mlcnt, lcapw = mlcap;
     if (!haveMeta) meta_of(d, loff, lcnt, lcapw);
+    if (isLive && C == 0) lcnt = 0;  // the local view: blocks' cachedLength as they are (no corrections)
     // remote-length corrections per child slot (partialLengths.ts:698 getPartialLength).  Entries at or
     // below minSeq sit in the reference's minLength whatever refSeq is, so the scan threshold is
     // max(refSeq, minSeq) (only a summary load's body inserts, at refSeq 0, ever see refSeq < minSeq).
@@ -450,7 +472,7 @@ struct Eng {
     wsync();
     if (lane < count) {
       k.id = w;
-      k.rl = (w & MTB_LEAF) ? seg_vis((int)flen, (int)k.seq, (int)k.rseq, k.cli, frcx, R, C) : (int)flen - sh->corr[lane];
+      k.rl = (w & MTB_LEAF) ? leaf_len((int)flen, (int)k.seq, (int)k.rseq, k.cli, frcx, R, C) : (int)flen - sh->corr[lane];
       V.rl[lane] = k.rl;
     }
     if (lane == 0) {
@@ -586,7 +608,8 @@ struct Eng {
   // Append (seqv, client, kind, delta) to the lists of the path blocks at depths [lo, hi), each entry
   // tagged with the slot the path takes at that depth.  One lane per depth; full lists are
   // re-allocated afterwards, one at a time.  A replay appends the current op's seq, never below any
-  // entry, so the lists stay sorted; a summary load's body appends any seq and marks them unsorted.
+  // entry, so the lists stay sorted; a summary load's body appends any seq, and a live document with
+  // unacked local entries (MTB_PEND + localSeq) appends below them: both mark the lists unsorted.
   __device__ __forceinline__ void append_levels(int lo, int hi, int seqv, int client, int kind, int delta) {
     if (hi <= lo) return;
     bool need = false;
@@ -604,7 +627,7 @@ struct Eng {
         lcnt = P.f[F_RSEQ][k];
         lcap = P.f[F_CLI][k];
       }
-      if constexpr (MODE == MODE_LOAD) {
+      if (MODE == MODE_LOAD || (isLive && pend_n > 0)) {
         if (lcnt < (lcap & ~MTB_LUNSORTED) && !(lcap & MTB_LUNSORTED)) {
           lcap |= MTB_LUNSORTED;
           if (i == 0) {
@@ -646,7 +669,8 @@ struct Eng {
       uint32_t live, cap;
       const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
       if (bad()) return;
-      const uint32_t flag = (MODE == MODE_LOAD) ? MTB_LUNSORTED : 0u;  // (cap carries the kept entries' order)
+      // (cap carries the kept entries' order; pending MTB_PEND + localSeq entries may sit above this seq)
+      const uint32_t flag = (MODE == MODE_LOAD || (isLive && pend_n > 0)) ? MTB_LUNSORTED : 0u;
       if (lane == 0) {
         WEnt e;
         e.seq = seqv;
@@ -1149,6 +1173,31 @@ struct Eng {
     }
   }
 
+  // blockInsert's continuePredicate (mergeTree.ts:1611-1615, forwardExcursion mergeTreeNodeWalk.ts:121-138):
+  // is the first segment after block b in tree order an unacked local insert?  From each ancestor, the
+  // next sibling's leftmost descent (an empty block there moves on to the following sibling).
+  __device__ __forceinline__ bool next_leaf_pending(uint32_t b) {
+    uint32_t cur = b;
+    for (int guard = 0; guard < MTB_VDEPTH; guard++) {
+      const uint32_t par = U(blk[cur].parent);
+      if (par == MTB_NONE) return false;
+      const uint32_t pc = U(blk[par].count);
+      for (uint32_t i = U(blk[cur].index) + 1; i < pc; i++) {
+        uint32_t c = U(blk[par].f[F_ID][i]);
+        uint32_t seq = U(blk[par].f[F_SEQ][i]);
+        while (!(c & MTB_LEAF)) {
+          if (U(blk[c].count) == 0) { c = MTB_NONE; break; }
+          seq = U(blk[c].f[F_SEQ][0]);
+          c = U(blk[c].f[F_ID][0]);
+        }
+        if (c != MTB_NONE) return (int)seq >= MTB_PEND;
+      }
+      cur = par;
+    }
+    fail(DERR_DEPTH);
+    return false;
+  }
+
   // ------------------------------------------------------------------ insertingWalk
   // mode 0: ensureIntervalBoundary (seq = TreeMaintenance, leaf = splitLeafSegment)
   // mode 1: blockInsert of the staged segment sh->nseg (seq S).  Returns false if it was not placed.
@@ -1168,6 +1217,7 @@ struct Eng {
     }
     walk_depth = -1;
     struct_changed = false;
+    int from = 0;  // MODE_LIVE: first slot to consider (a walk resumed past theUnfinishedNode)
     while (true) {
       if (d >= MTB_VDEPTH) { fail(DERR_DEPTH); return false; }
       if (lane == 0) {
@@ -1178,9 +1228,10 @@ struct Eng {
       Kid k;
       const int count = load_view(d, b, R, C, k, haveMeta, mo, mc, mk);
       const View& V = sh->v[d];
+      const int fromv = isLive ? from : 0;
       uint32_t cid = MTB_NONE;
       int clen = 0, cseq = 0;
-      if (lane < count) {
+      if (lane < count && lane >= fromv) {
         cid = k.id;
         clen = k.rl;
         cseq = (int)k.seq;
@@ -1188,9 +1239,9 @@ struct Eng {
       const int def = (lane < count && clen > 0) ? clen : 0;
       const int incl = cscan8(def);
       const int pj = p - (incl - def);
-      const bool isBlk = lane < count && !(cid & MTB_LEAF);
+      const bool isBlk = lane < count && lane >= fromv && !(cid & MTB_LEAF);
       const bool tie = isBlk || (insertMode && pj == 0 && S > cseq);
-      const bool qual = lane < count && clen != MTB_UNDEF && (pj < clen || (pj == clen && tie));
+      const bool qual = lane < count && lane >= fromv && clen != MTB_UNDEF && (pj < clen || (pj == clen && tie));
       const unsigned long long m = __ballot(qual);
       int at;
       if (m) {
@@ -1207,6 +1258,7 @@ struct Eng {
           b = cj;
           p = pjj;
           d++;
+          if (isLive) from = 0;
           continue;
         }
         walk_depth = d;
@@ -1221,6 +1273,17 @@ struct Eng {
         at = j;
       } else {
         const int total = rl(incl, 7);
+        if (isLive && p - total == 0 && insertMode && S < MTB_PEND && d > 0 && next_leaf_pending(b)) {
+          // theUnfinishedNode (mergeTree.ts:1785-1787, 1816-1824): a sequenced insert at the end of this
+          // block goes on past it when the next segment is an unacked local insert: the parent's scan
+          // continues after this child at position 0
+          d--;
+          b = U(sh->path[d]);
+          p = 0;
+          from = U(sh->slot[d]) + 1;
+          haveMeta = false;
+          continue;
+        }
         if (p - total == 0) walk_depth = d;
         if (p - total != 0 || !insertMode) return !insertMode;
         at = count;
@@ -1262,6 +1325,7 @@ struct Eng {
     n_mod += 2;
     wsync();
     insert_slot(d, j + 1);
+    if (isLive && pend_n > 0) grp_split(U(V.f[F_ID][j]) & ~MTB_LEAF, r);
   }
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
@@ -1366,6 +1430,138 @@ struct Eng {
       return true;
     }
     return false;
+  }
+
+  // ------------------------------------------------------------------ pending segment groups (MODE_LIVE)
+  // The FIFO of SegmentGroups (pendingSegments, mergeTree.ts:532): directory entry i (0 = oldest) is
+  // [localSeq, member list offset, count, capacity] in the aux arena.
+  __device__ __forceinline__ gptr<uint32_t> grp_ent(uint32_t i) const {
+    return UP(aux) + pend_dir + 4u * ((pend_head + i) % MTB_PEND_GROUPS);
+  }
+  // addToPendingList (mergeTree.ts:1324-1357): segment `sid` joins the current local op's group (made on
+  // its first segment)
+  __device__ __forceinline__ void grp_add(uint32_t sid) {
+    if (!grp_open) {
+      if (pend_n >= MTB_PEND_GROUPS) { fail(DERR_CAP_PEND); return; }
+      if (pend_dir == 0) {
+        pend_dir = alloc_aux(4 * MTB_PEND_GROUPS);
+        pend_head = 0;
+        if (bad()) return;
+      }
+      const uint32_t off = alloc_aux(8);
+      if (bad()) return;
+      const auto e = grp_ent(pend_n);
+      if (lane == 0) {
+        e[0] = (uint32_t)local_seq;
+        e[1] = off;
+        e[2] = 0;
+        e[3] = 8;
+      }
+      wsync();
+      pend_n++;
+      grp_open = true;
+    }
+    grp_push(pend_n - 1, sid);
+  }
+  // append a member to directory entry i (its list doubles when full)
+  __device__ __forceinline__ void grp_push(uint32_t i, uint32_t sid) {
+    const auto e = grp_ent(i);
+    uint32_t off = U(e[1]);
+    const uint32_t cnt = U(e[2]), cap = U(e[3]);
+    if (cnt >= cap) {
+      const uint32_t no = alloc_aux(2 * cap);
+      if (bad()) return;
+      for (uint32_t q = lane; q < cnt; q += 64) aux[no + q] = aux[off + q];
+      wsync();
+      if (lane == 0) {
+        e[1] = no;
+        e[3] = 2 * cap;
+      }
+      off = no;
+    }
+    if (lane == 0) {
+      aux[off + cnt] = sid;
+      e[2] = cnt + 1;
+    }
+    wsync();
+  }
+  // segmentGroups.copyTo (mergeTreeNodes.ts:239-245) for a split: the right half `r` joins every pending
+  // group that holds the left half `s`
+  __device__ __forceinline__ void grp_split(uint32_t s, uint32_t r) {
+    for (uint32_t i = 0; i < pend_n && !err; i++) {
+      const auto e = grp_ent(i);
+      const uint32_t off = U(e[1]), cnt = U(e[2]);
+      if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
+      bool found = false;
+      for (uint32_t q = 0; q < cnt; q += 64) found |= __ballot(q + lane < cnt && aux[off + q + lane] == s) != 0;
+      if (found) grp_push(i, r);
+    }
+  }
+  // The lists of every ancestor of block b from its parent up to the root, rebuilt bottom-up from their
+  // children (nodeUpdateLengthNewStructure along blockUpdatePathLengths, mergeTree.ts:2419-2434).
+  __device__ __forceinline__ void rebuild_up(uint32_t b) {
+    if (b >= blk_used) { fail(DERR_SHAPE); return; }
+    uint32_t X = U(blk[b].parent);
+    for (int guard = 0; X != MTB_NONE && !err; guard++) {
+      if (guard >= MTB_VDEPTH || X >= blk_used) { fail(DERR_SHAPE); return; }
+      const uint32_t par = U(blk[X].parent), idx = U(blk[X].index);
+      uint32_t ooff, ocap;
+      if (par == MTB_NONE) {
+        ooff = U(blk[X].loff);
+        ocap = U(blk[X].lcap);
+      } else {
+        ooff = U(blk[par].f[F_SEQ][idx]);
+        ocap = U(blk[par].f[F_CLI][idx]);
+      }
+      uint32_t a, c2, e;
+      rebuild(X, ooff, ocap, a, c2, e);
+      if (bad()) return;
+      store_meta_of(X, par, idx, a, c2, e);
+      X = par;
+    }
+  }
+  // ackPendingSegment (mergeTree.ts:1283-1322, BaseSegment.ack mergeTreeNodes.ts:439-480) for the client's
+  // own op sequenced at S: the oldest group's segments get seq S (insert) or removedSeq S (remove; already
+  // set when a remote remove overtook it), join the LRU in group order, and their paths' lists are rebuilt.
+  __device__ __forceinline__ void ack_group(int S, int opType) {
+    if (pend_n == 0) return;
+    const auto e = grp_ent(0);
+    const uint32_t off = U(e[1]), cnt = U(e[2]);
+    if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
+    pend_head = (pend_head + 1) % MTB_PEND_GROUPS;
+    pend_n--;
+    if (opType != 0 && opType != 1) { fail(DERR_LOCAL); return; }
+    for (uint32_t i = 0; i < cnt && !err; i++) {
+      const uint32_t sid = U(aux[off + i]);
+      if (sid >= seg_used) { fail(DERR_SHAPE); return; }
+      const uint32_t b = U(segp[sid]);
+      if (b >= blk_used) { fail(DERR_SHAPE); return; }
+      const uint32_t* rec = bw(b);
+      const uint32_t id = lane < MTB_MAXCH ? rec[F_ID * 8 + lane] : MTB_NONE;
+      const unsigned long long m = __ballot(id == (MTB_LEAF | sid));
+      if (!m) { fail(DERR_SHAPE); return; }
+      const int j = first_set(m);
+      const int sq = (int)U(rec[F_SEQ * 8 + j]), rs = (int)U(rec[F_RSEQ * 8 + j]);
+      const int sc = (int)U(blk[b].scour);
+      if (opType == 0) {
+        if (sq < MTB_PEND) { fail(DERR_ACK_INSERT); return; }
+        if (lane == 0) blk[b].f[F_SEQ][j] = (uint32_t)S;
+      } else {
+        if (rs < 0) { fail(DERR_ACK_REMOVE); return; }
+        if (rs >= MTB_PEND && lane == 0) blk[b].f[F_RSEQ][j] = (uint32_t)S;
+      }
+      n_mod += 1;
+      wsync();
+      lru_add(sid, b, sc, S);  // addToLRUSet(segment, seq)
+    }
+    // nodesToUpdate: the distinct parents, in order (a repeat only rebuilds again)
+    uint32_t prev = MTB_NONE;
+    for (uint32_t i = 0; i < cnt && !err; i++) {
+      const uint32_t b = U(segp[U(aux[off + i])]);  // (ids checked above)
+      if (b != prev) rebuild_up(b);
+      prev = b;
+    }
+    view_clear();
   }
 
   // ------------------------------------------------------------------ properties
@@ -1593,9 +1789,49 @@ struct Eng {
       if (lane == 0) sh->acc[d] += dsum;
       wsync();
       if (COLD(delta_on)) delta_emit(fresh, id & ~MTB_LEAF, (uint32_t)len, props);
+      if (isLive && S >= MTB_PEND) {  // a local remove: its fresh segments join its group, in order
+        unsigned long long fm = __ballot(fresh);
+        while (fm && !err) {
+          const int t = first_set(fm);
+          fm &= fm - 1;
+          grp_add(rlu(id, t) & ~MTB_LEAF);
+        }
+      }
+      if (isLive) {
+        // a remote remove of a segment removed by an unacked local op: the remote client goes to the
+        // head of removedClientIds and its seq becomes removedSeq (mergeTree.ts:1980-1988); the lists of
+        // the block's ancestors are rebuilt after the nodeMap (overwrite -> nodeUpdateLengthNewStructure)
+        unsigned long long pm = __ballot(visit && rseq >= MTB_PEND && S < MTB_PEND);
+        if (pm) {
+          while (pm && !err) {
+            const int t = first_set(pm);
+            pm &= pm - 1;
+            const uint32_t h = alloc_aux(2);
+            if (bad()) return 0;
+            if (lane == 0) {
+              aux[h] = 1;
+              aux[h + 1] = 0;  // the local client (short id 0)
+              const uint32_t ncli = (U(V.f[F_CLI][t]) & 0xFFFF) | ((uint32_t)C << 16);
+              V.f[F_RSEQ][t] = (uint32_t)S;
+              V.f[F_CLI][t] = ncli;
+              V.f[F_RCX][t] = h;
+              blk[b].f[F_RSEQ][t] = (uint32_t)S;
+              blk[b].f[F_CLI][t] = ncli;
+              blk[b].f[F_RCX][t] = h;
+            }
+            wsync();
+          }
+          if (lane == 0) {
+            const uint32_t nrb = sh->memo[2];
+            if (nrb < 64) sh->pk[nrb] = b;
+            sh->memo[2] = nrb + 1;
+          }
+          wsync();
+        }
+      }
       // overlapping removes (already removed): append C to removedClientIds (copy-on-write list) and an
       // OVERLAP entry on every ancestor list (no observer-length change)
-      unsigned long long om = __ballot(visit && rseq >= 0);
+      unsigned long long om = __ballot(visit && rseq >= 0 && !(isLive && rseq >= MTB_PEND));
       if (COLD(om))
       while (om) {
         const int t = first_set(om);
@@ -1636,7 +1872,7 @@ struct Eng {
     // addToLRUSet for the first visited segment (the block's needsScour then becomes true)
     const int t = first_set(vm);
     const uint32_t tid = rlu(id, t);
-    if (S > curSeq && U(V.scour) != 1) {
+    if (S > curSeq && U(V.scour) != 1 && !(isLive && S >= MTB_PEND)) {
       if (lane == 0) {
         V.scour = 1;
         blk[b].scour = 1;
@@ -2068,6 +2304,7 @@ struct Eng {
   __device__ __forceinline__ void pack_parent(uint32_t parent) {
     while (!err) {
       PROF_CNT(CN_PACK, 1);
+      uint64_t tp = PROF_T();
       stage_rec(parent);
       const int pc = U(sh->zr.count);
       const uint32_t pparent = U(sh->zr.parent), pindex = U(sh->zr.index);
@@ -2078,8 +2315,12 @@ struct Eng {
       const uint32_t ploff_v = pm[0], pcap_v = pparent == MTB_NONE ? pm[2] : pm[2 * MTB_MAXCH];
       stage_recs(pc, kids);
       const uint32_t ploff = U(ploff_v), pcap = U(pcap_v);
+      PROF_PADD(PH_HEAP, tp);
+      tp = PROF_T();
       const int nh = scour(pc, 0);
       if (bad()) return;
+      PROF_PADD(PH_STAGE, tp);
+      tp = PROF_T();
       int cc = 0;
       uint32_t nbs = 0;      // lane q: new block q, its observer length, whether its children are blocks
       int lens = 0, kbs = 0;
@@ -2132,6 +2373,7 @@ struct Eng {
       }
       if (lane == 0) blk[parent].count = (uint32_t)cc;
       wsync();
+      PROF_PADD(PH_PLACE, tp);
       // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
       // site; rebuild uses the union as scratch)
       uint32_t a = 0, c2 = 0, e = 0;
@@ -2333,13 +2575,13 @@ struct Eng {
       uint64_t tz = PROF_T();
       const uint32_t bp = segp[top.seg];  // in flight while the heap is fixed down
       heap_get();
-      PROF_ADD(PH_HEAP, tz);
+      PROF_ZADD(PH_HEAP, tz);
       tz = PROF_T();
       const uint32_t b = U(bp);
-      if (b == MTB_NONE) { PROF_CNT(CN_PSKIP, 1); PROF_ADD(PH_STAGE, tz); continue; }
+      if (b == MTB_NONE) { PROF_CNT(CN_PSKIP, 1); PROF_ZADD(PH_STAGE, tz); continue; }
       stage_recs(1, b);
       const int sc = U(sh->pr[0].scour);
-      PROF_ADD(PH_STAGE, tz);
+      PROF_ZADD(PH_STAGE, tz);
       if (sc == 0) { PROF_CNT(CN_PSKIP, 1); continue; }
       const int count = U(sh->pr[0].count);
       const uint32_t parent = U(sh->pr[0].parent);
@@ -2351,12 +2593,12 @@ struct Eng {
       // nh == count: nothing was dropped or appended, the record is unchanged
       if (nh < count) {
         place_children(b, 0, nh);
-        PROF_ADD(PH_PLACE, tz);
+        PROF_ZADD(PH_PLACE, tz);
         tz = PROF_T();
         if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);
         PROF_ADD(PH_PACK, tz);
       } else {
-        PROF_ADD(PH_PLACE, tz);
+        PROF_ZADD(PH_PLACE, tz);
       }
     }
   }
@@ -2425,12 +2667,43 @@ struct Eng {
     }
     if (o.flags & MTB_F_LDLAST) zamboni_p();
   }
+  // A live client's own op (client.ts:196-247 insertSegmentLocal / removeRangeLocal): applied in its own
+  // view at (currentSeq, own id) with UnassignedSequenceNumber (here MTB_PEND + the new localSeq), after
+  // getValidOpRange's bounds check (client.ts:527-592); no LRU, no zamboni, no sequence-number update.
+  __device__ __forceinline__ void apply_local(const mtb_op& o) {
+    grp_open = false;
+    const int len = (int)U(blk[root].len);  // the local view's length
+    if (o.type == MTB_OP_INSERT) {
+      if ((int)o.pos1 < 0 || (int)o.pos1 > len) { fail(DERR_RANGE); return; }
+    } else if (o.type == MTB_OP_REMOVE) {
+      if ((int)o.pos1 < 0 || (int)o.pos1 > len || o.pos2 < o.pos1 || (int)o.pos2 > len) { fail(DERR_RANGE); return; }
+    } else {
+      fail(DERR_LOCAL);
+      return;
+    }
+    mtb_op l = o;
+    l.seq = (uint32_t)(MTB_PEND + local_seq + 1);
+    l.ref_seq = (uint32_t)curSeq;
+    l.client = 0;
+    l.flags &= (uint8_t)~MTB_F_LAST;
+    local_seq++;  // (insertSegments / markRangeRemoved: ++collabWindow.localSeq)
+    if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_MARKER) && o.pos2 == 0) local_seq--;  // nothing inserted
+    apply_op(l);
+  }
   __device__ __forceinline__ void apply(const mtb_op& o) {
+    if (isLive && (o.flags & MTB_F_LOCAL)) {
+      apply_local(o);
+      return;
+    }
+    apply_op(o);
+  }
+  __device__ __forceinline__ void apply_op(const mtb_op& o) {
     const uint64_t tA = PROF_T();
     memo_old = MTB_NONE;
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)(int16_t)o.client;
-    if constexpr (MODE == MODE_REPLAY) delta_on = (o.flags & MTB_F_DELTA) != 0;
+    const bool local = isLive && S >= MTB_PEND;
+    if constexpr (MODE == MODE_REPLAY || MODE == MODE_LIVE) delta_on = (o.flags & MTB_F_DELTA) != 0;
     else delta_on = false;
     if constexpr (MODE == MODE_LOAD) {
       apply_loadseg(o, S, C);
@@ -2472,7 +2745,8 @@ struct Eng {
             return;
           }
           settle();
-          if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (local) grp_add(sid);  // saveIfLocal (mergeTree.ts:1617-1637)
+          else if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);
           if (COLD(delta_on)) {
             const uint32_t from = delta_used;
             delta_emit(lane == 0, sid, (uint32_t)len, o.props ? (MTB_GPROPS | UP(sh->tab.pidx)[2 * o.props + 1]) : 0u);
@@ -2481,7 +2755,7 @@ struct Eng {
           }
           PROF_ADD(PH_INSERT, t0);
         }
-        zamboni_p();
+        if (!local) zamboni_p();
         break;
       }
       case MTB_OP_REMOVE:
@@ -2497,23 +2771,33 @@ struct Eng {
         if (bad()) return;
         t0 = PROF_T();
         const uint32_t dfrom = delta_used;
+        if (isLive) sh->memo[2] = 0;
         node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);
         }
+        if (isLive) {  // blocks whose segments a remote remove took over from unacked local removes
+          const uint32_t nrb = U(sh->memo[2]);
+          if (nrb > 64) { fail(DERR_CAP_PEND); return; }
+          const uint32_t mine = (uint32_t)lane < nrb ? sh->pk[lane] : MTB_NONE;  // (pk shares the rebuild scratch)
+          wsync();
+          for (uint32_t i = 0; i < nrb && !err; i++) rebuild_up(rlu(mine, (int)i));
+          if (nrb) view_clear();
+        }
         PROF_ADD(PH_NODEMAP, t0);
-        zamboni_p();
+        if (!local) zamboni_p();
         break;
       }
       case MTB_OP_ACK:
+        if (isLive) ack_group(S, (int)o.pos2);
         zamboni_p();
         break;
       default:
         break;
     }
     if (bad()) return;
-    if (o.flags & MTB_F_LAST) {  // updateSeqNumbers (client.ts:877-887)
+    if ((o.flags & MTB_F_LAST) && !local) {  // updateSeqNumbers (client.ts:877-887)
       if (!(curSeq <= S)) { fail(DERR_ASSERT_SEQ); return; }
       curSeq = S;
       if (!((int)o.msn <= S)) { fail(DERR_ASSERT_MSN); return; }
@@ -2584,6 +2868,11 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.delta_used = ds->delta_used;
   e.cur_k = 0;
   e.sp_internal = false;
+  e.local_seq = ds->local_seq;
+  e.pend_dir = ds->pend_dir;
+  e.pend_head = ds->pend_head;
+  e.pend_n = ds->pend_n;
+  e.grp_open = false;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
   for (int i = 0; i < NPH; i++) e.prof[i] = 0;
@@ -2671,6 +2960,12 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
     ds->heap_cnt = e.heap_cnt;
     ds->aux_used = e.aux_used;
     ds->delta_used = e.delta_used;
+    if (MODE == MODE_LIVE) {
+      ds->local_seq = e.local_seq;
+      ds->pend_dir = e.pend_dir;
+      ds->pend_head = e.pend_head;
+      ds->pend_n = e.pend_n;
+    }
     ds->n_mod += e.n_mod;
     ds->ops_applied += e.ops_applied;
     ds->text_bytes += e.text_bytes;
@@ -2707,6 +3002,13 @@ extern "C" __global__ void __launch_bounds__(64, 1)
   __shared__ ScratchBig sh;
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+// Batches holding live clients (local ops, acks of them): the replay engine with the local-op paths.
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_live_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                    WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  replay_doc<MODE_LIVE>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
 // SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
@@ -2730,8 +3032,11 @@ extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
 #define MTB_FEW_DOCS 1024
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                             Tables tables) {
-  if (ndocs <= MTB_FEW_DOCS)
+                             Tables tables, int live) {
+  if (live)
+    hipLaunchKernelGGL(mtb_live_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
+                       aux, freel, tables);
+  else if (ndocs <= MTB_FEW_DOCS)
     hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
                        heap, aux, freel, tables);
   else
@@ -2886,9 +3191,9 @@ extern "C" __global__ void __launch_bounds__(64)
         h = dg_mix(h, K);
         h = dg_mix(h, t);
         h = dg_mix(h, len);
-        h = dg_mix(h, seq);
+        h = dg_mix(h, (int32_t)seq >= MTB_PEND ? 0xFFFFFFFFu : seq);  // unacked: UnassignedSequenceNumber
         h = dg_mix(h, (uint32_t)(int32_t)(int16_t)(cli & 0xFFFF));
-        h = dg_mix(h, rseq);
+        h = dg_mix(h, (int32_t)rseq >= MTB_PEND ? 0xFFFFFFFFu : rseq);
         h = dg_mix(h, Rc);
         h = dg_mix(h, Ph);
         acc += dg_fmix(h + (nsegs + (uint64_t)sg + 1) * 0xD6E8FEB86659FD93ull);
@@ -2941,14 +3246,14 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
 // DocState header, the root block and the initial segment's parent; ops and payload stay resident.
 extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, uint32_t* segp,
                                              const uint32_t* psegp, FBlk* blks, const FBlk* pblk) {
-  // one 64-lane wave per document: lanes copy the 256-byte header and the 320-byte root block
+  // one 64-lane wave per document: lanes copy the 384-byte header and the 320-byte root block
   const uint32_t i = blockIdx.x;
   const int l = threadIdx.x;
   if (i >= ndocs) return;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pristine + i);
   uint32_t* dst = reinterpret_cast<uint32_t*>(docs + i);
   dst[l] = src[l];
-  if (l < 16) dst[64 + l] = src[64 + l];
+  if (l < 32) dst[64 + l] = src[64 + l];
   const uint64_t bb = pristine[i].blk_base, sb = pristine[i].seg_base;
   const uint32_t* ps = reinterpret_cast<const uint32_t*>(pblk + i);
   uint32_t* bd = reinterpret_cast<uint32_t*>(blks + bb);

@@ -181,7 +181,8 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
     return msgs
 
 
-def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False):
+def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
+                   record=None):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
@@ -228,21 +229,45 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
             clients[k].apply_msg(log[seen[k]])
             seen[k] += 1
 
+    # record (a dict): per round, each client's events ("local", op) / ("msg", msg) and then its state
+    # (digest, text), for replaying the same farm on the engine
+    rounds = record.setdefault("rounds", []) if record is not None else None
+    if record is not None:
+        record["ids"] = ids
+        _deliver = deliver
+
+        def deliver(k, upto):  # noqa: F811
+            while seen[k] < upto:
+                rounds[-1][k].append(("msg", log[seen[k]]))
+                _deliver(k, seen[k] + 1)
+
+    def end_round():
+        if rounds is not None:
+            rounds[-1] = [(ev, clients[k].digest(), clients[k].get_text()) for k, ev in enumerate(rounds[-1])]
+
     for _ in range(n_rounds):
+        if rounds is not None:
+            rounds.append([[] for _ in range(n_clients)])
         for k in rng.sample(range(n_clients), rng.randint(1, n_clients)):
             for _ in range(rng.randint(1, 3)):
                 ref = clients[k].current_seq
                 op = local_op(clients[k])
                 if op is not None:
                     queue.append((ids[k], ref, op))
+                    if rounds is not None:
+                        rounds[-1][k].append(("local", op))
         for _ in range(rng.randint(0, len(queue))):
             sequence(None)
         for k in range(n_clients):
             deliver(k, seen[k] + rng.randint(0, len(log) - seen[k]))
+        end_round()
+    if rounds is not None:
+        rounds.append([[] for _ in range(n_clients)])
     while queue:
         sequence(None)
     for k in range(n_clients):
         deliver(k, len(log))
+    end_round()
     for m in log:
         obs.apply_msg(m)
     return clients, obs, log

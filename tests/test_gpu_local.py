@@ -1,0 +1,92 @@
+"""Live clients on the GPU engine: local inserts / removes
+with pending segment groups, acks, remote ops overtaking pending removes and theUnfinishedNode.
+
+Parity: the conflict farm of tests/helpers.run_local_farm (client.conflictFarm.spec.ts with
+TestClientLogger) runs on the oracle; every client's event stream -- its local ops and the sequenced
+messages as it received them -- is replayed on the engine, one document per client, and after every farm
+round each document's state digest and text equal its oracle client's (pending segments included: an
+unacked seq is UnassignedSequenceNumber in both).  Local annotates are not supported by the engine, so the
+farms here make inserts and removes only.
+"""
+import pytest
+
+from helpers import run_local_farm
+
+pytestmark = pytest.mark.gpu
+
+
+def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1):
+    from fluidframework_amd import MergeTreeBatch
+    rec = {}
+    run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=False, record=rec)
+    ids = rec["ids"]
+    B = MergeTreeBatch(n_clients, new_length_calc=new_mode)
+    for k, cid in enumerate(ids):
+        B[k].insertTextLocal(0, "hello world")
+        B[k].startOrUpdateCollaboration(cid)
+    checked = 0
+    for r, rnd in enumerate(rec["rounds"]):
+        for k, (events, _, _) in enumerate(rnd):
+            for kind, x in events:
+                if kind == "local":
+                    B[k].applyLocalOp(x)
+                else:
+                    B[k].applyMsg(x)
+        if (r + 1) % rounds_per_replay and r + 1 < len(rec["rounds"]):
+            continue
+        B.replay()
+        dig = B.digests()
+        for k, (_, odig, otext) in enumerate(rnd):
+            assert B.text(k) == otext, f"seed {seed} round {r} client {k}: text"
+            assert dig[k] == odig, f"seed {seed} round {r} client {k}: digest"
+            checked += 1
+    return checked
+
+
+@pytest.mark.parametrize("seed", list(range(1, 17)))
+def test_local_farm_every_round(seed):
+    """Replay after every round: pending groups, acks and remote ops interleave across replays."""
+    assert _replay_farm(seed, n_clients=4, n_rounds=40, new_mode=False) > 0
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_local_farm_new_length_calc(seed):
+    assert _replay_farm(seed, n_clients=4, n_rounds=40, new_mode=True) > 0
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23, 24])
+def test_local_farm_batched_rounds(seed):
+    """Many rounds per replay (local ops, acks and remote messages in one launch), more clients."""
+    assert _replay_farm(seed, n_clients=8, n_rounds=150, new_mode=seed % 2 == 0, rounds_per_replay=10) > 0
+
+
+def test_local_insert_then_ack_api():
+    """Client-level calls: insertTextLocal / removeRangeLocal while collaborating return the ops to send;
+    the sequenced messages ack them (client.ts:196-247, 641-662)."""
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1)
+    c = B[0]
+    c.insertTextLocal(0, "hello")
+    c.startOrUpdateCollaboration("me")
+    op1 = c.insertTextLocal(5, " world")
+    op2 = c.removeRangeLocal(0, 1)
+    B.replay()
+    assert c.getText() == "ello world"
+    for seq, op in ((1, op1), (2, op2)):
+        c.applyMsg({"clientId": "me", "sequenceNumber": seq, "referenceSequenceNumber": 0,
+                    "minimumSequenceNumber": 0, "type": "op", "contents": op})
+    c.applyMsg({"clientId": "other", "sequenceNumber": 3, "referenceSequenceNumber": 2, "minimumSequenceNumber": 2,
+                "type": "op", "contents": {"type": 0, "pos1": 0, "seg": "H"}})
+    B.replay()
+    assert c.getText() == "Hello world"
+
+
+def test_local_op_out_of_range_fails_at_replay():
+    from fluidframework_amd import MergeTreeBatch
+    from fluidframework_amd.client import MergeTreeError
+    B = MergeTreeBatch(1)
+    B[0].insertTextLocal(0, "abc")
+    B[0].startOrUpdateCollaboration("me")
+    B[0].removeRangeLocal(1, 9)
+    with pytest.raises(MergeTreeError):
+        B.replay()
