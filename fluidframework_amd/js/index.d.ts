@@ -13,6 +13,8 @@ export interface BatchOptions {
   mergeTreeUseNewLengthCalculations?: boolean;
   mergeTreeSnapshotChunkSize?: number;
   device?: number;
+  /** GPU indices to spread the documents over (documents placed by hash, one engine + stream per device) */
+  devices?: number[];
   /** false: SnapshotLegacy summaries with tracked catch-up messages (the reference default); default true here */
   newMergeTreeSnapshotFormat?: boolean;
 }
@@ -27,6 +29,9 @@ export interface ISequencedDocumentMessage {
 export declare class MergeTreeBatch {
   constructor(ndocs: number, options?: BatchOptions);
   readonly ndocs: number;
+  digests(first?: number, n?: number): string[];
+  summarizeV1Many(docs: number[], msn?: number, seq?: number, threads?: number):
+    { blobs: [string, string][]; summary: string }[];
   lastStats: ReplayStats | undefined;
   client(i: number): Client;
   flush(): ReplayStats;
@@ -55,7 +60,10 @@ export interface SegmentInfo {
   properties?: Record<string, unknown>;
 }
 export declare class Client {
-  insertTextLocal(pos: number, text: string): void;
+  insertTextLocal(pos: number, text: string, props?: Record<string, unknown>): unknown;
+  applyLocalOp(op: Record<string, unknown> | string): unknown;
+  insertSegmentLocal(pos: number, seg: unknown): Record<string, unknown>;
+  removeRangeLocal(start: number, end: number): Record<string, unknown>;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   load(runtime: { clientId?: string } | undefined,
        storage: { readBlob(path: string): Promise<ArrayBufferLike | Uint8Array | string> }): Promise<{ catchupOpsP: Promise<unknown[]> }>;

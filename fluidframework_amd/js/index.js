@@ -47,8 +47,10 @@ class MergeTreeBatch {
     this.ndocs = n;
     this.v1 = options.newMergeTreeSnapshotFormat !== false;
     const catchUp = !this.v1 && !(_flags & MTB_BATCH_MATRIX) ? MTB_BATCH_CATCHUP : 0;
+    // options.devices: GPU indices to spread the documents over (one engine and stream per device)
+    const mask = Array.isArray(options.devices) ? options.devices.reduce((m, d) => m | (1 << d), 0) >>> 0 : 0;
     this.handle = native.create(n, options.mergeTreeUseNewLengthCalculations ? 1 : 0,
-      options.mergeTreeSnapshotChunkSize || 0, options.device || 0, _flags | catchUp);
+      options.mergeTreeSnapshotChunkSize || 0, options.device || 0, _flags | catchUp, mask);
     this.dirty = false;
     this.busy = false;
     this.lastStats = undefined;
@@ -57,6 +59,21 @@ class MergeTreeBatch {
   }
 
   client(i) { return this.clients[i]; }
+
+  /** Per-document state digests (16-digit hex) of documents [first, first + n), computed on the GPU. */
+  digests(first = 0, n = this.ndocs - first) {
+    this.ensureFlushed();
+    return native.digests(this.handle, first, n);
+  }
+
+  /**
+   * SnapshotV1 summaries of many documents at once (one bulk download, `threads` host threads):
+   * [{blobs: [[path, content], ...], summary}] in the order of `docs`; msn / seq < 0: the current window.
+   */
+  summarizeV1Many(docs, msn = -1, seq = -1, threads = 0) {
+    this.ensureFlushed();
+    return native.summarizeV1Many(this.handle, docs, msn, seq, threads);
+  }
 
   checkIdle() {
     if (this.busy) throw new Error("MergeTreeBatch: an asynchronous flush is in progress");
@@ -162,10 +179,34 @@ class Client {
   }
 
   // ---- detached content (before collaboration) ------------------------------------------------
-  /** TestClient.insertTextLocal (testClient.ts:195) before startOrUpdateCollaboration. */
-  insertTextLocal(pos, text) {
-    if (this.longClientId !== undefined) throw unsupported("local ops while collaborating (observer engine)");
+  /**
+   * TestClient.insertTextLocal (testClient.ts:195): detached text before startOrUpdateCollaboration; while
+   * collaborating, a live client's local insert (insertSegmentLocal) whose op is returned.
+   */
+  insertTextLocal(pos, text, props) {
+    if (this.longClientId !== undefined) return this.insertSegmentLocal(pos, props === undefined ? text : { text, props });
+    if (props !== undefined) throw unsupported("detached text with properties");
     this.initial = this.initial.slice(0, pos) + text + this.initial.slice(pos);
+  }
+
+  // ---- a live client's own ops (client.ts:196-247): applied at the next flush in this client's view,
+  // acked when its sequenced message comes back through applyMsg
+  /** Queue an IMergeTreeOp (insert / remove, or a group of them) as this client's local op; returns it. */
+  applyLocalOp(op) {
+    this.batch.checkIdle();
+    native.localOp(this.batch.handle, this.doc, typeof op === "string" ? op : JSON.stringify(op));
+    this.batch.dirty = true;
+    return op;
+  }
+
+  /** Client.insertSegmentLocal (client.ts:196): `seg` is an IJSONSegment; returns the insert op to send. */
+  insertSegmentLocal(pos, seg) {
+    return this.applyLocalOp({ pos1: pos, seg, type: 0 });
+  }
+
+  /** Client.removeRangeLocal (client.ts:230): returns the remove op to send. */
+  removeRangeLocal(start, end) {
+    return this.applyLocalOp({ pos1: start, pos2: end, type: 1 });
   }
 
   /** Client.startOrUpdateCollaboration (client.ts:1133). */
@@ -200,8 +241,7 @@ class Client {
   // ---- op application ---------------------------------------------------------------------------
   /** Client.applyMsg (client.ts:858): `msg` is an ISequencedDocumentMessage (object or JSON text). */
   applyMsg(msg, local = false) {
-    if (local) throw unsupported("local (ack) application on the observer engine");
-    this.batch.checkIdle();
+    this.batch.checkIdle();  // (a message with this client's own id acks its oldest pending op)
     native.applyMsg(this.batch.handle, this.doc, typeof msg === "string" ? msg : JSON.stringify(msg));
     this.batch.dirty = true;
   }

@@ -132,17 +132,18 @@ static void batch_finalize(napi_env env, void* data, void* hint) {
   mtb_batch_destroy((mtb_batch*)data);
 }
 
-/* create(ndocs, newLengthCalc, chunkSize, device) -> handle            client.ts:107 ctor */
+/* create(ndocs, newLengthCalc, chunkSize, device, flags?, deviceMask?) -> handle   client.ts:107 ctor */
 static napi_value js_create(napi_env env, napi_callback_info info) {
-  napi_value argv[5];
-  size_t argc = 5;
+  napi_value argv[6];
+  size_t argc = 6;
   if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 4) {
     napi_throw_type_error(env, NULL, "wrong number of arguments");
     return NULL;
   }
-  uint32_t ndocs, nl, chunk, dev, flags = 0;
+  uint32_t ndocs, nl, chunk, dev, flags = 0, mask = 0;
   if (!get_u32(env, argv[0], &ndocs) || !get_u32(env, argv[1], &nl) || !get_u32(env, argv[2], &chunk) ||
-      !get_u32(env, argv[3], &dev) || (argc > 4 && !get_u32(env, argv[4], &flags)))
+      !get_u32(env, argv[3], &dev) || (argc > 4 && !get_u32(env, argv[4], &flags)) ||
+      (argc > 5 && !get_u32(env, argv[5], &mask)))
     return NULL;
   mtb_options o;
   memset(&o, 0, sizeof o);
@@ -151,7 +152,7 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
   o.threads_per_doc = 64;
   o.flags = (int32_t)flags;
   mtb_batch* b = NULL;
-  int rc = mtb_batch_create(&o, ndocs, 1u << dev, &b);
+  int rc = mtb_batch_create(&o, ndocs, mask ? mask : 1u << dev, &b);
   if (rc) return throw_rc(env, b, rc);
   napi_value h;
   CHECK_NAPI(env, napi_create_external(env, b, batch_finalize, NULL, &h));
@@ -271,6 +272,22 @@ static napi_value js_apply_msg(napi_env env, napi_callback_info info) {
   char* s = get_utf8(env, argv[2], &n);
   if (!s) return NULL;
   int rc = mtb_apply_msg_json(b, doc, s, n);
+  free(s);
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
+/* localOp(h, doc, JSON.stringify(IMergeTreeOp)): a live client's own op     client.ts:196-247 */
+static napi_value js_local_op(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc;
+  if (!b || !get_u32(env, argv[1], &doc)) return NULL;
+  size_t n = 0;
+  char* s = get_utf8(env, argv[2], &n);
+  if (!s) return NULL;
+  int rc = mtb_local_op_json(b, doc, s, n);
   free(s);
   if (rc) return throw_rc(env, b, rc);
   return undef(env);
@@ -523,6 +540,64 @@ static napi_value js_summarize_v1(napi_env env, napi_callback_info info) {
   return blob_list_object(env, &l);
 }
 
+/* summarizeV1Many(h, docs: number[], msn, seq, threads) -> [{blobs, summary}]: many channels at once */
+static napi_value js_summarize_v1_many(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  int64_t msn, seq;
+  uint32_t threads, n = 0;
+  if (!b || !get_i64(env, argv[2], &msn) || !get_i64(env, argv[3], &seq) || !get_u32(env, argv[4], &threads)) return NULL;
+  CHECK_NAPI(env, napi_get_array_length(env, argv[1], &n));
+  uint32_t* docs = (uint32_t*)calloc(n ? n : 1, sizeof(uint32_t));
+  mtb_blob_list* ls = (mtb_blob_list*)calloc(n ? n : 1, sizeof(mtb_blob_list));
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value e;
+    if (napi_get_element(env, argv[1], i, &e) != napi_ok || !get_u32(env, e, &docs[i])) {
+      free(docs);
+      free(ls);
+      return NULL;
+    }
+  }
+  int rc = mtb_summarize_v1_many(b, n, docs, msn, seq, threads, ls);
+  free(docs);
+  if (rc) {
+    free(ls);
+    return throw_rc(env, b, rc);
+  }
+  napi_value arr;
+  napi_create_array_with_length(env, n, &arr);
+  for (uint32_t i = 0; i < n; i++) napi_set_element(env, arr, i, blob_list_object(env, &ls[i]));
+  free(ls);
+  return arr;
+}
+
+/* digests(h, first, n) -> 16-digit hex strings: per-document state digests (mtb_doc_digests) */
+static napi_value js_digests(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t first, n;
+  if (!b || !get_u32(env, argv[1], &first) || !get_u32(env, argv[2], &n)) return NULL;
+  uint64_t* d = (uint64_t*)calloc(n ? n : 1, sizeof(uint64_t));
+  int rc = mtb_doc_digests(b, first, n, d);
+  if (rc) {
+    free(d);
+    return throw_rc(env, b, rc);
+  }
+  napi_value arr;
+  napi_create_array_with_length(env, n, &arr);
+  for (uint32_t i = 0; i < n; i++) {
+    char hex[24];
+    snprintf(hex, sizeof hex, "%016llx", (unsigned long long)d[i]);
+    napi_value s;
+    napi_create_string_utf8(env, hex, NAPI_AUTO_LENGTH, &s);
+    napi_set_element(env, arr, i, s);
+  }
+  free(d);
+  return arr;
+}
+
 /* summarizeLegacy(h, doc, msn, seq, catchupJson | null) -> {blobs, summary}   client.ts:999-1003,
  * snapshotlegacy.ts:122-259; null catch-up = the messages the batch tracked (MTB_BATCH_CATCHUP) */
 static napi_value js_summarize_legacy(napi_env env, napi_callback_info info) {
@@ -661,6 +736,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"matrixSummarize", js_matrix_summarize}, {"matrixGetCell", js_matrix_get_cell},
       {"matrixLoad", js_matrix_load},  {"summarizeLegacy", js_summarize_legacy},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
+      {"localOp", js_local_op},        {"summarizeV1Many", js_summarize_v1_many},
+      {"digests", js_digests},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},
       {"getText", js_get_text},        {"getLength", js_get_length},

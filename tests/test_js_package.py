@@ -80,3 +80,26 @@ def test_js_package_replays_reference_logs_on_gpu(tmp_path):
     assert "js gpu parity ok" in out
     assert "js gpu load ok" in out
     assert "js gpu matrix ok" in out
+
+
+@needs_node
+@pytest.mark.gpu
+def test_js_live_clients_on_gpu(tmp_path):
+    """Live clients through the JS package (insert / remove local ops and their acks): every client's text
+    after every round equals its oracle client's (tests/helpers.run_local_farm)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import run_local_farm
+    rec = {}
+    run_local_farm(7, n_clients=3, n_rounds=30, annotate=False, record=rec)
+    path = tmp_path / "farm.json"
+    path.write_text(json.dumps({"ids": rec["ids"], "initial": "hello world", "newMode": False,
+                                "rounds": [[ev for ev, _, _ in rnd] for rnd in rec["rounds"]]}))
+    r = subprocess.run(["node", os.path.join(JS, "test", "local_farm.js"), str(path)], capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    want = [[t for _, _, t in rnd] for rnd in rec["rounds"]]
+    assert got["texts"] == want
+    assert [int(h, 16) for h in got["digests"]] == [d for _, d, _ in rec["rounds"][-1]]
