@@ -54,6 +54,13 @@
 // segments): a FIFO directory of MTB_PEND_GROUPS entries [localSeq, member list offset, count, capacity]
 // in the aux arena; member lists (segment ids, group order) grow by doubling.
 #define MTB_PEND_GROUPS 64
+// Marker-relative positions (IRelativePosition, ops.ts:77-92; posFromRelativePos mergeTree.ts:1371-1395):
+// an insert / remove / annotate record with MTB_F_RELPOS has pos1 and/or pos2 = MTB_RELPOS | the
+// text-arena offset of a 6-unit descriptor [ordinal lo, ordinal hi, before, 0, offset lo, offset hi]
+// (ordinal: the marker's per-document id ordinal).  A marker insert / LOADSEG record carries its id's
+// ordinal + 1 in `payload` (0: no id).  Internal (never accepted from mtb_append_ops).
+#define MTB_F_RELPOS 0x20
+#define MTB_RELPOS 0x80000000u
 // PermutationVector documents (matrix/src/permutationvector.ts): segments carry a storage-handle start
 // in the F_TEXT field instead of a text offset; their handle table lives in the (otherwise unused) text
 // arena as u32 words [length, handles[0], handles[1], ...] (handletable.ts: handles[0] = free-list head).
@@ -161,7 +168,12 @@ struct DocState {     // 320 bytes
   uint32_t pend_dir;    // aux offset of the group directory (0: none yet)
   uint32_t pend_head;   // directory index of the oldest pending group
   uint32_t pend_n;      // pending groups
-  uint32_t pad3[12];
+  // idToSegment (mergeTree.ts:549) for marker-relative positions: marker ordinal (host-assigned per
+  // document, first-seen order of marker ids) -> segment id, MTB_NONE = not mapped
+  uint32_t mk_map;      // aux offset of the map (0: none yet)
+  uint32_t mk_n;        // entries allocated
+  uint32_t mk_cap;      // host: marker ordinals known for the document (the map grows to this)
+  uint32_t pad3[9];
 };
 static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
@@ -198,6 +210,7 @@ struct Tables {
 #define DERR_ACK_INSERT 17 // 0x045 "On insert, seq number already assigned!"
 #define DERR_ACK_REMOVE 18 // 0x046 "On remove ack, missing removal info!"
 #define DERR_LOCAL 19      // a local op the engine does not support (local annotate)
+#define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

@@ -18,6 +18,8 @@
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <optional>
+#include <cmath>
 #include <thread>
 #include <memory>
 #include <string>
@@ -210,6 +212,7 @@ struct LoadSeg {
   int16_t rc0 = -1;     // removedClientIds[0] (-1 = none)
   uint32_t rcx = 0;     // aux offset of the further removers [n, c1..cn] (0 = none)
   bool marker = false;
+  uint32_t mord = 0;    // marker id ordinal + 1 (0: no id)
 };
 // The header segments rebuilt as a tree (reloadFromSegments, mergeTree.ts:678-721) with the window
 // lists startCollaboration's recursive combine gives every internal block (partialLengths.ts:256-338),
@@ -220,6 +223,7 @@ struct LoadImage {
   std::vector<WEnt> lists;     // entry 0..MTB_LIST_RESERVED-1: the free-list heads
   std::vector<uint32_t> aux;   // word 0 unused, then the overlapping-remover lists
   uint32_t root = 0;
+  uint32_t mk_map = 0, mk_n = 0;  // idToSegment of the live header markers (in `aux`)
 };
 
 // ------------------------------------------------------------------ SharedMatrix cells
@@ -335,6 +339,12 @@ struct HostDoc {
   uint64_t totalSetcell = 0;
   std::unique_ptr<CellStore> cells;  // rows vector of a matrix: the matrix's cells (matrix.ts:96)
   LoadImage img;
+  // idToSegment keys (mergeTree.ts:549): marker id -> per-document ordinal (first-seen order).  An id met on
+  // a second marker is ambiguous (blockUpdate's re-mapping, :296-306, would decide), and an annotate that
+  // sets markerId changes ids at blockUpdate time: relative positions naming either are rejected.
+  std::unordered_map<std::string, uint32_t> markerOrd;
+  std::vector<uint8_t> markerAmbig;
+  bool markerIdsUnstable = false;
   // device mirror
   DocState st{};
   bool onDevice = false;
@@ -481,10 +491,75 @@ uint32_t u32field(const hj::Value& o, const char16_t* k, const char* what) {
   return (uint32_t)v->n;
 }
 
-uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel) {
+// Map keys of marker ids (Marker.getId, mergeTreeNodes.ts:612-617; idToSegment, mergeTree.ts:549): the
+// JS Map identity of the primitive values a JSON id can hold; falsy ids are no ids, object ids never match
+std::optional<std::string> marker_key(const hj::Value* v) {
+  if (!v || !v->truthy()) return std::nullopt;
+  switch (v->kind) {
+    case hj::Value::kStr: return "s" + hj::to_utf8(v->s.data(), v->s.size());
+    case hj::Value::kNum: return "n" + hj::number(v->n);
+    case hj::Value::kBool: return std::string("t");
+    default: return std::nullopt;
+  }
+}
+// The ordinal + 1 of the id of a marker inserted with `props` (0: no id); a reused id becomes ambiguous.
+uint32_t marker_ord(HostDoc& d, const hj::Value* props) {
+  if (!props || props->kind != hj::Value::kObj) return 0;
+  auto key = marker_key(member(*props, u"markerId"));
+  if (!key) return 0;
+  auto [it, fresh] = d.markerOrd.try_emplace(*key, (uint32_t)d.markerAmbig.size());
+  if (fresh) d.markerAmbig.push_back(0);
+  else d.markerAmbig[it->second] = 1;
+  return it->second + 1;
+}
+// the JSON text of an interned props id's markerId (property set, or op-props list), or nullptr
+const std::string* props_marker_json(const Interner& in, uint32_t props, bool opList) {
+  if (!props || props >= in.pidx.size() / 2) return nullptr;
+  auto k = in.keyId.find(U16(u"markerId"));
+  if (k == in.keyId.end()) return nullptr;
+  const uint32_t off = in.pidx[2 * props + (opList ? 0 : 1)];
+  for (uint32_t i = 0; i < in.pool[off]; i++)
+    if (in.pool[off + 1 + 2 * i] == k->second) {
+      static const std::string null = "null";
+      const uint32_t v = in.pool[off + 2 + 2 * i];
+      return v == MTB_NONE ? &null : &in.valJson[v];
+    }
+  return nullptr;
+}
+
+// getValidOpRange (client.ts:527-547): `pos1` / `pos2` when present, else the IRelativePosition
+// `relativePos1` / `relativePos2` (ops.ts:77-92), packed as a descriptor the kernel resolves with
+// posFromRelativePos (mergeTree.ts:1371-1395) in the op's view (MTB_F_RELPOS, mtb_device.h).
+uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, HostDoc* d = nullptr, mtb_op* r = nullptr) {
   const hj::Value* v = member(op, k);
   if (v && v->kind == hj::Value::kNum) return (uint32_t)v->n;
-  if (member(op, rel)) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions (marker-relative ops)");
+  const hj::Value* rp = member(op, rel);
+  if (rp && rp->truthy()) {
+    if (!d) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions here (local ops, catch-up or matrix batches)");
+    if (rp->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: relative position is not an object");
+    auto key = marker_key(member(*rp, u"id"));
+    if (!key) raise(MTB_E_UNSUPPORTED, "unsupported: relative position without a marker id (posFromRelativePos -1)");
+    auto it = d->markerOrd.find(*key);
+    if (it == d->markerOrd.end())
+      raise(MTB_E_UNSUPPORTED, "unsupported: relative position names no marker of the document (posFromRelativePos -1)");
+    if (d->markerAmbig[it->second] || d->markerIdsUnstable)
+      raise(MTB_E_UNSUPPORTED, "unsupported: relative position naming a marker id that is reused or set by an annotate");
+    const hj::Value* off = member(*rp, u"offset");
+    double o = 0;
+    if (off && off->kind != hj::Value::kNull) {
+      if (off->kind != hj::Value::kNum || off->n != std::floor(off->n) || std::fabs(off->n) > 1e9)
+        raise(MTB_E_UNSUPPORTED, "unsupported: non-integer relative position offset");
+      o = off->n;
+    }
+    const hj::Value* before = member(*rp, u"before");
+    const uint32_t ord = it->second, ov = (uint32_t)(int32_t)o;
+    const uint32_t at = (uint32_t)d->payload.size();
+    const uint16_t desc[6] = {(uint16_t)ord, (uint16_t)(ord >> 16), (uint16_t)(before && before->truthy()), 0,
+                              (uint16_t)ov, (uint16_t)(ov >> 16)};
+    d->payload.insert(d->payload.end(), desc, desc + 6);
+    r->flags |= MTB_F_RELPOS;
+    return MTB_RELPOS | at;
+  }
   raise(MTB_E_UNSUPPORTED, "unsupported: op without numeric position");
 }
 
@@ -493,8 +568,10 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
   const hj::Value* t = member(op, u"type");
   const int type = t && t->kind == hj::Value::kNum ? (int)t->n : -1;
   mtb_op r = base;
+  // relative positions: observer replay in plain SharedString batches
+  HostDoc* rel = (b->matrix || (b->opts.flags & MTB_BATCH_CATCHUP) || (base.flags & MTB_F_LOCAL)) ? nullptr : &d;
   if (type == 0) {
-    r.pos1 = position(op, u"pos1", u"relativePos1");
+    r.pos1 = position(op, u"pos1", u"relativePos1", rel, &r);
     const hj::Value* seg = member(op, u"seg");
     if (!seg || !seg->truthy()) {  // applyInsertOp: `if (op.seg)` -> no-op member
       r.type = MTB_OP_NOOP;
@@ -527,6 +604,7 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
       const hj::Value* rt = mk ? member(*mk, u"refType") : nullptr;
       r.pos2 = (rt && rt->kind == hj::Value::kNum) ? (uint32_t)rt->n : 0xFFFFFFFFu;
       props = member(*seg, u"props");
+      r.payload = marker_ord(d, props && props->truthy() ? props : nullptr);
     } else {
       raise(MTB_E_PARSE, "Unrecognized IJSONSegment type");
     }
@@ -542,10 +620,11 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
     out.push_back(r);
   } else if (type == 1 || type == 2) {
     r.type = type == 1 ? MTB_OP_REMOVE : MTB_OP_ANNOTATE;
-    r.pos1 = position(op, u"pos1", u"relativePos1");
-    r.pos2 = position(op, u"pos2", u"relativePos2");
+    r.pos1 = position(op, u"pos1", u"relativePos1", rel, &r);
+    r.pos2 = position(op, u"pos2", u"relativePos2", rel, &r);
     if (type == 2) {
       const hj::Value* props = member(op, u"props");
+      if (props && props->kind == hj::Value::kObj && member(*props, u"markerId")) d.markerIdsUnstable = true;
       hj::Value empty;
       empty.kind = hj::Value::kObj;
       r.props = b->in.props(props && props->kind == hj::Value::kObj ? *props : empty);
@@ -602,6 +681,7 @@ LoadSeg load_spec(mtb_dev* b, HostDoc& d, const hj::Value& spec, std::vector<uin
     g.len = 1;
     g.text = MTB_MARKER | ((rt && rt->kind == hj::Value::kNum) ? (uint32_t)rt->n + 1 : 0u);
     props = member(js, u"props");
+    g.mord = marker_ord(d, props && props->truthy() ? props : nullptr);
   } else {
     raise(MTB_E_PARSE, "Unrecognized IJSONSegment type");
   }
@@ -841,6 +921,15 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
   if (d.perm && !body.empty())
     raise(MTB_E_UNSUPPORTED, "unsupported: PermutationVector summary with body chunks (more than chunkSize rows/cols)");
   build_load_image(d, hdr);
+  // idToSegment after reloadFromSegments: blockUpdate maps the live header markers (mergeTree.ts:296-306)
+  if (!d.markerAmbig.empty()) {
+    LoadImage& im = d.img;
+    im.mk_map = (uint32_t)im.aux.size();
+    im.mk_n = (uint32_t)d.markerAmbig.size();
+    im.aux.resize(im.aux.size() + im.mk_n, MTB_NONE);
+    for (size_t i = 0; i < hdr.size(); i++)
+      if (hdr[i].mord && hdr[i].rseq < 0) im.aux[im.mk_map + hdr[i].mord - 1] = (uint32_t)i;
+  }
   // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
   // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
   std::vector<mtb_op>& recs = d.pending;
@@ -865,7 +954,7 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
       r.msn = (uint16_t)g.rc0;
       r.pos1 = g.rcx;
       r.pos2 = g.marker ? (g.text & ~MTB_MARKER) - 1 : g.len;  // marker: refType (0xFFFFFFFF = undefined)
-      r.payload = g.marker ? 0 : g.text;
+      r.payload = g.marker ? g.mord : g.text;  // marker: id ordinal + 1
       r.props = g.props;
       recs.push_back(r);
     }
@@ -1067,6 +1156,8 @@ void device_init(mtb_dev* b) {
       s.seg_used = (uint32_t)im.segp.size();
       s.list_used = (uint32_t)im.lists.size();
       s.aux_used = (uint32_t)im.aux.size();
+      s.mk_map = im.mk_map;
+      s.mk_n = im.mk_n;
       s.heap_cnt = 0;
       s.text_used = (uint32_t)d.initText.size();
       segc.add(recs.size(), s.seg_base, im.segp.size());
@@ -1291,6 +1382,7 @@ std::string derr_text(int e) {
     case DERR_ASSERT_MSN: return "0x04e/0x04f/0x039 minimum sequence number out of order";
     case DERR_DEPTH: return "tree depth limit exceeded";
     case DERR_HOST: return "host post-processing of the replay failed";
+    case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     default: return "device error " + std::to_string(e);
   }
 }
@@ -1461,8 +1553,13 @@ void replay(mtb_dev* b, mtb_stats* out) {
     s.n_ops = (uint32_t)d.pending.size();
     s.op_next = 0;
     mtb_op* out = ops.get() + opOff[i];
+    s.mk_cap = (uint32_t)d.markerAmbig.size();
     for (mtb_op o : d.pending) {
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER)) o.payload += base;
+      if ((o.flags & MTB_F_RELPOS) && o.type != MTB_OP_LOADSEG) {  // relative-position descriptors
+        if (o.pos1 & MTB_RELPOS) o.pos1 += base;
+        if (o.pos2 & MTB_RELPOS) o.pos2 += base;
+      }
       *out++ = o;
     }
   });
@@ -2683,9 +2780,22 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
       }
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_ANNOTATE) && o.props >= b->in.pidx.size() / 2)
         raise(MTB_E_ARG, "record props id out of range");
+      if (o.type == MTB_OP_INSERT && (o.flags & MTB_F_MARKER)) o.payload = 0;  // set below (marker id ordinal)
       if (o.client >= d.longIds.size() && o.type != MTB_OP_NOOP)
         raise(MTB_E_ARG, "record client id not registered (mtb_add_client)");
       staged.push_back(o);
+    }
+    for (mtb_op& o : staged) {  // idToSegment keys of markers / annotates setting markerId (as the JSON path)
+      if (o.type == MTB_OP_INSERT && (o.flags & MTB_F_MARKER)) {
+        if (const std::string* js = props_marker_json(b->in, o.props, false)) {
+          hj::Value mp;
+          mp.kind = hj::Value::kObj;
+          mp.members.push_back({U16(u"markerId"), hj::parse(js->data(), js->size())});
+          o.payload = marker_ord(d, &mp);
+        }
+      } else if (o.type == MTB_OP_ANNOTATE && props_marker_json(b->in, o.props, true)) {
+        d.markerIdsUnstable = true;
+      }
     }
     d.payload.insert(d.payload.end(), payload, payload + payload_len);
     d.totalPayload += payload_len;

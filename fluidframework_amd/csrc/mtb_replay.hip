@@ -2603,6 +2603,71 @@ struct Eng {
     }
   }
 
+  // ------------------------------------------------------------------ marker ids (idToSegment)
+  // mapIdToSegment (mergeTree.ts:668, from insertSegments :1658-1663): the marker inserted as segment `sid`
+  // carries id ordinal `ord` (its record's payload - 1).  The map lives in the aux arena and grows to the
+  // host's ordinal count; the host keeps every mapped id unique in its document (else relative positions
+  // naming it are rejected at pack time), so blockUpdate's re-mapping (:296-306) never changes an entry.
+  __device__ __forceinline__ void mk_set(uint32_t ord, uint32_t sid) {
+    uint32_t map = U(ds->mk_map), n = U(ds->mk_n);
+    if (ord >= n) {
+      const uint32_t hc = U(ds->mk_cap);
+      const uint32_t cap = hc > ord ? hc : ord + 1;
+      const uint32_t nm = alloc_aux(cap);
+      if (bad()) return;
+      for (uint32_t i = lane; i < cap; i += 64) aux[nm + i] = i < n ? aux[map + i] : MTB_NONE;
+      map = nm;
+      n = cap;
+      if (lane == 0) {
+        ds->mk_map = map;
+        ds->mk_n = n;
+      }
+    }
+    if (lane == 0) aux[map + ord] = sid;
+    wsync();
+  }
+  // posFromRelativePos (mergeTree.ts:1371-1395) of a record position field `v` in the op's (R, C) view:
+  // v itself, or for MTB_RELPOS | descriptor offset: getPosition (:768-785) of the mapped marker (0 once
+  // zamboni unlinked it), then `before` / `offset`.  An unmapped marker or a negative result fails the
+  // document (DERR_RELPOS).  The views loaded on the way up stay valid for the op's walks.
+  __device__ __forceinline__ int rel_pos(uint32_t v, int R, int C) {
+    if (!(v & MTB_RELPOS)) return (int)v;
+    const auto t = UP(sh->gtext) + (v & ~MTB_RELPOS);
+    const uint32_t ord = U((uint32_t)t[0] | ((uint32_t)t[1] << 16));
+    const uint32_t before = U((uint32_t)t[2]);
+    const int off = (int)U((uint32_t)t[4] | ((uint32_t)t[5] << 16));
+    if (ord >= U(ds->mk_n)) { fail(DERR_RELPOS); return 0; }
+    const uint32_t sid = U(aux[U(ds->mk_map) + ord]);
+    if (sid == MTB_NONE) { fail(DERR_RELPOS); return 0; }
+    int pos = 0;
+    const uint32_t b0 = U(segp[sid]);
+    if (b0 != MTB_NONE) {
+      uint32_t mine = MTB_NONE;  // lane i: the i-th ancestor block from the bottom
+      int n = 0;
+      for (uint32_t x = b0; x != MTB_NONE; x = U(blk[x].parent)) {
+        if (n >= MTB_VDEPTH) { fail(DERR_DEPTH); return 0; }
+        if (lane == n) mine = x;
+        n++;
+      }
+      for (int d = 0; d < n; d++) {
+        const uint32_t bd = rlu(mine, n - 1 - d);
+        if (d > 0) {
+          if (lane == 0) sh->slot[d - 1] = (int)blk[bd].index;
+          wsync();
+        }
+        Kid k;
+        const int cnt = load_view(d, bd, R, C, k);
+        const uint32_t target = d + 1 < n ? rlu(mine, n - 2 - d) : (MTB_LEAF | sid);
+        const int j = first_set(__ballot(lane < cnt && k.id == target));
+        if (j < 0) { fail(DERR_SHAPE); return 0; }
+        pos += csum8(lane < j && k.rl != MTB_UNDEF ? k.rl : 0);
+      }
+    }
+    pos += before ? -off : 1 + off;  // marker.cachedLength = 1
+    if (pos < 0) fail(DERR_RELPOS);
+    return pos;
+  }
+
   // ------------------------------------------------------------------ ops
   __device__ __forceinline__ void set_min_seq(int msn) {  // mergeTree.ts:1025-1044
     if (!(msn <= curSeq) || !(minSeq <= msn)) { fail(DERR_ASSERT_MSN); return; }
@@ -2656,6 +2721,10 @@ struct Eng {
       }
       wsync();
       n_mod += 1;
+      if (COLD(marker && o.payload != 0)) {  // body markers are mapped whatever their removal (:1658-1663)
+        mk_set(o.payload - 1, sid);
+        if (bad()) return;
+      }
       const bool ok = walk(ld_pos, 0, C, S, true, rseq >= 0 ? 0 : len, first);
       if (!ok) {
         fail(DERR_INSERT);
@@ -2714,7 +2783,13 @@ struct Eng {
         ops_applied++;
         view_clear();
         uint64_t t0 = PROF_T();
-        walk((int)o.pos1, R, C, -2, false, 0);  // ensureIntervalBoundary
+        int p1 = (int)o.pos1;
+        if constexpr (!isPerm)
+          if (COLD(o.flags & MTB_F_RELPOS)) {  // getValidOpRange (client.ts:531-537)
+            p1 = rel_pos(o.pos1, R, C);
+            if (bad()) return;
+          }
+        walk(p1, R, C, -2, false, 0);  // ensureIntervalBoundary
         settle();
         PROF_ADD(PH_BOUNDARY, t0);
         if (bad()) return;
@@ -2740,7 +2815,12 @@ struct Eng {
           wsync();
           n_mod += 1;
           text_bytes += (marker || (o.flags & MTB_F_PERMSEG)) ? 0u : 2u * (uint32_t)len;
-          if (!walk((int)o.pos1, R, C, S, true, len, true)) {
+          if constexpr (!isPerm)
+            if (COLD(marker && o.payload != 0)) {
+              mk_set(o.payload - 1, sid);
+              if (bad()) return;
+            }
+          if (!walk(p1, R, C, S, true, len, true)) {
             fail(DERR_INSERT);
             return;
           }
@@ -2763,16 +2843,24 @@ struct Eng {
         ops_applied++;
         view_clear();
         uint64_t t0 = PROF_T();
-        walk((int)o.pos1, R, C, -2, false, 0);
+        int p1 = (int)o.pos1, p2 = (int)o.pos2;
+        if constexpr (!isPerm)
+          if (COLD(o.flags & MTB_F_RELPOS)) {  // getValidOpRange (client.ts:531-547)
+            p1 = rel_pos(o.pos1, R, C);
+            if (bad()) return;
+            p2 = rel_pos(o.pos2, R, C);
+            if (bad()) return;
+          }
+        walk(p1, R, C, -2, false, 0);
         settle();
-        walk((int)o.pos2, R, C, -2, false, 0);
+        walk(p2, R, C, -2, false, 0);
         settle();
         PROF_ADD(PH_BOUNDARY, t0);
         if (bad()) return;
         t0 = PROF_T();
         const uint32_t dfrom = delta_used;
         if (isLive) sh->memo[2] = 0;
-        node_map((int)o.pos1, (int)o.pos2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
+        node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);

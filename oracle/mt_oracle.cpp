@@ -483,6 +483,7 @@ void MergeTree::ensureIntervalBoundary(int pos, int refSeq, int clientId) {
 // blockInsert (mergeTree.ts:1594-1685), single segment
 void MergeTree::blockInsert(int pos, int refSeq, int clientId, int seq, Seg* seg, int localSeq, SegGroup** group) {
   if (seg->cachedLength > 0) {
+    if (auto id = markerId(seg)) idToSegment[*id] = seg;  // mapIdToSegment (mergeTree.ts:1658-1663)
     seg->seq = seq;
     seg->localSeq = localSeq;
     seg->clientId = clientId;
@@ -557,15 +558,66 @@ void MergeTree::reloadFromSegments(const std::vector<Seg*>& segs) {
   }
 }
 
-// blockUpdate (mergeTree.ts:2392-2417): cachedLength = sum(nodeTotalLength ?? 0)
+// blockUpdate (mergeTree.ts:2392-2417): cachedLength = sum(nodeTotalLength ?? 0); addNodeReferences
+// (:296-306) maps every child marker with an id whose localNetLength is positive
 void MergeTree::blockUpdate(Block* b) {
   int len = 0;
   for (int i = 0; i < b->childCount; i++) {
     Node* c = b->children[i];
     int l = c->leaf ? localNetLength(static_cast<Seg*>(c)) : c->cachedLength;
     len += l == UNDEF_LEN ? 0 : l;
+    if (c->leaf && l > 0 && static_cast<Seg*>(c)->isMarker) {
+      if (auto id = markerId(static_cast<Seg*>(c))) idToSegment[*id] = static_cast<Seg*>(c);
+    }
   }
   b->cachedLength = len;
+}
+
+// Map keys of marker ids: JS Map identity (SameValueZero) of the primitive values a JSON id can be;
+// object ids never equal a parsed relativePos id, so they are never looked up (and not kept).
+std::optional<std::string> MergeTree::markerIdKey(const JVal* v) {
+  if (js_falsy(v)) return std::nullopt;  // `if (relativePos.id)` / `if (this.properties[reservedMarkerIdKey])`
+  switch (v->t) {
+    case JVal::Str: return "s" + u16_to_utf8(v->str);
+    case JVal::Num: return "n" + json_stringify(*v);
+    case JVal::True: return std::string("t");
+    default: return std::nullopt;
+  }
+}
+std::optional<std::string> MergeTree::markerId(const Seg* s) {
+  if (!s->isMarker || !s->props) return std::nullopt;
+  return markerIdKey(obj_get(*s->props, u"markerId"));
+}
+
+// getPosition (mergeTree.ts:768-785)
+int MergeTree::getPosition(Node* node, int refSeq, int clientId) {
+  int total = 0;
+  for (Block* parent = node->parent; parent; node = parent, parent = parent->parent)
+    for (int i = 0; i < parent->childCount && parent->children[i] != node; i++) {
+      int l = nodeLength(parent->children[i], refSeq, clientId);
+      total += l == UNDEF_LEN ? 0 : l;
+    }
+  return total;
+}
+
+// posFromRelativePos (mergeTree.ts:1371-1395)
+int MergeTree::posFromRelativePos(const JVal& rel, int refSeq, int clientId) {
+  if (rel.t != JVal::Obj) return -1;
+  auto key = markerIdKey(obj_get(rel.obj, u"id"));
+  if (!key) return -1;
+  auto it = idToSegment.find(*key);
+  if (it == idToSegment.end()) return -1;
+  Seg* marker = it->second;
+  int pos = getPosition(marker, refSeq, clientId);
+  const JVal* before = obj_get(rel.obj, u"before");
+  const JVal* offset = obj_get(rel.obj, u"offset");
+  if (offset && offset->t != JVal::Undef && offset->t != JVal::Null &&
+      (offset->t != JVal::Num || offset->num != (double)(int)offset->num))
+    fail_unsupported("non-integer relative position offset");
+  const int off = offset && offset->t == JVal::Num ? (int)offset->num : 0;
+  if (js_falsy(before)) pos += marker->cachedLength + off;
+  else pos -= off;
+  return pos;
 }
 
 // nodeUpdateLengthNewStructure (mergeTree.ts:2188-2194)
@@ -1192,10 +1244,17 @@ static Seg* makeSegFromSpec(MergeTree& mt, const JVal& spec) {  // testClient.ts
   throw OracleError(-8, "Unrecognized IJSONSegment type");
 }
 
-static int getPos(const JVal& op, const char16_t* key, const char16_t* relKey) {
+// getValidOpRange (client.ts:527-547): `pos1` / `pos2` if present, else posFromRelativePos of
+// `relativePos1` / `relativePos2` in the op's (refSeq, clientId) view
+static int getPos(MergeTree& mt, const JVal& op, const char16_t* key, const char16_t* relKey, int refSeq, int client) {
   const JVal* p = obj_get(op.obj, key);
   if (p && p->t == JVal::Num) return (int)p->num;
-  if (obj_get(op.obj, relKey)) fail_unsupported("relative positions");
+  const JVal* rel = obj_get(op.obj, relKey);
+  if (rel && !js_falsy(rel)) {
+    const int pos = mt.posFromRelativePos(*rel, refSeq, client);
+    if (pos < 0) fail_unsupported("relative position names no marker of the document");
+    return pos;
+  }
   fail_unsupported("missing position");
 }
 
@@ -1206,7 +1265,7 @@ void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
   mt.counters.ops += (t >= 0 && t <= 2) ? 1 : 0;
   switch (t) {
     case 0: {  // applyInsertOp (client.ts:489-524)
-      int pos = getPos(op, u"pos1", u"relativePos1");
+      int pos = getPos(mt, op, u"pos1", u"relativePos1", refSeq, client);
       const JVal* spec = obj_get(op.obj, u"seg");
       if (js_falsy(spec)) return;
       Seg* s = makeSegFromSpec(mt, *spec);
@@ -1218,14 +1277,14 @@ void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
       break;
     }
     case 1: {  // applyRemoveRangeOp (client.ts:430-455)
-      int a = getPos(op, u"pos1", u"relativePos1");
-      int b = getPos(op, u"pos2", u"relativePos2");
+      int a = getPos(mt, op, u"pos1", u"relativePos1", refSeq, client);
+      int b = getPos(mt, op, u"pos2", u"relativePos2", refSeq, client);
       mt.markRangeRemoved(a, b, refSeq, client, seq);
       break;
     }
     case 2: {  // applyAnnotateRangeOp (client.ts:457-487)
-      int a = getPos(op, u"pos1", u"relativePos1");
-      int b = getPos(op, u"pos2", u"relativePos2");
+      int a = getPos(mt, op, u"pos1", u"relativePos1", refSeq, client);
+      int b = getPos(mt, op, u"pos2", u"relativePos2", refSeq, client);
       const JVal* props = obj_get(op.obj, u"props");
       const JVal* comb = obj_get(op.obj, u"combiningOp");
       bool rewrite = false;

@@ -196,6 +196,16 @@ class MergeTree {
   // getContainingSegment (mergeTree.ts:787-813) and getPosition (:1240) for PermutationVector
   Seg* containingSegment(int pos, int refSeq, int clientId, int* offset);
   int localPosition(Seg* s);
+  // getPosition (mergeTree.ts:768-785) in any (refSeq, clientId) view; 0 for an unlinked node
+  int getPosition(Node* n, int refSeq, int clientId);
+  // idToSegment (mergeTree.ts:549): marker id -> marker.  Filled by insertSegments for every inserted
+  // marker with an id (:1658-1663) and by every blockUpdate for its live child markers (:2392 ->
+  // addNodeReferences :296-306, last child wins); never pruned.  Keys: markerIdKey of the JSON value.
+  std::map<std::string, Seg*> idToSegment;
+  static std::optional<std::string> markerIdKey(const JVal* v);
+  static std::optional<std::string> markerId(const Seg* s);  // Marker.getId (mergeTreeNodes.ts:612-617)
+  // posFromRelativePos (mergeTree.ts:1371-1395): -1 when the id names no marker
+  int posFromRelativePos(const JVal& rel, int refSeq, int clientId);
   void boundary(int pos, int refSeq, int clientId) { ensureIntervalBoundary(pos, refSeq, clientId); }
   // mapRange(action, refSeq, clientId) over the whole tree (mergeTree.ts mapRange -> nodeMap)
   void mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f);

@@ -268,6 +268,13 @@ int orc_get_text(orc_doc* d, uint16_t** out, size_t* n_units) {
   });
 }
 int orc_get_length(orc_doc* d) { return d->doc.mt.length(); }
+// posFromRelativePos (mergeTree.ts:1371-1395) of a JSON IRelativePosition in the (ref_seq, client) view;
+// -1 when the id names no marker, INT32_MIN on a malformed argument
+int orc_pos_from_relative(orc_doc* d, const char* rel_json, int ref_seq, int client) {
+  int pos = INT32_MIN;
+  guard(d, [&] { pos = d->doc.mt.posFromRelativePos(json_parse(rel_json, strlen(rel_json)), ref_seq, client); });
+  return pos;
+}
 int orc_get_remote_length(orc_doc* d, int ref_seq, int client) { return d->doc.mt.getLength(ref_seq, client); }
 int orc_current_seq(orc_doc* d) { return d->doc.mt.window.currentSeq; }
 int orc_min_seq(orc_doc* d) { return d->doc.mt.window.minSeq; }

@@ -37,6 +37,7 @@ def lib():
         L.orc_get_text.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_get_length.argtypes = [vp]
         L.orc_get_remote_length.argtypes = [vp, i, i]
+        L.orc_pos_from_relative.argtypes = [vp, cp, i, i]
         L.orc_current_seq.argtypes = [vp]
         L.orc_min_seq.argtypes = [vp]
         L.orc_num_clients.argtypes = [vp]
@@ -237,6 +238,10 @@ class OracleDoc:
 
     def get_length(self):
         return self._L.orc_get_length(self._h)
+
+    def pos_from_relative(self, rel, ref_seq, client):
+        """posFromRelativePos (mergeTree.ts:1371) of an IRelativePosition dict in the (ref_seq, client) view."""
+        return self._L.orc_pos_from_relative(self._h, json.dumps(rel).encode(), ref_seq, client)
 
     def remote_length(self, ref_seq, client):
         return self._L.orc_get_remote_length(self._h, ref_seq, client)

@@ -301,3 +301,96 @@ def load_logbatch(B, lb, docs=None, props_interned=False):
         # payload offsets in the generated records index the doc's text arena (initial text first)
         B.append_records(j, lb.doc_ops_bytes(u), lb.docs[u].n_ops, tb)
     return docs
+
+
+def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="hello marker world", p_rel=0.5):
+    """A sequenced op log with markers carrying unique `markerId`s and ops whose positions are marker-relative
+    (IRelativePosition, ops.ts:77-92): `annotateMarker` ops (opBuilder.ts:25-43, {id, before: true} ..
+    {id}) and inserts / removes / annotates with relativePos1/2 (before / offset), next to plain ones.  A
+    generator oracle (every message applied as it is made) resolves each candidate relative position in the
+    sender's (refSeq, client) view (posFromRelativePos) so that only in-range ops are emitted; markers that
+    were removed, or unlinked by zamboni, stay eligible.  Returns (initial text, messages)."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed)
+    ids = [f"client-{k}" for k in range(n_clients)]
+    gen = OracleDoc(new_length_calc=new_mode)
+    if initial:
+        gen.insert_text_local(0, initial)
+    gen.start_collab("gen-observer")
+    short = {}
+    for cid in ids:
+        gen.add_client(cid)
+        short[cid] = len(short) + 1
+    ref = [0] * n_clients
+    markers, msgs = [], []
+    words = ["ab", "c", "xyz", "\n", "long-ish text "]
+
+    def rel(pos_ok):
+        for _ in range(4):
+            if not markers:
+                return None
+            r = {"id": rng.choice(markers)}
+            if rng.random() < 0.5:
+                r["before"] = True
+            if rng.random() < 0.4:
+                r["offset"] = rng.randint(0, 3)
+            return r
+        return None
+
+    for seq in range(1, n_msgs + 1):
+        k = rng.randrange(n_clients)
+        ref[k] = max(ref[k], seq - 1 - rng.randint(0, lag))
+        R, C, cid = ref[k], short[ids[k]], ids[k]
+        n = gen.remote_length(R, C)
+        x = rng.random()
+        op = None
+        if x < 0.12 or n == 0:
+            mid = f"m{seed}-{seq}"
+            p = rng.randint(0, n)
+            op = {"type": 0, "pos1": p, "seg": {"marker": {"refType": rng.choice([0, 1, 2])},
+                                                 "props": {"markerId": mid, "kind": rng.randint(0, 2)}}}
+            markers.append(mid)
+        elif x < 0.25 and markers:  # annotateMarker
+            mid = rng.choice(markers)
+            p = gen.pos_from_relative({"id": mid, "before": True}, R, C)
+            if 0 <= p and p + 1 <= n:
+                op = {"type": 2, "relativePos1": {"id": mid, "before": True}, "relativePos2": {"id": mid},
+                      "props": {"state": rng.choice(["open", "closed", None])}}
+        if op is None:
+            t = rng.choice([0, 0, 1, 2])
+            if t == 0:
+                op = {"type": 0, "seg": rng.choice(words)}
+                r = rel(True) if rng.random() < p_rel else None
+                p = gen.pos_from_relative(r, R, C) if r else -1
+                if r and 0 <= p <= n:
+                    op["relativePos1"] = r
+                else:
+                    op["pos1"] = rng.randint(0, n)
+            elif n > 0:
+                a = rng.randrange(n)
+                b = min(n, a + rng.randint(1, 5))
+                op = {"type": t}
+                for key, val in (("1", a), ("2", b)):
+                    r = rel(True) if rng.random() < p_rel else None
+                    p = gen.pos_from_relative(r, R, C) if r else -1
+                    if r and 0 <= p <= n and (key == "1" and p < b or key == "2" and p > op.get("_a", a)):
+                        op["relativePos" + key] = r
+                        if key == "1":
+                            op["_a"] = p
+                    else:
+                        op["pos" + key] = val
+                        if key == "1":
+                            op["_a"] = val
+                op.pop("_a")
+                if t == 2:
+                    op["props"] = {"client": cid, "n": rng.randint(0, 3)}
+            else:
+                op = {"type": 0, "pos1": 0, "seg": "seed"}
+        msn = min(ref)
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": msn,
+             "type": "op", "contents": op}
+        gen.apply_msg(m)
+        msgs.append(m)
+    gen.close()
+    return initial, msgs

@@ -1,0 +1,127 @@
+"""GPU parity of marker-relative positions (IRelativePosition, ops.ts:77-92): getValidOpRange
+(client.ts:527-547) resolving relativePos1/2 with posFromRelativePos (mergeTree.ts:1371-1395) in the op's
+(refSeq, client) view, over idToSegment (:549) filled by marker inserts (:1658-1663), summary loads
+(reloadFromSegments -> blockUpdate :296-306; body inserts) — resolved on the GPU (the kernel's rel_pos walks
+the marker's ancestors, getPosition :768-785).
+
+Bar: bit-exact against the oracle (canonical segment dump, text, state digest, SnapshotV1) on
+* generated logs (tests/helpers.make_marker_log): markers with unique ids, annotateMarker ops
+  (opBuilder.ts:25-43), inserts / removes / annotates with relative positions (before / offset), lagging
+  views, removed and zamboni-unlinked markers; both length modes, two flushes;
+* the reference's withMarkers SnapshotV1 fixture (markers "marker0", "marker70", ... with markerId in
+  header and body chunks) loaded, then remote ops relative to its markers;
+* a relative position whose marker is a removed header marker (never mapped: posFromRelativePos -1) fails
+  its document with the engine's "relative position" error, the other documents replay.
+"""
+import random
+
+import pytest
+
+from helpers import first_diff, make_marker_log, snapshot_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(B, i, o, what):
+    gd, od = B.dump_segments(i), o.dump_segments()
+    assert gd == od, f"{what}: segment dump differs: {first_diff(gd, od)}"
+    assert B.text(i) == o.get_text(), f"{what}: text differs"
+    assert B.digests(i, 1)[0] == o.digest(), f"{what}: digest differs"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_marker_relative_logs(new_mode):
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    logs = [make_marker_log(100 + s, 900, n_clients=3 + s % 4, lag=8 + 6 * s, new_mode=new_mode) for s in range(10)]
+    B = MergeTreeBatch(len(logs), new_length_calc=new_mode)
+    orc = []
+    for i, (init, _) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("obs")
+        orc.append(o)
+    for part in (slice(0, 450), slice(450, None)):
+        for i, (_, msgs) in enumerate(logs):
+            for m in msgs[part]:
+                B[i].applyMsg(m)
+                orc[i].apply_msg(m)
+        st = B.replay()
+        assert st["errors"] == 0, st
+        for i, o in enumerate(orc):
+            _same(B, i, o, f"log {i} {part}")
+    for i, o in enumerate(orc):
+        gb, gs = B.summarize_v1(i)
+        assert [list(x) for x in gb] == o.summarize_v1()["blobs"], f"log {i}: SnapshotV1 differs"
+
+
+def test_relative_ops_on_the_reference_withMarkers_summary():
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    blobs = snapshot_fixture("withMarkers")
+    rng = random.Random(5)
+    o = OracleDoc()
+    o.load_v1(blobs, "obs")
+    ids = [f"marker{70 * k}" for k in range(0, 140)]
+    ids = [m for m in ids if o.pos_from_relative({"id": m, "before": True}, 0, 0) >= 0]
+    assert len(ids) > 100  # header and body markers
+    B = MergeTreeBatch(1)
+    B[0].load(dict(blobs), "obs")
+    msgs, seq = [], 0
+    for k in range(300):
+        seq += 1
+        cid = rng.choice(["a", "b", "c"])
+        ref = max(0, seq - 1 - rng.randint(0, 10))
+        mid = rng.choice(ids)
+        r = rng.random()
+        if r < 0.4:
+            op = {"type": 2, "relativePos1": {"id": mid, "before": True}, "relativePos2": {"id": mid},
+                  "props": {"Properties": {"Bold": rng.random() < 0.5}}}
+        elif r < 0.8:
+            op = {"type": 0, "relativePos1": {"id": mid, "offset": rng.randint(0, 4)}, "seg": rng.choice(["x", "yz", "\n"])}
+        else:
+            op = {"type": 1, "relativePos1": {"id": mid}, "relativePos2": {"id": mid, "offset": rng.randint(1, 3)}}
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+             "minimumSequenceNumber": max(0, seq - 12), "type": "op", "contents": op}
+        o.apply_msg(m)
+        B[0].applyMsg(m)
+        if k % 100 == 99:
+            st = B.replay()
+            assert st["errors"] == 0, st
+            _same(B, 0, o, f"after {k + 1} ops")
+
+
+def test_unmapped_marker_fails_its_document_only():
+    """A removed header marker is never mapped (blockUpdate maps live markers only): the reference's
+    posFromRelativePos gives -1, which the engine (and the oracle) rejects for that document."""
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from pyoracle import OracleDoc, OracleError
+    summary_src = OracleDoc()
+    summary_src.insert_text_local(0, "abcdef")
+    summary_src.insert_marker_local(3, 1, {"markerId": "gone"})
+    summary_src.insert_marker_local(1, 1, {"markerId": "live"})
+    summary_src.start_collab("w")
+    summary_src.add_client("x")
+    summary_src.apply_msg({"clientId": "x", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                           "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 1, "pos1": 4, "pos2": 5}})
+    blobs = summary_src.summarize_v1()["blobs"]
+    bad = {"clientId": "y", "sequenceNumber": 2, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0, "type": "op",
+           "contents": {"type": 0, "relativePos1": {"id": "gone"}, "seg": "!"}}
+    good = dict(bad, contents={"type": 0, "relativePos1": {"id": "live"}, "seg": "!"})
+    o = OracleDoc()
+    o.load_v1(blobs, "obs")
+    with pytest.raises(OracleError, match="names no marker"):
+        o.apply_msg(bad)
+    B = MergeTreeBatch(2)
+    for i in range(2):
+        B[i].load([tuple(x) for x in blobs], "obs")
+    B[0].applyMsg(bad)
+    B[1].applyMsg(good)
+    with pytest.raises(MergeTreeError, match="relative position"):
+        B.replay()
+    o2 = OracleDoc()
+    o2.load_v1(blobs, "obs")
+    o2.apply_msg(good)
+    assert B.text(1) == o2.get_text()

@@ -48,7 +48,7 @@ def test_unsupported_inputs_are_rejected_at_pack_time():
     B = MergeTreeBatch(1)
     B[0].startOrUpdateCollaboration("A")
     base = {"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0, "type": "op"}
-    with pytest.raises(MergeTreeError, match="relative positions"):
+    with pytest.raises(MergeTreeError, match="names no marker"):
         B[0].applyMsg(dict(base, contents={"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
     with pytest.raises(MergeTreeError, match="combiningOp"):
         B[0].applyMsg(dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
