@@ -40,7 +40,7 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              const uint32_t* psegp, FBlk* blks, const FBlk* pblk);
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                             Tables tables, int live);
+                             Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
@@ -1464,8 +1464,14 @@ void launch_main(mtb_dev* b, const Tables& t) {
     HIPCHK(mtb_launch_matrix(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
   else
+  {
+    // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
+    // batches where some document met a marker id
+    bool markers = false;
+    for (uint32_t i = 0; i < b->ndocs && !markers; i++) markers = !b->docs[i].markerAmbig.empty();
     HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
-                             b->dHeap.p, b->dAux.p, b->dFree.p, t, b->live ? 1 : 0));
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t, b->live ? 1 : markers ? 2 : 0));
+  }
 }
 
 void replay(mtb_dev* b, mtb_stats* out) {

@@ -196,9 +196,10 @@ using ScratchBig = ScratchT<MTB_LDS_HEAP_LONG>;
 // Engine variants: MODE_REPLAY (mtb_replay_kernel); MODE_LOAD applies only the LOADSEG records at
 // the head of each document's records (mtb_load_kernel); MODE_MATRIX replays SharedMatrix vector pairs
 // with setCell handle allocation (mtb_matrix_kernel); MODE_LIVE is MODE_REPLAY plus the local ops, acks and
-// pending segment groups of live clients (mtb_live_kernel).  Each variant carries
-// only its own code.
-enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3 };
+// pending segment groups of live clients (mtb_live_kernel); MODE_MARKERS is MODE_REPLAY
+// plus marker ids and marker-relative positions (mtb_markers_kernel, for batches whose documents met a
+// marker id).  Each variant carries only its own code.
+enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3, MODE_MARKERS = 4 };
 template <int MODE, class SCR>
 struct Eng {
   DocState* ds;
@@ -229,6 +230,8 @@ struct Eng {
   uint32_t delta_used;          // entries written in this document's delta slice
   static constexpr bool isPerm = MODE == MODE_MATRIX;  // matrix batches hold PermutationVectors only
   static constexpr bool isLive = MODE == MODE_LIVE;    // local ops / acks of the document's own client (id 0)
+  // idToSegment upkeep and relative positions (the observer-only replay kernel carries none of it)
+  static constexpr bool hasMk = MODE == MODE_MARKERS || MODE == MODE_LIVE || MODE == MODE_LOAD;
   int local_seq;                // MODE_LIVE: collabWindow.localSeq
   uint32_t pend_dir, pend_head, pend_n;  // MODE_LIVE: pending segment-group FIFO (DocState)
   bool grp_open;                // MODE_LIVE: the current local op already has its group
@@ -2772,7 +2775,7 @@ struct Eng {
     memo_new = 0;
     const int S = (int)o.seq, R = (int)o.ref_seq, C = (int)(int16_t)o.client;
     const bool local = isLive && S >= MTB_PEND;
-    if constexpr (MODE == MODE_REPLAY || MODE == MODE_LIVE) delta_on = (o.flags & MTB_F_DELTA) != 0;
+    if constexpr (MODE == MODE_REPLAY || MODE == MODE_MARKERS || MODE == MODE_LIVE) delta_on = (o.flags & MTB_F_DELTA) != 0;
     else delta_on = false;
     if constexpr (MODE == MODE_LOAD) {
       apply_loadseg(o, S, C);
@@ -2784,7 +2787,7 @@ struct Eng {
         view_clear();
         uint64_t t0 = PROF_T();
         int p1 = (int)o.pos1;
-        if constexpr (!isPerm)
+        if constexpr (hasMk)
           if (COLD(o.flags & MTB_F_RELPOS)) {  // getValidOpRange (client.ts:531-537)
             p1 = rel_pos(o.pos1, R, C);
             if (bad()) return;
@@ -2815,7 +2818,7 @@ struct Eng {
           wsync();
           n_mod += 1;
           text_bytes += (marker || (o.flags & MTB_F_PERMSEG)) ? 0u : 2u * (uint32_t)len;
-          if constexpr (!isPerm)
+          if constexpr (hasMk)
             if (COLD(marker && o.payload != 0)) {
               mk_set(o.payload - 1, sid);
               if (bad()) return;
@@ -2844,7 +2847,7 @@ struct Eng {
         view_clear();
         uint64_t t0 = PROF_T();
         int p1 = (int)o.pos1, p2 = (int)o.pos2;
-        if constexpr (!isPerm)
+        if constexpr (hasMk)
           if (COLD(o.flags & MTB_F_RELPOS)) {  // getValidOpRange (client.ts:531-547)
             p1 = rel_pos(o.pos1, R, C);
             if (bad()) return;
@@ -3097,6 +3100,13 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   __shared__ Scratch sh;
   replay_doc<MODE_LIVE>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+// Batches whose documents carry marker ids: the replay engine with idToSegment and relative positions.
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_markers_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                       WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  replay_doc<MODE_MARKERS>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
 // SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
@@ -3120,10 +3130,13 @@ extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
 #define MTB_FEW_DOCS 1024
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                             Tables tables, int live) {
-  if (live)
+                             Tables tables, int variant) {
+  if (variant == 1)
     hipLaunchKernelGGL(mtb_live_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
                        aux, freel, tables);
+  else if (variant == 2)
+    hipLaunchKernelGGL(mtb_markers_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
+                       heap, aux, freel, tables);
   else if (ndocs <= MTB_FEW_DOCS)
     hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
                        heap, aux, freel, tables);

@@ -125,3 +125,36 @@ def test_unmapped_marker_fails_its_document_only():
     o2.load_v1(blobs, "obs")
     o2.apply_msg(good)
     assert B.text(1) == o2.get_text()
+
+
+def test_relative_positions_in_a_live_client_batch():
+    """A live client's own marker (local insert, pending then acked) named by remote relative ops: the
+    live-client kernel carries the marker map too."""
+    import json
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    o = OracleDoc()
+    o.insert_text_local(0, "hello world")
+    o.start_collab("me")
+    B = MergeTreeBatch(1)
+    B[0].insertTextLocal(0, "hello world")
+    B[0].startOrUpdateCollaboration("me")
+    op = o.insert_local_op(5, {"marker": {"refType": 1}, "props": {"markerId": "L"}})
+    op = json.loads(op) if isinstance(op, str) else op
+    B[0].applyLocalOp(op)
+    msgs = [
+        {"clientId": "x", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0, "type": "op",
+         "contents": {"type": 0, "pos1": 0, "seg": "AB"}},
+        {"clientId": "me", "sequenceNumber": 2, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0, "type": "op",
+         "contents": op},
+        {"clientId": "x", "sequenceNumber": 3, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0, "type": "op",
+         "contents": {"type": 0, "relativePos1": {"id": "L", "before": True}, "seg": "<"}},
+        {"clientId": "y", "sequenceNumber": 4, "referenceSequenceNumber": 3, "minimumSequenceNumber": 1, "type": "op",
+         "contents": {"type": 2, "relativePos1": {"id": "L", "before": True}, "relativePos2": {"id": "L"},
+                      "props": {"seen": True}}},
+    ]
+    for k, m in enumerate(msgs):
+        o.apply_msg(m)
+        B[0].applyMsg(m)
+        B.replay()
+        _same(B, 0, o, f"after message {k + 1}")
