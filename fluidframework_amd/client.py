@@ -366,6 +366,13 @@ class Client:
         """removeRangeLocal (client.ts:230): returns the IMergeTreeRemoveMsg to send."""
         return self.applyLocalOp({"pos1": start, "pos2": end, "type": 1})
 
+    def annotateRangeLocal(self, start, end, props, combiningOp=None):
+        """annotateRangeLocal (client.ts:206): the keys stay pending on the annotated segments until the
+        op's ack; returns the IMergeTreeAnnotateMsg to send."""
+        if combiningOp is not None:
+            raise MergeTreeError(-6, "unsupported: local annotate with a combiningOp")
+        return self.applyLocalOp({"pos1": start, "pos2": end, "props": props, "type": 2})
+
     def getText(self):
         return self._b.text(self._doc)
 

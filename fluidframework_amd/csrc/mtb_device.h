@@ -51,9 +51,12 @@
 // it after sequenced segments (UnassignedSequenceNumber -> Number.MAX_SAFE_INTEGER - 1, mergeTree.ts:1719).
 #define MTB_PEND 0x40000000
 // Pending segment groups (pendingSegments, mergeTree.ts:532; one SegmentGroup per local op that touched
-// segments): a FIFO directory of MTB_PEND_GROUPS entries [localSeq, member list offset, count, capacity]
-// in the aux arena; member lists (segment ids, group order) grow by doubling.
+// segments): a FIFO directory of MTB_PEND_GROUPS entries [localSeq, member list offset, count, capacity,
+// op type, op props id, 0, 0] in the aux arena; member lists (segment ids, group order) grow by doubling.
+// A segment's pending property keys (PropertiesManager.pendingKeyUpdateCount, segmentPropertiesManager.ts)
+// are the keys of the pending ANNOTATE groups holding it.
 #define MTB_PEND_GROUPS 64
+#define MTB_PEND_ENT 8  // words per directory entry
 // Marker-relative positions (IRelativePosition, ops.ts:77-92; posFromRelativePos mergeTree.ts:1371-1395):
 // an insert / remove / annotate record with MTB_F_RELPOS has pos1 and/or pos2 = MTB_RELPOS | the
 // text-arena offset of a 6-unit descriptor [ordinal lo, ordinal hi, before, 0, offset lo, offset hi]
@@ -173,7 +176,8 @@ struct DocState {     // 320 bytes
   uint32_t mk_map;      // aux offset of the map (0: none yet)
   uint32_t mk_n;        // entries allocated
   uint32_t mk_cap;      // host: marker ordinals known for the document (the map grows to this)
-  uint32_t pad3[9];
+  uint32_t pend_ann;    // pending groups of local annotates
+  uint32_t pad3[8];
 };
 static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
@@ -209,7 +213,7 @@ struct Tables {
 #define DERR_CAP_PEND 16   // more than MTB_PEND_GROUPS unacked local ops
 #define DERR_ACK_INSERT 17 // 0x045 "On insert, seq number already assigned!"
 #define DERR_ACK_REMOVE 18 // 0x046 "On remove ack, missing removal info!"
-#define DERR_LOCAL 19      // a local op the engine does not support (local annotate)
+#define DERR_LOCAL 19      // a local op the engine does not support (a local rewrite annotate)
 #define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

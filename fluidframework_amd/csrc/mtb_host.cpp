@@ -2645,7 +2645,7 @@ int mtbx_apply_msg_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) 
 
 // A live client's own op (client.ts:196-247 insertSegmentLocal / removeRangeLocal): the IMergeTreeOp it
 // sends, applied at the document's next replay in its own view with UnassignedSequenceNumber
-// (DESIGN.md section 10).  Local annotates are not supported.
+// (DESIGN.md section 10).  Local rewrite annotates are not supported.
 int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
   return guarded(b, [&] {
     if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: local ops on a matrix batch");
@@ -2661,8 +2661,10 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     try {
       pack_delta(b, d, op, base, recs);
       for (const mtb_op& r : recs) {
-        if (r.type == MTB_OP_ANNOTATE) raise(MTB_E_UNSUPPORTED, "unsupported: local annotate (pending property keys)");
-        if (r.type != MTB_OP_INSERT && r.type != MTB_OP_REMOVE) raise(MTB_E_ARG, "local op without an effect");
+        if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE))
+          raise(MTB_E_UNSUPPORTED, "unsupported: local rewrite annotate (pendingRewriteCount)");
+        if (r.type != MTB_OP_INSERT && r.type != MTB_OP_REMOVE && r.type != MTB_OP_ANNOTATE)
+          raise(MTB_E_ARG, "local op without an effect");
         if (r.type == MTB_OP_INSERT && !(r.flags & MTB_F_MARKER) && r.pos2 == 0) raise(MTB_E_ARG, "empty local insert");
       }
     } catch (...) {

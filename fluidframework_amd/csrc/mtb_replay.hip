@@ -1437,17 +1437,17 @@ struct Eng {
 
   // ------------------------------------------------------------------ pending segment groups (MODE_LIVE)
   // The FIFO of SegmentGroups (pendingSegments, mergeTree.ts:532): directory entry i (0 = oldest) is
-  // [localSeq, member list offset, count, capacity] in the aux arena.
+  // [localSeq, member list offset, count, capacity, op type, op props id] in the aux arena.
   __device__ __forceinline__ gptr<uint32_t> grp_ent(uint32_t i) const {
-    return UP(aux) + pend_dir + 4u * ((pend_head + i) % MTB_PEND_GROUPS);
+    return UP(aux) + pend_dir + MTB_PEND_ENT * ((pend_head + i) % MTB_PEND_GROUPS);
   }
   // addToPendingList (mergeTree.ts:1324-1357): segment `sid` joins the current local op's group (made on
-  // its first segment)
-  __device__ __forceinline__ void grp_add(uint32_t sid) {
+  // its first segment; `type` / `props` name the op: an ANNOTATE group's keys are pending on its members)
+  __device__ __forceinline__ void grp_add(uint32_t sid, uint32_t type, uint32_t props) {
     if (!grp_open) {
       if (pend_n >= MTB_PEND_GROUPS) { fail(DERR_CAP_PEND); return; }
       if (pend_dir == 0) {
-        pend_dir = alloc_aux(4 * MTB_PEND_GROUPS);
+        pend_dir = alloc_aux(MTB_PEND_ENT * MTB_PEND_GROUPS);
         pend_head = 0;
         if (bad()) return;
       }
@@ -1459,12 +1459,51 @@ struct Eng {
         e[1] = off;
         e[2] = 0;
         e[3] = 8;
+        e[4] = type;
+        e[5] = props;
+        if (type == MTB_OP_ANNOTATE) ds->pend_ann = ds->pend_ann + 1;
       }
       wsync();
       pend_n++;
       grp_open = true;
     }
     grp_push(pend_n - 1, sid);
+  }
+  // PropertiesManager.pendingKeyUpdateCount of segment `sid` (segmentPropertiesManager.ts:60-157): the keys
+  // of the pending ANNOTATE groups holding it, collected at sh->hold[2] (at most 64); returns their number
+  __device__ __forceinline__ uint32_t pending_keys(uint32_t sid) {
+    uint32_t nk = 0;
+    for (uint32_t i = 0; i < pend_n && !err; i++) {
+      const auto e = grp_ent(i);
+      if (U(e[4]) != MTB_OP_ANNOTATE) continue;
+      const uint32_t off = U(e[1]), cnt = U(e[2]);
+      bool found = false;
+      for (uint32_t q = 0; q < cnt && !found; q += 64) found = __ballot(q + lane < cnt && aux[off + q + lane] == sid) != 0;
+      if (!found) continue;
+      const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * U(e[5])]);
+      const uint32_t nop = U(op[0]);
+      for (uint32_t q = lane; q < nop; q += 64)
+        if (nk + q < 64) sh->hold[2][nk + q] = op[1 + 2 * q];
+      nk = nk + nop < 64 ? nk + nop : 64;
+      wsync();
+    }
+    return nk;
+  }
+  // hold mask for scourNode (zamboni.ts:122-193): a segment with pending groups stays as it is; pending
+  // inserts / removes carry MTB_PEND tags, segments of pending annotates are found in their groups
+  __device__ __forceinline__ bool annotate_pending(uint32_t id) {
+    bool held = false;
+    for (uint32_t i = 0; i < pend_n && !err; i++) {
+      const auto e = grp_ent(i);
+      if (U(e[4]) != MTB_OP_ANNOTATE) continue;
+      const uint32_t off = U(e[1]), cnt = U(e[2]);
+      for (uint32_t q = 0; q < cnt; q += 64) {
+        const uint32_t m = q + lane < cnt ? aux[off + q + lane] : MTB_NONE;
+        const uint32_t nq = cnt - q < 64 ? cnt - q : 64;
+        for (uint32_t t = 0; t < nq; t++) held |= (id & ~MTB_LEAF) == rlu(m, (int)t) && (id & MTB_LEAF);
+      }
+    }
+    return held;
   }
   // append a member to directory entry i (its list doubles when full)
   __device__ __forceinline__ void grp_push(uint32_t i, uint32_t sid) {
@@ -1533,7 +1572,11 @@ struct Eng {
     if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
     pend_head = (pend_head + 1) % MTB_PEND_GROUPS;
     pend_n--;
-    if (opType != 0 && opType != 1) { fail(DERR_LOCAL); return; }
+    if (opType != 0 && opType != 1 && opType != 2) { fail(DERR_LOCAL); return; }
+    if (U(e[4]) == MTB_OP_ANNOTATE) {  // ackPendingProperties: the group's keys stop being pending
+      if (lane == 0) ds->pend_ann = ds->pend_ann - 1;
+      wsync();
+    }
     for (uint32_t i = 0; i < cnt && !err; i++) {
       const uint32_t sid = U(aux[off + i]);
       if (sid >= seg_used) { fail(DERR_SHAPE); return; }
@@ -1546,7 +1589,9 @@ struct Eng {
       const int j = first_set(m);
       const int sq = (int)U(rec[F_SEQ * 8 + j]), rs = (int)U(rec[F_RSEQ * 8 + j]);
       const int sc = (int)U(blk[b].scour);
-      if (opType == 0) {
+      if (opType == 2) {
+        // (annotate: no seq to stamp; the lengths are unchanged, so no list needs rebuilding below)
+      } else if (opType == 0) {
         if (sq < MTB_PEND) { fail(DERR_ACK_INSERT); return; }
         if (lane == 0) blk[b].f[F_SEQ][j] = (uint32_t)S;
       } else {
@@ -1559,7 +1604,7 @@ struct Eng {
     }
     // nodesToUpdate: the distinct parents, in order (a repeat only rebuilds again)
     uint32_t prev = MTB_NONE;
-    for (uint32_t i = 0; i < cnt && !err; i++) {
+    for (uint32_t i = 0; i < cnt && !err && opType != 2; i++) {
       const uint32_t b = U(segp[U(aux[off + i])]);  // (ids checked above)
       if (b != prev) rebuild_up(b);
       prev = b;
@@ -1600,7 +1645,13 @@ struct Eng {
     if (HOT(old == mo && mn)) return mn;
     return props_apply_slow(old, opId, rewrite);
   }
-  __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite) {
+  // nex > 0: the first nex words of sh->hold[2] are keys this edit leaves alone (pending local keys)
+  __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite, uint32_t nex = 0) {
+    auto excluded = [&](uint32_t k) {
+      bool x = false;
+      for (uint32_t i = 0; i < nex; i++) x |= sh->hold[2][i] == k;
+      return x;
+    };
     const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * opId]);
     const uint32_t nop = U(op[0]);
     uint32_t n = 0;
@@ -1626,6 +1677,7 @@ struct Eng {
             keep = v != MTB_NONE && !sh->tab.val_falsy[v];
           }
         }
+        if (!keep && nex && excluded(k)) keep = true;
         if (keep) {
           wsync();
           sh->pk[w] = k;
@@ -1639,6 +1691,7 @@ struct Eng {
     for (uint32_t q = 0; q < nop; q++) {
       const uint32_t k = op[1 + 2 * q];
       const uint32_t v = op[2 + 2 * q];
+      if (nex && excluded(k)) continue;
       int at = -1;
       for (uint32_t i = 0; i < n; i++)
         if (sh->pk[i] == k) at = (int)i;
@@ -1797,7 +1850,7 @@ struct Eng {
         while (fm && !err) {
           const int t = first_set(fm);
           fm &= fm - 1;
-          grp_add(rlu(id, t) & ~MTB_LEAF);
+          grp_add(rlu(id, t) & ~MTB_LEAF, MTB_OP_REMOVE, 0);
         }
       }
       if (isLive) {
@@ -1856,13 +1909,41 @@ struct Eng {
       }
     } else {
       // annotate: one new property set per distinct old set (memoized per op)
-      unsigned long long am = vm;
+      unsigned long long am = vm, handled = 0;
+      if (isLive && S >= MTB_PEND) {  // a local annotate: every annotated segment joins its group, in order
+        unsigned long long gm = vm;
+        while (gm && !err) {
+          const int t = first_set(gm);
+          gm &= gm - 1;
+          grp_add(rlu(id, t) & ~MTB_LEAF, MTB_OP_ANNOTATE, opId);
+        }
+      } else if (isLive && COLD(U(ds->pend_ann) != 0)) {
+        // a remote annotate leaves the keys of pending local annotates alone (shouldModifyKey,
+        // segmentPropertiesManager.ts:95-106): segments holding pending keys get their own edit
+        unsigned long long xm = vm;
+        while (xm && !err) {
+          const int t = first_set(xm);
+          xm &= xm - 1;
+          const uint32_t nk = pending_keys(rlu(id, t) & ~MTB_LEAF);
+          if (!nk) continue;
+          const uint32_t np = props_apply_slow(rlu(props, t), opId, rewrite, nk);
+          if (bad()) return 0;
+          memo_old = MTB_NONE;  // (an edit with exclusions is never reused)
+          if (lane == t) {
+            V.f[F_PROPS][lane] = np;
+            blk[b].f[F_PROPS][lane] = np;
+          }
+          am &= ~(1ull << t);
+          handled |= 1ull << t;
+          wsync();
+        }
+      }
       while (am) {
         const int t = first_set(am);
         const uint32_t old = rlu(props, t);
         const uint32_t np = props_apply(old, opId, rewrite);
         if (bad()) return 0;
-        const bool mine = visit && props == old;
+        const bool mine = visit && props == old && !((handled >> lane) & 1);
         if (mine) {
           V.f[F_PROPS][lane] = np;
           blk[b].f[F_PROPS][lane] = np;
@@ -2069,6 +2150,9 @@ struct Eng {
         if (kind == 2 && hasNL && !(f[F_TEXT] & MTB_MARKER) && (int)f[F_LEN] > 0)
           last = UP(sh->gtext)[f[F_TEXT] + f[F_LEN] - 1];
       }
+    }
+    if constexpr (isLive) {
+      if (COLD(U(ds->pend_ann) != 0) && annotate_pending(s < count ? f[F_ID] : MTB_NONE)) kind = 0;
     }
     // property signatures only where matchProperties can decide a merge: an acked segment whose left
     // neighbour is also acked and carries a different property-set handle (equal handles match)
@@ -2747,8 +2831,10 @@ struct Eng {
     const int len = (int)U(blk[root].len);  // the local view's length
     if (o.type == MTB_OP_INSERT) {
       if ((int)o.pos1 < 0 || (int)o.pos1 > len) { fail(DERR_RANGE); return; }
-    } else if (o.type == MTB_OP_REMOVE) {
-      if ((int)o.pos1 < 0 || (int)o.pos1 > len || o.pos2 < o.pos1 || (int)o.pos2 > len) { fail(DERR_RANGE); return; }
+    } else if (o.type == MTB_OP_REMOVE || (o.type == MTB_OP_ANNOTATE && !(o.flags & MTB_F_REWRITE))) {
+      // getValidOpRange (client.ts:550-585): start in [0, length), end > start (end past the length is
+      // not checked; nodeMap stops at the tree's end)
+      if ((int)o.pos1 < 0 || (int)o.pos1 >= len || (int)o.pos2 <= (int)o.pos1) { fail(DERR_RANGE); return; }
     } else {
       fail(DERR_LOCAL);
       return;
@@ -2828,7 +2914,7 @@ struct Eng {
             return;
           }
           settle();
-          if (local) grp_add(sid);  // saveIfLocal (mergeTree.ts:1617-1637)
+          if (local) grp_add(sid, MTB_OP_INSERT, 0);  // saveIfLocal (mergeTree.ts:1617-1637)
           else if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);
           if (COLD(delta_on)) {
             const uint32_t from = delta_used;

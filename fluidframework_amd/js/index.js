@@ -209,6 +209,12 @@ class Client {
     return this.applyLocalOp({ pos1: start, pos2: end, type: 1 });
   }
 
+  /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
+  annotateRangeLocal(start, end, props, combiningOp) {
+    if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");
+    return this.applyLocalOp({ pos1: start, pos2: end, props, type: 2 });
+  }
+
   /** Client.startOrUpdateCollaboration (client.ts:1133). */
   startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
     if (this.longClientId !== undefined) throw unsupported("re-keying the observer id");

@@ -150,12 +150,15 @@ int mtb_docs_load_v1(mtb_batch* b, uint32_t n, const uint32_t* docs, const mtb_b
 /* Client.applyMsg(msg) with msg = JSON.stringify(ISequencedDocumentMessage).  Validates, interns the
  * long client id and props, packs records and appends them to the document (no GPU work). */
 int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
-/* A live client's own op: Client.insertSegmentLocal / removeRangeLocal (client.ts:196-247) with the
- * IMergeTreeOp it sends as JSON ({"type":0,"pos1","seg"} or {"type":1,"pos1","pos2"}; a group of them).
+/* A live client's own op: Client.insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:196-247)
+ * with the IMergeTreeOp it sends as JSON ({"type":0,"pos1","seg"}, {"type":1,"pos1","pos2"} or
+ * {"type":2,"pos1","pos2","props"}; a group of them).
  * The document's observer id (mtb_doc_init) is the client; the op is applied at the next replay in its own
  * view with UnassignedSequenceNumber, after getValidOpRange's bounds check (a failure is reported by that
  * replay).  Its sequenced message, passed to mtb_apply_msg_json, is the ack (ackPendingSegment,
- * client.ts:641-662).  Local annotates are MTB_E_UNSUPPORTED; so are matrix and catch-up batches. */
+ * client.ts:641-662).  A local annotate's keys stay pending on its segments until its ack (remote annotates
+ * leave them alone, segmentPropertiesManager.ts:60-157).  Local rewrite annotates, marker-relative
+ * positions, matrix and catch-up batches are MTB_E_UNSUPPORTED. */
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
 /* Pre-packed path: append records whose `payload` offsets index `payload` (UTF-16 units). */
 int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n,

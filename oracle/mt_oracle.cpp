@@ -1519,7 +1519,9 @@ void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::ve
 // applyRemoveRangeOp / applyAnnotateRangeOp with the local client's (currentSeq, clientId) and
 // UnassignedSequenceNumber; getValidOpRange (client.ts:527-592) bounds-checks the local positions.
 static void validLocalRange(int start, int end, int len, bool insert) {
-  if (start < 0 || start > len || (!insert && (end < start || end > len)))
+  // start outside [0, length] (or at the length for a remove / annotate), or end <= start for a range;
+  // an end past the length is not checked (nodeMap stops at the tree's end)
+  if (start < 0 || start > len || (start == len && !insert) || (!insert && end <= start))
     throw OracleError(-1, "RangeOutOfBounds");
 }
 std::string Doc::insertLocalOp(int pos, const JVal& segSpec) {

@@ -1,12 +1,12 @@
-"""Live clients on the GPU engine: local inserts / removes
-with pending segment groups, acks, remote ops overtaking pending removes and theUnfinishedNode.
+"""Live clients on the GPU engine: local inserts / removes /
+annotates with pending segment groups, acks, remote ops overtaking pending removes, remote annotates
+leaving pending local keys alone (segmentPropertiesManager.ts:60-157) and theUnfinishedNode.
 
 Parity: the conflict farm of tests/helpers.run_local_farm (client.conflictFarm.spec.ts with
 TestClientLogger) runs on the oracle; every client's event stream -- its local ops and the sequenced
 messages as it received them -- is replayed on the engine, one document per client, and after every farm
 round each document's state digest and text equal its oracle client's (pending segments included: an
-unacked seq is UnassignedSequenceNumber in both).  Local annotates are not supported by the engine, so the
-farms here make inserts and removes only.
+unacked seq is UnassignedSequenceNumber in both).  Farms run without and with local annotates.
 """
 import pytest
 
@@ -15,10 +15,10 @@ from helpers import run_local_farm
 pytestmark = pytest.mark.gpu
 
 
-def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1):
+def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False):
     from fluidframework_amd import MergeTreeBatch
     rec = {}
-    run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=False, record=rec)
+    run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=annotate, record=rec)
     ids = rec["ids"]
     B = MergeTreeBatch(n_clients, new_length_calc=new_mode)
     for k, cid in enumerate(ids):
@@ -60,6 +60,49 @@ def test_local_farm_batched_rounds(seed):
     assert _replay_farm(seed, n_clients=8, n_rounds=150, new_mode=seed % 2 == 0, rounds_per_replay=10) > 0
 
 
+@pytest.mark.parametrize("seed", list(range(31, 47)))
+def test_local_annotate_farm_every_round(seed):
+    """Local annotates: pending keys on the annotated segments (and on split-off halves), remote annotates
+    skipping them, zamboni holding the segments until the ack."""
+    assert _replay_farm(seed, n_clients=4, n_rounds=40, new_mode=False, annotate=True) > 0
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53, 54])
+def test_local_annotate_farm_new_length_calc(seed):
+    assert _replay_farm(seed, n_clients=4, n_rounds=40, new_mode=True, annotate=True) > 0
+
+
+@pytest.mark.parametrize("seed", [61, 62, 63, 64])
+def test_local_annotate_farm_batched_rounds(seed):
+    assert _replay_farm(seed, n_clients=8, n_rounds=120, new_mode=seed % 2 == 0, rounds_per_replay=10,
+                        annotate=True) > 0
+
+
+def test_pending_local_key_survives_a_remote_annotate():
+    """annotateRangeLocal then a remote annotate of the same key before the ack: the local value stays
+    (shouldModifyKey); after the ack a remote annotate applies again."""
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1)
+    c = B[0]
+    c.insertTextLocal(0, "abcdef")
+    c.startOrUpdateCollaboration("me")
+    op = c.annotateRangeLocal(1, 4, {"color": "red", "size": 1})
+    c.applyMsg({"clientId": "x", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                "type": "op", "contents": {"type": 2, "pos1": 0, "pos2": 6, "props": {"color": "blue", "w": 2}}})
+    B.replay()
+    segs = [(e["segment"].get("text"), e["segment"].get("properties")) for e in B.map_range(0)]
+    assert segs == [("a", {"color": "blue", "w": 2}), ("bcd", {"color": "red", "size": 1, "w": 2}),
+                    ("ef", {"color": "blue", "w": 2})], segs
+    c.applyMsg({"clientId": "me", "sequenceNumber": 2, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                "type": "op", "contents": op})
+    c.applyMsg({"clientId": "x", "sequenceNumber": 3, "referenceSequenceNumber": 2, "minimumSequenceNumber": 0,
+                "type": "op", "contents": {"type": 2, "pos1": 2, "pos2": 3, "props": {"color": "green"}}})
+    B.replay()
+    segs = [(e["segment"].get("text"), e["segment"].get("properties")) for e in B.map_range(0)]
+    assert segs[1:4] == [("b", {"color": "red", "size": 1, "w": 2}), ("c", {"color": "green", "size": 1, "w": 2}),
+                         ("d", {"color": "red", "size": 1, "w": 2})], segs
+
+
 def test_local_insert_then_ack_api():
     """Client-level calls: insertTextLocal / removeRangeLocal while collaborating return the ops to send;
     the sequenced messages ack them (client.ts:196-247, 641-662)."""
@@ -87,6 +130,9 @@ def test_local_op_out_of_range_fails_at_replay():
     B = MergeTreeBatch(1)
     B[0].insertTextLocal(0, "abc")
     B[0].startOrUpdateCollaboration("me")
-    B[0].removeRangeLocal(1, 9)
+    B[0].removeRangeLocal(1, 9)  # getValidOpRange does not check the end against the length
+    B.replay()
+    assert B.text(0) == "a"
+    B[0].removeRangeLocal(1, 2)  # start at the length: RangeOutOfBounds
     with pytest.raises(MergeTreeError):
         B.replay()
