@@ -24,7 +24,7 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
            "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
-           "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json"]
+           "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op"]
 
 
 class MtbOptions(ctypes.Structure):
@@ -84,6 +84,8 @@ def lib():
     L.mtb_matrix_get_cell.argtypes = [vp, u32, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.mtb_apply_msg_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
     L.mtb_local_op_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    L.mtb_regenerate_pending_op.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(sz)]
     L.mtb_append_ops.argtypes = [vp, u32, vp, u32, vp, sz]
     L.mtb_add_client.argtypes = [vp, u32, ctypes.c_char_p]
     L.mtb_intern_props.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(u32)]

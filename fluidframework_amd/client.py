@@ -366,6 +366,21 @@ class Client:
         """removeRangeLocal (client.ts:230): returns the IMergeTreeRemoveMsg to send."""
         return self.applyLocalOp({"pos1": start, "pos2": end, "type": 1})
 
+    def regeneratePendingOp(self, resetOp, segmentGroup=None):
+        """Client.regeneratePendingOp (client.ts:917-960) after a reconnect: `resetOp` is the oldest pending op
+        as it was submitted (its segment groups are the oldest pending ones); returns the op to resubmit."""
+        s = resetOp if isinstance(resetOp, (bytes, bytearray)) else (
+            resetOp.encode() if isinstance(resetOp, str) else json.dumps(resetOp).encode())
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        L = self._b._L
+        self._b._chk(L.mtb_regenerate_pending_op(self._b._h, self._doc, s, len(s), ctypes.byref(p), ctypes.byref(n)))
+        self._b._dirty = False
+        try:
+            return json.loads(ctypes.string_at(p, n.value).decode("utf-8"))
+        finally:
+            L.mtb_free(p)
+
     def annotateRangeLocal(self, start, end, props, combiningOp=None):
         """annotateRangeLocal (client.ts:206): the keys stay pending on the annotated segments until the
         op's ack; returns the IMergeTreeAnnotateMsg to send."""

@@ -46,6 +46,10 @@
 // records carrying MTB_F_LOCAL are applied at (currentSeq, own id) with UnassignedSequenceNumber; an
 // MTB_OP_ACK record (the client's own sequenced op) has pos2 = the acked op's type.
 #define MTB_F_LOCAL 0x10
+// Client.regeneratePendingOp (client.ts:917-960) of the head pending op with pos1 member ops (MODE_LIVE):
+// normalizeSegmentsOnRebase when currentSeq moved, then per member group the regenerated ops' entries
+// [record, op type | group index << 8, segment, position] in the document's delta slice.
+#define MTB_OP_REGEN 7
 // A pending (unacked) local insert / remove stores MTB_PEND + localSeq in the segment's F_SEQ / F_RSEQ:
 // larger than every sequence number, so every remote perspective sees it as "not yet" and breakTie orders
 // it after sequenced segments (UnassignedSequenceNumber -> Number.MAX_SAFE_INTEGER - 1, mergeTree.ts:1719).
@@ -55,7 +59,7 @@
 // op type, op props id, 0, 0] in the aux arena; member lists (segment ids, group order) grow by doubling.
 // A segment's pending property keys (PropertiesManager.pendingKeyUpdateCount, segmentPropertiesManager.ts)
 // are the keys of the pending ANNOTATE groups holding it.
-#define MTB_PEND_GROUPS 64
+#define MTB_PEND_GROUPS 256
 #define MTB_PEND_ENT 8  // words per directory entry
 // Marker-relative positions (IRelativePosition, ops.ts:77-92; posFromRelativePos mergeTree.ts:1371-1395):
 // an insert / remove / annotate record with MTB_F_RELPOS has pos1 and/or pos2 = MTB_RELPOS | the
@@ -177,7 +181,10 @@ struct DocState {     // 320 bytes
   uint32_t mk_n;        // entries allocated
   uint32_t mk_cap;      // host: marker ordinals known for the document (the map grows to this)
   uint32_t pend_ann;    // pending groups of local annotates
-  uint32_t pad3[8];
+  int32_t last_norm;    // Client.lastNormalizationRefSeq (client.ts:909): currentSeq of the last normalization
+  uint32_t orphans;     // aux offset of [n, cap, (props id, segment)*]: pending keys whose annotate group a
+                        // reconnect dropped without a new op (they stay pending, as the reference's counts do)
+  uint32_t pad3[6];
 };
 static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
@@ -215,6 +222,7 @@ struct Tables {
 #define DERR_ACK_REMOVE 18 // 0x046 "On remove ack, missing removal info!"
 #define DERR_LOCAL 19      // a local op the engine does not support (a local rewrite annotate)
 #define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
+#define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

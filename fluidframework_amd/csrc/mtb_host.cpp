@@ -1382,6 +1382,7 @@ std::string derr_text(int e) {
     case DERR_ASSERT_MSN: return "0x04e/0x04f/0x039 minimum sequence number out of order";
     case DERR_DEPTH: return "tree depth limit exceeded";
     case DERR_HOST: return "host post-processing of the replay failed";
+    case DERR_REGEN: return "0x033/0x035 regeneratePendingOp: segment group not at the head of the pending queue";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     default: return "device error " + std::to_string(e);
   }
@@ -1582,8 +1583,10 @@ void replay(mtb_dev* b, mtb_stats* out) {
         // three created per record)
         cap = s.seg_cap + 4ull * b->docs[i].pending.size() + 1;
       } else if (!s.err) {
-        for (const mtb_op& o : b->docs[i].pending)
+        for (const mtb_op& o : b->docs[i].pending) {
           if (o.flags & MTB_F_DELTA) cap += o.type == MTB_OP_INSERT ? 1 : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1;
+          if (o.type == MTB_OP_REGEN) cap += (uint64_t)o.pos1 * (s.seg_used + 16);  // one entry per regenerated op
+        }
       }
       s.delta_cap = (uint32_t)cap;
       tot += cap;
@@ -2675,6 +2678,116 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     d.totalPayload += d.payload.size() - payloadBefore;
     d.pending.insert(d.pending.end(), recs.begin(), recs.end());
     d.totalOps += recs.size();
+  });
+}
+
+// Client.regeneratePendingOp (client.ts:917-960): the op(s) a live client resubmits after a reconnect for
+// its oldest pending op `op_json` (one pending segment group per member op).  Runs as a REGEN record on
+// the GPU (normalizeSegmentsOnRebase, positions at the groups' localSeq, new pending groups); the ops are
+// composed here from the kernel's entries as the reference's opBuilder writes them.
+int mtbx_regenerate_pending_op(mtb_dev* b, uint32_t doc, const char* json, size_t len, char** out, size_t* out_len) {
+  return guarded(b, [&] {
+    if (!out) raise(MTB_E_ARG, "null output");
+    if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: local ops on a matrix batch");
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    const hj::Value op = hj::parse(json, len);
+    if (op.kind != hj::Value::kObj) raise(MTB_E_PARSE, "op is not an object");
+    std::vector<const hj::Value*> members;
+    const hj::Value* t = member(op, u"type");
+    if (t && t->kind == hj::Value::kNum && (int)t->n == 3) {
+      const hj::Value* ops = member(op, u"ops");
+      if (ops && ops->kind == hj::Value::kArr)
+        for (auto& m : ops->items) members.push_back(&m);
+    } else {
+      members.push_back(&op);
+    }
+    for (const hj::Value* m : members) {
+      const hj::Value* mt = member(*m, u"type");
+      const int ty = mt && mt->kind == hj::Value::kNum ? (int)mt->n : -1;
+      if (ty < 0 || ty > 2) raise(MTB_E_ARG, "Invalid op type");
+    }
+    std::vector<std::string> ops;
+    if (!members.empty()) {
+      mtb_op r{};
+      r.type = MTB_OP_REGEN;
+      r.pos1 = (uint32_t)members.size();
+      d.pending.push_back(r);
+      d.totalOps++;
+      b->live = true;
+      const uint32_t k = (uint32_t)d.pending.size() - 1;  // the record's index in this replay
+      mtb_stats st{};
+      replay(b, &st);
+      const DocState& s = b->hst[doc];
+      if (s.err) raise(derr_code(s.err), derr_text(s.err));
+      std::vector<uint32_t> ent(4ull * s.delta_used);
+      if (s.delta_used)
+        HIPCHK(hipMemcpy(ent.data(), b->dDelta.p + 4ull * s.delta_base, ent.size() * 4, hipMemcpyDeviceToHost));
+      download_doc(b, doc);
+      for (uint32_t e = 0; e < s.delta_used; e++) {
+        if (ent[4 * e] != k) continue;
+        const uint32_t ty = ent[4 * e + 1] & 0xFF, g = ent[4 * e + 1] >> 8, sid = ent[4 * e + 2];
+        const int pos = (int)ent[4 * e + 3];
+        if (g >= members.size() || sid >= d.segs.size()) raise(MTB_E_HIP, "regenerate: bad kernel entry");
+        const Seg& sg = d.segs[sid];
+        const hj::Value& reset = *members[g];
+        std::string o = "{\"pos1\":" + std::to_string(pos);
+        if (ty == MTB_OP_INSERT) {  // createInsertSegmentOp(pos, segment): segment.toJSONObject()
+          const hj::Value* rseg = member(reset, u"seg");
+          const hj::Value* rprops = rseg && rseg->kind == hj::Value::kObj ? member(*rseg, u"props") : nullptr;
+          std::string pj;
+          bool hasProps = false;
+          if (rprops && rprops->kind != hj::Value::kUndef) {  // segment.clone() with resetOp.seg.props
+            hasProps = rprops->kind == hj::Value::kObj;
+            if (hasProps) pj = hj::dump(*rprops);
+          } else if (sg.props) {
+            hasProps = true;
+            props_json(b, pj, props_of(b, d, sg.props));
+          }
+          o += ",\"seg\":";
+          if (is_marker(sg)) {
+            const uint32_t rt = sg.text & ~MTB_MARKER;
+            o += "{\"marker\":{";
+            if (rt) o += "\"refType\":" + std::to_string(rt - 1);
+            o += "}";
+            if (hasProps) o += ",\"props\":" + pj;
+            o += "}";
+          } else {
+            const U16 text(reinterpret_cast<const char16_t*>(d.text.data() + sg.text), (size_t)sg.len);
+            if (hasProps) {
+              o += "{\"text\":";
+              hj::quote(o, text);
+              o += ",\"props\":" + pj + "}";
+            } else {
+              hj::quote(o, text);
+            }
+          }
+          o += ",\"type\":0}";
+        } else {
+          o += ",\"pos2\":" + std::to_string(pos + sg.len);
+          if (ty == MTB_OP_ANNOTATE) {
+            const hj::Value* pr = member(reset, u"props");
+            if (pr) o += ",\"props\":" + hj::dump(*pr);
+            o += ",\"type\":2}";
+          } else {
+            o += ",\"type\":1}";
+          }
+        }
+        ops.push_back(std::move(o));
+      }
+    }
+    std::string res;
+    if (ops.size() == 1) {
+      res = ops[0];
+    } else {  // createGroupOp(...ops)
+      res = "{\"ops\":[";
+      for (size_t i = 0; i < ops.size(); i++) res += (i ? "," : "") + ops[i];
+      res += "],\"type\":3}";
+    }
+    *out = (char*)malloc(res.size() + 1);
+    memcpy(*out, res.data(), res.size());
+    (*out)[res.size()] = 0;
+    if (out_len) *out_len = res.size();
   });
 }
 

@@ -279,6 +279,9 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len) {
   DOC_CALL(doc, mtbx_local_op_json(d_, l_, json_utf8, len));
 }
+int mtb_regenerate_pending_op(mtb_batch* b, uint32_t doc, const char* op_json, size_t len, char** out, size_t* out_len) {
+  DOC_CALL(doc, mtbx_regenerate_pending_op(d_, l_, op_json, len, out, out_len));
+}
 
 int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n, const uint16_t* payload, size_t payload_len) {
   DOC_CALL(doc, mtbx_append_ops(d_, l_, ops, n, payload, payload_len));

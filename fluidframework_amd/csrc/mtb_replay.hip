@@ -1328,7 +1328,7 @@ struct Eng {
     n_mod += 2;
     wsync();
     insert_slot(d, j + 1);
-    if (isLive && pend_n > 0) grp_split(U(V.f[F_ID][j]) & ~MTB_LEAF, r);
+    if (isLive && (pend_n > 0 || COLD(U(ds->orphans) != 0))) grp_split(U(V.f[F_ID][j]) & ~MTB_LEAF, r);
   }
 
   // ------------------------------------------------------------------ LRU heap (collections/heap.ts)
@@ -1487,6 +1487,19 @@ struct Eng {
       nk = nk + nop < 64 ? nk + nop : 64;
       wsync();
     }
+    const uint32_t orp = U(ds->orphans);
+    if (COLD(orp != 0)) {  // keys a reconnect left pending without a group
+      const uint32_t n = U(aux[orp]);
+      for (uint32_t i = 0; i < n && !err; i++) {
+        if (U(aux[orp + 3 + 2 * i]) != sid) continue;
+        const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * U(aux[orp + 2 + 2 * i])]);
+        const uint32_t nop = U(op[0]);
+        for (uint32_t q = lane; q < nop; q += 64)
+          if (nk + q < 64) sh->hold[2][nk + q] = op[1 + 2 * q];
+        nk = nk + nop < 64 ? nk + nop : 64;
+        wsync();
+      }
+    }
     return nk;
   }
   // hold mask for scourNode (zamboni.ts:122-193): a segment with pending groups stays as it is; pending
@@ -1537,6 +1550,15 @@ struct Eng {
       bool found = false;
       for (uint32_t q = 0; q < cnt; q += 64) found |= __ballot(q + lane < cnt && aux[off + q + lane] == s) != 0;
       if (found) grp_push(i, r);
+    }
+    // keys a reconnect left pending on `s` are copied too (PropertiesManager.copyTo)
+    const uint32_t orp = U(ds->orphans);
+    if (COLD(orp != 0)) {
+      const uint32_t n = U(aux[orp]);
+      for (uint32_t i = 0; i < n && !err; i++) {
+        const uint32_t o = U(ds->orphans);  // (orphan_add may move the list)
+        if (U(aux[o + 3 + 2 * i]) == s) orphan_add(U(aux[o + 2 + 2 * i]), r);
+      }
     }
   }
   // The lists of every ancestor of block b from its parent up to the root, rebuilt bottom-up from their
@@ -1608,6 +1630,349 @@ struct Eng {
       const uint32_t b = U(segp[U(aux[off + i])]);  // (ids checked above)
       if (b != prev) rebuild_up(b);
       prev = b;
+    }
+    view_clear();
+  }
+
+  // ------------------------------------------------------------------ reconnect (MODE_LIVE)
+  // The leaf-level blocks (children are segments) in tree order: f(block) for each, over an explicit
+  // stack in sh->path / sh->sidx (no walk is active while a REGEN record runs).
+  template <class F>
+  __device__ __forceinline__ void each_leaf_block(F&& f) {
+    int d = 0;
+    if (lane == 0) {
+      sh->path[0] = root;
+      sh->sidx[0] = 0;
+    }
+    wsync();
+    for (int guard = 0; !err; guard++) {
+      if (guard > (int)(4 * blk_used + 64)) { fail(DERR_SHAPE); return; }
+      const uint32_t b = U(sh->path[d]);
+      const int cnt = (int)U(blk[b].count);
+      const uint32_t c0 = cnt ? U(blk[b].f[F_ID][0]) : MTB_NONE;
+      int k = U(sh->sidx[d]);
+      if (cnt == 0 || (c0 & MTB_LEAF)) {
+        if (cnt && k == 0) f(b);
+        k = cnt;
+      }
+      if (k >= cnt) {
+        if (d == 0) return;
+        d--;
+        continue;
+      }
+      if (d + 1 >= MTB_VDEPTH) { fail(DERR_DEPTH); return; }
+      const uint32_t c = U(blk[b].f[F_ID][k]);
+      if (lane == 0) {
+        sh->sidx[d] = k + 1;
+        sh->path[d + 1] = c;
+        sh->sidx[d + 1] = 0;
+      }
+      wsync();
+      d++;
+    }
+  }
+  // a new pending group with one member at the FIFO's tail (resetPendingDeltaToOps' newSegmentGroup)
+  __device__ __forceinline__ void grp_new(uint32_t lseq, uint32_t type, uint32_t props, uint32_t sid) {
+    if (pend_n >= MTB_PEND_GROUPS) { fail(DERR_CAP_PEND); return; }
+    if (pend_dir == 0) {
+      pend_dir = alloc_aux(MTB_PEND_ENT * MTB_PEND_GROUPS);
+      pend_head = 0;
+      if (bad()) return;
+    }
+    const uint32_t off = alloc_aux(8);
+    if (bad()) return;
+    const auto e = grp_ent(pend_n);
+    if (lane == 0) {
+      e[0] = lseq;
+      e[1] = off;
+      e[2] = 1;
+      e[3] = 8;
+      e[4] = type;
+      e[5] = props;
+      aux[off] = sid;
+      if (type == MTB_OP_ANNOTATE) ds->pend_ann = ds->pend_ann + 1;
+    }
+    wsync();
+    pend_n++;
+  }
+  // an annotate group member that a reconnect regenerated no op for keeps its pending keys
+  __device__ __forceinline__ void orphan_add(uint32_t props, uint32_t sid) {
+    uint32_t o = U(ds->orphans);
+    const uint32_t n = o ? U(aux[o]) : 0, cap = o ? U(aux[o + 1]) : 0;
+    if (n >= cap) {
+      const uint32_t nc = cap ? 2 * cap : 8;
+      const uint32_t no = alloc_aux(2 + 2 * nc);
+      if (bad()) return;
+      for (uint32_t i = lane; i < 2 * n; i += 64) aux[no + 2 + i] = aux[o + 2 + i];
+      if (lane == 0) {
+        aux[no + 1] = nc;
+        ds->orphans = no;
+      }
+      o = no;
+    }
+    if (lane == 0) {
+      aux[o] = n + 1;
+      aux[o + 2 + 2 * n] = props;
+      aux[o + 3 + 2 * n] = sid;
+    }
+    wsync();
+  }
+  // localNetLength(segment, currentSeq, localSeq) (mergeTree.ts:636-664): the local view as it was after
+  // local op L (later local ops hidden; every sequenced op is at or below currentSeq)
+  __device__ __forceinline__ int len_at(int len, int seq, int rseq, int L) const {
+    const bool lrem = rseq >= MTB_PEND && rseq - MTB_PEND <= L;
+    if (seq < MTB_PEND) return ((rseq >= 0 && rseq < MTB_PEND) || lrem) ? 0 : len;
+    return (seq - MTB_PEND > L || lrem) ? 0 : len;
+  }
+  // cachedLength of leaf-level block b from its children, the difference carried up the ancestors
+  __device__ __forceinline__ void fix_len(uint32_t b) {
+    const uint32_t* r = bw(b);
+    const int cnt = (int)U(r[FB_HDR]);
+    int ol = 0;
+    if (lane < cnt) ol = child_olen(r[F_ID * 8 + lane], (int)r[F_LEN * 8 + lane], (int)r[F_RSEQ * 8 + lane]);
+    const int nl = csum8(ol);
+    const int delta = nl - (int)U(blk[b].len);
+    if (!delta) return;
+    uint32_t X = b;
+    if (lane == 0) blk[b].len = nl;
+    for (int guard = 0; guard < MTB_VDEPTH; guard++) {
+      const uint32_t P = U(blk[X].parent);
+      if (P == MTB_NONE) break;
+      const uint32_t ix = U(blk[X].index);
+      if (lane == 0) {
+        blk[P].f[F_LEN][ix] = (uint32_t)((int)blk[P].f[F_LEN][ix] + delta);
+        blk[P].len = blk[P].len + delta;
+      }
+      wsync();
+      X = P;
+    }
+    wsync();
+  }
+  // normalizeAdjacentSegments (mergeTree.ts:2234-2336) of run entries [0, n) at scratch `sc` (6 words
+  // each: segment, block, slot, kind, localSeq, localRemovedSeq; kind 1 = removed and acked, 2 = removed);
+  // the order list L is at sc + 6n, the gathered fields at sc + 7n.
+  __device__ __forceinline__ void normalize_run(uint32_t sc, uint32_t n) {
+    const auto E = [&](uint32_t i, int w) { return U(aux[sc + 6 * i + w]); };
+    const uint32_t lo = sc + 6 * n;
+    for (uint32_t i = lane; i < n; i += 64) aux[lo + i] = i;
+    wsync();
+    const auto Lr = [&](uint32_t i) { return U(aux[lo + i]); };
+    const auto acked = [&](uint32_t e) { return (E(e, 3) & 1) != 0; };
+    const auto idx = [&](uint32_t e) {
+      uint32_t at = 0;
+      for (uint32_t q = 0; q < n; q += 64) {
+        const unsigned long long m = __ballot(q + lane < n && aux[lo + q + lane] == e);
+        if (m) { at = q + (uint32_t)first_set(m); break; }
+      }
+      return at;
+    };
+    const auto erase = [&](uint32_t p) {
+      for (uint32_t i = p; i + 1 < n; i++) {
+        const uint32_t v = Lr(i + 1);
+        if (lane == 0) aux[lo + i] = v;
+        wsync();
+      }
+    };
+    const auto insert = [&](uint32_t p, uint32_t e) {  // at index p of the n-1 remaining
+      for (uint32_t i = n - 1; i > p; i--) {
+        const uint32_t v = Lr(i - 1);
+        if (lane == 0) aux[lo + i] = v;
+        wsync();
+      }
+      if (lane == 0) aux[lo + p] = e;
+      wsync();
+    };
+    int last = (int)n - 1;
+    while (last >= 0 && acked(Lr((uint32_t)last))) last--;
+    if (last < 0) return;
+    const uint32_t lastLocal = Lr((uint32_t)last);
+    uint32_t toSlide = lastLocal, nearer = last > 0 ? Lr((uint32_t)last - 1) : MTB_NONE;
+    for (uint32_t guard = 0; toSlide != MTB_NONE && !err; guard++) {
+      if (guard > n) { fail(DERR_SHAPE); return; }
+      const uint32_t p = idx(toSlide);
+      if (acked(toSlide)) {
+        erase(p);
+        insert(idx(lastLocal) + 1, toSlide);
+      } else if (E(toSlide, 3) & 2) {
+        const int lrs = (int)E(toSlide, 5);
+        uint32_t cur = p;
+        for (uint32_t sc2 = p + 1; sc2 < n; sc2++) {
+          const uint32_t e = Lr(sc2);
+          if (acked(e) || (int)E(e, 4) < 0 || (int)E(e, 4) <= lrs) break;
+          cur = sc2;
+        }
+        if (cur != p) {
+          erase(p);
+          insert(cur, toSlide);
+        }
+      }
+      toSlide = nearer;
+      if (nearer != MTB_NONE) {
+        const uint32_t q = idx(nearer);
+        nearer = q > 0 ? Lr(q - 1) : MTB_NONE;
+      }
+    }
+    // the run's slots keep their places; each takes the fields of its new segment
+    const uint32_t F = sc + 7 * n;
+    for (uint32_t t = lane; t < 8 * n; t += 64) {
+      const uint32_t j = t >> 3, q = t & 7;
+      aux[F + t] = blk[aux[sc + 6 * j + 1]].f[q][aux[sc + 6 * j + 2]];
+    }
+    wsync();
+    for (uint32_t t = lane; t < 8 * n; t += 64) {
+      const uint32_t i = t >> 3, q = t & 7;
+      const uint32_t j = aux[lo + i];
+      const uint32_t b = aux[sc + 6 * i + 1], sl = aux[sc + 6 * i + 2];
+      blk[b].f[q][sl] = aux[F + 8 * j + q];
+      if (q == 0) segp[aux[sc + 6 * j]] = b;
+    }
+    wsync();
+    n_mod += n;
+    // nodeUpdateLengthNewStructure of the ancestors: block lengths, then the window lists
+    uint32_t prev = MTB_NONE;
+    for (uint32_t i = 0; i < n && !err; i++) {
+      const uint32_t b = E(i, 1);
+      if (b != prev) fix_len(b);
+      prev = b;
+    }
+    prev = MTB_NONE;
+    for (uint32_t i = 0; i < n && !err; i++) {
+      const uint32_t b = E(i, 1);
+      if (b != prev) rebuild_up(b);
+      prev = b;
+    }
+  }
+  // normalizeSegmentsOnRebase (mergeTree.ts:2357-2390): runs of removed / unacked segments holding both an
+  // unacked insert and a remotely removed segment are normalized
+  __device__ __forceinline__ void normalize() {
+    const uint32_t save = aux_used;
+    const uint32_t room = ds->aux_cap > aux_used ? ds->aux_cap - aux_used : 0;
+    const uint32_t cap = room / 16 < 4096 ? room / 16 : 4096;  // run entries the scratch holds
+    if (cap < 2) return;
+    const uint32_t sc = alloc_aux(16 * cap);
+    if (bad()) return;
+    uint32_t rn = 0;
+    bool hasLocal = false, hasRR = false;
+    auto flush = [&]() {
+      if (hasLocal && hasRR && rn > 1) {
+        if (rn > cap) { fail(DERR_CAP_AUX); return; }
+        normalize_run(sc, rn);
+      }
+      rn = 0;
+      hasLocal = hasRR = false;
+    };
+    each_leaf_block([&](uint32_t b) {
+      const uint32_t* r = bw(b);
+      const int cnt = (int)U(r[FB_HDR]);
+      uint32_t id = 0, sq = 0, rs = 0;
+      if (lane < MTB_MAXCH) {
+        id = r[F_ID * 8 + lane];
+        sq = r[F_SEQ * 8 + lane];
+        rs = r[F_RSEQ * 8 + lane];
+      }
+      for (int k = 0; k < cnt && !err; k++) {
+        const int seq = rl((int)sq, k), rseq = rl((int)rs, k);
+        if (rseq >= 0 || seq >= MTB_PEND) {
+          const bool rr = rseq >= 0 && rseq < MTB_PEND;
+          hasRR |= rr;
+          hasLocal |= seq >= MTB_PEND;
+          if (rn < cap && lane == 0) {
+            const uint32_t o = sc + 6 * rn;
+            aux[o] = rlu(id, k) & ~MTB_LEAF;
+            aux[o + 1] = b;
+            aux[o + 2] = (uint32_t)k;
+            aux[o + 3] = (rr ? 1u : 0u) | (rseq >= 0 ? 2u : 0u);
+            aux[o + 4] = (uint32_t)(seq >= MTB_PEND ? seq - MTB_PEND : -1);
+            aux[o + 5] = (uint32_t)(rseq >= MTB_PEND ? rseq - MTB_PEND : -1);
+          }
+          wsync();
+          rn++;
+        } else {
+          flush();
+        }
+      }
+    });
+    flush();
+    aux_used = save;  // (the scratch is released; the rebuilds allocate list entries, not aux words)
+    view_clear();
+  }
+  // Client.regeneratePendingOp (client.ts:917-960) / resetPendingDeltaToOps (:708-800) for the n groups at
+  // the head of the FIFO (one per member op): each group's segments in tree order, each one's position in
+  // the local view after the group's localSeq (findReconnectionPosition), an entry per regenerated op and a
+  // new one-segment group for it at the FIFO's tail
+  __device__ __forceinline__ void regen(uint32_t n) {
+    if (curSeq != (int)U(ds->last_norm)) {
+      normalize();
+      if (bad()) return;
+      if (lane == 0) ds->last_norm = curSeq;
+      wsync();
+    }
+    for (uint32_t g = 0; g < n && !err; g++) {
+      if (pend_n == 0) { fail(DERR_REGEN); return; }
+      const auto e = grp_ent(0);
+      const int L = (int)U(e[0]);
+      const uint32_t off = U(e[1]), cnt = U(e[2]), type = U(e[4]), props = U(e[5]);
+      pend_head = (pend_head + 1) % MTB_PEND_GROUPS;
+      pend_n--;
+      if (type == MTB_OP_ANNOTATE) {
+        if (lane == 0) ds->pend_ann = ds->pend_ann - 1;
+        wsync();
+      }
+      if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
+      int pos = 0;
+      uint32_t found = 0;
+      each_leaf_block([&](uint32_t b) {
+        const uint32_t* r = bw(b);
+        const int bc = (int)U(r[FB_HDR]);
+        uint32_t id = MTB_NONE;
+        int l = 0, sq = 0, rs = -1;
+        if (lane < bc) {
+          id = r[F_ID * 8 + lane];
+          sq = (int)r[F_SEQ * 8 + lane];
+          rs = (int)r[F_RSEQ * 8 + lane];
+          l = len_at((int)r[F_LEN * 8 + lane], sq, rs, L);
+        }
+        const int excl = cscan8(l) - l;
+        unsigned mm = 0;  // slots of this block holding group members
+        for (uint32_t q = 0; q < cnt; q += 64) {
+          const uint32_t m = q + lane < cnt ? aux[off + q + lane] : MTB_NONE;
+          for (int k = 0; k < bc; k++)
+            if (__ballot(m == (rlu(id, k) & ~MTB_LEAF))) mm |= 1u << k;
+        }
+        while (mm && !err) {
+          const int k = __ffs(mm) - 1;
+          mm &= mm - 1;
+          found++;
+          const uint32_t sid = rlu(id, k) & ~MTB_LEAF;
+          const int sqk = rl(sq, k), rsk = rl(rs, k);
+          bool emit;
+          if (type == MTB_OP_INSERT) {
+            if (sqk < MTB_PEND) { fail(DERR_ACK_INSERT); return; }  // 0x037
+            emit = true;
+          } else if (type == MTB_OP_REMOVE) {
+            emit = rsk >= MTB_PEND;
+          } else {
+            emit = rsk < 0 || rsk >= MTB_PEND;
+          }
+          if (emit) {
+            if (delta_used + 1 > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+            if (lane == 0) {
+              const auto o = dslice() + 4 * delta_used;
+              o[0] = cur_k;
+              o[1] = type | (g << 8);
+              o[2] = sid;
+              o[3] = (uint32_t)(pos + rl(excl, k));
+            }
+            wsync();
+            delta_used++;
+            grp_new((uint32_t)L, type, props, sid);
+          } else if (type == MTB_OP_ANNOTATE) {
+            orphan_add(props, sid);
+          }
+        }
+        pos += rl(cscan8(l), 7);
+      });
+      if (!err && found != cnt) { fail(DERR_REGEN); return; }
     }
     view_clear();
   }
@@ -1917,7 +2282,7 @@ struct Eng {
           gm &= gm - 1;
           grp_add(rlu(id, t) & ~MTB_LEAF, MTB_OP_ANNOTATE, opId);
         }
-      } else if (isLive && COLD(U(ds->pend_ann) != 0)) {
+      } else if (isLive && COLD((U(ds->pend_ann) | U(ds->orphans)) != 0)) {
         // a remote annotate leaves the keys of pending local annotates alone (shouldModifyKey,
         // segmentPropertiesManager.ts:95-106): segments holding pending keys get their own edit
         unsigned long long xm = vm;
@@ -2969,6 +3334,9 @@ struct Eng {
       case MTB_OP_ACK:
         if (isLive) ack_group(S, (int)o.pos2);
         zamboni_p();
+        break;
+      case MTB_OP_REGEN:
+        if constexpr (isLive) regen(o.pos1);
         break;
       default:
         break;

@@ -64,6 +64,7 @@ export declare class Client {
   applyLocalOp(op: Record<string, unknown> | string): unknown;
   insertSegmentLocal(pos: number, seg: unknown): Record<string, unknown>;
   removeRangeLocal(start: number, end: number): Record<string, unknown>;
+  regeneratePendingOp(resetOp: Record<string, unknown> | string, segmentGroup?: unknown): Record<string, unknown>;
   annotateRangeLocal(start: number, end: number, props: Record<string, unknown>, combiningOp?: unknown): Record<string, unknown>;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   load(runtime: { clientId?: string } | undefined,

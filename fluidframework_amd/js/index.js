@@ -209,6 +209,15 @@ class Client {
     return this.applyLocalOp({ pos1: start, pos2: end, type: 1 });
   }
 
+  /** Client.regeneratePendingOp (client.ts:917-960): the op to resubmit after a reconnect for the oldest
+   * pending op `resetOp` (the batch is flushed first). */
+  regeneratePendingOp(resetOp, segmentGroup) {
+    this.batch.checkIdle();
+    const out = native.regeneratePendingOp(this.batch.handle, this.doc, typeof resetOp === "string" ? resetOp : JSON.stringify(resetOp));
+    this.batch.dirty = false;
+    return JSON.parse(out);
+  }
+
   /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
   annotateRangeLocal(start, end, props, combiningOp) {
     if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");

@@ -293,6 +293,28 @@ static napi_value js_local_op(napi_env env, napi_callback_info info) {
   return undef(env);
 }
 
+/* regeneratePendingOp(h, doc, JSON.stringify(resetOp)) -> JSON of the op(s) to resubmit   client.ts:917-960 */
+static napi_value js_regenerate(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc;
+  if (!b || !get_u32(env, argv[1], &doc)) return NULL;
+  size_t n = 0;
+  char* s = get_utf8(env, argv[2], &n);
+  if (!s) return NULL;
+  char* out = NULL;
+  size_t on = 0;
+  int rc = mtb_regenerate_pending_op(b, doc, s, n, &out, &on);
+  free(s);
+  if (rc) return throw_rc(env, b, rc);
+  napi_value r;
+  napi_status ok = napi_create_string_utf8(env, out, on, &r);
+  mtb_free(out);
+  CHECK_NAPI(env, ok);
+  return r;
+}
+
 /* appendOps(h, doc, records: Uint8Array (32 B each), payload: Uint16Array) */
 static napi_value js_append_ops(napi_env env, napi_callback_info info) {
   napi_value argv[4];
@@ -742,7 +764,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"replay", js_replay},           {"replayAsync", js_replay_async},
       {"getText", js_get_text},        {"getLength", js_get_length},
       {"getSeq", js_get_seq},          {"dumpSegments", js_dump_segments},
-      {"mapRange", js_map_range},
+      {"mapRange", js_map_range},      {"regeneratePendingOp", js_regenerate},
       {"checksum", js_checksum},       {"summarizeV1", js_summarize_v1},
       {"rewind", js_rewind},           {"replayResident", js_replay_resident},
       {"clientLongId", js_client_long_id},

@@ -160,6 +160,13 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
  * leave them alone, segmentPropertiesManager.ts:60-157).  Local rewrite annotates, marker-relative
  * positions, matrix and catch-up batches are MTB_E_UNSUPPORTED. */
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
+/* Client.regeneratePendingOp (client.ts:917-960) after a reconnect: `op_json` is the live client's oldest
+ * pending op (as submitted; a GROUP names one pending op per member).  Replays the batch, then on the GPU
+ * normalizes the segment order around pending segments (normalizeSegmentsOnRebase, mergeTree.ts:2357-2390)
+ * when currentSeq moved, pops the op's segment groups and computes each segment's position in the local view
+ * at the group's localSeq (findReconnectionPosition); *out = the op(s) to resubmit (JSON, a GROUP when
+ * several; free with mtb_free), whose new segment groups are queued for their acks. */
+int mtb_regenerate_pending_op(mtb_batch* b, uint32_t doc, const char* op_json, size_t len, char** out, size_t* out_len);
 /* Pre-packed path: append records whose `payload` offsets index `payload` (UTF-16 units). */
 int mtb_append_ops(mtb_batch* b, uint32_t doc, const mtb_op* ops, uint32_t n,
                    const uint16_t* payload, size_t payload_len);

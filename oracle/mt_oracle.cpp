@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cassert>
 #include <functional>
+#include <unordered_map>
 
 namespace orc {
 
@@ -1552,6 +1553,201 @@ std::string Doc::annotateLocalOp(int start, int end, const JObj& props) {
   pv.obj = props;
   return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"props\":" + json_stringify(pv) +
          ",\"type\":2}";
+}
+
+// ---------------------------------------------------------------- reconnect
+// localNetLength with a localSeq (mergeTree.ts:636-664): the local view as it was right after local op
+// `localSeq` (later local ops and remote ops above refSeq hidden)
+int MergeTree::localNetLengthAt(const Seg* s, int refSeq, int localSeq) const {
+  const bool lremoved = s->localRemovedSeq != INT32_MIN && s->localRemovedSeq <= localSeq;
+  if (s->seq != UnassignedSeq) {
+    if (s->seq > refSeq || (s->removed && s->removedSeq != UnassignedSeq && s->removedSeq <= refSeq) || lremoved) return 0;
+    return s->cachedLength;
+  }
+  if (s->localSeq == INT32_MIN) fail_assert("0x39a", "unacked segment with undefined localSeq");
+  if (s->localSeq > localSeq || lremoved) return 0;
+  return s->cachedLength;
+}
+// findReconnectionPosition (client.ts:690-706) -> getPosition(segment, currentSeq, clientId, localSeq)
+// (mergeTree.ts:768-785): block lengths come from the local partials (computeLocalPartials), which sum
+// the leaves' localNetLength(leaf, refSeq, localSeq)
+int MergeTree::reconnectPosition(Seg* s, int localSeq) {
+  if (localSeq > window.localSeq) fail_assert("0x032", "localSeq greater than collab window");
+  const int refSeq = window.currentSeq;
+  std::function<int(Node*)> len = [&](Node* n) -> int {
+    if (n->leaf) return localNetLengthAt(static_cast<Seg*>(n), refSeq, localSeq);
+    Block* b = static_cast<Block*>(n);
+    int t = 0;
+    for (int i = 0; i < b->childCount; i++) t += len(b->children[i]);
+    return t;
+  };
+  int total = 0;
+  Node* node = s;
+  for (Block* parent = s->parent; parent; node = parent, parent = parent->parent)
+    for (int i = 0; i < parent->childCount && parent->children[i] != node; i++) total += len(parent->children[i]);
+  return total;
+}
+static bool isRemovedAndAcked(const Seg* s) { return s->removed && s->removedSeq != UnassignedSeq; }
+// normalizeAdjacentSegments (mergeTree.ts:2234-2336): in a run of removed / unacked segments, remotely
+// removed (acked) segments slide after the last locally affected one, and each locally removed one slides
+// forward past later unacked inserts made after its removal; the run's slots keep their places
+void MergeTree::normalizeAdjacentSegments(std::vector<Seg*>& run) {
+  struct Slot { Block* parent; int index; };
+  std::vector<Slot> order;
+  for (Seg* s : run) order.push_back({s->parent, s->index});
+  std::vector<Seg*> list(run);  // the affected-segments List, as an array
+  int last = (int)list.size() - 1;
+  while (last >= 0 && isRemovedAndAcked(list[last])) last--;
+  if (last < 0) return;
+  Seg* lastLocal = list[last];
+  auto indexOf = [&](Seg* x) { return (int)(std::find(list.begin(), list.end(), x) - list.begin()); };
+  Seg* toSlide = lastLocal;
+  Seg* nearer = last > 0 ? list[last - 1] : nullptr;
+  while (toSlide) {
+    if (isRemovedAndAcked(toSlide)) {
+      list.erase(list.begin() + indexOf(toSlide));
+      list.insert(list.begin() + indexOf(lastLocal) + 1, toSlide);
+    } else if (toSlide->removed) {
+      if (toSlide->localRemovedSeq == INT32_MIN)
+        fail_assert("0x54d", "Removed segment that hasnt had its removal acked should be locally removed");
+      int cur = indexOf(toSlide);
+      int scan = cur + 1;
+      while (scan < (int)list.size() && !isRemovedAndAcked(list[scan]) && list[scan]->localSeq != INT32_MIN &&
+             list[scan]->localSeq > toSlide->localRemovedSeq) {
+        cur = scan;
+        scan++;
+      }
+      if (list[cur] != toSlide) {
+        Seg* after = list[cur];
+        list.erase(list.begin() + indexOf(toSlide));
+        list.insert(list.begin() + indexOf(after) + 1, toSlide);
+      }
+    }
+    toSlide = nearer;
+    if (nearer) {
+      const int ni = indexOf(nearer);
+      nearer = ni > 0 ? list[ni - 1] : nullptr;
+    }
+  }
+  for (size_t i = 0; i < list.size(); i++) order[i].parent->assignChild(list[i], order[i].index);
+  // ancestors of the moved segments, deepest first (nodeUpdateLengthNewStructure)
+  std::vector<std::pair<int, Block*>> blocks;
+  for (Seg* sg : list)
+    for (Block* b = sg->parent; b; b = b->parent) {
+      int depth = 0;
+      for (Block* x = b->parent; x; x = x->parent) depth++;
+      bool seen = false;
+      for (auto& e : blocks) seen |= e.second == b;
+      if (!seen) blocks.push_back({depth, b});
+    }
+  std::stable_sort(blocks.begin(), blocks.end(), [](auto& a, auto& b) { return a.first > b.first; });
+  for (auto& e : blocks) nodeUpdateLengthNewStructure(e.second, false);
+}
+// normalizeSegmentsOnRebase (mergeTree.ts:2357-2390)
+void MergeTree::normalizeSegmentsOnRebase() {
+  std::vector<Seg*> run;
+  bool hasLocal = false, hasRemoteRemoved = false;
+  std::vector<std::vector<Seg*>> todo;
+  auto flush = [&] {
+    if (hasLocal && hasRemoteRemoved && run.size() > 1) todo.push_back(run);
+    run.clear();
+    hasLocal = hasRemoteRemoved = false;
+  };
+  walkAllSegments([&](Seg* s) {
+    if (s->removed || s->seq == UnassignedSeq) {
+      if (isRemovedAndAcked(s)) hasRemoteRemoved = true;
+      if (s->seq == UnassignedSeq) hasLocal = true;
+      run.push_back(s);
+    } else {
+      flush();
+    }
+  });
+  flush();
+  // (the runs are disjoint and normalizing one moves only its own segments among its own slots)
+  for (auto& r : todo) normalizeAdjacentSegments(r);
+}
+
+// Client.regeneratePendingOp (client.ts:917-960) with resetPendingDeltaToOps (:708-800)
+std::string Doc::regeneratePendingOp(const JVal& op) {
+  if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
+  const int rebaseTo = mt.window.currentSeq;
+  if (rebaseTo != lastNormalizationRefSeq) {
+    mt.normalizeSegmentsOnRebase();
+    lastNormalizationRefSeq = rebaseTo;
+  }
+  std::vector<const JVal*> members;
+  const JVal* type = obj_get(op.obj, u"type");
+  if (type && type->t == JVal::Num && (int)type->num == 3) {
+    const JVal* ops = obj_get(op.obj, u"ops");
+    if (ops && ops->t == JVal::Arr)
+      for (auto& m : ops->arr) members.push_back(&m);
+  } else {
+    members.push_back(&op);
+  }
+  std::vector<JVal> opList;
+  for (const JVal* resetOp : members) {
+    if (mt.pendingSegments.empty()) fail_assert("0x033", "Segment group undefined");
+    SegGroup* group = mt.pendingSegments.front();
+    mt.pendingSegments.pop_front();
+    // the group's segments in tree order (ordinal)
+    std::unordered_map<const Seg*, size_t> ord;
+    mt.walkAllSegments([&](Seg* s) { ord.emplace(s, ord.size()); });
+    std::vector<Seg*> segs = group->segments;
+    std::stable_sort(segs.begin(), segs.end(), [&](Seg* a, Seg* b) { return ord.at(a) < ord.at(b); });
+    const JVal* rt = obj_get(resetOp->obj, u"type");
+    const int t = rt && rt->t == JVal::Num ? (int)rt->num : -1;
+    for (Seg* s : segs) {
+      if (s->groups.empty() || s->groups.front() != group) fail_assert("0x035", "Segment group not at head of segment pending queue");
+      s->groups.erase(s->groups.begin());
+      const int pos = mt.reconnectPosition(s, group->localSeq);
+      JVal newOp;
+      bool have = false;
+      if (t == 2) {
+        if (!s->removed || (s->localRemovedSeq != INT32_MIN && s->removedSeq == UnassignedSeq)) {
+          newOp = jop({{u"pos1", JVal::number(pos)}, {u"pos2", JVal::number(pos + s->cachedLength)}});
+          const JVal* pr = obj_get(resetOp->obj, u"props");
+          if (pr) newOp.obj.push_back({u"props", *pr});
+          newOp.obj.push_back({u"type", JVal::number(2)});
+          have = true;
+        }
+      } else if (t == 0) {
+        if (s->seq != UnassignedSeq) fail_assert("0x037", "Segment already has assigned sequence number");
+        JVal segj = segJson(s);
+        const JVal* rseg = obj_get(resetOp->obj, u"seg");
+        const JVal* rprops = rseg && rseg->t == JVal::Obj ? obj_get(rseg->obj, u"props") : nullptr;
+        if (rprops && rprops->t != JVal::Undef) {  // segment.clone() with properties = resetOp.seg.props
+          Seg c = *s;
+          c.groups.clear();
+          c.props = rprops->t == JVal::Obj ? std::optional<JObj>(rprops->obj) : std::nullopt;
+          segj = segJson(&c);
+        }
+        newOp = jop({{u"pos1", JVal::number(pos)}, {u"seg", segj}, {u"type", JVal::number(0)}});
+        have = true;
+      } else if (t == 1) {
+        if (s->localRemovedSeq != INT32_MIN && s->removedSeq == UnassignedSeq) {
+          newOp = jop({{u"pos1", JVal::number(pos)}, {u"pos2", JVal::number(pos + s->cachedLength)}, {u"type", JVal::number(1)}});
+          have = true;
+        }
+      } else {
+        throw OracleError(-8, "Invalid op type");
+      }
+      if (have) {
+        mt.groupPool.push_back(std::make_unique<SegGroup>());
+        SegGroup* g = mt.groupPool.back().get();
+        g->localSeq = group->localSeq;
+        g->refSeq = mt.window.currentSeq;
+        g->segments.push_back(s);
+        s->groups.push_back(g);
+        mt.pendingSegments.push_back(g);
+        opList.push_back(std::move(newOp));
+      }
+    }
+  }
+  if (opList.size() == 1) return json_stringify(opList[0]);
+  JVal arr;
+  arr.t = JVal::Arr;
+  arr.arr = std::move(opList);
+  return json_stringify(jop({{u"ops", arr}, {u"type", JVal::number(3)}}));
 }
 
 // ---------------------------------------------------------------- local (detached) edits

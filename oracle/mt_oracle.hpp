@@ -206,6 +206,15 @@ class MergeTree {
   static std::optional<std::string> markerId(const Seg* s);  // Marker.getId (mergeTreeNodes.ts:612-617)
   // posFromRelativePos (mergeTree.ts:1371-1395): -1 when the id names no marker
   int posFromRelativePos(const JVal& rel, int refSeq, int clientId);
+  // ---- reconnect (client.ts:690-800, 917-960; mergeTree.ts:2234-2390)
+  // localNetLength(segment, refSeq, localSeq) with a localSeq (mergeTree.ts:613-665)
+  int localNetLengthAt(const Seg* s, int refSeq, int localSeq) const;
+  // findReconnectionPosition (client.ts:690-706): getPosition(segment, currentSeq, clientId, localSeq), the
+  // local view without the pending ops after localSeq, as the sum over the leaves before the segment
+  int reconnectPosition(Seg* s, int localSeq);
+  // normalizeSegmentsOnRebase (mergeTree.ts:2357-2390) / normalizeAdjacentSegments (:2234-2336)
+  void normalizeSegmentsOnRebase();
+  void normalizeAdjacentSegments(std::vector<Seg*>& run);
   void boundary(int pos, int refSeq, int clientId) { ensureIntervalBoundary(pos, refSeq, clientId); }
   // mapRange(action, refSeq, clientId) over the whole tree (mergeTree.ts mapRange -> nodeMap)
   void mapAll(int refSeq, int clientId, const std::function<void(Seg*)>& f);
@@ -275,6 +284,10 @@ class Doc {
   std::string insertLocalOp(int pos, const JVal& segSpec);
   std::string removeLocalOp(int start, int end);
   std::string annotateLocalOp(int start, int end, const JObj& props);
+  // Client.regeneratePendingOp (client.ts:917-960) for the op at the head of the pending queue (one segment
+  // group per member op): the op(s) to resubmit after a reconnect, as JSON
+  std::string regeneratePendingOp(const JVal& op);
+  int lastNormalizationRefSeq = 0;
   // local, non-collaborating edits (detached documents; used for the V1 snapshot fixtures)
   void insertTextLocal(int pos, const u16str& text, const std::optional<JObj>& props);
   void insertMarkerLocal(int pos, int refType, const std::optional<JObj>& props);

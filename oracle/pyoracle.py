@@ -79,6 +79,7 @@ def lib():
         L.orc_local_remove.argtypes = [vp, i, i, pp, ctypes.POINTER(sz)]
         L.orc_local_annotate.argtypes = [vp, i, i, cp, pp, ctypes.POINTER(sz)]
         L.orc_pending_groups.argtypes = [vp]
+        L.orc_regenerate.argtypes = [vp, cp, pp, ctypes.POINTER(sz)]
         L.orc_map_range.argtypes = [vp, i, i, i, cp, ctypes.c_uint, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.orc_sa2d_create.restype = vp
         L.orc_sa2d_destroy.argtypes = [vp]
@@ -220,6 +221,10 @@ class OracleDoc:
 
     def annotate_local_op(self, start, end, props):
         return self._op(self._L.orc_local_annotate, start, end, json.dumps(props).encode())
+
+    def regenerate_pending_op(self, op):
+        """Client.regeneratePendingOp (client.ts:917-960) for the op at the head of the pending queue."""
+        return self._op(self._L.orc_regenerate, json.dumps(op).encode())
 
     def pending_groups(self):
         return self._L.orc_pending_groups(self._h)

@@ -182,12 +182,15 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
 
 
 def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
-                   record=None):
+                   record=None, reconnect=0.0):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
     receives the sequenced stream with its own lag (its own ops come back as acks).  An observer receives
-    everything.  Returns (clients, observer, sequenced messages)."""
+    everything.  With `reconnect` > 0 a client disconnects (probability per round) in the style of
+    client.reconnectFarm.spec.ts: its ops still in the sequencer's queue are dropped, it catches up on the
+    sequenced stream, then regenerates each dropped op (Client.regeneratePendingOp, client.ts:917-960) and
+    resubmits the result at its current seq.  Returns (clients, observer, sequenced messages)."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -248,6 +251,18 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     for _ in range(n_rounds):
         if rounds is not None:
             rounds.append([[] for _ in range(n_clients)])
+        if reconnect and rng.random() < reconnect:
+            k = rng.randrange(n_clients)
+            dropped = [q for q in queue if q[0] == ids[k]]
+            queue[:] = [q for q in queue if q[0] != ids[k]]
+            deliver(k, len(log))
+            n_groups = sum(len(op["ops"]) if op.get("type") == 3 else 1 for (_, _, op) in dropped)
+            assert clients[k].pending_groups() == n_groups, (clients[k].pending_groups(), n_groups)
+            for (_, _, op) in dropped:
+                new = clients[k].regenerate_pending_op(op)
+                if rounds is not None:
+                    rounds[-1][k].append(("regen", (op, new)))
+                queue.append((ids[k], clients[k].current_seq, new))
         for k in rng.sample(range(n_clients), rng.randint(1, n_clients)):
             for _ in range(rng.randint(1, 3)):
                 ref = clients[k].current_seq
@@ -279,8 +294,9 @@ def chars_with_props(doc):
     out = []
     for e in doc.map_range():
         s = e["segment"]
-        t = s.get("text", "￼")
-        out.extend((ch, json.dumps(s.get("properties"), sort_keys=True)) for ch in t)
+        t = s.get("text", "￼").encode("utf-16-le", "surrogatepass")  # per UTF-16 code unit (a split may cut a pair)
+        p = json.dumps(s.get("properties"), sort_keys=True)
+        out.extend((t[i:i + 2], p) for i in range(0, len(t), 2))
     return out
 
 

@@ -15,10 +15,12 @@ from helpers import run_local_farm
 pytestmark = pytest.mark.gpu
 
 
-def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False):
+def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False, reconnect=0.0):
+    import json
     from fluidframework_amd import MergeTreeBatch
     rec = {}
-    run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=annotate, record=rec)
+    run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=annotate, record=rec,
+                   reconnect=reconnect)
     ids = rec["ids"]
     B = MergeTreeBatch(n_clients, new_length_calc=new_mode)
     for k, cid in enumerate(ids):
@@ -30,6 +32,10 @@ def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annot
             for kind, x in events:
                 if kind == "local":
                     B[k].applyLocalOp(x)
+                elif kind == "regen":  # the engine regenerates the same op(s), key order included
+                    op, want = x
+                    got = B[k].regeneratePendingOp(op)
+                    assert json.dumps(got) == json.dumps(want), f"seed {seed} round {r} client {k}: regenerated op"
                 else:
                     B[k].applyMsg(x)
         if (r + 1) % rounds_per_replay and r + 1 < len(rec["rounds"]):
@@ -76,6 +82,21 @@ def test_local_annotate_farm_new_length_calc(seed):
 def test_local_annotate_farm_batched_rounds(seed):
     assert _replay_farm(seed, n_clients=8, n_rounds=120, new_mode=seed % 2 == 0, rounds_per_replay=10,
                         annotate=True) > 0
+
+
+@pytest.mark.parametrize("seed", list(range(71, 87)))
+def test_reconnect_farm(seed):
+    """Reconnects (client.reconnectFarm.spec.ts): a client's unsequenced ops are dropped, it catches up, and
+    regeneratePendingOp on the engine gives the oracle's ops (normalizeSegmentsOnRebase, positions at each
+    group's localSeq, new pending groups); states stay equal to the oracle clients' after every round."""
+    assert _replay_farm(seed, n_clients=3 + seed % 4, n_rounds=50, new_mode=seed % 2 == 0, annotate=True,
+                        reconnect=0.35) > 0
+
+
+@pytest.mark.parametrize("seed", [92, 93, 94, 95])
+def test_reconnect_farm_batched_rounds(seed):
+    assert _replay_farm(seed, n_clients=6, n_rounds=100, new_mode=seed % 2 == 0, rounds_per_replay=5, annotate=True,
+                        reconnect=0.25) > 0
 
 
 def test_pending_local_key_survives_a_remote_annotate():
