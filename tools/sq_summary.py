@@ -25,7 +25,7 @@ def main():
            "totals": dict(tot), "per_op": per_op}
     if tot.get("SQ_WAVE_CYCLES"):
         res["wait_any_frac"] = tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"]
-        res["issue_frac"] = tot.get("SQ_WAIT_INST_ANY", 0) / tot["SQ_WAVE_CYCLES"]
+        res["issue_frac"] = tot.get("SQ_ACTIVE_INST_ANY", 0) / tot["SQ_WAVE_CYCLES"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: round(v, 1) for k, v in per_op.items()}))
 
