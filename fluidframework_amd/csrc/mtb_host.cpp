@@ -2709,6 +2709,15 @@ int mtbx_regenerate_pending_op(mtb_dev* b, uint32_t doc, const char* json, size_
     }
     std::vector<std::string> ops;
     if (!members.empty()) {
+      // flush the batch first, so that an error of another document (reported by the replay that hits it)
+      // surfaces here before anything is regenerated; the REGEN record then runs alone
+      bool pendingWork = false;
+      for (uint32_t i = 0; i < b->ndocs && !pendingWork; i++) pendingWork = !b->docs[i].pending.empty();
+      if (pendingWork || !b->devInit) {
+        mtb_stats st0{};
+        replay(b, &st0);
+      }
+      if (b->hst[doc].err) raise(derr_code(b->hst[doc].err), derr_text(b->hst[doc].err));
       mtb_op r{};
       r.type = MTB_OP_REGEN;
       r.pos1 = (uint32_t)members.size();
