@@ -381,6 +381,14 @@ class Client:
         finally:
             L.mtb_free(p)
 
+    def annotateMarker(self, markerId, props, combiningOp=None):
+        """Client.annotateMarker (client.ts:190-197, createAnnotateMarkerOp opBuilder.ts:25-43) for the marker
+        carrying `markerId`: a local annotate with marker-relative positions; returns the op to send."""
+        if combiningOp is not None:
+            raise MergeTreeError(-6, "unsupported: local annotate with a combiningOp")
+        return self.applyLocalOp({"props": props, "relativePos1": {"id": markerId, "before": True},
+                                  "relativePos2": {"id": markerId}, "type": 2})
+
     def annotateRangeLocal(self, start, end, props, combiningOp=None):
         """annotateRangeLocal (client.ts:206): the keys stay pending on the annotated segments until the
         op's ack; returns the IMergeTreeAnnotateMsg to send."""

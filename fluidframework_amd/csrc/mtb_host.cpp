@@ -535,7 +535,7 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, H
   if (v && v->kind == hj::Value::kNum) return (uint32_t)v->n;
   const hj::Value* rp = member(op, rel);
   if (rp && rp->truthy()) {
-    if (!d) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions here (local ops, catch-up or matrix batches)");
+    if (!d) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions here (catch-up or matrix batches)");
     if (rp->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: relative position is not an object");
     auto key = marker_key(member(*rp, u"id"));
     if (!key) raise(MTB_E_UNSUPPORTED, "unsupported: relative position without a marker id (posFromRelativePos -1)");
@@ -569,7 +569,7 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
   const int type = t && t->kind == hj::Value::kNum ? (int)t->n : -1;
   mtb_op r = base;
   // relative positions: observer replay in plain SharedString batches
-  HostDoc* rel = (b->matrix || (b->opts.flags & MTB_BATCH_CATCHUP) || (base.flags & MTB_F_LOCAL)) ? nullptr : &d;
+  HostDoc* rel = (b->matrix || (b->opts.flags & MTB_BATCH_CATCHUP)) ? nullptr : &d;
   if (type == 0) {
     r.pos1 = position(op, u"pos1", u"relativePos1", rel, &r);
     const hj::Value* seg = member(op, u"seg");

@@ -3191,9 +3191,20 @@ struct Eng {
   // A live client's own op (client.ts:196-247 insertSegmentLocal / removeRangeLocal): applied in its own
   // view at (currentSeq, own id) with UnassignedSequenceNumber (here MTB_PEND + the new localSeq), after
   // getValidOpRange's bounds check (client.ts:527-592); no LRU, no zamboni, no sequence-number update.
-  __device__ __forceinline__ void apply_local(const mtb_op& o) {
+  __device__ __forceinline__ void apply_local(const mtb_op& oin) {
     grp_open = false;
     const int len = (int)U(blk[root].len);  // the local view's length
+    mtb_op o = oin;
+    if (COLD(o.flags & MTB_F_RELPOS)) {  // getValidOpRange in the client's own view (Client.annotateMarker)
+      view_clear();
+      const int p1 = rel_pos(o.pos1, curSeq, 0);
+      const int p2 = o.type == MTB_OP_INSERT ? 0 : rel_pos(o.pos2, curSeq, 0);
+      if (err == DERR_RELPOS) err = DERR_RANGE;  // an unknown marker is -1: RangeOutOfBounds
+      if (bad()) return;
+      o.pos1 = (uint32_t)p1;
+      if (o.type != MTB_OP_INSERT) o.pos2 = (uint32_t)p2;
+      o.flags &= (uint8_t)~MTB_F_RELPOS;
+    }
     if (o.type == MTB_OP_INSERT) {
       if ((int)o.pos1 < 0 || (int)o.pos1 > len) { fail(DERR_RANGE); return; }
     } else if (o.type == MTB_OP_REMOVE || (o.type == MTB_OP_ANNOTATE && !(o.flags & MTB_F_REWRITE))) {

@@ -66,6 +66,7 @@ export declare class Client {
   removeRangeLocal(start: number, end: number): Record<string, unknown>;
   regeneratePendingOp(resetOp: Record<string, unknown> | string, segmentGroup?: unknown): Record<string, unknown>;
   annotateRangeLocal(start: number, end: number, props: Record<string, unknown>, combiningOp?: unknown): Record<string, unknown>;
+  annotateMarker(markerId: string, props: Record<string, unknown>, combiningOp?: unknown): Record<string, unknown>;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   load(runtime: { clientId?: string } | undefined,
        storage: { readBlob(path: string): Promise<ArrayBufferLike | Uint8Array | string> }): Promise<{ catchupOpsP: Promise<unknown[]> }>;

@@ -218,6 +218,12 @@ class Client {
     return JSON.parse(out);
   }
 
+  /** Client.annotateMarker (client.ts:190) for the marker carrying `markerId`: returns the op to send. */
+  annotateMarker(markerId, props, combiningOp) {
+    if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");
+    return this.applyLocalOp({ props, relativePos1: { id: markerId, before: true }, relativePos2: { id: markerId }, type: 2 });
+  }
+
   /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
   annotateRangeLocal(start, end, props, combiningOp) {
     if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");

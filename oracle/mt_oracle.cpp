@@ -1555,6 +1555,38 @@ std::string Doc::annotateLocalOp(int start, int end, const JObj& props) {
          ",\"type\":2}";
 }
 
+std::string Doc::localOpJson(const JVal& op) {
+  if (op.t != JVal::Obj) throw OracleError(-8, "op is not an object");
+  const JVal* t = obj_get(op.obj, u"type");
+  const int type = t && t->t == JVal::Num ? (int)t->num : -1;
+  const int refSeq = mt.window.currentSeq, client = mt.window.clientId;
+  auto pos = [&](const char16_t* k, const char16_t* rk, bool opt) -> int {
+    const JVal* p = obj_get(op.obj, k);
+    if (p && p->t == JVal::Num) return (int)p->num;
+    const JVal* r = obj_get(op.obj, rk);
+    if (r && !js_falsy(r)) return mt.posFromRelativePos(*r, refSeq, client);  // -1 fails the range check
+    if (opt) return INT32_MIN;
+    throw OracleError(-1, "RangeOutOfBounds");
+  };
+  const bool rel = obj_get(op.obj, u"relativePos1") || obj_get(op.obj, u"relativePos2");
+  std::string out;
+  if (type == 0) {
+    const JVal* seg = obj_get(op.obj, u"seg");
+    if (!seg) throw OracleError(-8, "insert without seg");
+    out = insertLocalOp(pos(u"pos1", u"relativePos1", false), *seg);
+  } else if (type == 1) {
+    out = removeLocalOp(pos(u"pos1", u"relativePos1", false), pos(u"pos2", u"relativePos2", false));
+  } else if (type == 2) {
+    const JVal* pr = obj_get(op.obj, u"props");
+    if (obj_get(op.obj, u"combiningOp")) fail_unsupported("local annotate with a combiningOp");
+    out = annotateLocalOp(pos(u"pos1", u"relativePos1", false), pos(u"pos2", u"relativePos2", false),
+                          pr && pr->t == JVal::Obj ? pr->obj : JObj());
+  } else {
+    throw OracleError(-8, "unsupported local op type");
+  }
+  return rel ? json_stringify(op) : out;
+}
+
 // ---------------------------------------------------------------- reconnect
 // localNetLength with a localSeq (mergeTree.ts:636-664): the local view as it was right after local op
 // `localSeq` (later local ops and remote ops above refSeq hidden)

@@ -284,6 +284,10 @@ class Doc {
   std::string insertLocalOp(int pos, const JVal& segSpec);
   std::string removeLocalOp(int start, int end);
   std::string annotateLocalOp(int start, int end, const JObj& props);
+  // a live client's local op given as the IMergeTreeOp JSON it sends (pos1 / pos2 or marker-relative
+  // relativePos1 / relativePos2, resolved in the local view by getValidOpRange, client.ts:527-547); returns
+  // the op to send (the input itself when it names relative positions, as Client.annotateMarker does)
+  std::string localOpJson(const JVal& op);
   // Client.regeneratePendingOp (client.ts:917-960) for the op at the head of the pending queue (one segment
   // group per member op): the op(s) to resubmit after a reconnect, as JSON
   std::string regeneratePendingOp(const JVal& op);

@@ -235,6 +235,9 @@ int orc_local_annotate(orc_doc* d, int start, int end, const char* props_json, c
   });
 }
 int orc_pending_groups(orc_doc* d) { return (int)d->doc.mt.pendingSegments.size(); }
+int orc_local_op_json(orc_doc* d, const char* op_json, char** out, size_t* len) {
+  return guard(d, [&] { *out = dupstr(d->doc.localOpJson(json_parse(op_json, strlen(op_json))), len); });
+}
 // Client.regeneratePendingOp (client.ts:917-960) for the op at the head of the pending queue
 int orc_regenerate(orc_doc* d, const char* op_json, char** out, size_t* len) {
   return guard(d, [&] { *out = dupstr(d->doc.regeneratePendingOp(json_parse(op_json, strlen(op_json))), len); });

@@ -80,6 +80,7 @@ def lib():
         L.orc_local_annotate.argtypes = [vp, i, i, cp, pp, ctypes.POINTER(sz)]
         L.orc_pending_groups.argtypes = [vp]
         L.orc_regenerate.argtypes = [vp, cp, pp, ctypes.POINTER(sz)]
+        L.orc_local_op_json.argtypes = [vp, cp, pp, ctypes.POINTER(sz)]
         L.orc_map_range.argtypes = [vp, i, i, i, cp, ctypes.c_uint, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.orc_sa2d_create.restype = vp
         L.orc_sa2d_destroy.argtypes = [vp]
@@ -221,6 +222,10 @@ class OracleDoc:
 
     def annotate_local_op(self, start, end, props):
         return self._op(self._L.orc_local_annotate, start, end, json.dumps(props).encode())
+
+    def local_op_json(self, op):
+        """A live client's local op given as the IMergeTreeOp it sends (absolute or marker-relative positions)."""
+        return self._op(self._L.orc_local_op_json, json.dumps(op).encode())
 
     def regenerate_pending_op(self, op):
         """Client.regeneratePendingOp (client.ts:917-960) for the op at the head of the pending queue."""

@@ -158,3 +158,48 @@ def test_relative_positions_in_a_live_client_batch():
         B[0].applyMsg(m)
         B.replay()
         _same(B, 0, o, f"after message {k + 1}")
+
+
+def test_annotate_marker_of_a_live_client():
+    """Client.annotateMarker (client.ts:190-197): a live client's local annotate whose positions are
+    relative to a marker, resolved in its own view; its keys stay pending against a concurrent remote
+    annotate until the ack; then a remote relative op and a reconnect-free continuation."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    o = OracleDoc(new_length_calc=True)
+    o.insert_text_local(0, "hello world")
+    o.start_collab("me")
+    B = MergeTreeBatch(1, new_length_calc=True)
+    c = B[0]
+    c.insertTextLocal(0, "hello world")
+    c.startOrUpdateCollaboration("me")
+    steps = [
+        ("msg", {"clientId": "x", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                 "type": "op", "contents": {"type": 0, "pos1": 5, "seg": {"marker": {"refType": 1},
+                                                                          "props": {"markerId": "p1"}}}}),
+        ("mark", ("p1", {"color": "red", "n": 1})),
+        ("msg", {"clientId": "x", "sequenceNumber": 2, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0,
+                 "type": "op", "contents": {"type": 2, "relativePos1": {"id": "p1", "before": True},
+                                            "relativePos2": {"id": "p1"}, "props": {"color": "blue", "w": 2}}}),
+        ("ack", 3),
+        ("msg", {"clientId": "x", "sequenceNumber": 4, "referenceSequenceNumber": 3, "minimumSequenceNumber": 1,
+                 "type": "op", "contents": {"type": 2, "relativePos1": {"id": "p1", "before": True},
+                                            "relativePos2": {"id": "p1", "offset": 3}, "props": {"color": "green"}}}),
+    ]
+    last = None
+    for kind, x in steps:
+        if kind == "msg":
+            o.apply_msg(x)
+            c.applyMsg(x)
+        elif kind == "mark":
+            last = c.annotateMarker(x[0], x[1])
+            assert o.local_op_json(last) == last
+        else:
+            ack = {"clientId": "me", "sequenceNumber": x, "referenceSequenceNumber": 1, "minimumSequenceNumber": 1,
+                   "type": "op", "contents": last}
+            o.apply_msg(ack)
+            c.applyMsg(ack)
+        B.replay()
+        _same(B, 0, o, f"after {kind}")
+    segs = [e["segment"] for e in B.map_range(0) if e["segment"].get("type") == "Marker"]
+    assert segs[0]["properties"]["color"] == "green" and segs[0]["properties"]["n"] == 1
