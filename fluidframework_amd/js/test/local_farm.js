@@ -1,6 +1,6 @@
 // A live-client conflict farm through the JS drop-in (tests/test_js_package.py): every client of the
 // recorded farm is one Client slot; its local ops go through applyLocalOp, its received messages (acks
-// included) through applyMsg.  Prints every client's text after each round as one JSON line.
+// included) through applyMsg, its reconnects through regeneratePendingOp.  Prints every client's text after each round as one JSON line.
 "use strict";
 const fs = require("fs");
 const { MergeTreeBatch } = require("..");
@@ -18,7 +18,11 @@ for (const round of rec.rounds) {
   round.forEach((events, k) => {
     for (const [kind, x] of events) {
       if (kind === "local") clients[k].applyLocalOp(x);
-      else clients[k].applyMsg(x);
+      else if (kind === "regen") {
+        // a reconnect: the regenerated op must equal the oracle's (x = [resetOp, expected]), key order included
+        const got = JSON.stringify(clients[k].regeneratePendingOp(x[0]));
+        if (got !== JSON.stringify(x[1])) throw new Error(`regeneratePendingOp: ${got} != ${JSON.stringify(x[1])}`);
+      } else clients[k].applyMsg(x);
     }
   });
   texts.push(clients.map((c) => c.getText()));

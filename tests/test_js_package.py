@@ -85,16 +85,18 @@ def test_js_package_replays_reference_logs_on_gpu(tmp_path):
 @needs_node
 @pytest.mark.gpu
 def test_js_live_clients_on_gpu(tmp_path):
-    """Live clients through the JS package (insert / remove / annotate local ops and their acks): every client's text
+    """Live clients through the JS package (insert / remove / annotate local ops, their acks and reconnects
+    through regeneratePendingOp): every client's text
     after every round equals its oracle client's (tests/helpers.run_local_farm)."""
     import json
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import run_local_farm
     rec = {}
-    run_local_farm(7, n_clients=3, n_rounds=30, annotate=True, record=rec)
+    run_local_farm(7, n_clients=3, n_rounds=30, annotate=True, record=rec, new_mode=True, reconnect=0.3)
     path = tmp_path / "farm.json"
-    path.write_text(json.dumps({"ids": rec["ids"], "initial": "hello world", "newMode": False,
+    assert any(kind == "regen" for rnd in rec["rounds"] for ev, _, _ in rnd for kind, _ in ev)
+    path.write_text(json.dumps({"ids": rec["ids"], "initial": "hello world", "newMode": True,
                                 "rounds": [[ev for ev, _, _ in rnd] for rnd in rec["rounds"]]}))
     r = subprocess.run(["node", os.path.join(JS, "test", "local_farm.js"), str(path)], capture_output=True,
                        text=True, timeout=240)
