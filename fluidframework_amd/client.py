@@ -396,8 +396,20 @@ class Client:
             raise MergeTreeError(-6, "unsupported: local annotate with a combiningOp")
         return self.applyLocalOp({"pos1": start, "pos2": end, "props": props, "type": 2})
 
-    def getText(self):
-        return self._b.text(self._doc)
+    def getText(self, start=None, end=None):
+        """TestClient.getText (testClient.ts:185): the local view's text, or of [start, end) in positions that
+        count markers (MergeTreeTextHelper.getText's mapRange + gatherText; markers add no text)."""
+        if start is None and end is None:
+            return self._b.text(self._doc)
+        out = []
+        for h in self._b.map_range(self._doc, start or 0, -1 if end is None else end):
+            seg = h["segment"]
+            if seg.get("type") != "TextSegment":
+                continue
+            t = seg["text"]
+            s0 = max(0, h["start"])
+            out.append(t[s0:] if h["end"] >= len(t) else t[s0:h["end"]])
+        return "".join(out)
 
     def getContainingSegment(self, pos, sequenceArgs=None):
         """client.ts:1065: {"segment": dict | None, "offset": int | None} in the local view, or in the

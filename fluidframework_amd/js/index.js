@@ -273,8 +273,18 @@ class Client {
   /** TestClient.getText (testClient.ts:185). */
   getText(start, end) {
     this.batch.ensureFlushed();
-    const t = native.getText(this.batch.handle, this.doc);
-    return start === undefined && end === undefined ? t : t.substring(start || 0, end === undefined ? t.length : end);
+    if (start === undefined && end === undefined) return native.getText(this.batch.handle, this.doc);
+    // a range: MergeTreeTextHelper.getText's mapRange + gatherText over [start, end) in the local view
+    // (positions count markers; markers add no text)
+    const hits = JSON.parse(native.mapRange(this.batch.handle, this.doc, start || 0, end === undefined ? -1 : end, -1, null, 0));
+    let t = "";
+    for (const h of hits) {
+      if (h.segment.type !== "TextSegment") continue;
+      const seg = h.segment.text;
+      const s0 = h.start < 0 ? 0 : h.start;
+      t += h.end >= seg.length ? seg.substring(s0) : seg.substring(s0, h.end);
+    }
+    return t;
   }
 
   /** Client.getLength (client.ts:1129). */

@@ -203,3 +203,20 @@ def test_annotate_marker_of_a_live_client():
         _same(B, 0, o, f"after {kind}")
     segs = [e["segment"] for e in B.map_range(0) if e["segment"].get("type") == "Marker"]
     assert segs[0]["properties"]["color"] == "green" and segs[0]["properties"]["n"] == 1
+
+
+def test_get_text_range_counts_markers():
+    """TestClient.getText(start, end) (testClient.ts:185, MergeTreeTextHelper.ts:20-81): positions count
+    markers (length 1), which add no text."""
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1)
+    c = B[0]
+    c.insertTextLocal(0, "hello world")
+    c.startOrUpdateCollaboration("me")
+    c.applyMsg({"clientId": "x", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                "type": "op", "contents": {"type": 0, "pos1": 5, "seg": {"marker": {"refType": 1}}}})
+    assert c.getText() == "hello world"
+    assert c.getText(3, 8) == "lo w"  # l o [marker] ' ' w
+    assert c.getText(5, 6) == ""
+    assert c.getText(6) == " world"
+    assert c.getText(None, 2) == "he"
