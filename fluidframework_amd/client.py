@@ -411,6 +411,41 @@ class Client:
             out.append(t[s0:] if h["end"] >= len(t) else t[s0:h["end"]])
         return "".join(out)
 
+    # ---- TestClient helpers (test/testClient.ts:224-327): sequenced messages of other clients
+    def makeOpMessage(self, op, seq=-1, refSeq=None, longClientId=None, minSeqNumber=0):
+        """TestClient.makeOpMessage (testClient.ts:303-327)."""
+        if op is None:
+            raise MergeTreeError(-1, "op cannot be undefined")
+        return {"clientId": longClientId if longClientId is not None else (self.longClientId or ""),
+                "clientSequenceNumber": 1, "contents": op, "minimumSequenceNumber": minSeqNumber,
+                "referenceSequenceNumber": self.getCurrentSeq() if refSeq is None else refSeq,
+                "sequenceNumber": seq, "term": 1, "traces": [], "type": "op"}
+
+    def insertTextRemote(self, pos, text, props, seq, refSeq, longClientId):
+        seg = {"text": text, "props": props} if props else text
+        self.applyMsg(self.makeOpMessage({"pos1": pos, "seg": seg, "type": 0}, seq, refSeq, longClientId))
+
+    def removeRangeRemote(self, start, end, seq, refSeq, longClientId):
+        self.applyMsg(self.makeOpMessage({"pos1": start, "pos2": end, "type": 1}, seq, refSeq, longClientId))
+
+    def annotateRangeRemote(self, start, end, props, seq, refSeq, longClientId):
+        self.applyMsg(self.makeOpMessage({"pos1": start, "pos2": end, "props": props, "type": 2}, seq, refSeq,
+                                         longClientId))
+
+    def insertMarkerRemote(self, pos, markerDef, props, seq, refSeq, longClientId):
+        """markerDef {refType?} (default ReferenceType.Tile = 1, testClient.ts:281)."""
+        seg = {"marker": {"refType": (markerDef or {}).get("refType", 1)}}
+        if props:
+            seg["props"] = props
+        self.applyMsg(self.makeOpMessage({"pos1": pos, "seg": seg, "type": 0}, seq, refSeq, longClientId))
+
+    def insertMarkerLocal(self, pos, behaviors, props=None):
+        """A live client's marker insert (testClient.ts:270-276); returns the op to send."""
+        seg = {"marker": {"refType": behaviors}}
+        if props:
+            seg["props"] = props
+        return self.insertSegmentLocal(pos, seg)
+
     def getContainingSegment(self, pos, sequenceArgs=None):
         """client.ts:1065: {"segment": dict | None, "offset": int | None} in the local view, or in the
         view of sequenceArgs = {"referenceSequenceNumber", "clientId"} (a remote message's perspective)."""
@@ -458,6 +493,9 @@ class Client:
 
 
 MTB_BATCH_MATRIX = 1
+
+
+TestClient = Client  # testClient.ts:54: the same slot with the TestClient helpers above
 
 
 class MatrixBatch(MergeTreeBatch):

@@ -33,7 +33,7 @@ export declare class MergeTreeBatch {
   summarizeV1Many(docs: number[], msn?: number, seq?: number, threads?: number):
     { blobs: [string, string][]; summary: string }[];
   lastStats: ReplayStats | undefined;
-  client(i: number): Client;
+  client(i: number): TestClient;
   flush(): ReplayStats;
   flushAsync(): Promise<ReplayStats>;
   internProps(props: object | string): number;
@@ -85,7 +85,14 @@ export declare class Client {
   summarize(runtime?: { deltaManager?: { minimumSequenceNumber?: number; lastSequenceNumber?: number } }, handle?: unknown,
             serializer?: unknown, catchUpMsgs?: unknown[]): unknown;
 }
-export declare const TestClient: typeof Client;
+export declare class TestClient extends Client {
+  makeOpMessage(op: Record<string, unknown>, seq?: number, refSeq?: number, longClientId?: string, minSeqNumber?: number): Record<string, unknown>;
+  insertTextRemote(pos: number, text: string, props: Record<string, unknown> | undefined, seq: number, refSeq: number, longClientId: string): void;
+  removeRangeRemote(start: number, end: number, seq: number, refSeq: number, longClientId: string): void;
+  annotateRangeRemote(start: number, end: number, props: Record<string, unknown>, seq: number, refSeq: number, longClientId: string): void;
+  insertMarkerRemote(pos: number, markerDef: { refType?: number } | undefined, props: Record<string, unknown> | undefined, seq: number, refSeq: number, longClientId: string): void;
+  insertMarkerLocal(pos: number, behaviors: number, props?: Record<string, unknown>): Record<string, unknown>;
+}
 
 /** A batch of SharedMatrix observers (rows / cols PermutationVectors replayed on the GPU). */
 export declare class MatrixBatch extends MergeTreeBatch {

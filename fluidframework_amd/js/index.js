@@ -55,7 +55,8 @@ class MergeTreeBatch {
     this.busy = false;
     this.lastStats = undefined;
     this.clients = [];
-    for (let i = 0; i < ndocs; i++) this.clients.push(new Client(this, i));
+    // every slot is a TestClient (a Client plus the testClient.ts message helpers)
+    for (let i = 0; i < ndocs; i++) this.clients.push(new TestClient(this, i));
   }
 
   client(i) { return this.clients[i]; }
@@ -436,7 +437,38 @@ class SharedMatrix {
   }
 }
 
-/** TestClient alias: the same observer slot plus getText (testClient.ts:54). */
-const TestClient = Client;
+/** TestClient (testClient.ts:54): the same slot plus the helpers that make other clients' sequenced messages. */
+class TestClient extends Client {
+  /** TestClient.makeOpMessage (testClient.ts:303-327). */
+  makeOpMessage(op, seq = -1, refSeq = this.getCurrentSeq(), longClientId, minSeqNumber = 0) {
+    if (op === undefined) throw new Error("op cannot be undefined");
+    return {
+      clientId: longClientId !== undefined ? longClientId : this.longClientId !== undefined ? this.longClientId : "",
+      clientSequenceNumber: 1, contents: op, metadata: undefined,
+      minimumSequenceNumber: minSeqNumber, referenceSequenceNumber: refSeq, sequenceNumber: seq,
+      timestamp: Date.now(), term: 1, traces: [], type: "op",
+    };
+  }
+  insertTextRemote(pos, text, props, seq, refSeq, longClientId) {
+    const seg = props ? { text, props } : text;
+    this.applyMsg(this.makeOpMessage({ pos1: pos, seg, type: 0 }, seq, refSeq, longClientId));
+  }
+  removeRangeRemote(start, end, seq, refSeq, longClientId) {
+    this.applyMsg(this.makeOpMessage({ pos1: start, pos2: end, type: 1 }, seq, refSeq, longClientId));
+  }
+  annotateRangeRemote(start, end, props, seq, refSeq, longClientId) {
+    this.applyMsg(this.makeOpMessage({ pos1: start, pos2: end, props, type: 2 }, seq, refSeq, longClientId));
+  }
+  insertMarkerRemote(pos, markerDef, props, seq, refSeq, longClientId) {
+    const seg = { marker: { refType: markerDef && markerDef.refType !== undefined ? markerDef.refType : 1 } };
+    if (props) seg.props = props;
+    this.applyMsg(this.makeOpMessage({ pos1: pos, seg, type: 0 }, seq, refSeq, longClientId));
+  }
+  insertMarkerLocal(pos, behaviors, props) {
+    const seg = { marker: { refType: behaviors } };
+    if (props) seg.props = props;
+    return this.insertSegmentLocal(pos, seg);
+  }
+}
 
 module.exports = { MergeTreeBatch, MatrixBatch, SharedMatrix, Client, TestClient, native };

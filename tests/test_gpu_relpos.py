@@ -220,3 +220,23 @@ def test_get_text_range_counts_markers():
     assert c.getText(5, 6) == ""
     assert c.getText(6) == " world"
     assert c.getText(None, 2) == "he"
+
+
+def test_test_client_helpers_reference_applymsg_kat():
+    """TestClient helpers (testClient.ts:224-327) driving client.applyMsg.spec.ts-style steps: remote insert,
+    marker, annotate and remove messages made by makeOpMessage."""
+    from fluidframework_amd import MergeTreeBatch
+    from fluidframework_amd.client import TestClient
+    B = MergeTreeBatch(1)
+    c = B[0]
+    assert isinstance(c, TestClient)
+    c.insertTextLocal(0, "hello world")
+    c.startOrUpdateCollaboration("me")
+    c.insertTextRemote(0, "ab", None, 1, 0, "a")
+    c.insertMarkerRemote(2, {"refType": 1}, {"markerId": "m"}, 2, 1, "b")
+    c.annotateRangeRemote(0, 2, {"x": 1}, 3, 2, "a")
+    c.removeRangeRemote(3, 9, 4, 3, "b")
+    assert c.getText() == "abworld"
+    assert c.getText(0, 3) == "ab"
+    props = [e["segment"].get("properties") for e in B.map_range(0, 0, 2)]
+    assert props == [{"x": 1}]
