@@ -105,3 +105,33 @@ def test_js_live_clients_on_gpu(tmp_path):
     want = [[t for _, _, t in rnd] for rnd in rec["rounds"]]
     assert got["texts"] == want
     assert [int(h, 16) for h in got["digests"]] == [d for _, d, _ in rec["rounds"][-1]]
+
+
+@needs_node
+@pytest.mark.gpu
+def test_js_client_api_on_gpu():
+    """TestClient helpers, getText ranges, Client.annotateMarker (pending keys, ack) and a remote relative op
+    through the JS package: text, the op it returns and the state digest equal the oracle's."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import OracleDoc
+    r = subprocess.run(["node", os.path.join(JS, "test", "client_api.js")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["ranges"] == ["abhello world", "ab", "he", "ello world"]
+    want_op = {"props": {"color": "red"}, "relativePos1": {"id": "m", "before": True}, "relativePos2": {"id": "m"}, "type": 2}
+    assert got["op"] == want_op
+    o = OracleDoc(new_length_calc=True)
+    o.insert_text_local(0, "hello world")
+    o.start_collab("me")
+    mk = lambda op, seq, ref, cid: {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,  # noqa: E731
+                                    "minimumSequenceNumber": 0, "type": "op", "contents": op}
+    o.apply_msg(mk({"pos1": 0, "seg": "ab", "type": 0}, 1, 0, "a"))
+    o.apply_msg(mk({"pos1": 2, "seg": {"marker": {"refType": 1}, "props": {"markerId": "m"}}, "type": 0}, 2, 1, "b"))
+    assert o.local_op_json(want_op) == want_op
+    o.apply_msg(mk({"pos1": 0, "pos2": 4, "props": {"color": "blue", "w": 1}, "type": 2}, 3, 2, "a"))
+    o.apply_msg(mk(want_op, 4, 2, "me"))
+    o.apply_msg(mk({"relativePos1": {"id": "m"}, "seg": "!", "type": 0}, 5, 4, "b"))
+    assert got["text"] == o.get_text()
+    assert int(got["digest"], 16) == o.digest()
