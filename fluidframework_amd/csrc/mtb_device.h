@@ -55,11 +55,12 @@
 // it after sequenced segments (UnassignedSequenceNumber -> Number.MAX_SAFE_INTEGER - 1, mergeTree.ts:1719).
 #define MTB_PEND 0x40000000
 // Pending segment groups (pendingSegments, mergeTree.ts:532; one SegmentGroup per local op that touched
-// segments): a FIFO directory of MTB_PEND_GROUPS entries [localSeq, member list offset, count, capacity,
+// segments): a FIFO directory (MTB_PEND_GROUPS entries, doubling when full) of [localSeq, member list offset, count, capacity,
 // op type, op props id, 0, 0] in the aux arena; member lists (segment ids, group order) grow by doubling.
 // A segment's pending property keys (PropertiesManager.pendingKeyUpdateCount, segmentPropertiesManager.ts)
 // are the keys of the pending ANNOTATE groups holding it.
-#define MTB_PEND_GROUPS 256
+#define MTB_PEND_GROUPS 256      // initial directory entries
+#define MTB_PEND_MAX (1u << 20)  // unacked local ops per document
 #define MTB_PEND_ENT 8  // words per directory entry
 // Marker-relative positions (IRelativePosition, ops.ts:77-92; posFromRelativePos mergeTree.ts:1371-1395):
 // an insert / remove / annotate record with MTB_F_RELPOS has pos1 and/or pos2 = MTB_RELPOS | the
@@ -184,7 +185,8 @@ struct DocState {     // 320 bytes
   int32_t last_norm;    // Client.lastNormalizationRefSeq (client.ts:909): currentSeq of the last normalization
   uint32_t orphans;     // aux offset of [n, cap, (props id, segment)*]: pending keys whose annotate group a
                         // reconnect dropped without a new op (they stay pending, as the reference's counts do)
-  uint32_t pad3[6];
+  uint32_t pend_cap;    // directory entries (a power of two, 0: none yet; doubles when full)
+  uint32_t pad3[5];
 };
 static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
@@ -217,7 +219,7 @@ struct Tables {
 #define DERR_HANDLE 12     // handle allocation did not isolate one position (never produced by the reference)
 #define DERR_HOST 14       // host-side post-processing of the document's replay failed (HostDoc::hostErr)
 #define DERR_RANGE 15      // a local op outside the local view (getValidOpRange, client.ts:527-592)
-#define DERR_CAP_PEND 16   // more than MTB_PEND_GROUPS unacked local ops
+#define DERR_CAP_PEND 16   // more than MTB_PEND_MAX unacked local ops
 #define DERR_ACK_INSERT 17 // 0x045 "On insert, seq number already assigned!"
 #define DERR_ACK_REMOVE 18 // 0x046 "On remove ack, missing removal info!"
 #define DERR_LOCAL 19      // a local op the engine does not support (a local rewrite annotate)

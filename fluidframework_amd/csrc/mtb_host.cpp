@@ -323,6 +323,7 @@ struct HostDoc {
   std::string hostErr;            // message of a sticky host-side failure (DERR_HOST)
   int64_t lastSeq = 0;            // last appended message seq (host-side 0x038 check)
   uint64_t totalOps = 0;          // all records ever appended (capacity sizing)
+  uint64_t totalLocal = 0;        // local-op records, and groups a REGEN may re-queue (aux sizing)
   uint64_t totalPayload = 0;
   // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
   bool loaded = false;
@@ -1063,6 +1064,8 @@ Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
     c.list += (uint32_t)d.img.lists.size() * 2;
     c.aux += (uint32_t)d.img.aux.size();
   }
+  // a live client's pending groups: directory entries (8 words, doubling) and member lists
+  c.aux += (uint32_t)std::min<uint64_t>(48 * d.totalLocal, 1u << 30);
   return c;
 }
 bool fits(const DocState& s, const Caps& c) {
@@ -2678,6 +2681,7 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     d.totalPayload += d.payload.size() - payloadBefore;
     d.pending.insert(d.pending.end(), recs.begin(), recs.end());
     d.totalOps += recs.size();
+    d.totalLocal += recs.size();
   });
 }
 
@@ -2723,6 +2727,7 @@ int mtbx_regenerate_pending_op(mtb_dev* b, uint32_t doc, const char* json, size_
       r.pos1 = (uint32_t)members.size();
       d.pending.push_back(r);
       d.totalOps++;
+      d.totalLocal += 4 * members.size();
       b->live = true;
       const uint32_t k = (uint32_t)d.pending.size() - 1;  // the record's index in this replay
       mtb_stats st{};

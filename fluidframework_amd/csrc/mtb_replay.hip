@@ -233,7 +233,7 @@ struct Eng {
   // idToSegment upkeep and relative positions (the observer-only replay kernel carries none of it)
   static constexpr bool hasMk = MODE == MODE_MARKERS || MODE == MODE_LIVE || MODE == MODE_LOAD;
   int local_seq;                // MODE_LIVE: collabWindow.localSeq
-  uint32_t pend_dir, pend_head, pend_n;  // MODE_LIVE: pending segment-group FIFO (DocState)
+  uint32_t pend_dir, pend_head, pend_n, pend_cap;  // MODE_LIVE: pending segment-group FIFO (DocState)
   bool grp_open;                // MODE_LIVE: the current local op already has its group
   int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
@@ -1439,18 +1439,29 @@ struct Eng {
   // The FIFO of SegmentGroups (pendingSegments, mergeTree.ts:532): directory entry i (0 = oldest) is
   // [localSeq, member list offset, count, capacity, op type, op props id] in the aux arena.
   __device__ __forceinline__ gptr<uint32_t> grp_ent(uint32_t i) const {
-    return UP(aux) + pend_dir + MTB_PEND_ENT * ((pend_head + i) % MTB_PEND_GROUPS);
+    return UP(aux) + pend_dir + MTB_PEND_ENT * ((pend_head + i) & (pend_cap - 1));
+  }
+  // room for one more group at the FIFO's tail: the directory starts at MTB_PEND_GROUPS entries and doubles
+  // when full (the pending entries move to the front of the new one, oldest first)
+  __device__ bool grp_room() {
+    if (pend_n < pend_cap) return true;
+    const uint32_t ncap = pend_cap ? 2 * pend_cap : MTB_PEND_GROUPS;
+    if (ncap > MTB_PEND_MAX) { fail(DERR_CAP_PEND); return false; }
+    const uint32_t nd = alloc_aux(MTB_PEND_ENT * ncap);
+    if (bad()) return false;
+    const auto dst = UP(aux) + nd;
+    for (uint32_t w = (uint32_t)lane; w < MTB_PEND_ENT * pend_n; w += 64) dst[w] = grp_ent(w / MTB_PEND_ENT)[w % MTB_PEND_ENT];  // (per lane)
+    wsync();
+    pend_dir = nd;
+    pend_head = 0;
+    pend_cap = ncap;
+    return true;
   }
   // addToPendingList (mergeTree.ts:1324-1357): segment `sid` joins the current local op's group (made on
   // its first segment; `type` / `props` name the op: an ANNOTATE group's keys are pending on its members)
   __device__ __forceinline__ void grp_add(uint32_t sid, uint32_t type, uint32_t props) {
     if (!grp_open) {
-      if (pend_n >= MTB_PEND_GROUPS) { fail(DERR_CAP_PEND); return; }
-      if (pend_dir == 0) {
-        pend_dir = alloc_aux(MTB_PEND_ENT * MTB_PEND_GROUPS);
-        pend_head = 0;
-        if (bad()) return;
-      }
+      if (!grp_room()) return;
       const uint32_t off = alloc_aux(8);
       if (bad()) return;
       const auto e = grp_ent(pend_n);
@@ -1592,7 +1603,7 @@ struct Eng {
     const auto e = grp_ent(0);
     const uint32_t off = U(e[1]), cnt = U(e[2]);
     if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
-    pend_head = (pend_head + 1) % MTB_PEND_GROUPS;
+    pend_head = (pend_head + 1) & (pend_cap - 1);
     pend_n--;
     if (opType != 0 && opType != 1 && opType != 2) { fail(DERR_LOCAL); return; }
     if (U(e[4]) == MTB_OP_ANNOTATE) {  // ackPendingProperties: the group's keys stop being pending
@@ -1673,12 +1684,7 @@ struct Eng {
   }
   // a new pending group with one member at the FIFO's tail (resetPendingDeltaToOps' newSegmentGroup)
   __device__ __forceinline__ void grp_new(uint32_t lseq, uint32_t type, uint32_t props, uint32_t sid) {
-    if (pend_n >= MTB_PEND_GROUPS) { fail(DERR_CAP_PEND); return; }
-    if (pend_dir == 0) {
-      pend_dir = alloc_aux(MTB_PEND_ENT * MTB_PEND_GROUPS);
-      pend_head = 0;
-      if (bad()) return;
-    }
+    if (!grp_room()) return;
     const uint32_t off = alloc_aux(8);
     if (bad()) return;
     const auto e = grp_ent(pend_n);
@@ -1912,7 +1918,7 @@ struct Eng {
       const auto e = grp_ent(0);
       const int L = (int)U(e[0]);
       const uint32_t off = U(e[1]), cnt = U(e[2]), type = U(e[4]), props = U(e[5]);
-      pend_head = (pend_head + 1) % MTB_PEND_GROUPS;
+      pend_head = (pend_head + 1) & (pend_cap - 1);
       pend_n--;
       if (type == MTB_OP_ANNOTATE) {
         if (lane == 0) ds->pend_ann = ds->pend_ann - 1;
@@ -3428,6 +3434,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.pend_dir = ds->pend_dir;
   e.pend_head = ds->pend_head;
   e.pend_n = ds->pend_n;
+  e.pend_cap = ds->pend_cap;
   e.grp_open = false;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
@@ -3521,6 +3528,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
       ds->pend_dir = e.pend_dir;
       ds->pend_head = e.pend_head;
       ds->pend_n = e.pend_n;
+      ds->pend_cap = e.pend_cap;
     }
     ds->n_mod += e.n_mod;
     ds->ops_applied += e.ops_applied;

@@ -288,6 +288,102 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     return clients, obs, log
 
 
+def _doover(lo, hi, grow):
+    """doOverRange (mergeTreeOperationRunner.ts:90-107): lo, grow(lo), ... up to hi; a non-growing step +1."""
+    v, last = lo, None
+    while v <= hi:
+        if v == last:
+            v += 1
+        last = v
+        yield v
+        v = grow(v)
+
+
+REF_CLIENT_NAMES = [chr(ord("A") + i) for i in range(26)] + [chr(ord("a") + i) for i in range(26)]
+
+
+def run_ref_reconnect_farm(seed, n_clients, ops_range=(40, 320), rounds=3, record=None):
+    """The reference's own reconnect farm shape (client.reconnectFarm.spec.ts:25-121 over
+    mergeTreeOperationRunner.ts:200-307, new length calculations), on oracle clients: `n_clients` clients
+    start empty; per round `ops` local ops (ops doubling over `ops_range`, `rounds` rounds each) are made by
+    clients 1.. against the round-start view (insert while shorter than 16, else annotate / remove / insert
+    of the client's name); client 1 (and, on a coin flip with more than two clients, client 2) has its ops of
+    the round held back, catches up on everyone else's, and resubmits regeneratePendingOp's result at its
+    current seq.  After every round all clients' characters and per-character properties must agree
+    (TestClientLogger.validate) -- an AssertionError names the round otherwise.  `record` (a dict) gets the
+    same per-round event format as run_local_farm's.  Returns the clients."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed * 1000 + n_clients)
+    names = REF_CLIENT_NAMES[:n_clients]
+    clients = []
+    for cid in names:
+        c = OracleDoc(new_length_calc=True)
+        c.start_collab(cid)
+        clients.append(c)
+    log_rounds = record.setdefault("rounds", []) if record is not None else None
+    if record is not None:
+        record["ids"] = names
+    seq = 0
+
+    def send(cid, ref, msn, op):
+        nonlocal seq
+        seq += 1
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+             "minimumSequenceNumber": msn, "type": "op", "contents": op}
+        for k, c in enumerate(clients):
+            c.apply_msg(m)
+            if log_rounds is not None:
+                log_rounds[-1][k].append(("msg", m))
+
+    for n_ops in _doover(ops_range[0], ops_range[1], lambda x: x * 2):
+        for rnd in range(rounds):
+            if log_rounds is not None:
+                log_rounds.append([[] for _ in clients])
+            msn, msgs = seq, []
+            for _ in range(n_ops):
+                k = rng.randint(1, n_clients - 1)
+                c = clients[k]
+                n = c.get_length()
+                name = names[k] * rng.randint(1, 3)
+                if n < 16:
+                    op = c.insert_local_op(rng.randint(0, n), name)
+                else:
+                    which, a = rng.randint(0, 2), rng.randint(0, n - 1)
+                    b = rng.randint(a + 1, n)
+                    if which == 0:
+                        op = c.annotate_local_op(a, b, {"client": names[k]})
+                    elif which == 1:
+                        op = c.remove_local_op(a, b)
+                    else:
+                        op = c.insert_local_op(rng.randint(0, n), name)
+                msgs.append((k, c.current_seq, op))
+                if log_rounds is not None:
+                    log_rounds[-1][k].append(("local", op))
+            recon = [1, 2] if n_clients > 2 and rng.random() < 0.5 else [1]
+            held = []
+            for k, ref, op in msgs:
+                if k in recon:
+                    held.append((k, op))
+                else:
+                    send(names[k], ref, msn, op)
+            again = []
+            for k, op in held:
+                new = clients[k].regenerate_pending_op(op)
+                if log_rounds is not None:
+                    log_rounds[-1][k].append(("regen", (op, new)))
+                again.append((k, clients[k].current_seq, new))
+            for k, ref, op in again:
+                send(names[k], ref, msn, op)
+            base = chars_with_props(clients[0])
+            for k, c in enumerate(clients[1:], 1):
+                assert chars_with_props(c) == base, f"seed {seed}: {n_ops} ops/round, round {rnd}, client {k}"
+            if log_rounds is not None:
+                log_rounds[-1] = [(ev, clients[k].digest(), clients[k].get_text())
+                                  for k, ev in enumerate(log_rounds[-1])]
+    return clients
+
+
 def chars_with_props(doc):
     """(character, properties) per visible character of a document's local view (TestClientLogger.validate
     compares text and the properties at every position)."""

@@ -16,15 +16,21 @@ pytestmark = pytest.mark.gpu
 
 
 def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False, reconnect=0.0):
-    import json
-    from fluidframework_amd import MergeTreeBatch
     rec = {}
     run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=annotate, record=rec,
                    reconnect=reconnect)
+    return _replay_record(rec, seed, new_mode, rounds_per_replay, "hello world")
+
+
+def _replay_record(rec, seed, new_mode, rounds_per_replay, initial):
+    import json
+    from fluidframework_amd import MergeTreeBatch
     ids = rec["ids"]
+    n_clients = len(ids)
     B = MergeTreeBatch(n_clients, new_length_calc=new_mode)
     for k, cid in enumerate(ids):
-        B[k].insertTextLocal(0, "hello world")
+        if initial:
+            B[k].insertTextLocal(0, initial)
         B[k].startOrUpdateCollaboration(cid)
     checked = 0
     for r, rnd in enumerate(rec["rounds"]):
@@ -97,6 +103,19 @@ def test_reconnect_farm(seed):
 def test_reconnect_farm_batched_rounds(seed):
     assert _replay_farm(seed, n_clients=6, n_rounds=100, new_mode=seed % 2 == 0, rounds_per_replay=5, annotate=True,
                         reconnect=0.25) > 0
+
+
+@pytest.mark.parametrize("n_clients", [2, 4, 8])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_reference_shaped_reconnect_farm(seed, n_clients):
+    """client.reconnectFarm.spec.ts's own shape (helpers.run_ref_reconnect_farm: empty start, 40..320 ops per
+    round against the round-start view, clients 1 (and 2) reconnecting every round): every client's local
+    ops, regenerations and received messages replayed on the engine give the oracle's ops, digests and
+    texts after every round."""
+    from helpers import run_ref_reconnect_farm
+    rec = {}
+    run_ref_reconnect_farm(seed, n_clients, record=rec)
+    assert _replay_record(rec, seed, True, 1, "") > 0
 
 
 def test_pending_local_key_survives_a_remote_annotate():

