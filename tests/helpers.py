@@ -312,9 +312,22 @@ def run_ref_reconnect_farm(seed, n_clients, ops_range=(40, 320), rounds=3, recor
     current seq.  After every round all clients' characters and per-character properties must agree
     (TestClientLogger.validate) -- an AssertionError names the round otherwise.  `record` (a dict) gets the
     same per-round event format as run_local_farm's.  Returns the clients."""
+    return run_ref_farm(seed, n_clients, 16, ops_range, rounds, True, record)
+
+
+def run_ref_conflict_farm(seed, n_clients, min_length, ops_range=(1, 128), rounds=8, record=None):
+    """The reference's conflict farm shape (client.conflictFarm.spec.ts, defaultOptions: ops per round
+    1..128 doubling, 8 rounds each, clients made from one snapshot, everyone in lock step): inserts while
+    the document is shorter than `min_length`, then remove / annotate / insert-at-a-segment-start
+    (insertAtRefPos, mergeTreeOperationRunner.ts:32-69, places text at an existing segment's position; here
+    at the start of a visible segment of the client's view, since local references are outside the path)."""
+    return run_ref_farm(seed, n_clients, min_length, ops_range, rounds, False, record)
+
+
+def run_ref_farm(seed, n_clients, min_length, ops_range, rounds, reconnect, record=None):
     import random
     from pyoracle import OracleDoc
-    rng = random.Random(seed * 1000 + n_clients)
+    rng = random.Random(seed * 1000 + n_clients * 10 + (0 if reconnect else min_length))
     names = REF_CLIENT_NAMES[:n_clients]
     clients = []
     for cid in names:
@@ -336,6 +349,16 @@ def run_ref_reconnect_farm(seed, n_clients, ops_range=(40, 320), rounds=3, recor
             if log_rounds is not None:
                 log_rounds[-1][k].append(("msg", m))
 
+    def segment_start(c, a):
+        """the start of the visible segment holding position a of c's view"""
+        pos = 0
+        for e in c.map_range():
+            n = len(e["segment"].get("text", "x").encode("utf-16-le", "surrogatepass")) // 2
+            if pos + n > a:
+                return pos
+            pos += n
+        return pos
+
     for n_ops in _doover(ops_range[0], ops_range[1], lambda x: x * 2):
         for rnd in range(rounds):
             if log_rounds is not None:
@@ -346,7 +369,7 @@ def run_ref_reconnect_farm(seed, n_clients, ops_range=(40, 320), rounds=3, recor
                 c = clients[k]
                 n = c.get_length()
                 name = names[k] * rng.randint(1, 3)
-                if n < 16:
+                if n == 0 or n < min_length:
                     op = c.insert_local_op(rng.randint(0, n), name)
                 else:
                     which, a = rng.randint(0, 2), rng.randint(0, n - 1)
@@ -355,12 +378,14 @@ def run_ref_reconnect_farm(seed, n_clients, ops_range=(40, 320), rounds=3, recor
                         op = c.annotate_local_op(a, b, {"client": names[k]})
                     elif which == 1:
                         op = c.remove_local_op(a, b)
-                    else:
+                    elif reconnect:
                         op = c.insert_local_op(rng.randint(0, n), name)
+                    else:
+                        op = c.insert_local_op(segment_start(c, a), name)
                 msgs.append((k, c.current_seq, op))
                 if log_rounds is not None:
                     log_rounds[-1][k].append(("local", op))
-            recon = [1, 2] if n_clients > 2 and rng.random() < 0.5 else [1]
+            recon = ([1, 2] if n_clients > 2 and rng.random() < 0.5 else [1]) if reconnect else []
             held = []
             for k, ref, op in msgs:
                 if k in recon:

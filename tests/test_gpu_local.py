@@ -118,6 +118,18 @@ def test_reference_shaped_reconnect_farm(seed, n_clients):
     assert _replay_record(rec, seed, True, 1, "") > 0
 
 
+@pytest.mark.parametrize("n_clients", [2, 4, 8])
+@pytest.mark.parametrize("min_length", [1, 16, 512])
+def test_reference_shaped_conflict_farm(min_length, n_clients):
+    """client.conflictFarm.spec.ts's shape (helpers.run_ref_conflict_farm: 1..128 ops per round, 8 rounds
+    each, lock step, inserts at segment starts): the engine gives the oracle's digests and texts after
+    every round."""
+    from helpers import run_ref_conflict_farm
+    rec = {}
+    run_ref_conflict_farm(0, n_clients, min_length, record=rec)
+    assert _replay_record(rec, 0, True, 1, "") > 0
+
+
 def test_pending_local_key_survives_a_remote_annotate():
     """annotateRangeLocal then a remote annotate of the same key before the ack: the local value stays
     (shouldModifyKey); after the ack a remote annotate applies again."""

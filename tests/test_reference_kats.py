@@ -359,3 +359,13 @@ def test_reference_shaped_reconnect_farm(seed, n_clients):
     from helpers import run_ref_reconnect_farm
     clients = run_ref_reconnect_farm(seed, n_clients)
     assert len({c.get_text() for c in clients}) == 1
+
+
+@pytest.mark.parametrize("n_clients", [2, 4, 8])
+@pytest.mark.parametrize("min_length", [1, 16, 512])
+def test_reference_shaped_conflict_farm(min_length, n_clients):
+    """client.conflictFarm.spec.ts's shape (defaultOptions: 1..128 ops per round, 8 rounds each, lock step,
+    minLength 1..512): all clients agree on text and per-character properties after every round."""
+    from helpers import run_ref_conflict_farm
+    clients = run_ref_conflict_farm(0, n_clients, min_length)
+    assert len({c.get_text() for c in clients}) == 1
