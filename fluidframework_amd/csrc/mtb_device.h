@@ -225,6 +225,7 @@ struct Tables {
 #define DERR_LOCAL 19      // a local op the engine does not support (a local rewrite annotate)
 #define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
 #define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
+#define DERR_SCHED 22      // the ticket scheduler aborted (a wait timed out) before the document's records ran
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

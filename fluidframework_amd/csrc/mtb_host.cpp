@@ -41,6 +41,10 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
+hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t quantum, uint32_t nchunks,
+                                   uint32_t waves);
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
@@ -434,6 +438,8 @@ struct mtb_dev {
   DevBuf<FBlk> dPBlk;
   DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
+  DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_sched_kernel)
+  uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x 4 SIMDs x 4 waves)
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
   bool live = false;                // a document of the batch has made local ops (mtb_local_op_json)
@@ -447,7 +453,7 @@ struct mtb_dev {
   ~mtb_dev() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
-    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release(); dKHash.release(); dVHash.release(); dDigest.release();
+    dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release(); dSched.release(); dKHash.release(); dVHash.release(); dDigest.release();
     dMvSrc.release(); dMvDst.release(); dMvLen.release(); dStageW.release(); dStageH.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1386,6 +1392,7 @@ std::string derr_text(int e) {
     case DERR_DEPTH: return "tree depth limit exceeded";
     case DERR_HOST: return "host post-processing of the replay failed";
     case DERR_REGEN: return "0x033/0x035 regeneratePendingOp: segment group not at the head of the pending queue";
+    case DERR_SCHED: return "replay scheduler aborted (a ticket wait timed out); the document's records did not all run";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     default: return "device error " + std::to_string(e);
   }
@@ -1394,6 +1401,7 @@ int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
   if (e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) return MTB_E_CAPACITY;
   if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN) return MTB_E_ASSERT;
+  if (e == DERR_SCHED) return MTB_E_HIP;
   return MTB_E_UNSUPPORTED;
 }
 
@@ -1473,6 +1481,27 @@ void launch_main(mtb_dev* b, const Tables& t) {
     // batches where some document met a marker id
     bool markers = false;
     for (uint32_t i = 0; i < b->ndocs && !markers; i++) markers = !b->docs[i].markerAmbig.empty();
+    // more documents than wave slots: the ticket-scheduled kernel (MTB_SCHED=0 turns it off, MTB_CHUNKS sets
+    // the tickets per document)
+    if (!b->live && !markers && !b->waveSlots) {
+      hipDeviceProp_t prop;
+      HIPCHK(hipGetDeviceProperties(&prop, b->device));
+      b->waveSlots = (uint32_t)prop.multiProcessorCount * 16u;
+    }
+    const char* sv = getenv("MTB_SCHED");
+    if (!b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0')) {
+      const char* cv = getenv("MTB_CHUNKS");
+      const uint32_t nchunks = std::max(1, std::min(64, cv ? atoi(cv) : 16));
+      uint64_t most = 0;
+      for (uint32_t i = 0; i < b->ndocs; i++) most = std::max<uint64_t>(most, b->hst[i].n_ops - b->hst[i].op_next);
+      const uint32_t quantum = (uint32_t)std::max<uint64_t>(1, (most + nchunks - 1) / nchunks);
+      b->dSched.ensure(2 + (size_t)b->ndocs);
+      HIPCHK(hipMemsetAsync(b->dSched.p, 0, (2 + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
+      HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
+                                     b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, quantum, nchunks,
+                                     b->waveSlots));
+      return;
+    }
     HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t, b->live ? 1 : markers ? 2 : 0));
   }
@@ -1629,6 +1658,9 @@ void replay(mtb_dev* b, mtb_stats* out) {
       const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
       if (e) b->hst[i].err = b->hst[i + 1].err = e;
     }
+  // every document without an error ran all of its records (the ticket scheduler's abort leaves some short)
+  for (uint32_t i = 0; i < b->ndocs; i++)
+    if (!b->hst[i].err && b->hst[i].op_next != b->hst[i].n_ops) b->hst[i].err = DERR_SCHED;
   // the records are consumed now: whatever the host post-processing below does, they never run again
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];

@@ -124,3 +124,68 @@ def test_multi_shard_batch_on_one_device(monkeypatch):
     st2 = B.replay_resident()
     assert st2["checksum"] == st["checksum"] and st2["ops_applied"] == st["ops_applied"]
     assert B.digests() == [lb.docs[j].digest for j in range(lb.n)]
+
+
+def _prefix_digest(lb, u, m):
+    """the oracle's digest of log u's first m records (an observer set up as load_logbatch sets up the engine)"""
+    import sys
+    from pyoracle import OracleDoc
+    tb = lb.doc_text_bytes(u)
+    o = OracleDoc()
+    o.insert_text_local(0, tb[: lb.docs[u].initial_len * 2].decode("utf-16-le"))
+    o.start_collab("obs")
+    for cid in lb.client_ids(u)[1:]:
+        o.add_client(cid)
+    o.apply_records(lb.doc_ops_bytes(u)[: 32 * m], m, tb, lb.props_json())
+    return o.digest()
+
+
+def _message_cut(lb, u, frac):
+    """a record count at a message boundary (the record before it carries the LAST flag) near frac"""
+    ob = lb.doc_ops_bytes(u)
+    m = int(lb.docs[u].n_ops * frac)
+    while m > 0 and not (ob[32 * (m - 1) + 1] & 1):
+        m -= 1
+    return m
+
+
+@pytest.mark.parametrize("chunks", ["16", "3"])
+def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks):
+    """More documents than the device's resident replay waves runs the ticket-scheduled kernel (persistent
+    waves, documents advanced chunk by chunk in round-robin): 4,608 documents with ragged record counts --
+    whole 300-message logs, message-boundary prefixes of them, and documents with no records -- every
+    state digest equal to the oracle's, for 16 and 3 tickets per document (MTB_CHUNKS)."""
+    from pyloggen import LogBatch, make_cfg
+    monkeypatch.setenv("MTB_CHUNKS", chunks)
+    lb = LogBatch(make_cfg(seed=606, n_ops=300), 0, 48)
+    n = 4608
+    B = _batch(n)
+    props = lb.props_json()
+    assert [B.intern_props(p) if p else 0 for p in props] == list(range(len(props)))
+    want = []
+    prefix = {}
+    for j in range(n):
+        u = (j * 7) % lb.n
+        tb = lb.doc_text_bytes(u)
+        B.init_doc(j, tb[: lb.docs[u].initial_len * 2].decode("utf-16-le"), "obs")
+        for cid in lb.client_ids(u)[1:]:
+            B.add_client(j, cid)
+        if j % 211 == 5:
+            m = 0
+        elif j % 97 == 3:
+            m = _message_cut(lb, u, 0.1 + 0.8 * ((j // 97) % 5) / 5)
+        else:
+            m = lb.docs[u].n_ops
+        if m:
+            B.append_records(j, lb.doc_ops_bytes(u)[: 32 * m], m, tb)
+        if m == lb.docs[u].n_ops:
+            want.append(lb.docs[u].digest)
+        else:
+            if (u, m) not in prefix:
+                prefix[(u, m)] = _prefix_digest(lb, u, m)
+            want.append(prefix[(u, m)])
+    st = B.replay()
+    assert st["errors"] == 0
+    dg = B.digests()
+    bad = [j for j in range(n) if dg[j] != want[j]]
+    assert not bad, f"{len(bad)}/{n} documents' digests differ from the oracle (first: {bad[:5]})"
