@@ -1,4 +1,4 @@
-"""Summarize rocprofv3 --pmc counter CSVs (SQ block) for mtb_replay_kernel: totals and per op.
+"""Summarize rocprofv3 --pmc counter CSVs (SQ block) for the replay kernel (plain or ticket-scheduled): totals and per op.
 usage: python tools/sq_summary.py OPS_PER_DISPATCH out.json csv [csv ...]"""
 import csv
 import json
@@ -14,13 +14,13 @@ def main():
     for path in sys.argv[3:]:
         with open(path) as f:
             for r in csv.DictReader(f):
-                if r["Kernel_Name"] != "mtb_replay_kernel":
+                if r["Kernel_Name"] not in ("mtb_replay_kernel", "mtb_replay_sched_kernel"):
                     continue
                 disp.add((path, r["Dispatch_Id"]))
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
     nd = len({d for _, d in disp}) or 1
     per_op = {k: v / (ops * nd) for k, v in tot.items()}
-    res = {"what": f"rocprofv3 --pmc SQ counters of mtb_replay_kernel, {nd} dispatch(es) per pass x {ops:.0f} ops; "
+    res = {"what": f"rocprofv3 --pmc SQ counters of the replay kernel, {nd} dispatch(es) per pass x {ops:.0f} ops; "
                    "totals and per op (SQ_*_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* are per-wave quad-cycle counts)",
            "totals": dict(tot), "per_op": per_op}
     if tot.get("SQ_WAVE_CYCLES"):
