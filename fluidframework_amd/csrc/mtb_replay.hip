@@ -3592,7 +3592,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     const uint32_t d = t % ndocs, c = t / ndocs;
     if (c > 0) {
       uint32_t spins = 0;
-      while (U(__hip_atomic_load(&sched[2 + d], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) < c && spins < MTB_SCHED_SPINS) {
+      while (U(__hip_atomic_load(&sched[2 + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c && spins < MTB_SCHED_SPINS) {
         spins++;
         __builtin_amdgcn_s_sleep(16);
       }
@@ -3600,6 +3600,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
         if (lane == 0) __hip_atomic_store(&sched[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
     }
     sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, quantum);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
