@@ -1491,7 +1491,8 @@ void launch_main(mtb_dev* b, const Tables& t) {
     const char* sv = getenv("MTB_SCHED");
     if (!b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0')) {
       const char* cv = getenv("MTB_CHUNKS");
-      const uint32_t nchunks = std::max(1, std::min(64, cv ? atoi(cv) : 16));
+      uint32_t nchunks = (uint32_t)std::max(1, std::min(64, cv ? atoi(cv) : 16));
+      nchunks = std::max<uint32_t>(1, std::min<uint32_t>(nchunks, 0x7FFFFFFFu / b->ndocs));  // tickets fit 31 bits
       uint64_t most = 0;
       for (uint32_t i = 0; i < b->ndocs; i++) most = std::max<uint64_t>(most, b->hst[i].n_ops - b->hst[i].op_next);
       const uint32_t quantum = (uint32_t)std::max<uint64_t>(1, (most + nchunks - 1) / nchunks);
