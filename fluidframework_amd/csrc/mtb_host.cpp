@@ -43,8 +43,7 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t quantum, uint32_t nchunks,
-                                   uint32_t waves);
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves);
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
@@ -440,6 +439,7 @@ struct mtb_dev {
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
   DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_sched_kernel)
   uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x 4 SIMDs x 4 waves)
+  std::vector<uint32_t> schedPlan;  // the ticket scheduler's chunk plan (host copy of the uploaded one)
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
   bool live = false;                // a document of the batch has made local ops (mtb_local_op_json)
@@ -1490,16 +1490,43 @@ void launch_main(mtb_dev* b, const Tables& t) {
     }
     const char* sv = getenv("MTB_SCHED");
     if (!b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0')) {
-      const char* cv = getenv("MTB_CHUNKS");
-      uint32_t nchunks = (uint32_t)std::max(1, std::min(64, cv ? atoi(cv) : 16));
-      nchunks = std::max<uint32_t>(1, std::min<uint32_t>(nchunks, 0x7FFFFFFFu / b->ndocs));  // tickets fit 31 bits
-      uint64_t most = 0;
-      for (uint32_t i = 0; i < b->ndocs; i++) most = std::max<uint64_t>(most, b->hst[i].n_ops - b->hst[i].op_next);
-      const uint32_t quantum = (uint32_t)std::max<uint64_t>(1, (most + nchunks - 1) / nchunks);
-      b->dSched.ensure(2 + (size_t)b->ndocs);
+      // the chunk plan: cumulative fractions (1/4096) of every document's records per ticket; MTB_CHUNKS=n
+      // makes n equal chunks, MTB_CHUNK_PLAN="a,b,..." (relative chunk sizes) any other split.  Chunk c's
+      // ticket comes ndocs tickets after chunk c-1's, so a chunk at most ~2x the next keeps waits rare.
+      std::vector<double> sizes;
+      if (const char* pv = getenv("MTB_CHUNK_PLAN")) {
+        for (const char* q = pv; *q;) {
+          char* end = nullptr;
+          const double v = strtod(q, &end);
+          if (end == q) break;
+          if (v > 0) sizes.push_back(v);
+          q = *end ? end + 1 : end;
+        }
+      }
+      if (sizes.empty()) {
+        if (const char* cv = getenv("MTB_CHUNKS"))
+          sizes.assign((size_t)std::max(1, std::min(64, atoi(cv))), 1.0);
+        else  // default: shrinking chunks (6/16, 4/16, 2/16, then four of 1/16): few hand-overs, a fine tail
+          sizes = {6, 4, 2, 1, 1, 1, 1};
+      }
+      if (sizes.size() > 64) sizes.resize(64);
+      while (sizes.size() > 1 && (uint64_t)sizes.size() * b->ndocs > 0x7FFFFFFFull) sizes.pop_back();  // tickets fit 31 bits
+      const uint32_t nchunks = (uint32_t)sizes.size();
+      double tot = 0, run = 0;
+      for (double v : sizes) tot += v;
+      std::vector<uint32_t> plan(nchunks);
+      for (uint32_t c = 0; c < nchunks; c++) {
+        run += sizes[c];
+        plan[c] = c + 1 == nchunks ? 4096u : std::max<uint32_t>(1, std::min<uint32_t>(4096, (uint32_t)(4096.0 * run / tot)));
+      }
+      const size_t nw = 2 + (size_t)b->ndocs + nchunks;
+      b->dSched.ensure(nw);
       HIPCHK(hipMemsetAsync(b->dSched.p, 0, (2 + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
+      b->schedPlan = plan;  // (kept alive until the stream has consumed the copy)
+      HIPCHK(hipMemcpyAsync(b->dSched.p + 2 + b->ndocs, b->schedPlan.data(), nchunks * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, b->stream));
       HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
-                                     b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, quantum, nchunks,
+                                     b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks,
                                      b->waveSlots));
       return;
     }

@@ -3383,7 +3383,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
                                            DocState* __restrict__ docs,
                                            uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
                                            uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                                           const Tables& tables, uint32_t quantum = 0) {
+                                           const Tables& tables, uint32_t upto = 0) {
   if (doc >= ndocs) return;
   DocState* ds = &docs[doc];
   Eng<MODE, SCR> e;
@@ -3420,7 +3420,8 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.text_bytes = 0;
   uint32_t k = ds->op_next;
   const uint32_t n = ds->n_ops;
-  const uint32_t kend = quantum && n - k > quantum ? k + quantum : n;  // a scheduler ticket's share
+  // a scheduler ticket replays up to upto/4096 of the document's records (0: all of them)
+  const uint32_t kend = upto ? (uint32_t)(((uint64_t)n * upto + 4095) >> 12) : n;
   uint32_t errk = n;  // MODE_MATRIX: index after the record that failed
   e.walk_depth = -1;
   e.vmask = 0;
@@ -3466,7 +3467,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
     uint32_t cw = e.lane < 8 ? opw[k * 8 + e.lane] : 0u;
     int par = 0;  // MODE_MATRIX: setCell exchange parity
     // a matrix wave keeps walking its records after an error: its partner waits for it at every setCell
-    for (; k < kend && (MODE == MODE_MATRIX || !e.err); k++) {
+    for (; k < kend && k < n && (MODE == MODE_MATRIX || !e.err); k++) {
       const uint32_t nk = k + 1 < n ? k + 1 : k;
       const uint32_t nw = e.lane < 8 ? opw[nk * 8 + e.lane] : 0u;  // prefetch the next record
       mtb_op cur;
@@ -3559,27 +3560,28 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
 // Batches with more documents than wave slots: persistent waves (one grid of the resident slots) take
-// tickets t = (chunk c, document d) in round-robin order, t = c * ndocs + d, and replay `quantum` records of
-// document d per ticket.  Every document then advances at the same pace and the launch ends within about
+// tickets t = (chunk c, document d) in round-robin order, t = c * ndocs + d; ticket c replays document d's
+// records up to the fraction plan[c] / 4096 of them (the host's chunk plan).  Every document then advances at the same pace and the launch ends within about
 // one ticket of the ideal, instead of a last partial "round" of whole documents (10,000 documents on 4,096
 // slots = 2.44 rounds).  Ticket t waits for ticket t - ndocs (the same document's previous chunk), which a
 // running wave took earlier, so the waits always drain; the document state moves between waves through HBM
 // with an agent-scope release / acquire pair.  A wait that exceeds MTB_SCHED_SPINS raises the abort flag
 // and every wave leaves (the host reports the unfinished documents).
-// sched: [0] next ticket, [1] abort flag, [2 + d] chunks of document d completed; zeroed before launch.
+// sched: [0] next ticket, [1] abort flag, [2 + d] chunks of document d completed (zeroed before launch),
+// [2 + ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096).
 #define MTB_SCHED_SPINS (1u << 22)
 // one ticket: the replay engine as a called function (its register allocation stays the replay kernel's
 // instead of being shaped by the ticket loop around it)
 __device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, DocState* docs, uint32_t ndocs,
                                                        const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
                                                        uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                                                       const Tables& tables, uint32_t quantum) {
-  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, quantum);
+                                                       const Tables& tables, uint32_t upto) {
+  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, upto);
 }
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_replay_sched_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
-                            uint32_t* sched, uint32_t quantum, uint32_t nchunks) {
+                            uint32_t* sched, uint32_t nchunks) {
   __shared__ Scratch sh;
   const int lane = lane_id();
   const uint32_t total = ndocs * nchunks;
@@ -3602,7 +3604,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
     }
-    sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, quantum);
+    sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, U(sched[2 + ndocs + c]));
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0) __hip_atomic_store(&sched[2 + d], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -3670,10 +3672,9 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
 }
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t quantum, uint32_t nchunks,
-                                   uint32_t waves) {
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves) {
   hipLaunchKernelGGL(mtb_replay_sched_kernel, dim3(waves), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
-                     heap, aux, freel, tables, sched, quantum, nchunks);
+                     heap, aux, freel, tables, sched, nchunks);
   return hipGetLastError();
 }
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,

@@ -149,14 +149,19 @@ def _message_cut(lb, u, frac):
     return m
 
 
-@pytest.mark.parametrize("chunks", ["16", "3"])
+@pytest.mark.parametrize("chunks", [None, "16", "3"])
 def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks):
     """More documents than the device's resident replay waves runs the ticket-scheduled kernel (persistent
     waves, documents advanced chunk by chunk in round-robin): 4,608 documents with ragged record counts --
     whole 300-message logs, message-boundary prefixes of them, and documents with no records -- every
-    state digest equal to the oracle's, for 16 and 3 tickets per document (MTB_CHUNKS)."""
+    state digest equal to the oracle's, for the default shrinking-chunk plan and for 16 and 3 equal chunks
+    per document (MTB_CHUNKS)."""
     from pyloggen import LogBatch, make_cfg
-    monkeypatch.setenv("MTB_CHUNKS", chunks)
+    monkeypatch.delenv("MTB_CHUNK_PLAN", raising=False)
+    if chunks is None:
+        monkeypatch.delenv("MTB_CHUNKS", raising=False)
+    else:
+        monkeypatch.setenv("MTB_CHUNKS", chunks)
     lb = LogBatch(make_cfg(seed=606, n_ops=300), 0, 48)
     n = 4608
     B = _batch(n)
