@@ -3569,7 +3569,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
 // and every wave leaves (the host reports the unfinished documents).
 // sched: [0] next ticket, [1] abort flag, [2 + d] chunks of document d completed (zeroed before launch),
 // [2 + ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096).
-#define MTB_SCHED_SPINS (1u << 22)
+#define MTB_SCHED_SPINS (1u << 27)  // x s_sleep(16) ~ 1,024 clocks: about a minute, far above any chunk
 // one ticket: the replay engine as a called function (its register allocation stays the replay kernel's
 // instead of being shaped by the ticket loop around it)
 __device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, DocState* docs, uint32_t ndocs,
