@@ -157,3 +157,60 @@ class MatrixLogBatch:
             self.close()
         except Exception:
             pass
+
+
+def _cache_key(cfg, begin, end):
+    f = [getattr(cfg, n) for n, _ in LoggenCfg._fields_]
+    return "logs_" + "_".join(str(int(x)) for x in f) + f"_{begin}_{end}.npz"
+
+
+def cached_log_batch(cfg, begin, end, threads=None, cache_dir=None):
+    """LogBatch for docs [begin, end), reused from `cache_dir` (env MTB_LOG_CACHE) when a run with the same
+    config already generated it: profiling child runs of bench.py replay the same 10^8 ops without paying
+    the generator again.  Without a cache dir this is LogBatch."""
+    cache_dir = cache_dir if cache_dir is not None else os.environ.get("MTB_LOG_CACHE")
+    if not cache_dir:
+        return LogBatch(cfg, begin, end, threads)
+    path = os.path.join(cache_dir, _cache_key(cfg, begin, end))
+    if os.path.exists(path):
+        return LoadedLogBatch(cfg, path)
+    lb = LogBatch(cfg, begin, end, threads)
+    os.makedirs(cache_dir, exist_ok=True)
+    lb.save(path + ".tmp.npz")
+    os.replace(path + ".tmp.npz", path)
+    return lb
+
+
+def _save(self, path):
+    import numpy as np
+    n = self.n
+    meta = np.frombuffer(ctypes.string_at(ctypes.addressof(self.docs), ctypes.sizeof(self.docs)), dtype=np.uint8)
+    ops = b"".join(self.doc_ops_bytes(i) for i in range(n))
+    text = b"".join(self.doc_text_bytes(i) for i in range(n))
+    np.savez(path, meta=meta, ops=np.frombuffer(ops, dtype=np.uint8), text=np.frombuffer(text, dtype=np.uint8))
+
+
+LogBatch.save = _save
+
+
+class LoadedLogBatch(LogBatch):
+    """A LogBatch read back from LogBatch.save: the C records point into numpy buffers this object owns."""
+
+    def __init__(self, cfg, path):
+        import numpy as np
+        self.cfg = cfg
+        z = np.load(path)
+        meta = z["meta"]
+        self.n = meta.size // ctypes.sizeof(LoggenDoc)
+        self.docs = (LoggenDoc * self.n).from_buffer_copy(meta.tobytes())
+        self._ops = np.ascontiguousarray(z["ops"])
+        self._text = np.ascontiguousarray(z["text"])
+        po, pt = self._ops.ctypes.data, self._text.ctypes.data
+        for i in range(self.n):
+            d = self.docs[i]
+            d.ops, d.text = po, pt
+            po += d.n_ops * 32
+            pt += d.n_text * 2
+
+    def close(self):
+        self.docs = None

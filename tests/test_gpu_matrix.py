@@ -139,3 +139,27 @@ def test_matrix_load_mid_stream_then_continue(new_mode):
         for r in range(0, nr, max(1, nr // 10)):
             for c in range(0, nc, max(1, nc // 10)):
                 assert B.get_cell(i, r, c) == o.get_cell(r, c), f"matrix {i} cell ({r}, {c})"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_reference_conflict_kats_gpu(new_mode):
+    """matrix.spec.ts:349-607 two-client conflict cases (tests/matrix_kats.py) on the engine: each case's
+    grid equals the spec's literal, and dumps / summaries equal the oracle's (all cases in one batch)."""
+    import json
+    from fluidframework_amd import MatrixBatch
+    from matrix_kats import CASES, case_messages, grid
+    from test_matrix_kats import oracle_grid
+    B = MatrixBatch(len(CASES), new_length_calc=new_mode)
+    logs = [case_messages(c[2]) for c in CASES]
+    for i, msgs in enumerate(logs):
+        B[i].startOrUpdateCollaboration("observer")
+        for m in msgs:
+            B[i].applyMsg(m)
+    B.flush()
+    for i, (name, line, _, expected) in enumerate(CASES):
+        og, o = oracle_grid(logs[i], new_mode)
+        gg = grid(B.length(2 * i), B.length(2 * i + 1), lambda r, c: B[i].getCell(r, c))
+        assert gg == og, f"matrix.spec.ts:{line} {name!r}: engine grid {gg} != oracle {og}"
+        if expected is not None:
+            assert gg == expected, f"matrix.spec.ts:{line} {name!r}"
+        _check(B, i, o, name)
