@@ -24,7 +24,17 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
            "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
-           "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op"]
+           "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op",
+           "mtb_get_launch_info"]
+
+
+class MtbLaunchInfo(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_uint32), ("wave_slots", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
+                ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 2: "mtb_replay_sched_kernel", 3: "mtb_replay_few_kernel",
+                4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel"}
 
 
 class MtbOptions(ctypes.Structure):
@@ -96,6 +106,7 @@ def lib():
     L.mtb_dump_segments.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.mtb_doc_checksum.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_uint64)]
     L.mtb_doc_digests.argtypes = [vp, u32, u32, ctypes.POINTER(ctypes.c_uint64)]
+    L.mtb_get_launch_info.argtypes = [vp, ctypes.POINTER(MtbLaunchInfo)]
     L.mtb_summarize_v1.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(MtbBlobList)]
     L.mtb_summarize_legacy.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, sz,
                                        ctypes.POINTER(MtbBlobList)]

@@ -31,12 +31,46 @@ def needs_build():
     return _stale(OUT, deps)
 
 
+# the kernel file is compiled once per kernel group (mtb_replay.hip MTB_TU_*), in parallel with the host
+# sources; objects are kept under build/ and rebuilt when a source or header is newer
+KERNEL_GROUPS = (1, 2, 3, 4, 5)
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+
+
+def _headers():
+    return [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith((".h", ".hpp"))] + \
+        [os.path.join(ROOT, "include", "mtb.h")]
+
+
 def build(force=False, arch="gfx950", out=OUT, defines=()):
     if not force and out == OUT and not needs_build():
         return OUT
-    cmd = ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result"] + [f"-D{d}" for d in defines] + ["-o", out] + SRCS
-    subprocess.check_call(cmd)
+    from concurrent.futures import ThreadPoolExecutor
+    tag = "_".join(d.replace("=", "") for d in defines) or "base"
+    odir = os.path.join(OBJ_DIR, f"{arch}_{tag}")
+    os.makedirs(odir, exist_ok=True)
+    base = ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
+        [f"-D{d}" for d in defines]
+    jobs = []  # (object, command, sources it depends on)
+    hip = SRCS[0]
+    for g in KERNEL_GROUPS:
+        o = os.path.join(odir, f"mtb_replay_tu{g}.o")
+        jobs.append((o, base + [f"-DMTB_TU={g}", "-c", hip, "-o", o], [hip]))
+    for src in SRCS[1:]:
+        o = os.path.join(odir, os.path.basename(src) + ".o")
+        jobs.append((o, base + ["-c", src, "-o", o], [src]))
+    hdrs = _headers()
+
+    def run(job):
+        o, cmd, deps = job
+        if force or _stale(o, deps + hdrs):
+            subprocess.check_call(cmd)
+        return o
+
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(workers) as ex:
+        objs = list(ex.map(run, jobs))
+    subprocess.check_call(["hipcc", f"--offload-arch={arch}", "-shared", "-fPIC", "-o", out] + objs)
     return out
 
 

@@ -225,7 +225,12 @@ struct Tables {
 #define DERR_LOCAL 19      // a local op the engine does not support (a local rewrite annotate)
 #define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
 #define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
-#define DERR_SCHED 22      // the ticket scheduler aborted (a wait timed out) before the document's records ran
+#define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
+// ticket scheduler words (mtb_replay_sched_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
+// 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
+#define MTB_SCHED_TICK 32
+#define MTB_SCHED_ABORT 256
+#define MTB_SCHED_HDR 288
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)

@@ -43,7 +43,8 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves);
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
+                                   uint32_t nq, uint32_t spins);  // + mtb_replay_finish_kernel
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables);
@@ -439,6 +440,9 @@ struct mtb_dev {
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
   DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_sched_kernel)
   uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x 4 SIMDs x 4 waves)
+  uint32_t nXcc = 0;                // XCDs of the device (the ticket scheduler's queues)
+  mtb_launch_info launch{};         // what the last replay launched (mtb_launch_info)
+  uint32_t schedAbortHost = 0;
   std::vector<uint32_t> schedPlan;  // the ticket scheduler's chunk plan (host copy of the uploaded one)
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
@@ -1392,7 +1396,7 @@ std::string derr_text(int e) {
     case DERR_DEPTH: return "tree depth limit exceeded";
     case DERR_HOST: return "host post-processing of the replay failed";
     case DERR_REGEN: return "0x033/0x035 regeneratePendingOp: segment group not at the head of the pending queue";
-    case DERR_SCHED: return "replay scheduler aborted (a ticket wait timed out); the document's records did not all run";
+    case DERR_SCHED: return "internal: the document's records did not all run (replay scheduler invariant)";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     default: return "device error " + std::to_string(e);
   }
@@ -1401,7 +1405,7 @@ int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
   if (e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) return MTB_E_CAPACITY;
   if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN) return MTB_E_ASSERT;
-  if (e == DERR_SCHED) return MTB_E_HIP;
+  if (e == DERR_SCHED) return MTB_E_INTERNAL;
   return MTB_E_UNSUPPORTED;
 }
 
@@ -1471,11 +1475,21 @@ void apply_cell_events(mtb_dev* b, uint32_t matrix);
 
 // the batch's replay kernel: matrix pairs, live clients (local ops anywhere in the batch so far), or the
 // observer replay engine
+// the scheduler's abort flag, copied back with the stream's next synchronization
+void sched_readback(mtb_dev* b) {
+  b->schedAbortHost = 0;
+  if (b->launch.kernel == MTB_KERNEL_SCHED)
+    HIPCHK(hipMemcpyAsync(&b->schedAbortHost, b->dSched.p + MTB_SCHED_ABORT, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          b->stream));
+}
+
 void launch_main(mtb_dev* b, const Tables& t) {
-  if (b->matrix)
+  if (b->matrix) {
     HIPCHK(mtb_launch_matrix(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
-  else
+    b->launch = mtb_launch_info{};
+    b->launch.kernel = MTB_KERNEL_MATRIX;
+  } else
   {
     // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
     // batches where some document met a marker id
@@ -1487,7 +1501,12 @@ void launch_main(mtb_dev* b, const Tables& t) {
       hipDeviceProp_t prop;
       HIPCHK(hipGetDeviceProperties(&prop, b->device));
       b->waveSlots = (uint32_t)prop.multiProcessorCount * 16u;
+      int nx = 1;
+      if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, b->device) != hipSuccess) nx = 1;
+      b->nXcc = (uint32_t)std::max(1, std::min(8, nx));
     }
+    b->launch = mtb_launch_info{};
+    b->launch.wave_slots = b->waveSlots;
     const char* sv = getenv("MTB_SCHED");
     if (!b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0')) {
       // the chunk plan: cumulative fractions (1/4096) of every document's records per ticket; MTB_CHUNKS=n
@@ -1519,19 +1538,30 @@ void launch_main(mtb_dev* b, const Tables& t) {
         run += sizes[c];
         plan[c] = c + 1 == nchunks ? 4096u : std::max<uint32_t>(1, std::min<uint32_t>(4096, (uint32_t)(4096.0 * run / tot)));
       }
-      const size_t nw = 2 + (size_t)b->ndocs + nchunks;
+      // queues: one per XCD (L2 affinity); MTB_SCHED_QUEUES overrides (1 = one global queue)
+      uint32_t nq = b->nXcc ? b->nXcc : 1;
+      if (const char* qv = getenv("MTB_SCHED_QUEUES")) nq = (uint32_t)std::max(1, std::min(8, atoi(qv)));
+      // a wait bound far above any chunk (about a minute); MTB_SCHED_SPINS lowers it (tests force the abort)
+      uint32_t spins = 1u << 27;
+      if (const char* sp = getenv("MTB_SCHED_SPINS")) spins = (uint32_t)std::max(0L, std::min(1L << 30, atol(sp)));
+      const size_t nw = MTB_SCHED_HDR + (size_t)b->ndocs + nchunks;
       b->dSched.ensure(nw);
-      HIPCHK(hipMemsetAsync(b->dSched.p, 0, (2 + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
+      HIPCHK(hipMemsetAsync(b->dSched.p, 0, (MTB_SCHED_HDR + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
       b->schedPlan = plan;  // (kept alive until the stream has consumed the copy)
-      HIPCHK(hipMemcpyAsync(b->dSched.p + 2 + b->ndocs, b->schedPlan.data(), nchunks * sizeof(uint32_t),
+      HIPCHK(hipMemcpyAsync(b->dSched.p + MTB_SCHED_HDR + b->ndocs, b->schedPlan.data(), nchunks * sizeof(uint32_t),
                             hipMemcpyHostToDevice, b->stream));
       HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
                                      b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks,
-                                     b->waveSlots));
+                                     b->waveSlots, nq, spins));
+      b->launch.kernel = MTB_KERNEL_SCHED;
+      b->launch.chunks = nchunks;
+      b->launch.queues = nq;
       return;
     }
     HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t, b->live ? 1 : markers ? 2 : 0));
+    b->launch.kernel = b->live ? MTB_KERNEL_LIVE : markers ? MTB_KERNEL_MARKERS
+                       : b->ndocs <= 1024 ? MTB_KERNEL_FEW : MTB_KERNEL_REPLAY;
   }
 }
 
@@ -1675,18 +1705,21 @@ void replay(mtb_dev* b, mtb_stats* out) {
                            b->dHeap.p, b->dAux.p, b->dFree.p, t));
   launch_main(b, t);
   HIPCHK(hipEventRecord(b->ev1, b->stream));
+  sched_readback(b);
   HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
+  b->launch.aborted = b->launch.kernel == MTB_KERNEL_SCHED ? b->schedAbortHost : 0u;
   pc.mark("kernels");
   if (b->matrix)
     for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
       const int e = b->hst[i].err ? b->hst[i].err : b->hst[i + 1].err;
       if (e) b->hst[i].err = b->hst[i + 1].err = e;
     }
-  // every document without an error ran all of its records (the ticket scheduler's abort leaves some short)
+  // every document without an error ran all of its records (after a scheduler abort the finish kernel ran
+  // the rest): an engine invariant, checked
   for (uint32_t i = 0; i < b->ndocs; i++)
     if (!b->hst[i].err && b->hst[i].op_next != b->hst[i].n_ops) b->hst[i].err = DERR_SCHED;
   // the records are consumed now: whatever the host post-processing below does, they never run again
@@ -3019,6 +3052,13 @@ int mtbx_rewind(mtb_dev* b) {
 }
 
 // Replay the records already resident on the device (after mtb_rewind); no host->device traffic.
+int mtbx_get_launch_info(mtb_dev* b, mtb_launch_info* out) {
+  return guarded(b, [&] {
+    if (!out) raise(MTB_E_ARG, "null output");
+    *out = b->launch;
+  });
+}
+
 int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
   return guarded(b, [&] {
     if (!b->haveRewind) raise(MTB_E_ARG, "no resident records");
@@ -3035,15 +3075,22 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
     launch_main(b, t);
     HIPCHK(hipEventRecord(b->ev1, b->stream));
+    sched_readback(b);
     HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    b->launch.aborted = b->launch.kernel == MTB_KERNEL_SCHED ? b->schedAbortHost : 0u;
     mtb_stats st{};
     st.kernel_ms = ms;
+    uint32_t short_docs = 0;
     for (uint32_t i = 0; i < b->ndocs; i++) {
-      const DocState& s = b->hst[i];
+      DocState& s = b->hst[i];
       b->docs[i].cached = false;
+      if (!s.err && s.op_next != s.n_ops) {  // the same invariant as replay(): every record ran
+        s.err = DERR_SCHED;
+        short_docs++;
+      }
       st.docs++;
       st.ops_applied += s.ops_applied;
       st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
@@ -3051,6 +3098,8 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     }
     run_digest(b, st);
     if (out) *out = st;
+    if (short_docs)
+      raise(MTB_E_INTERNAL, std::to_string(short_docs) + " document(s) did not run all of their records");
   });
 }
 

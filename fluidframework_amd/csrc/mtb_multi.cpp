@@ -367,6 +367,20 @@ int mtb_dump_segments(mtb_batch* b, uint32_t doc, char** out, size_t* out_len) {
 
 int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out) { DOC_CALL(doc, mtbx_doc_checksum(d_, l_, out)); }
 
+int mtb_get_launch_info(mtb_batch* b, mtb_launch_info* out) {
+  if (!b || !out) return MTB_E_ARG;
+  mtb_launch_info acc{};
+  for (uint32_t s = 0; s < (uint32_t)b->shards.size(); s++) {
+    mtb_launch_info x{};
+    const int rc = on_shard(b, s, [&](mtb_dev* d) { return mtbx_get_launch_info(d, &x); });
+    if (rc) return rc;
+    if (s == 0) acc = x;
+    acc.aborted |= x.aborted;
+  }
+  *out = acc;
+  return 0;
+}
+
 int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out) {
   if (!b) return MTB_E_ARG;
   if (!out && n) {

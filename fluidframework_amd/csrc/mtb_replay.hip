@@ -33,6 +33,19 @@
 #include "../../include/mtb.h"
 #include "mtb_device.h"
 
+// The kernels are compiled in groups (build.py compiles this file once per group, in parallel, with
+// -DMTB_TU=g; MTB_TU 0 or undefined = every kernel in one translation unit).  Each group instantiates the
+// engine for its own variants only.
+#ifndef MTB_TU
+#define MTB_TU 0
+#endif
+#define MTB_TU_HAS(g) (MTB_TU == 0 || MTB_TU == (g))
+#define MTB_TU_OBS 1      // observer replay: one wave per document, ticket-scheduled, few documents
+#define MTB_TU_LIVE 2     // live clients
+#define MTB_TU_MARKERS 3  // marker ids / relative positions
+#define MTB_TU_LOADMAT 4  // SnapshotV1 body load, SharedMatrix
+#define MTB_TU_MISC 5     // digest, rewind, moves, launch dispatch
+
 namespace mtbk {
 
 // MTB_PROFILE builds accumulate s_memtime cycles per replay phase and event counts into DocState
@@ -3553,6 +3566,8 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   }
 }
 
+#define KARGS docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables
+#if MTB_TU_HAS(MTB_TU_OBS)
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_replay_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                       WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
@@ -3560,16 +3575,24 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
 // Batches with more documents than wave slots: persistent waves (one grid of the resident slots) take
-// tickets t = (chunk c, document d) in round-robin order, t = c * ndocs + d; ticket c replays document d's
-// records up to the fraction plan[c] / 4096 of them (the host's chunk plan).  Every document then advances at the same pace and the launch ends within about
-// one ticket of the ideal, instead of a last partial "round" of whole documents (10,000 documents on 4,096
-// slots = 2.44 rounds).  Ticket t waits for ticket t - ndocs (the same document's previous chunk), which a
-// running wave took earlier, so the waits always drain; the document state moves between waves through HBM
-// with an agent-scope release / acquire pair.  A wait that exceeds MTB_SCHED_SPINS raises the abort flag
-// and every wave leaves (the host reports the unfinished documents).
-// sched: [0] next ticket, [1] abort flag, [2 + d] chunks of document d completed (zeroed before launch),
-// [2 + ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096).
-#define MTB_SCHED_SPINS (1u << 27)  // x s_sleep(16) ~ 1,024 clocks: about a minute, far above any chunk
+// tickets (chunk c, document d); ticket c replays document d's records up to the fraction plan[c] / 4096 of
+// them (the host's chunk plan).  Every document then advances at the same pace and the launch ends within
+// about one ticket of the ideal, instead of a last partial "round" of whole documents (10,000 documents on
+// 4,096 slots = 2.44 rounds).
+//
+// Queues (L2 affinity, speed only): documents are split into nq queues (d mod nq, nq = the device's XCD
+// count); a wave serves the queue of the XCD it runs on (HW_REG_XCC_ID) first, so a document's chunks
+// normally run on one XCD and the next chunk finds the document's hot records in that XCD's L2; a wave
+// whose queue is exhausted helps the others.  Correctness never depends on where a wave runs: every
+// hand-over is an agent-scope release (after the chunk's stores) and acquire (before the next chunk's
+// loads), as for any two workgroups.  In queue q, ticket t = c * n_q + j names document d = j * nq + q;
+// it waits for ticket t - n_q (the same document's previous chunk), which a running wave took earlier, so
+// the waits always drain.  A wait longer than `spins` polls raises the abort flag and every wave leaves
+// between tickets (each document's state is then consistent at its op_next); mtb_replay_finish_kernel,
+// launched right after, replays the rest of every document when the flag is set.
+// sched: [32 q] next ticket of queue q (one line each), [MTB_SCHED_ABORT] abort flag, [MTB_SCHED_HDR + d]
+// chunks of document d completed (zeroed before launch), [MTB_SCHED_HDR + ndocs + c] the plan: cumulative
+// record fraction of chunk c in 1/4096 (the last one 4096).
 // one ticket: the replay engine as a called function (its register allocation stays the replay kernel's
 // instead of being shaped by the ticket loop around it)
 __device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, DocState* docs, uint32_t ndocs,
@@ -3578,36 +3601,62 @@ __device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, 
                                                        const Tables& tables, uint32_t upto) {
   replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, upto);
 }
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_replay_sched_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
-                            uint32_t* sched, uint32_t nchunks) {
+                            uint32_t* sched, uint32_t nchunks, uint32_t nq, uint32_t spins) {
   __shared__ Scratch sh;
   const int lane = lane_id();
-  const uint32_t total = ndocs * nchunks;
-  for (;;) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&sched[0], 1u);
-    t = U(t);
-    if (t >= total) break;
-    if (U(__hip_atomic_load(&sched[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) break;
-    const uint32_t d = t % ndocs, c = t / ndocs;
-    if (c > 0) {
-      uint32_t spins = 0;
-      while (U(__hip_atomic_load(&sched[2 + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c && spins < MTB_SCHED_SPINS) {
-        spins++;
-        __builtin_amdgcn_s_sleep(16);
+  const uint32_t home = xcc_id() % nq;
+  for (uint32_t qi = 0; qi < nq; qi++) {
+    const uint32_t q = (home + qi) % nq;
+    if (q >= ndocs) continue;
+    const uint32_t nqd = (ndocs - q + nq - 1) / nq;  // documents of queue q
+    const uint32_t total = nqd * nchunks;
+    for (;;) {
+      if (U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) return;
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(&sched[MTB_SCHED_TICK * q], 1u);
+      t = U(t);
+      if (t >= total) break;
+      const uint32_t j = t % nqd, c = t / nqd;
+      const uint32_t d = j * nq + q;
+      uint32_t* prog = &sched[MTB_SCHED_HDR + d];
+      if (c > 0) {
+        uint32_t n = 0;
+        bool ready;
+        while (!(ready = U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= c) && n < spins) {
+          n++;
+          __builtin_amdgcn_s_sleep(16);
+        }
+        if (!ready) {
+          if (lane == 0) __hip_atomic_store(&sched[MTB_SCHED_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
       }
-      if (spins >= MTB_SCHED_SPINS) {
-        if (lane == 0) __hip_atomic_store(&sched[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
+      sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
+                   U(sched[MTB_SCHED_HDR + ndocs + c]));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X guide: the write-back completes before the flag)
+      if (lane == 0) __hip_atomic_store(prog, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, U(sched[2 + ndocs + c]));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (lane == 0) __hip_atomic_store(&sched[2 + d], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+// After an aborted scheduled launch: every document continues from its op_next (one wave per document;
+// documents that finished have nothing left).  Without an abort every wave leaves at once.
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_replay_finish_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
+                             const uint32_t* sched) {
+  __shared__ Scratch sh;
+  if (U(sched[MTB_SCHED_ABORT]) == 0) return;
+  replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
 // The same engine for batches of few documents (at most a few per CU, e.g. BASELINE configs[3]'s single
 // long document): LDS is not what limits occupancy there, so the zamboni LRU heap keeps up to 2,047
@@ -3618,21 +3667,27 @@ extern "C" __global__ void __launch_bounds__(64, 1)
   __shared__ ScratchBig sh;
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+#endif
 // Batches holding live clients (local ops, acks of them): the replay engine with the local-op paths.
+#if MTB_TU_HAS(MTB_TU_LIVE)
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_live_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                     WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
   __shared__ Scratch sh;
   replay_doc<MODE_LIVE>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+#endif
 // Batches whose documents carry marker ids: the replay engine with idToSegment and relative positions.
+#if MTB_TU_HAS(MTB_TU_MARKERS)
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_markers_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                        WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
   __shared__ Scratch sh;
   replay_doc<MODE_MARKERS>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+#endif
 // SnapshotV1 body append (LOADSEG records), run before mtb_replay_kernel when a load is pending.
+#if MTB_TU_HAS(MTB_TU_LOADMAT)
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_load_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                     WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
@@ -3651,47 +3706,63 @@ extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
                           aux, freel, tables);
 }
 
-// Up to MTB_FEW_DOCS documents (at most ~4 per CU) replay on the large-LDS-heap variant.
-#define MTB_FEW_DOCS 1024
-hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
-                             FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                             Tables tables, int variant) {
-  if (variant == 1)
-    hipLaunchKernelGGL(mtb_live_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
-                       aux, freel, tables);
-  else if (variant == 2)
-    hipLaunchKernelGGL(mtb_markers_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
-                       heap, aux, freel, tables);
-  else if (ndocs <= MTB_FEW_DOCS)
-    hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
-                       heap, aux, freel, tables);
-  else
-    hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
-                       aux, freel, tables);
-  return hipGetLastError();
-}
-hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
-                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves) {
-  hipLaunchKernelGGL(mtb_replay_sched_kernel, dim3(waves), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text,
-                     heap, aux, freel, tables, sched, nchunks);
-  return hipGetLastError();
-}
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables) {
-  hipLaunchKernelGGL(mtb_matrix_kernel, dim3((ndocs + 1) / 2), dim3(128), 0, stream, docs, ndocs, ops, segp, blks, lists,
-                     text, heap, aux, freel, tables);
+  hipLaunchKernelGGL(mtb_matrix_kernel, dim3((ndocs + 1) / 2), dim3(128), 0, stream, KARGS);
   return hipGetLastError();
 }
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables) {
-  hipLaunchKernelGGL(mtb_load_kernel, dim3(ndocs), dim3(64), 0, stream, docs, ndocs, ops, segp, blks, lists, text, heap,
-                     aux, freel, tables);
+  hipLaunchKernelGGL(mtb_load_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
   return hipGetLastError();
 }
-
+#endif
+#define KPARAMS hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp, FBlk* blks, \
+                WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables
+#if MTB_TU_HAS(MTB_TU_OBS)
+// Up to MTB_FEW_DOCS documents (at most ~4 per CU) replay on the large-LDS-heap variant.
+#define MTB_FEW_DOCS 1024
+hipError_t mtb_launch_observer(KPARAMS) {
+  if (ndocs <= MTB_FEW_DOCS)
+    hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  else
+    hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  return hipGetLastError();
+}
+hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
+                                   uint32_t nq, uint32_t spins) {
+  hipLaunchKernelGGL(mtb_replay_sched_kernel, dim3(waves), dim3(64), 0, stream, KARGS, sched, nchunks, nq, spins);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mtb_replay_finish_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS, (const uint32_t*)sched);
+  return hipGetLastError();
+}
+#endif
+#if MTB_TU_HAS(MTB_TU_LIVE)
+hipError_t mtb_launch_live(KPARAMS) {
+  hipLaunchKernelGGL(mtb_live_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  return hipGetLastError();
+}
+#endif
+#if MTB_TU_HAS(MTB_TU_MARKERS)
+hipError_t mtb_launch_markers(KPARAMS) {
+  hipLaunchKernelGGL(mtb_markers_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  return hipGetLastError();
+}
+#endif
+#if MTB_TU_HAS(MTB_TU_MISC)
+hipError_t mtb_launch_observer(KPARAMS);
+hipError_t mtb_launch_live(KPARAMS);
+hipError_t mtb_launch_markers(KPARAMS);
+hipError_t mtb_launch_replay(KPARAMS, int variant) {
+  if (variant == 1) return mtb_launch_live(stream, ndocs, docs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+  if (variant == 2) return mtb_launch_markers(stream, ndocs, docs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+  return mtb_launch_observer(stream, ndocs, docs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
 // ---------------------------------------------------------------------- state digest v1
 // One wave per document folds the replayed state -- every segment in tree order with its tree path,
 // text (or marker / handle span), seq, client, removal info and properties -- into 64 bits
@@ -3933,3 +4004,4 @@ hipError_t mtb_launch_move_u16(hipStream_t stream, const uint16_t* src, const ui
   hipLaunchKernelGGL(mtb_move_u16_kernel, dim3(n), dim3(64), 0, stream, src, src_off, dst, dst_off, len, n);
   return hipGetLastError();
 }
+#endif  // MTB_TU_HAS(MTB_TU_MISC)

@@ -111,8 +111,29 @@ enum {
   MTB_E_INSERT = -5,      /* UsageError("MergeTree insert failed") mergeTree.ts:1671 */
   MTB_E_UNSUPPORTED = -6, /* input outside the engine's supported subset */
   MTB_E_CAPACITY = -7,    /* a per-document arena overflowed */
-  MTB_E_PARSE = -8        /* malformed JSON message */
+  MTB_E_PARSE = -8,       /* malformed JSON message */
+  MTB_E_INTERNAL = -9     /* an engine invariant failed (e.g. a document did not run all of its records) */
 };
+
+/* What the last mtb_replay / mtb_replay_resident launched (diagnostics; no reference counterpart: the
+ * reference applies each message synchronously in Client.applyMsg, client.ts:858). */
+enum {
+  MTB_KERNEL_NONE = 0,
+  MTB_KERNEL_REPLAY = 1,   /* one wave per document */
+  MTB_KERNEL_SCHED = 2,    /* ticket-scheduled persistent waves (more documents than resident waves) */
+  MTB_KERNEL_FEW = 3,      /* one wave per document, large LDS heap (few documents) */
+  MTB_KERNEL_LIVE = 4,     /* live clients (local ops, acks, reconnect) */
+  MTB_KERNEL_MARKERS = 5,  /* marker ids / relative positions */
+  MTB_KERNEL_MATRIX = 6    /* SharedMatrix vector pairs */
+};
+typedef struct mtb_launch_info {
+  uint32_t kernel;      /* MTB_KERNEL_* */
+  uint32_t wave_slots;  /* resident replay waves of the device (CUs x 16) */
+  uint32_t chunks;      /* MTB_KERNEL_SCHED: tickets per document */
+  uint32_t queues;      /* MTB_KERNEL_SCHED: ticket queues (one per XCD) */
+  uint32_t aborted;     /* MTB_KERNEL_SCHED: a ticket wait hit its bound and the finish kernel ran the rest */
+  uint32_t pad;
+} mtb_launch_info;
 
 /* device_mask: the HIP devices the batch spreads over (bit k = device k; 0 = device 0).  With several,
  * documents are assigned by hash(document index) mod the device count (SharedMatrix batches: whole
@@ -214,6 +235,9 @@ int mtb_doc_checksum(mtb_batch* b, uint32_t doc, uint64_t* out);
 /* State digests v1 (DESIGN.md "State digest": the canonical dump's content folded into 64 bits on the
  * GPU by every replay) of documents [first, first + n), from the last replay; 0 for a failed document. */
 int mtb_doc_digests(mtb_batch* b, uint32_t first, uint32_t n, uint64_t* out);
+
+/* The kernel the last replay launched (first device of a multi-device batch; `aborted` of any). */
+int mtb_get_launch_info(mtb_batch* b, mtb_launch_info* out);
 /* MergeTree.mapRange / nodeMap (mergeTree.ts:2456-2474, 2531-2582) over [start, end) (end < 0: to the end)
  * in the view of (ref_seq, long_client_id) (ref_seq < 0: currentSeq; long_client_id NULL: the observer,
  * i.e. the local view).  Serves Client.walkSegments (client.ts:286), getContainingSegment (:1065) and

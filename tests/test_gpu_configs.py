@@ -149,21 +149,27 @@ def _message_cut(lb, u, frac):
     return m
 
 
-@pytest.mark.parametrize("chunks", [None, "16", "3"])
-def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks):
+@pytest.mark.parametrize("chunks,queues,spins", [(None, None, None), ("16", None, None), ("3", "1", None),
+                                                 (None, None, "0"), ("16", "1", "40")])
+def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, queues, spins):
     """More documents than the device's resident replay waves runs the ticket-scheduled kernel (persistent
     waves, documents advanced chunk by chunk in round-robin): 4,608 documents with ragged record counts --
     whole 300-message logs, message-boundary prefixes of them, and documents with no records -- every
     state digest equal to the oracle's, for the default shrinking-chunk plan and for 16 and 3 equal chunks
-    per document (MTB_CHUNKS)."""
+    per document (MTB_CHUNKS), per-XCD ticket queues and one global queue (MTB_SCHED_QUEUES=1), and with
+    the ticket waits bounded so low that the scheduler aborts (MTB_SCHED_SPINS): the finish kernel then
+    replays the rest of every document and the results are the same."""
+    import torch
     from pyloggen import LogBatch, make_cfg
     monkeypatch.delenv("MTB_CHUNK_PLAN", raising=False)
-    if chunks is None:
-        monkeypatch.delenv("MTB_CHUNKS", raising=False)
-    else:
-        monkeypatch.setenv("MTB_CHUNKS", chunks)
+    for var, val in (("MTB_CHUNKS", chunks), ("MTB_SCHED_QUEUES", queues), ("MTB_SCHED_SPINS", spins)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, val)
     lb = LogBatch(make_cfg(seed=606, n_ops=300), 0, 48)
-    n = 4608
+    slots = torch.cuda.get_device_properties(0).multi_processor_count * 16
+    n = slots + slots // 8  # more documents than resident replay waves
     B = _batch(n)
     props = lb.props_json()
     assert [B.intern_props(p) if p else 0 for p in props] == list(range(len(props)))
@@ -191,6 +197,10 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks):
             want.append(prefix[(u, m)])
     st = B.replay()
     assert st["errors"] == 0
+    li = B.launch_info()
+    assert li["kernel"] == "mtb_replay_sched_kernel" and li["wave_slots"] == slots, li
+    if spins == "0":
+        assert li["aborted"], li  # every hand-over wait gives up at once
     dg = B.digests()
     bad = [j for j in range(n) if dg[j] != want[j]]
     assert not bad, f"{len(bad)}/{n} documents' digests differ from the oracle (first: {bad[:5]})"
