@@ -584,6 +584,9 @@ static napi_value js_summarize_v1_many(napi_env env, napi_callback_info info) {
   int rc = mtb_summarize_v1_many(b, n, docs, msn, seq, threads, ls);
   free(docs);
   if (rc) {
+    /* the documents (and shards) that succeeded filled their lists before the call failed */
+    for (uint32_t i = 0; i < n; i++)
+      if (ls[i].count || ls[i].blobs || ls[i].summary_json) mtb_blob_list_free(&ls[i]);
     free(ls);
     return throw_rc(env, b, rc);
   }

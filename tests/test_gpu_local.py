@@ -188,3 +188,11 @@ def test_local_op_out_of_range_fails_at_replay():
     B[0].removeRangeLocal(1, 2)  # start at the length: RangeOutOfBounds
     with pytest.raises(MergeTreeError):
         B.replay()
+
+
+@pytest.mark.parametrize("seed,n_clients", [(36, 2), (9, 6)])
+def test_reconnect_farm_reference_divergence(seed, n_clients):
+    """General reconnect farms whose clients end up diverged by the reference's own normalizeAdjacentSegments
+    (tests/test_reference_kats.py::test_reconnect_normalization_reorders_sequenced_segments): the engine
+    still equals each oracle client after every round, diverged state included."""
+    assert _replay_farm(seed, n_clients=n_clients, n_rounds=60, new_mode=True, annotate=True, reconnect=0.2) > 0

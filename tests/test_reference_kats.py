@@ -369,3 +369,68 @@ def test_reference_shaped_conflict_farm(min_length, n_clients):
     from helpers import run_ref_conflict_farm
     clients = run_ref_conflict_farm(0, n_clients, min_length)
     assert len({c.get_text() for c in clients}) == 1
+
+
+def _acked_order(doc):
+    """Text of every sequenced segment (removed ones included) in tree order, from the canonical dump."""
+    import json as _json
+    out = []
+    for line in doc.dump_segments().split("\n")[1:]:
+        if line.strip():
+            _, _, text, seq, *_ = _json.loads(line)
+            if seq != -1:
+                out.append(text)
+    return "".join(out).encode("utf-16-le", "surrogatepass").decode("utf-16-le", "surrogatepass")
+
+
+def test_reconnect_normalization_reorders_sequenced_segments():
+    """Why ~1 in 100 general reconnect farms (helpers.run_local_farm, reconnect > 0) diverge: the reference's
+    normalizeAdjacentSegments (mergeTree.ts:2234-2336), run by regeneratePendingOp (client.ts:917-960), slides
+    remotely removed (acked) segments after the run's last segment that is not removed-and-acked -- and that
+    segment may be an acked insert that is only *locally* removed.  The reconnecting client then holds two
+    sequenced segments in an order no other client has.  Farm (seed 36, 2 clients, new length calculation),
+    client c1, regeneration at currentSeq 51: the run [f (local insert, local remove), "\\n", "x" (removed at
+    49), "xyzx" (removed at 50), "yzxy", "z" (seq 45, local remove)] becomes [f, "yzxy", "z", "\\n", "x",
+    "xyzx"], while every receiver of the regenerated ops keeps [f, "\\n", "x", "xyzx", "yzxy", "z"]
+    (insertingWalk places f before the zero-length tombstones; removes move nothing).  c0's insert at seq 58
+    (refSeq 47: "xyzx" and "yzxy" both still visible to it) then resolves pos 23 at different places on c1
+    and on the rest, and the texts diverge.  The reference's own reconnect farm
+    (client.reconnectFarm.spec.ts:25-121) never sends an op whose refSeq predates the overlapped removes, so
+    it cannot see this; the oracle follows mergeTree.ts step for step here, and the engine matches the oracle
+    client for client on this farm (tests/test_gpu_local.py::test_reconnect_farm_reference_divergence)."""
+    from helpers import run_local_farm
+    from pyoracle import OracleDoc
+    rec = {}
+    clients, obs, _ = run_local_farm(36, n_clients=2, n_rounds=60, new_mode=True, annotate=True, reconnect=0.2,
+                                     record=rec)
+    c1 = OracleDoc(new_length_calc=True)
+    c1.insert_text_local(0, "hello world")
+    c1.start_collab(rec["ids"][1])
+    o = OracleDoc(new_length_calc=True)
+    o.insert_text_local(0, "hello world")
+    o.start_collab("obs")
+    stop = False
+    for rnd in rec["rounds"]:
+        for kind, x in rnd[1][0]:
+            if kind == "msg" and x["sequenceNumber"] == 58:
+                stop = True
+                break
+            if kind == "local":
+                if x["type"] == 0:
+                    c1.insert_local_op(x["pos1"], x["seg"])
+                elif x["type"] == 1:
+                    c1.remove_local_op(x["pos1"], x["pos2"])
+                else:
+                    c1.annotate_local_op(x["pos1"], x["pos2"], x["props"])
+            elif kind == "regen":
+                c1.regenerate_pending_op(x[0])
+            else:
+                c1.apply_msg(x)
+                o.apply_msg(x)
+        if stop:
+            break
+    assert c1.current_seq == o.current_seq == 57
+    mine, theirs = _acked_order(c1), _acked_order(o)
+    assert "\U0001F600def" + "yzxyz" + "\nx" + "xyzx" + "yzxy" in mine
+    assert "\U0001F600def" + "\nx" + "xyzx" + "yzxyz" + "yzxy" in theirs
+    assert clients[0].get_text() == obs.get_text() and clients[1].get_text() != obs.get_text()

@@ -7,7 +7,7 @@ mkdir -p $O
 export TMPDIR=/tmp MTB_LOG_CACHE=/tmp/mtb_logs
 (while sleep 50; do echo "hb $(date +%T)" >> $O/heartbeat; done) & HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_configs.py -k scheduled > $O/pytest_sched.log 2>&1
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_configs.py tests/test_gpu_local.py tests/test_gpu_matrix.py -k "scheduled or divergence or conflict_kats" > $O/pytest_sched.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_sched.log; [ $rc -ne 0 ] && exit $rc
 B="bench.py --no-cpu --no-summary --steps 3 --warmup 1 --traffic off"
 for q in 8 1; do
