@@ -7,6 +7,8 @@ export TMPDIR=/tmp MTB_LOG_CACHE=/tmp/mtb_logs MTB_NO_TORCH=1
 (while sleep 50; do echo "hb $(date +%T)" >> $O/heartbeat; done) & HB=$!
 trap "kill $HB" EXIT
 B="bench.py --no-cpu --no-summary --steps 1 --warmup 0 --parity-sample 4 --traffic off"
+timeout -k 10 600 python3 bench.py --no-cpu --no-summary --steps 3 --warmup 1 --traffic off > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json; [ $rc -ne 0 ] && exit $rc
 for v in prof profpack; do
   MTB_LIB=fluidframework_amd/libmtb_$v.so MTB_PROFILE_OUT=1 timeout -k 10 600 python3 $B > $O/bench_$v.json 2> $O/bench_$v.err
   rc=$?; echo "$v rc=$rc"; grep mtb_profile $O/bench_$v.err; [ $rc -ne 0 ] && exit $rc
