@@ -51,6 +51,10 @@ hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, c
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables);
+hipError_t mtb_launch_extract_v1(hipStream_t stream, const DocState* docs, const uint32_t* list, uint32_t n,
+                                 const FBlk* blks, const uint16_t* text, const uint32_t* aux, const uint32_t* pool,
+                                 const uint32_t* vcl, uint32_t* cnt, const uint64_t* off, uint32_t* items,
+                                 uint16_t* otext, uint32_t* owords);
 hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState* docs, const FBlk* blks,
                              const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint64_t* khash,
                              const uint64_t* vhash, uint64_t* out);
@@ -1976,6 +1980,12 @@ uint64_t utf8_byte_length(const std::string& utf8) {
   return (uint64_t)n;
 }
 
+void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::string>& segJson, const std::vector<int>& segLen,
+                    std::vector<std::pair<std::string, std::string>>& blobs, std::string& tree, uint64_t& totalBytes);
+#define EX_INLINE_HOST 0x40000000u  // mtb_extract_v1_kernel: a property set copied into the words output
+void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni, const uint16_t* txt, const uint32_t* words,
+                     std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson);
+
 // SnapshotV1.extractSync + emit (snapshotV1.ts:122-312) over the downloaded document.
 void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
   download_doc(b, i);
@@ -2029,7 +2039,9 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
   for (auto& f : fl) {
     const Seg& g = d.segs[f.id];
     if (seg_pending(g.seq)) continue;                         // seq === UnassignedSequenceNumber
-    if (seg_removed(g) && g.rseq <= minSeq) continue;  // elided
+    // elided: removedSeq <= minSeq, which includes an unacked local removal (removedSeq ===
+    // UnassignedSequenceNumber = -1, snapshotV1.ts:218)
+    if (seg_removed(g) && (seg_pending(g.rseq) || g.rseq <= minSeq)) continue;
     if (g.seq <= minSeq && (!seg_removed(g) || seg_pending(g.rseq))) {
       const bool marker = !perm && is_marker(g);
       if (perm) {  // PermutationSegment.canAppend: both unallocated, or contiguous handles
@@ -2099,6 +2111,32 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
     segLen.push_back(g.len);
   }
   pushPrev();
+  std::string tree;
+  uint64_t totalBytes = 0;
+  emit_v1_chunks(b, minSeq, curSeq, segJson, segLen, blobs, tree, totalBytes);
+  if (perm) {
+    // PermutationVector.summarize (permutationvector.ts:310-325): {segments: <SnapshotV1>, handleTable}
+    const std::string ht = handle_table_json(d);
+    std::string outer = "{\"segments\":{\"type\":1,\"tree\":" + tree + "},\"handleTable\":{\"type\":2,\"content\":";
+    hj::quote(outer, hj::from_utf8(ht));
+    outer += "}}";
+    totalBytes += utf8_byte_length(ht);
+    summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + outer + "},\"stats\":{\"treeNodeCount\":2,\"blobNodeCount\":" +
+                  std::to_string(blobs.size() + 1) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
+                  ",\"unreferencedBlobSize\":0}}";
+    for (auto& bl : blobs) bl.first = "segments/" + bl.first;
+    blobs.push_back({"handleTable", ht});
+    return;
+  }
+  summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
+                std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
+                ",\"unreferencedBlobSize\":0}}";
+}
+
+// SnapshotV1.emit (snapshotV1.ts:122-178): the serialized segments cut into chunks of about chunkSize
+// UTF-16 units (header + body_i) and the summary tree's blobs (runtime-utils summaryUtils.ts:138-198)
+void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::string>& segJson, const std::vector<int>& segLen,
+                    std::vector<std::pair<std::string, std::string>>& blobs, std::string& tree, uint64_t& totalBytes) {
   const int chunkSize = b->opts.chunk_size > 0 ? b->opts.chunk_size : 10000;
   struct Chunk { int start = 0, count = 0, length = 0; };
   std::vector<Chunk> chunks;
@@ -2138,8 +2176,8 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
   blobs.push_back({"header", chunkText(chunks[0], true)});
   for (size_t k = 1; k < chunks.size(); k++) blobs.push_back({"body_" + std::to_string(k - 1), chunkText(chunks[k], false)});
   // ISummaryTreeWithStats (runtime-utils summaryUtils.ts:138-198)
-  std::string tree = "{";
-  uint64_t totalBytes = 0;
+  tree = "{";
+  totalBytes = 0;
   for (size_t k = 0; k < blobs.size(); k++) {
     if (k) tree += ',';
     tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
@@ -2148,20 +2186,84 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
     totalBytes += utf8_byte_length(blobs[k].second);
   }
   tree += "}";
-  if (perm) {
-    // PermutationVector.summarize (permutationvector.ts:310-325): {segments: <SnapshotV1>, handleTable}
-    const std::string ht = handle_table_json(d);
-    std::string outer = "{\"segments\":{\"type\":1,\"tree\":" + tree + "},\"handleTable\":{\"type\":2,\"content\":";
-    hj::quote(outer, hj::from_utf8(ht));
-    outer += "}}";
-    totalBytes += utf8_byte_length(ht);
-    summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + outer + "},\"stats\":{\"treeNodeCount\":2,\"blobNodeCount\":" +
-                  std::to_string(blobs.size() + 1) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
-                  ",\"unreferencedBlobSize\":0}}";
-    for (auto& bl : blobs) bl.first = "segments/" + bl.first;
-    blobs.push_back({"handleTable", ht});
-    return;
+}
+
+// SnapshotV1 of a SharedString document from the device extraction (mtb_extract_v1_kernel): the same JSON
+// as summarize() without downloading the tree.
+void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni, const uint16_t* txt, const uint32_t* words,
+                     std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
+  const HostDoc& d = b->docs[i];
+  const DocState& s = b->hst[i];
+  const int minSeq = s.min_seq, curSeq = s.cur_seq;
+  std::vector<std::string> segJson;
+  std::vector<int> segLen;
+  segJson.reserve(ni);
+  segLen.reserve(ni);
+  auto pview = [&](uint32_t h) {
+    PropView v;
+    if (!h) return v;
+    if (h & MTB_GPROPS) v.p = b->in.pool.data() + (h & ~MTB_GPROPS);
+    else v.p = words + (h & ~EX_INLINE_HOST);
+    return v;
+  };
+  for (uint32_t k = 0; k < ni; k++) {
+    const uint32_t* it = items + 8 * (size_t)k;
+    const uint32_t fl = it[0], len = it[1], toff = it[2];
+    const bool marker = (fl & 2u) != 0;
+    const uint32_t refType = fl >> 8;
+    std::string o;
+    PropView pv = pview(it[3]);
+    const bool hasProps = pv.n() > 0;  // empty props normalized to undefined (snapshotV1.ts:199-206)
+    std::string js;
+    if (marker) {
+      js += "{\"marker\":{";
+      if (refType) js += "\"refType\":" + std::to_string(refType - 1);
+      js += "}";
+      if (hasProps) { js += ",\"props\":"; props_json(b, js, pv); }
+      js += "}";
+    } else if (hasProps) {
+      js += "{\"text\":";
+      hj::quote(js, reinterpret_cast<const char16_t*>(txt + toff), len);
+      js += ",\"props\":";
+      props_json(b, js, pv);
+      js += "}";
+    } else {
+      hj::quote(js, reinterpret_cast<const char16_t*>(txt + toff), len);
+    }
+    if (!(fl & 1u)) {  // a coalesced (or single) segment below the MSN
+      segJson.push_back(std::move(js));
+      segLen.push_back((int)len);
+      continue;
+    }
+    const int seq = (int)it[4], rseq = (int)it[6];
+    const uint32_t cli = it[5];
+    o = "{\"json\":" + js;
+    if (seq > minSeq) {
+      o += ",\"seq\":" + std::to_string(seq) + ",\"client\":";
+      hj::quote(o, hj::from_utf8(d.longId((int)(int16_t)(cli & 0xFFFF))));
+    }
+    if (rseq >= 0) {
+      const int rc0 = (int)(int16_t)(cli >> 16);
+      o += ",\"removedSeq\":" + std::to_string(rseq) + ",\"removedClient\":";
+      hj::quote(o, hj::from_utf8(d.longId(rc0)));
+      o += ",\"removedClientIds\":[";
+      hj::quote(o, hj::from_utf8(d.longId(rc0)));
+      if (it[7] != MTB_NONE) {
+        const uint32_t* rc = words + it[7];
+        for (uint32_t q = 0; q < rc[0]; q++) {
+          o += ',';
+          hj::quote(o, hj::from_utf8(d.longId((int)rc[1 + q])));
+        }
+      }
+      o += "]";
+    }
+    o += "}";
+    segJson.push_back(std::move(o));
+    segLen.push_back((int)len);
   }
+  std::string tree;
+  uint64_t totalBytes = 0;
+  emit_v1_chunks(b, minSeq, curSeq, segJson, segLen, blobs, tree, totalBytes);
   summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
                 std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
                 ",\"unreferencedBlobSize\":0}}";
@@ -3255,7 +3357,77 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
       }
       replay(b, nullptr);
     }
-    download_docs(b, list);
+    PhaseClock pc;
+    // SharedString documents: extractSync on the device (mtb_extract_v1_kernel), only its output comes back;
+    // PermutationVectors and failed documents take the host path over the downloaded tree
+    std::vector<uint32_t> fast, slow;  // positions in `list`
+    for (uint32_t k = 0; k < n; k++) {
+      const uint32_t i = list[k];
+      const bool dev = b->devInit && i < b->hst.size() && b->docs[i].onDevice && !b->docs[i].perm && !b->hst[i].err &&
+                       !getenv("MTB_HOST_SUMMARY");
+      (dev ? fast : slow).push_back(k);
+    }
+    const uint32_t nf = (uint32_t)fast.size();
+    std::unique_ptr<uint32_t[]> hItems, hWords;
+    std::unique_ptr<uint16_t[]> hText;
+    std::vector<uint64_t> off(3 * (size_t)nf + 3, 0);
+    std::vector<uint32_t> cnt(3 * (size_t)nf + 3, 0);
+    if (nf) {
+      std::vector<uint32_t> ids(nf);
+      for (uint32_t f = 0; f < nf; f++) ids[f] = list[fast[f]];
+      DevBuf<uint32_t> dl, dc;
+      DevBuf<uint64_t> doff;
+      dl.ensure(nf);
+      dc.ensure(3 * (size_t)nf);
+      HIPCHK(hipMemcpyAsync(dl.p, ids.data(), nf * sizeof(uint32_t), hipMemcpyHostToDevice, b->stream));
+      HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
+                                   b->dValClass.p, dc.p, nullptr, nullptr, nullptr, nullptr));
+      HIPCHK(hipMemcpyAsync(cnt.data(), dc.p, 3 * (size_t)nf * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+      HIPCHK(hipStreamSynchronize(b->stream));
+      pc.mark("extract_count");
+      uint64_t ti = 0, tt = 0, tw = 0;
+      for (uint32_t f = 0; f < nf; f++) {
+        if (cnt[3 * f] == MTB_NONE) {  // the device walk did not trust the tree: host path
+          slow.push_back(fast[f]);
+          cnt[3 * f] = cnt[3 * f + 1] = cnt[3 * f + 2] = 0;
+        }
+        off[3 * f] = 8 * ti;
+        off[3 * f + 1] = tt;
+        off[3 * f + 2] = tw;
+        ti += cnt[3 * f];
+        tt += cnt[3 * f + 1];
+        tw += cnt[3 * f + 2];
+      }
+      DevBuf<uint32_t> di, dw;
+      DevBuf<uint16_t> dt;
+      di.ensure(8 * ti + 8);
+      dt.ensure(tt + 1);
+      dw.ensure(tw + 1);
+      doff.ensure(3 * (size_t)nf);
+      HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
+      HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
+                                   b->dValClass.p, dc.p, doff.p, di.p, dt.p, dw.p));
+      hItems.reset(new uint32_t[8 * ti + 8]);
+      hText.reset(new uint16_t[tt + 1]);
+      hWords.reset(new uint32_t[tw + 1]);
+      if (ti) HIPCHK(hipMemcpyAsync(hItems.get(), di.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+      if (tt) HIPCHK(hipMemcpyAsync(hText.get(), dt.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
+      if (tw) HIPCHK(hipMemcpyAsync(hWords.get(), dw.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+      HIPCHK(hipStreamSynchronize(b->stream));
+      pc.mark("extract_emit_download");
+    }
+    std::vector<uint8_t> onDev(n, 0);
+    std::vector<uint32_t> fpos(n, 0);
+    for (uint32_t f = 0; f < nf; f++) {
+      onDev[fast[f]] = 1;
+      fpos[fast[f]] = f;
+    }
+    for (uint32_t k : slow) onDev[k] = 0;
+    if (!slow.empty()) {
+      std::vector<uint32_t> sl;
+      for (uint32_t k : slow) sl.push_back(list[k]);
+      download_docs(b, sl);
+    }
     std::vector<std::string> errs(n);
     std::atomic<uint32_t> next{0};
     auto work = [&] {
@@ -3263,7 +3435,13 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
         try {
           std::vector<std::pair<std::string, std::string>> blobs;
           std::string summary;
-          summarize(b, list[k], blobs, summary);
+          if (onDev[k]) {
+            const uint32_t f = fpos[k];
+            summarize_items(b, list[k], hItems.get() + off[3 * f], cnt[3 * f], hText.get() + off[3 * f + 1],
+                            hWords.get() + off[3 * f + 2], blobs, summary);
+          } else {
+            summarize(b, list[k], blobs, summary);
+          }
           fill_blob_list(blobs, summary, &out[k]);
         } catch (const MtbError& e) {
           errs[k] = e.msg;
@@ -3279,6 +3457,7 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
     work();
     for (auto& t : ts) t.join();
+    pc.mark("serialize");
     for (uint32_t k = 0; k < n; k++)
       if (!errs[k].empty()) raise(MTB_E_ARG, "document " + std::to_string(list[k]) + ": " + errs[k]);
   });

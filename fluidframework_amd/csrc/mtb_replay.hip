@@ -3929,6 +3929,214 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------- SnapshotV1 extraction
+// SnapshotV1.extractSync (snapshotV1.ts:180-312) on the device, one wave per listed document: the leaves in
+// tree order, elided (unacked inserts; removedSeq <= minSeq, which includes an unacked removal), coalesced
+// (below the MSN and not removed: TextSegment.canAppend + matchProperties, or PermutationSegment.canAppend)
+// or kept with their merge info.  The host serializes the result (mtb_host.cpp summarize_items) instead of
+// downloading the whole tree.  Per document the output is
+//   items : 8 words per snapshot segment: [flags (EX_META, EX_MARKER | refType+1 << 8), length, text offset
+//           (PermutationSegment: its start), props (0; MTB_GPROPS | pool offset; EX_INLINE | word offset of a
+//           copied [n, (k, v)*n] set), seq, client | removedClientIds[0] << 16, removedSeq, word offset of
+//           [n, c1..cn] further removers (MTB_NONE: none)]
+//   text  : the UTF-16 of every item (a coalesced run's pieces back to back)
+//   words : inlined per-document property sets and remover lists
+// Pass 1 (off == nullptr) counts (items, text units, words) into cnt[3 k]; pass 2 writes at off[3 k..].
+#define EX_META 1u
+#define EX_MARKER 2u
+#define EX_INLINE 0x40000000u
+namespace mtbk {
+__device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uint32_t* pool, const uint32_t* A,
+                                               const uint32_t* vcl) {
+  if (a == b) return true;
+  const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + a) : nullptr;
+  const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + b) : nullptr;
+  const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
+  if (na != nb) return false;
+  for (uint32_t i = 0; i < na; i++) {
+    const uint32_t k = pa[1 + 2 * i];
+    bool found = false;
+    for (uint32_t q = 0; q < nb; q++)
+      if (pb[1 + 2 * q] == k) {
+        if (vcl[pa[2 + 2 * i]] != vcl[pb[2 + 2 * q]]) return false;
+        found = true;
+        break;
+      }
+    if (!found) return false;
+  }
+  return true;
+}
+}  // namespace mtbk
+extern "C" __global__ void __launch_bounds__(64)
+    mtb_extract_v1_kernel(const DocState* __restrict__ docs, const uint32_t* list, uint32_t n, const FBlk* blks,
+                          const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint32_t* vcl,
+                          uint32_t* cnt, const uint64_t* off, uint32_t* items, uint16_t* otext, uint32_t* owords) {
+  __shared__ uint32_t ids[MTB_DG_DEPTH][MTB_MAXCH];
+  __shared__ int32_t bc[MTB_DG_DEPTH], nxt[MTB_DG_DEPTH];
+  __shared__ uint32_t rec[64];
+  const uint32_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (k >= n) return;
+  const DocState& s = docs[list[k]];
+  const FBlk* B = blks + s.blk_base;
+  const uint16_t* T = text + s.text_base;
+  const uint32_t* A = aux + s.aux_base;
+  const bool perm = (s.flags & DSF_PERM) != 0;
+  const int minSeq = s.min_seq;
+  const bool emit = off != nullptr;
+  uint32_t* I = emit ? items + off[3 * k] : nullptr;
+  uint16_t* OT = emit ? otext + off[3 * k + 1] : nullptr;
+  uint32_t* OW = emit ? owords + off[3 * k + 2] : nullptr;
+  uint32_t ni = 0, nt = 0, nw = 0;  // counts so far (uniform)
+  // the open coalescing candidate (`prev`): its item index, length, last UTF-16 unit, marker, props
+  bool open = false;
+  uint32_t p_item = 0, p_len = 0, p_props = 0, p_start = 0;
+  uint16_t p_last = 0;
+  bool p_marker = false;
+  // inline a per-document property set (global ones are referenced by pool offset)
+  auto props_out = [&](uint32_t h) -> uint32_t {
+    if (!h || (h & MTB_GPROPS)) return h;
+    const uint32_t m = 1 + 2 * U(A[h]);
+    if (emit)
+      for (uint32_t i = (uint32_t)lane; i < m; i += 64) OW[nw + i] = A[h + i];
+    const uint32_t o = EX_INLINE | nw;
+    nw += m;
+    return o;
+  };
+  auto copy_text = [&](uint32_t src, uint32_t len) {
+    if (emit)
+      for (uint32_t i = (uint32_t)lane; i < len; i += 64) OT[nt + i] = T[src + i];
+    nt += len;
+  };
+  auto close_prev = [&]() {
+    if (open && emit && lane == 0) I[8 * p_item + 1] = p_len;
+    open = false;
+  };
+  int d = 0;
+  auto enter = [&](uint32_t b, int dd) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(B + b);
+    const uint32_t v = w[lane];
+    const uint32_t c = w[FB_HDR];
+    rec[lane] = v;
+    if (lane < MTB_MAXCH) ids[dd][lane] = v;
+    if (lane == 0) {
+      bc[dd] = (int32_t)(c > MTB_MAXCH ? MTB_MAXCH : c);
+      nxt[dd] = 0;
+    }
+    __syncthreads();
+  };
+  const bool bad = s.err != 0 || s.root >= s.blk_used;
+  if (!bad) enter(s.root, 0);
+  while (!bad) {
+    const int c = bc[d], kk = nxt[d];
+    if (kk >= c) {
+      if (d == 0) break;
+      d--;
+      continue;
+    }
+    const uint32_t child = ids[d][kk];
+    if (!(child & MTB_LEAF)) {
+      if (lane == 0) nxt[d] = kk + 1;
+      __syncthreads();
+      if (d + 1 >= MTB_DG_DEPTH) break;
+      d++;
+      enter(child, d);
+      continue;
+    }
+    // a leaf-level block: its segments in order (uniform decisions, lane-parallel copies)
+    for (int j = 0; j < c; j++) {
+      const uint32_t len = U(rec[F_LEN * 8 + j]);
+      const int seq = (int)U(rec[F_SEQ * 8 + j]);
+      const int rseq = (int)U(rec[F_RSEQ * 8 + j]);
+      const uint32_t cli = U(rec[F_CLI * 8 + j]);
+      const uint32_t rcx = U(rec[F_RCX * 8 + j]);
+      const uint32_t props = U(rec[F_PROPS * 8 + j]);
+      const uint32_t txt = U(rec[F_TEXT * 8 + j]);
+      const bool removed = rseq >= 0;
+      if (seq >= MTB_PEND) continue;                                    // unacked insert
+      if (removed && (rseq >= MTB_PEND || rseq <= minSeq)) continue;    // removedSeq <= minSeq (-1 unacked)
+      const bool marker = !perm && (txt & MTB_MARKER);
+      if (seq <= minSeq && !removed) {
+        bool append = false;
+        if (open) {
+          if (perm) {
+            append = p_start == MTB_HANDLE_UNALLOC ? txt == MTB_HANDLE_UNALLOC : txt == p_start + p_len;
+          } else {
+            append = !p_marker && !marker && !(p_len > 0 && p_last == u'\n') && (p_len <= 256 || len <= 256) &&
+                     ex_props_match(p_props, props, pool, A, vcl);
+          }
+        }
+        if (append) {
+          if (!perm) {
+            copy_text(txt, len);
+            if (len) p_last = U((uint32_t)T[txt + len - 1]);
+          }
+          p_len += len;
+          continue;
+        }
+        close_prev();
+        // a new candidate item (its length is written when it closes)
+        const uint32_t po = perm ? 0u : props_out(props);
+        if (emit && lane < 8) {
+          const uint32_t v = lane == 0 ? (marker ? (EX_MARKER | (((txt & ~MTB_MARKER)) << 8)) : 0u)
+                             : lane == 2 ? (perm ? txt : marker ? 0u : nt) : lane == 3 ? po : 0u;
+          I[8 * ni + lane] = v;
+        }
+        open = true;
+        p_item = ni++;
+        p_len = len;
+        p_props = props;
+        p_start = txt;
+        p_marker = marker;
+        p_last = 0;
+        if (!perm && !marker) {
+          copy_text(txt, len);
+          if (len) p_last = U((uint32_t)T[txt + len - 1]);
+        }
+        continue;
+      }
+      // merge info kept: the candidate is emitted first
+      close_prev();
+      const uint32_t po = perm ? 0u : props_out(props);
+      uint32_t ro = MTB_NONE;
+      if (removed && rcx) {
+        const uint32_t m = 1 + U(A[rcx]);
+        if (emit)
+          for (uint32_t i = (uint32_t)lane; i < m; i += 64) OW[nw + i] = A[rcx + i];
+        ro = nw;
+        nw += m;
+      }
+      const uint32_t toff = nt;
+      if (!perm && !marker) copy_text(txt, len);
+      if (emit && lane < 8) {
+        const uint32_t v = lane == 0 ? (EX_META | (marker ? (EX_MARKER | (((txt & ~MTB_MARKER)) << 8)) : 0u))
+                           : lane == 1 ? len : lane == 2 ? (perm ? txt : toff) : lane == 3 ? po
+                           : lane == 4 ? (uint32_t)seq : lane == 5 ? cli : lane == 6 ? (uint32_t)rseq : ro;
+        I[8 * ni + lane] = v;
+      }
+      ni++;
+    }
+    __syncthreads();
+    if (lane == 0) nxt[d] = c;
+    __syncthreads();
+  }
+  close_prev();
+  if (!emit && lane == 0) {
+    cnt[3 * k] = bad ? MTB_NONE : ni;
+    cnt[3 * k + 1] = nt;
+    cnt[3 * k + 2] = nw;
+  }
+}
+hipError_t mtb_launch_extract_v1(hipStream_t stream, const DocState* docs, const uint32_t* list, uint32_t n,
+                                 const FBlk* blks, const uint16_t* text, const uint32_t* aux, const uint32_t* pool,
+                                 const uint32_t* vcl, uint32_t* cnt, const uint64_t* off, uint32_t* items,
+                                 uint16_t* otext, uint32_t* owords) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(mtb_extract_v1_kernel, dim3(n), dim3(64), 0, stream, docs, list, n, blks, text, aux, pool, vcl, cnt,
+                     off, items, otext, owords);
+  return hipGetLastError();
+}
+
 // Rewind every document to its post-init state (benchmark / re-replay utility): restores the
 // DocState header, the root block and the initial segment's parent; ops and payload stay resident.
 extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, uint32_t* segp,

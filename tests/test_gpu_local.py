@@ -196,3 +196,51 @@ def test_reconnect_farm_reference_divergence(seed, n_clients):
     (tests/test_reference_kats.py::test_reconnect_normalization_reorders_sequenced_segments): the engine
     still equals each oracle client after every round, diverged state included."""
     assert _replay_farm(seed, n_clients=n_clients, n_rounds=60, new_mode=True, annotate=True, reconnect=0.2) > 0
+
+
+@pytest.mark.parametrize("seed,reconnect", [(101, 0.0), (102, 0.0), (103, 0.3), (104, 0.3)])
+def test_live_client_summaries_match_oracle(seed, reconnect):
+    """SnapshotV1 of live clients with pending local ops (Client.summarize, snapshotV1.ts:180-312): unacked
+    inserts are elided and so are segments whose removal is still unacked (removedSeq ===
+    UnassignedSequenceNumber = -1 <= minSeq); engine summaries equal the oracle clients' after every round."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    rec = {}
+    run_local_farm(seed, n_clients=4, n_rounds=30, new_mode=seed % 2 == 0, annotate=True, record=rec,
+                   reconnect=reconnect)
+    ids = rec["ids"]
+    B = MergeTreeBatch(len(ids), new_length_calc=seed % 2 == 0)
+    orc = []
+    for k, cid in enumerate(ids):
+        B[k].insertTextLocal(0, "hello world")
+        B[k].startOrUpdateCollaboration(cid)
+        o = OracleDoc(new_length_calc=seed % 2 == 0)
+        o.insert_text_local(0, "hello world")
+        o.start_collab(cid)
+        orc.append(o)
+    pending_seen = 0
+    for r, rnd in enumerate(rec["rounds"]):
+        for k, (events, _, _) in enumerate(rnd):
+            for kind, x in events:
+                if kind == "local":
+                    B[k].applyLocalOp(x)
+                    if x["type"] == 0:
+                        orc[k].insert_local_op(x["pos1"], x["seg"])
+                    elif x["type"] == 1:
+                        orc[k].remove_local_op(x["pos1"], x["pos2"])
+                    else:
+                        orc[k].annotate_local_op(x["pos1"], x["pos2"], x["props"])
+                elif kind == "regen":
+                    B[k].regeneratePendingOp(x[0])
+                    orc[k].regenerate_pending_op(x[0])
+                else:
+                    B[k].applyMsg(x)
+                    orc[k].apply_msg(x)
+        B.replay()
+        for k in range(len(ids)):
+            pending_seen += orc[k].pending_groups() > 0
+            gb, gs = B.summarize_v1(k)
+            osum = orc[k].summarize_v1()
+            assert [list(b) for b in gb] == osum["blobs"], f"seed {seed} round {r} client {k}: summary blobs"
+            assert gs == osum["summary"], f"seed {seed} round {r} client {k}: summary tree"
+    assert pending_seen > 0
