@@ -2269,6 +2269,81 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
                 ",\"unreferencedBlobSize\":0}}";
 }
 
+// mtb_extract_v1_kernel over documents `ids` (count pass, offsets, emit pass, one download per output).
+// ok[k]: document ids[k] was extracted (a SharedString document replayed without error).
+struct Extracted {
+  std::vector<uint8_t> ok;
+  std::vector<uint32_t> cnt;
+  std::vector<uint64_t> off;
+  std::unique_ptr<uint32_t[]> items, words;
+  std::unique_ptr<uint16_t[]> text;
+};
+void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
+  const uint32_t n = (uint32_t)ids.size();
+  ex.ok.assign(n, 0);
+  ex.cnt.assign(3 * (size_t)n + 3, 0);
+  ex.off.assign(3 * (size_t)n + 3, 0);
+  std::vector<uint32_t> dev;  // positions in ids
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t i = ids[k];
+    if (b->devInit && i < b->hst.size() && b->docs[i].onDevice && !b->docs[i].perm && !b->hst[i].err &&
+        !getenv("MTB_HOST_SUMMARY"))
+      dev.push_back(k);
+  }
+  const uint32_t nf = (uint32_t)dev.size();
+  if (!nf) return;
+  std::vector<uint32_t> di(nf), cnt(3 * (size_t)nf);
+  for (uint32_t f = 0; f < nf; f++) di[f] = ids[dev[f]];
+  DevBuf<uint32_t> dl, dc, dItems, dWords;
+  DevBuf<uint16_t> dText;
+  DevBuf<uint64_t> doff;
+  dl.ensure(nf);
+  dc.ensure(3 * (size_t)nf);
+  HIPCHK(hipMemcpyAsync(dl.p, di.data(), nf * sizeof(uint32_t), hipMemcpyHostToDevice, b->stream));
+  HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
+                               b->dValClass.p, dc.p, nullptr, nullptr, nullptr, nullptr));
+  HIPCHK(hipMemcpyAsync(cnt.data(), dc.p, 3 * (size_t)nf * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  std::vector<uint64_t> off(3 * (size_t)nf);
+  uint64_t ti = 0, tt = 0, tw = 0;
+  for (uint32_t f = 0; f < nf; f++) {
+    const bool good = cnt[3 * f] != MTB_NONE;  // else the device walk did not trust the tree: host path
+    if (!good) cnt[3 * f] = cnt[3 * f + 1] = cnt[3 * f + 2] = 0;
+    off[3 * f] = 8 * ti;
+    off[3 * f + 1] = tt;
+    off[3 * f + 2] = tw;
+    ti += cnt[3 * f];
+    tt += cnt[3 * f + 1];
+    tw += cnt[3 * f + 2];
+    const uint32_t k = dev[f];
+    ex.ok[k] = good;
+    ex.cnt[3 * k] = cnt[3 * f];
+    for (int q = 0; q < 3; q++) ex.off[3 * k + q] = off[3 * f + q];
+  }
+  dItems.ensure(8 * ti + 8);
+  dText.ensure(tt + 1);
+  dWords.ensure(tw + 1);
+  doff.ensure(3 * (size_t)nf);
+  HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
+  HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
+                               b->dValClass.p, dc.p, doff.p, dItems.p, dText.p, dWords.p));
+  ex.items.reset(new uint32_t[8 * ti + 8]);
+  ex.text.reset(new uint16_t[tt + 1]);
+  ex.words.reset(new uint32_t[tw + 1]);
+  if (ti) HIPCHK(hipMemcpyAsync(ex.items.get(), dItems.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  if (tt) HIPCHK(hipMemcpyAsync(ex.text.get(), dText.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
+  if (tw) HIPCHK(hipMemcpyAsync(ex.words.get(), dWords.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+}
+
+// SnapshotV1 of one document: the device extraction when it applies, else the host path
+void summarize_any(mtb_dev* b, uint32_t doc, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summary) {
+  Extracted ex;
+  extract_docs(b, {doc}, ex);
+  if (ex.ok[0]) summarize_items(b, doc, ex.items.get(), ex.cnt[0], ex.text.get(), ex.words.get(), blobs, summary);
+  else summarize(b, doc, blobs, summary);
+}
+
 // processMinSequenceNumberChanged (sequence.ts:737-748)
 void drop_catch_up(HostDoc& d, int64_t minSeq) {
   size_t i = 0;
@@ -3324,7 +3399,7 @@ int mtbx_summarize_v1(mtb_dev* b, uint32_t doc, int64_t msn, int64_t seq, mtb_bl
     }
     std::vector<std::pair<std::string, std::string>> blobs;
     std::string summary;
-    summarize(b, doc, blobs, summary);
+    summarize_any(b, doc, blobs, summary);
     out->count = (uint32_t)blobs.size();
     out->blobs = (mtb_blob*)calloc(blobs.size(), sizeof(mtb_blob));
     for (size_t k = 0; k < blobs.size(); k++) {
@@ -3360,69 +3435,14 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     PhaseClock pc;
     // SharedString documents: extractSync on the device (mtb_extract_v1_kernel), only its output comes back;
     // PermutationVectors and failed documents take the host path over the downloaded tree
-    std::vector<uint32_t> fast, slow;  // positions in `list`
-    for (uint32_t k = 0; k < n; k++) {
-      const uint32_t i = list[k];
-      const bool dev = b->devInit && i < b->hst.size() && b->docs[i].onDevice && !b->docs[i].perm && !b->hst[i].err &&
-                       !getenv("MTB_HOST_SUMMARY");
-      (dev ? fast : slow).push_back(k);
-    }
+    std::vector<uint32_t> ids(list);
+    Extracted ex;
+    extract_docs(b, ids, ex);
+    pc.mark("extract");
+    std::vector<uint32_t> fast, slow;
+    for (uint32_t k = 0; k < n; k++) (ex.ok[k] ? fast : slow).push_back(k);
     const uint32_t nf = (uint32_t)fast.size();
-    std::unique_ptr<uint32_t[]> hItems, hWords;
-    std::unique_ptr<uint16_t[]> hText;
-    std::vector<uint64_t> off(3 * (size_t)nf + 3, 0);
-    std::vector<uint32_t> cnt(3 * (size_t)nf + 3, 0);
-    if (nf) {
-      std::vector<uint32_t> ids(nf);
-      for (uint32_t f = 0; f < nf; f++) ids[f] = list[fast[f]];
-      DevBuf<uint32_t> dl, dc;
-      DevBuf<uint64_t> doff;
-      dl.ensure(nf);
-      dc.ensure(3 * (size_t)nf);
-      HIPCHK(hipMemcpyAsync(dl.p, ids.data(), nf * sizeof(uint32_t), hipMemcpyHostToDevice, b->stream));
-      HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
-                                   b->dValClass.p, dc.p, nullptr, nullptr, nullptr, nullptr));
-      HIPCHK(hipMemcpyAsync(cnt.data(), dc.p, 3 * (size_t)nf * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-      HIPCHK(hipStreamSynchronize(b->stream));
-      pc.mark("extract_count");
-      uint64_t ti = 0, tt = 0, tw = 0;
-      for (uint32_t f = 0; f < nf; f++) {
-        if (cnt[3 * f] == MTB_NONE) {  // the device walk did not trust the tree: host path
-          slow.push_back(fast[f]);
-          cnt[3 * f] = cnt[3 * f + 1] = cnt[3 * f + 2] = 0;
-        }
-        off[3 * f] = 8 * ti;
-        off[3 * f + 1] = tt;
-        off[3 * f + 2] = tw;
-        ti += cnt[3 * f];
-        tt += cnt[3 * f + 1];
-        tw += cnt[3 * f + 2];
-      }
-      DevBuf<uint32_t> di, dw;
-      DevBuf<uint16_t> dt;
-      di.ensure(8 * ti + 8);
-      dt.ensure(tt + 1);
-      dw.ensure(tw + 1);
-      doff.ensure(3 * (size_t)nf);
-      HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
-      HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
-                                   b->dValClass.p, dc.p, doff.p, di.p, dt.p, dw.p));
-      hItems.reset(new uint32_t[8 * ti + 8]);
-      hText.reset(new uint16_t[tt + 1]);
-      hWords.reset(new uint32_t[tw + 1]);
-      if (ti) HIPCHK(hipMemcpyAsync(hItems.get(), di.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-      if (tt) HIPCHK(hipMemcpyAsync(hText.get(), dt.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
-      if (tw) HIPCHK(hipMemcpyAsync(hWords.get(), dw.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-      HIPCHK(hipStreamSynchronize(b->stream));
-      pc.mark("extract_emit_download");
-    }
-    std::vector<uint8_t> onDev(n, 0);
-    std::vector<uint32_t> fpos(n, 0);
-    for (uint32_t f = 0; f < nf; f++) {
-      onDev[fast[f]] = 1;
-      fpos[fast[f]] = f;
-    }
-    for (uint32_t k : slow) onDev[k] = 0;
+    (void)nf;
     if (!slow.empty()) {
       std::vector<uint32_t> sl;
       for (uint32_t k : slow) sl.push_back(list[k]);
@@ -3435,10 +3455,9 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
         try {
           std::vector<std::pair<std::string, std::string>> blobs;
           std::string summary;
-          if (onDev[k]) {
-            const uint32_t f = fpos[k];
-            summarize_items(b, list[k], hItems.get() + off[3 * f], cnt[3 * f], hText.get() + off[3 * f + 1],
-                            hWords.get() + off[3 * f + 2], blobs, summary);
+          if (ex.ok[k]) {
+            summarize_items(b, list[k], ex.items.get() + ex.off[3 * k], ex.cnt[3 * k], ex.text.get() + ex.off[3 * k + 1],
+                            ex.words.get() + ex.off[3 * k + 2], blobs, summary);
           } else {
             summarize(b, list[k], blobs, summary);
           }
