@@ -291,7 +291,10 @@ class MergeTreeBatch:
         n = len(docs)
         lists = (_lib.MtbBlobList * max(1, n))()
         ids = (ctypes.c_uint32 * max(1, n))(*docs)
+        import time
+        t0 = time.perf_counter()
         self._chk(self._L.mtb_summarize_v1_many(self._h, n, ids, msn, seq, threads, lists))
+        self.last_summary_seconds = time.perf_counter() - t0  # the summaries themselves (no copies, no hashing)
         out = []
         for k in range(n):
             if fingerprints:

@@ -1029,11 +1029,14 @@ struct Eng {
     const int lenAll = csum8(ol);
     const int lenL = csum8(lane < half ? ol : 0);
     const uint32_t vpar = U(V.parent);
-    // both headers in one store: b.count, b.len, nb.count, nb.len, nb.parent
-    if (lane < 5)
-      bw(lane < 2 ? b : nb)[FB_HDR + (lane == 0 || lane == 2 ? 0 : lane == 4 ? 1 : 4)] =
-          lane == 0 || lane == 2 ? (uint32_t)half : lane == 1 ? (uint32_t)lenL : lane == 3 ? (uint32_t)(lenAll - lenL) : vpar;
-    if (lane == 0) V.count = half;  // (all views are cleared after fix_overflow)
+    if (lane == 0) {
+      blk[b].count = half;
+      blk[b].len = lenL;
+      blk[nb].count = half;
+      blk[nb].len = lenAll - lenL;
+      blk[nb].parent = vpar;
+      V.count = half;  // (all views are cleared after fix_overflow)
+    }
     wsync();
     sp_lenL = (uint32_t)lenL;
     sp_lenR = (uint32_t)(lenAll - lenL);
@@ -1117,11 +1120,16 @@ struct Eng {
         // link (b, nb) into the parent at depth level-1, then rebuild the parent's list
         const int k = U(sh->slot[L]);
         View& P = sh->v[L];
-        // slot k's length and list metadata (fields F_LEN..F_CLI, one lane each) in the view and the record
-        if (lane >= F_LEN && lane <= F_CLI) {
-          const uint32_t v = lane == F_LEN ? sp_lenL : lane == F_SEQ ? sp_loffL : lane == F_RSEQ ? sp_lcntL : sp_lcapL;
-          P.f[lane][k] = v;
-          bw(U(P.b))[lane * MTB_MAXCH + k] = v;
+        if (lane == 0) {
+          P.f[F_LEN][k] = sp_lenL;
+          P.f[F_SEQ][k] = sp_loffL;
+          P.f[F_RSEQ][k] = sp_lcntL;
+          P.f[F_CLI][k] = sp_lcapL;
+          FBlk& PB = blk[P.b];
+          PB.f[F_LEN][k] = sp_lenL;
+          PB.f[F_SEQ][k] = sp_loffL;
+          PB.f[F_RSEQ][k] = sp_lcntL;
+          PB.f[F_CLI][k] = sp_lcapL;
         }
         wsync();
         stage_block_child(nb, sp_lenR, sp_loffR, sp_lcntR, sp_lcapR);
@@ -2725,8 +2733,7 @@ struct Eng {
     return nh + __popcll(km);
   }
   // Write hold[.][from, from+n) as the children of block nb (slots 0..n-1, the rest cleared), point the
-  // children at nb and return their observer-view length.  The caller writes the header (count ...) with
-  // its other header words in one store.
+  // children at nb and return their observer-view length.
   __device__ __forceinline__ int place_children(uint32_t nb, int from, int n) {
     const int fld = lane >> 3, s = lane & 7;
     uint32_t v = fld == F_ID ? MTB_NONE : 0u;
@@ -2739,6 +2746,7 @@ struct Eng {
       ol = child_olen(c, (int)sh->hold[F_LEN][from + lane], (int)sh->hold[F_RSEQ][from + lane]);
     }
     const int len = csum8(ol);
+    if (lane == 0) blk[nb].count = (uint32_t)n;
     wsync();
     return len;
   }
@@ -2820,10 +2828,12 @@ struct Eng {
             lens = len;
             kbs = kb;
           }
-          // header: count, parent, index, needsScour undefined (a new block, makeBlock), cachedLength
-          if (lane < 5)
-            bw(nb)[FB_HDR + lane] = lane == 0 ? (uint32_t)n : lane == 1 ? parent : lane == 2 ? (uint32_t)q
-                                    : lane == 3 ? (uint32_t)-1 : (uint32_t)len;
+          if (lane == 0) {
+            blk[nb].parent = parent;
+            blk[nb].index = (uint32_t)q;
+            blk[nb].len = len;
+            blk[nb].scour = -1;  // a new block (makeBlock): needsScour undefined
+          }
           wsync();
           taken += n;
         }
@@ -2848,10 +2858,17 @@ struct Eng {
         }
         if (isP) break;
         const int len = rl(lens, q);
-        // slot q of P: the new block, its cachedLength and list metadata (lane = field)
-        if (lane < 8)
-          bw(parent)[lane * MTB_MAXCH + q] = lane == F_ID ? nb : lane == F_LEN ? (uint32_t)len : lane == F_SEQ ? a
-                                             : lane == F_RSEQ ? c2 : lane == F_CLI ? e : 0u;
+        if (lane == 0) {
+          FBlk& P = blk[parent];
+          P.f[F_ID][q] = nb;
+          P.f[F_LEN][q] = (uint32_t)len;
+          P.f[F_SEQ][q] = a;
+          P.f[F_RSEQ][q] = c2;
+          P.f[F_CLI][q] = e;
+          P.f[F_RCX][q] = 0;
+          P.f[F_PROPS][q] = 0;
+          P.f[F_TEXT][q] = 0;
+        }
         wsync();
       }
       store_meta_of(parent, pparent, pindex, a, c2, e);
@@ -3042,11 +3059,11 @@ struct Eng {
       const int nh = scour(1, 0);
       if (bad()) return;
       tz = PROF_T();
-      // nh == count: nothing was dropped or appended, the record is unchanged (only needsScour = false)
-      if (nh < count) place_children(b, 0, nh);
-      if (lane == 0 || (lane == 3 && nh < count)) bw(b)[FB_HDR + (lane == 0 ? 3 : 0)] = lane == 0 ? 0u : (uint32_t)nh;
+      if (lane == 0) blk[b].scour = 0;
       wsync();
+      // nh == count: nothing was dropped or appended, the record is unchanged
       if (nh < count) {
+        place_children(b, 0, nh);
         PROF_ZADD(PH_PLACE, tz);
         tz = PROF_T();
         if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);

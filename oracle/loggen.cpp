@@ -557,4 +557,63 @@ double loggen_cpu_replay(const loggen_cfg* cfg, const loggen_doc* docs, uint32_t
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// CPU baseline of Client.summarize -> SnapshotV1: every document of the sample is replayed first
+// (not timed), then summarizeV1 runs over all of them on `threads` threads (timed).  mismatches: summaries whose
+// fingerprint differs from the generator's (docs[i].summary_fnv).
+double loggen_cpu_summarize(const loggen_cfg* cfg, const loggen_doc* docs, uint32_t n, int threads, int32_t* mismatches) {
+  std::vector<std::optional<JVal>> props = parse_table(props_table(cfg->n_clients, std::max(1, cfg->annotate_keys)));
+  std::vector<std::unique_ptr<Doc>> done(n);
+  if (threads < 1) threads = 1;
+  auto run = [&](auto&& body) {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; t++)
+      ts.emplace_back([&, t] {
+        for (uint32_t i = t; i < n; i += threads) body(i);
+      });
+    for (auto& th : ts) th.join();
+  };
+  run([&](uint32_t i) {
+    Options o;
+    o.newLengthCalc = cfg->new_length_calc != 0;
+    auto doc = std::make_unique<Doc>(o);
+    const loggen_doc& d = docs[i];
+    try {
+      if (d.initial_len > 0)
+        doc->insertTextLocal(0, u16str(reinterpret_cast<const char16_t*>(d.text), d.initial_len), std::nullopt);
+      doc->startOrUpdateCollaboration("obs", 0, 0);
+      for (uint32_t s = 1; s < d.n_short; s++) doc->getOrAddShortClientId("c" + std::to_string(d.client_writer[s]));
+      const Doc::Record* r = static_cast<const Doc::Record*>(d.ops);
+      for (uint32_t k = 0; k < d.n_ops; k++) doc->applyRecordParsed(r[k], d.text, props);
+      done[i] = std::move(doc);
+    } catch (const OracleError&) {
+    }
+  });
+  std::vector<uint64_t> fp(n, 0);
+  auto t0 = std::chrono::steady_clock::now();
+  run([&](uint32_t i) {
+    if (!done[i]) return;
+    std::string summary;
+    const auto blobs = done[i]->summarizeV1(&summary);
+    uint64_t h = 1469598103934665603ull;
+    auto add = [&](const std::string& x, bool zero) {
+      for (unsigned char c : x) {
+        h ^= c;
+        h *= 1099511628211ull;
+      }
+      if (zero) h *= 1099511628211ull;
+    };
+    for (auto& bl : blobs) {
+      add(bl.first, true);
+      add(bl.second, true);
+    }
+    add(summary, false);
+    fp[i] = h;
+  });
+  auto t1 = std::chrono::steady_clock::now();
+  int32_t bad = 0;
+  for (uint32_t i = 0; i < n; i++) bad += !done[i] || fp[i] != docs[i].summary_fnv;
+  if (mismatches) *mismatches = bad;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
 }  // extern "C"

@@ -46,6 +46,9 @@ def _lib():
         L.loggen_generate_batch.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.POINTER(LoggenDoc)]
         L.loggen_free.argtypes = [ctypes.POINTER(LoggenDoc)]
+        L.loggen_cpu_summarize.restype = ctypes.c_double
+        L.loggen_cpu_summarize.argtypes = [ctypes.POINTER(LoggenCfg), ctypes.POINTER(LoggenDoc), ctypes.c_uint32,
+                                           ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
         L.loggen_props_count.argtypes = [ctypes.c_int, ctypes.c_int]
         L.loggen_props_json.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.loggen_cpu_replay.restype = ctypes.c_double
@@ -103,6 +106,14 @@ class LogBatch:
         n = self.n if n is None else n
         secs = L.loggen_cpu_replay(ctypes.byref(self.cfg), self.docs, n, threads, ctypes.byref(ck), ctypes.byref(err))
         return secs, ck.value, err.value
+
+    def cpu_summarize(self, n=None, threads=1):
+        """(seconds, mismatches): the oracle's summarizeV1 of the first n documents (replayed beforehand, untimed)
+        on `threads` threads, each fingerprint checked against the generator's."""
+        bad = ctypes.c_int32()
+        n = self.n if n is None else n
+        secs = _lib().loggen_cpu_summarize(ctypes.byref(self.cfg), self.docs, n, threads, ctypes.byref(bad))
+        return secs, bad.value
 
     def close(self):
         if self.docs is not None:
