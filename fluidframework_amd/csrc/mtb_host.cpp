@@ -47,7 +47,7 @@ hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState*
                                    uint32_t nq, uint32_t spins);  // + mtb_replay_finish_kernel
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                           Tables tables);
+                           Tables tables, int perm);
 hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables);
@@ -933,8 +933,6 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
       if (cs && cs->kind == hj::Value::kArr)
         for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload, pc));
     }
-  if (d.perm && !body.empty())
-    raise(MTB_E_UNSUPPORTED, "unsupported: PermutationVector summary with body chunks (more than chunkSize rows/cols)");
   build_load_image(d, hdr);
   // idToSegment after reloadFromSegments: blockUpdate maps the live header markers (mergeTree.ts:296-306)
   if (!d.markerAmbig.empty()) {
@@ -1656,7 +1654,8 @@ void replay(mtb_dev* b, mtb_stats* out) {
     mtb_op* out = ops.get() + opOff[i];
     s.mk_cap = (uint32_t)d.markerAmbig.size();
     for (mtb_op o : d.pending) {
-      if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER)) o.payload += base;
+      // text offsets move with the arena; a PermutationSegment's LOADSEG payload is its handle start
+      if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER) && !d.perm) o.payload += base;
       if ((o.flags & MTB_F_RELPOS) && o.type != MTB_OP_LOADSEG) {  // relative-position descriptors
         if (o.pos1 & MTB_RELPOS) o.pos1 += base;
         if (o.pos2 & MTB_RELPOS) o.pos2 += base;
@@ -1706,7 +1705,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
     HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
-                           b->dHeap.p, b->dAux.p, b->dFree.p, t));
+                           b->dHeap.p, b->dAux.p, b->dFree.p, t, b->matrix ? 1 : 0));
   launch_main(b, t);
   HIPCHK(hipEventRecord(b->ev1, b->stream));
   sched_readback(b);
@@ -2503,6 +2502,9 @@ void apply_cell_events(mtb_dev* b, uint32_t m) {
     for (uint32_t e = 0; e < s.delta_used; e++) {
       const uint32_t k = ent[4 * e], kind = ent[4 * e + 1];
       if (k >= recs.size()) raise(MTB_E_ASSERT, "cell event names no record");
+      // handles recycled while a summary body loads clear the cells of the store that loadCore replaces
+      // afterwards (matrix.ts:611-634: rows and cols load before the cells blob), so they touch nothing
+      if (recs[k].type == MTB_OP_LOADSEG) continue;
       ev[v].push_back({ordinal[k], kind, ent[4 * e + 2], ent[4 * e + 3]});
     }
   }
@@ -3249,7 +3251,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     HIPCHK(hipEventRecord(b->ev0, b->stream));
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
-                             b->dHeap.p, b->dAux.p, b->dFree.p, t));
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t, b->matrix ? 1 : 0));
     launch_main(b, t);
     HIPCHK(hipEventRecord(b->ev1, b->stream));
     sched_readback(b);

@@ -212,7 +212,8 @@ using ScratchBig = ScratchT<MTB_LDS_HEAP_LONG>;
 // pending segment groups of live clients (mtb_live_kernel); MODE_MARKERS is MODE_REPLAY
 // plus marker ids and marker-relative positions (mtb_markers_kernel, for batches whose documents met a
 // marker id).  Each variant carries only its own code.
-enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3, MODE_MARKERS = 4 };
+// MODE_LOADPERM is MODE_LOAD for PermutationVector documents (a SharedMatrix summary with body chunks).
+enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3, MODE_MARKERS = 4, MODE_LOADPERM = 5 };
 template <int MODE, class SCR>
 struct Eng {
   DocState* ds;
@@ -241,7 +242,8 @@ struct Eng {
   uint32_t cur_k;               // index of the record being applied (catch-up delta entries name it)
   bool delta_on;                // the record asks for its delta ranges (MTB_F_DELTA)
   uint32_t delta_used;          // entries written in this document's delta slice
-  static constexpr bool isPerm = MODE == MODE_MATRIX;  // matrix batches hold PermutationVectors only
+  static constexpr bool isPerm = MODE == MODE_MATRIX || MODE == MODE_LOADPERM;  // PermutationVectors only
+  static constexpr bool isLoad = MODE == MODE_LOAD || MODE == MODE_LOADPERM;  // LOADSEG records only
   static constexpr bool isLive = MODE == MODE_LIVE;    // local ops / acks of the document's own client (id 0)
   // idToSegment upkeep and relative positions (the observer-only replay kernel carries none of it)
   static constexpr bool hasMk = MODE == MODE_MARKERS || MODE == MODE_LIVE || MODE == MODE_LOAD;
@@ -643,7 +645,7 @@ struct Eng {
         lcnt = P.f[F_RSEQ][k];
         lcap = P.f[F_CLI][k];
       }
-      if (MODE == MODE_LOAD || (isLive && pend_n > 0)) {
+      if (isLoad || (isLive && pend_n > 0)) {
         if (lcnt < (lcap & ~MTB_LUNSORTED) && !(lcap & MTB_LUNSORTED)) {
           lcap |= MTB_LUNSORTED;
           if (i == 0) {
@@ -686,7 +688,7 @@ struct Eng {
       const uint32_t no = list_regrow(loff, lcnt, lcap, 1, live, cap);
       if (bad()) return;
       // (cap carries the kept entries' order; pending MTB_PEND + localSeq entries may sit above this seq)
-      const uint32_t flag = (MODE == MODE_LOAD || (isLive && pend_n > 0)) ? MTB_LUNSORTED : 0u;
+      const uint32_t flag = (isLoad || (isLive && pend_n > 0)) ? MTB_LUNSORTED : 0u;
       if (lane == 0) {
         WEnt e;
         e.seq = seqv;
@@ -1313,7 +1315,7 @@ struct Eng {
       wsync();
       insert_slot(d, at);
       add_len_levels(0, d, d, candLen);
-      if constexpr (MODE == MODE_LOAD) load_entries(d, S, C);
+      if constexpr (isLoad) load_entries(d, S, C);
       else append_levels(0, d, S, C, WK_MAIN, candLen);
       pending_fix = d;
       return true;
@@ -3172,7 +3174,7 @@ struct Eng {
       settle();
       if (bad()) return;
     }
-    const bool marker = (o.flags & MTB_F_MARKER) != 0;
+    const bool marker = !isPerm && (o.flags & MTB_F_MARKER) != 0;
     const int len = marker ? 1 : (int)o.pos2;
     const int rseq = (int)o.ref_seq;
     if (len > 0) {
@@ -3258,7 +3260,7 @@ struct Eng {
     const bool local = isLive && S >= MTB_PEND;
     if constexpr (MODE == MODE_REPLAY || MODE == MODE_MARKERS || MODE == MODE_LIVE) delta_on = (o.flags & MTB_F_DELTA) != 0;
     else delta_on = false;
-    if constexpr (MODE == MODE_LOAD) {
+    if constexpr (isLoad) {
       apply_loadseg(o, S, C);
       return;
     }
@@ -3495,7 +3497,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
       cur.pos2 = rlu(cw, 5);
       cur.payload = rlu(cw, 6);
       cur.props = rlu(cw, 7);
-      if constexpr (MODE == MODE_LOAD) {
+      if constexpr (MODE == MODE_LOAD || MODE == MODE_LOADPERM) {
         if (cur.type != MTB_OP_LOADSEG) break;  // the summary body precedes every op
       }
       e.cur_k = k;
@@ -3694,6 +3696,13 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   __shared__ Scratch sh;
   replay_doc<MODE_LOAD>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+// The same for the PermutationVectors of a matrix batch (segments carry handle starts, no text).
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_load_perm_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                         WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables) {
+  __shared__ Scratch sh;
+  replay_doc<MODE_LOADPERM>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
+}
 // SharedMatrix batches: one 128-lane workgroup per matrix, wave 0 = rows vector (document 2m), wave 1 =
 // cols vector (document 2m + 1); setCell records meet at a workgroup barrier (matrix.ts:668-676).
 extern "C" __global__ void __launch_bounds__(128, MTB_WAVES_PER_SIMD)
@@ -3714,8 +3723,11 @@ hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs,
 }
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                           Tables tables) {
-  hipLaunchKernelGGL(mtb_load_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+                           Tables tables, int perm) {
+  if (perm)
+    hipLaunchKernelGGL(mtb_load_perm_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  else
+    hipLaunchKernelGGL(mtb_load_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
   return hipGetLastError();
 }
 #endif

@@ -140,18 +140,23 @@ def make_v1_summary(seed, n_segments, chunk_len, msn, seq, n_clients=4, p_remove
 UNALLOCATED = -2147483648  # Handle.unallocated (matrix/src/handletable.ts:11)
 
 
-def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, new_mode=False):
+def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, new_mode=False, start=None):
     """A SharedMatrix op stream (matrix.ts message shapes) valid in each author's (refSeq, client) view:
     row/col inserts and removes of 1..max_count, and setCell at a row/col inside the author's view.
-    Generated by driving the oracle as the observer; returns the messages."""
+    Generated by driving the oracle as the observer; returns the messages.  start=(oracle, seq0): continue
+    from that observer's state (e.g. a loaded summary) with every client caught up at seq0."""
     import random
     from pyoracle import OracleMatrix
     rng = random.Random(seed)
-    m = OracleMatrix(new_length_calc=new_mode)
-    m.start_collab("obs")
+    if start is None:
+        m = OracleMatrix(new_length_calc=new_mode)
+        m.start_collab("obs")
+        seq0 = 0
+    else:
+        m, seq0 = start
     clients = [f"w{k}" for k in range(n_clients)]
-    ref = {c: 0 for c in clients}
-    msgs, seq = [], 0
+    ref = {c: seq0 for c in clients}
+    msgs, seq = [], seq0
 
     def vlen(doc, w, r):
         doc.add_client(w)

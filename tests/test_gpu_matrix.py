@@ -107,25 +107,27 @@ def test_generated_matrix_records_match_oracle_checksums(new_mode):
 
 
 @pytest.mark.parametrize("new_mode", [False, True])
-def test_matrix_load_mid_stream_then_continue(new_mode):
+def test_matrix_load_mid_stream_then_continue(new_mode, chunk_size=0):
     """SharedMatrix.loadCore (matrix.ts:611-634) on the engine: an oracle summary taken mid-stream is loaded
     (rows / cols handle tables + segments, cells) and the rest of the log replayed; summaries and getCell
     equal the oracle that loaded the same summary."""
     from fluidframework_amd import MatrixBatch
     from pyoracle import OracleMatrix
     n = 12
-    B = MatrixBatch(n, new_length_calc=new_mode)
+    B = MatrixBatch(n, new_length_calc=new_mode, chunk_size=chunk_size)
     oracles = []
+    bodies = 0
     for i in range(n):
         msgs = make_matrix_log(700 + 3 * i + int(new_mode), 600 + 20 * i, n_clients=2 + i % 4, lag=3 + 2 * (i % 6),
                                new_mode=new_mode)
-        src = OracleMatrix(new_length_calc=new_mode)
+        src = OracleMatrix(new_length_calc=new_mode, chunk_size=chunk_size)
         src.start_collab("obs")
         half = len(msgs) // 2
         for m in msgs[:half]:
             src.apply_msg(m)
         blobs = src.summarize()["blobs"]
-        o = OracleMatrix(new_length_calc=new_mode)
+        bodies += sum(1 for p, _ in blobs if "/body_" in p)
+        o = OracleMatrix(new_length_calc=new_mode, chunk_size=chunk_size)
         o.load(blobs, "obs")
         B[i].load(blobs, "obs")
         for m in msgs[half:]:
@@ -138,6 +140,56 @@ def test_matrix_load_mid_stream_then_continue(new_mode):
         nr, nc = o.rows.get_length(), o.cols.get_length()
         for r in range(0, nr, max(1, nr // 10)):
             for c in range(0, nc, max(1, nc // 10)):
+                assert B.get_cell(i, r, c) == o.get_cell(r, c), f"matrix {i} cell ({r}, {c})"
+    assert (bodies > 0) == (chunk_size > 0)
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_matrix_load_body_chunks_at_quiescence(new_mode):
+    """PermutationVector summaries with body chunks (permutationvector.ts:310-325, chunkSize 5) loaded on the
+    engine (mtb_load_perm_kernel appends the bodies, snapshotLoader.ts:169-220): each vector summarized with
+    the runtime's MSN = lastSequenceNumber (Client.summarize, client.ts:966-1005), the matrix loaded, then a
+    continuation generated against the loaded state; dumps, summaries and the getCell grid equal the oracle
+    that loaded the same summary.  (Mid-stream summaries whose header holds segments above the MSN can make
+    the reference's body insert fail, as the oracle and engine both reproduce in test_gpu_load.py.)"""
+    import json as _json
+    from fluidframework_amd import MatrixBatch
+    from pyoracle import OracleMatrix
+    n, cs = 8, 5
+    B = MatrixBatch(n, new_length_calc=new_mode, chunk_size=cs)
+    oracles = []
+    bodies = 0
+    for i in range(n):
+        msgs = make_matrix_log(900 + 5 * i + int(new_mode), 400 + 40 * i, n_clients=2 + i % 3, lag=2 + i % 4,
+                               new_mode=new_mode)
+        src = OracleMatrix(new_length_calc=new_mode, chunk_size=cs)
+        src.start_collab("obs")
+        for m in msgs:
+            src.apply_msg(m)
+        last = msgs[-1]["sequenceNumber"]
+        blobs = []
+        for name, vec in (("rows", src.rows), ("cols", src.cols)):
+            for p, c in vec.summarize_v1(last, last)["blobs"]:
+                blobs.append([f"{name}/{p}", c])
+        blobs += [b for b in src.summarize()["blobs"] if b[0] == "cells"]
+        bodies += sum(1 for p, _ in blobs if "/body_" in p)
+        o = OracleMatrix(new_length_calc=new_mode, chunk_size=cs)
+        o.load(blobs, "obs")
+        gen = OracleMatrix(new_length_calc=new_mode, chunk_size=cs)
+        gen.load(blobs, "obs")
+        rest = make_matrix_log(950 + i, 150, n_clients=2 + i % 3, lag=2, new_mode=new_mode, start=(gen, last))
+        B[i].load(blobs, "obs")
+        for m in rest:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    assert bodies > 0
+    for i, o in enumerate(oracles):
+        _check(B, i, o, f"loaded matrix {i}")
+        nr, nc = o.rows.get_length(), o.cols.get_length()
+        for r in range(0, nr, max(1, nr // 8)):
+            for c in range(0, nc, max(1, nc // 8)):
                 assert B.get_cell(i, r, c) == o.get_cell(r, c), f"matrix {i} cell ({r}, {c})"
 
 
