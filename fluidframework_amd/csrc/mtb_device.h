@@ -199,6 +199,8 @@ struct Tables {
   const uint8_t* val_falsy;  // JS falsiness of each value id
   const uint32_t* key_rank;  // array-index keys: numeric value; other keys: MTB_NONE
   uint32_t* delta;           // catch-up delta pool (per-document slices at DocState.delta_base, 4 words/entry)
+  uint32_t class_trivial;    // every matchProperties class holds one value id: classes compare as value ids
+  uint32_t pad_;
 };
 
 // device error codes (DocState.err)

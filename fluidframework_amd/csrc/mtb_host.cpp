@@ -1701,6 +1701,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   t.val_falsy = b->dValFalsy.p;
   t.key_rank = b->dKeyRank.p;
   t.delta = b->dDelta.p;
+  t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
   b->residentLoad = anyLoad;
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
@@ -3248,6 +3249,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     t.val_falsy = b->dValFalsy.p;
     t.key_rank = b->dKeyRank.p;
     t.delta = b->dDelta.p;
+    t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
     HIPCHK(hipEventRecord(b->ev0, b->stream));
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,

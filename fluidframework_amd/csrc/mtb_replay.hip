@@ -73,7 +73,9 @@ enum { PH_BOUNDARY = 0, PH_INSERT = 1, PH_NODEMAP = 2, PH_ZAMBONI = 3, PH_TOTAL 
 enum { CN_SCOUR = 0, CN_PACK = 1, CN_REBUILD = 2, CN_VIEW = 3, CN_ENTRIES = 4, CN_ZCALL = 5, CN_POP = 6, CN_PSKIP = 7, CN_PSIG = 8,
        NCN = 9, CN_SPLIT = 99, CN_GROW = 99, CN_ZRECORD = 99 };
 
+#ifndef MTB_LDS_HEAP
 #define MTB_LDS_HEAP 128        // LRU heap entries kept in LDS by the batch kernels (more spill to HBM)
+#endif
 #define MTB_LDS_HEAP_LONG 2048  // ... by the few-document kernel (long documents keep big heaps)
 #define MTB_VDEPTH 12  // depth of the LDS path cache; 4^12 segments per document is far beyond any input
 
@@ -2015,8 +2017,12 @@ struct Eng {
       for (uint32_t q = 0; q < nb; q++) {
         if (pb[1 + 2 * q] == k) {
           found = true;
-          const auto vcl = UP(sh->tab.val_class);
-          if (vcl[pa[2 + 2 * i]] != vcl[pb[2 + 2 * q]]) return false;
+          const uint32_t va = pa[2 + 2 * i], vb = pb[2 + 2 * q];
+          if (va != vb) {
+            if (U(sh->tab.class_trivial)) return false;
+            const auto vcl = UP(sh->tab.val_class);
+            if (vcl[va] != vcl[vb]) return false;
+          }
           break;
         }
       }
@@ -2501,9 +2507,15 @@ struct Eng {
       const uint32_t v0 = p[2];
       g.k1 = p[3];
       const uint32_t v1 = p[4];
-      const auto vc = UP(sh->tab.val_class);
-      if (g.n >= 1) g.c0 = vc[v0];
-      if (g.n >= 2) g.c1 = vc[v1];
+      // (classes are the value ids themselves when no class holds two values: no dependent table load)
+      if (U(sh->tab.class_trivial)) {
+        g.c0 = g.n >= 1 ? v0 : 0u;
+        g.c1 = g.n >= 2 ? v1 : 0u;
+      } else {
+        const auto vc = UP(sh->tab.val_class);
+        if (g.n >= 1) g.c0 = vc[v0];
+        if (g.n >= 2) g.c1 = vc[v1];
+      }
     }
     return g;
   }
