@@ -186,7 +186,8 @@ struct DocState {     // 320 bytes
   uint32_t orphans;     // aux offset of [n, cap, (props id, segment)*]: pending keys whose annotate group a
                         // reconnect dropped without a new op (they stay pending, as the reference's counts do)
   uint32_t pend_cap;    // directory entries (a power of two, 0: none yet; doubles when full)
-  uint32_t pad3[5];
+  uint32_t mk_all;      // aux offset of [n, cap, (segment, ordinal)*]: every marker inserted with an id (0: none)
+  uint32_t pad3[4];
 };
 static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
 
@@ -200,7 +201,7 @@ struct Tables {
   const uint32_t* key_rank;  // array-index keys: numeric value; other keys: MTB_NONE
   uint32_t* delta;           // catch-up delta pool (per-document slices at DocState.delta_base, 4 words/entry)
   uint32_t class_trivial;    // every matchProperties class holds one value id: classes compare as value ids
-  uint32_t pad_;
+  uint32_t mk_key;           // key id of "markerId" (MTB_NONE: no property set names it)
 };
 
 // device error codes (DocState.err)
@@ -228,6 +229,7 @@ struct Tables {
 #define DERR_RELPOS 20     // a relative position whose marker is not mapped, or resolves below 0
 #define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
 #define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
+#define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
 // ticket scheduler words (mtb_replay_sched_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32
@@ -236,3 +238,4 @@ struct Tables {
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)
+#define DSF_MKDUP 4        // a marker id is carried by two markers: blockUpdate re-maps ids (mergeTree.ts:296-306)

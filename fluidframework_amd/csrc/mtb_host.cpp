@@ -232,6 +232,7 @@ struct LoadImage {
   std::vector<uint32_t> aux;   // word 0 unused, then the overlapping-remover lists
   uint32_t root = 0;
   uint32_t mk_map = 0, mk_n = 0;  // idToSegment of the live header markers (in `aux`)
+  uint32_t mk_all = 0;            // DocState.mk_all: the live header markers with an id (in `aux`)
 };
 
 // ------------------------------------------------------------------ SharedMatrix cells
@@ -349,11 +350,13 @@ struct HostDoc {
   std::unique_ptr<CellStore> cells;  // rows vector of a matrix: the matrix's cells (matrix.ts:96)
   LoadImage img;
   // idToSegment keys (mergeTree.ts:549): marker id -> per-document ordinal (first-seen order).  An id met on
-  // a second marker is ambiguous (blockUpdate's re-mapping, :296-306, would decide), and an annotate that
-  // sets markerId changes ids at blockUpdate time: relative positions naming either are rejected.
+  // a second marker is reused: blockUpdate's re-mapping (:296-306) decides which marker it names, which the
+  // marker kernel reproduces (DSF_MKDUP); a live client's batch rejects relative positions naming one.
   std::unordered_map<std::string, uint32_t> markerOrd;
   std::vector<uint8_t> markerAmbig;
-  bool markerIdsUnstable = false;
+  bool markerDup = false;      // some id is reused
+  bool markerIdAnnot = false;  // an annotate names markerId (assert 0x5ad is checked on the device)
+  bool relOnDup = false;       // a relative position named a reused id
   // device mirror
   DocState st{};
   bool onDevice = false;
@@ -524,8 +527,12 @@ uint32_t marker_ord(HostDoc& d, const hj::Value* props) {
   if (!key) return 0;
   auto [it, fresh] = d.markerOrd.try_emplace(*key, (uint32_t)d.markerAmbig.size());
   if (fresh) d.markerAmbig.push_back(0);
-  else d.markerAmbig[it->second] = 1;
+  else d.markerAmbig[it->second] = d.markerDup = true;
   return it->second + 1;
+}
+uint32_t marker_key_id(const Interner& in) {
+  auto k = in.keyId.find(U16(u"markerId"));
+  return k == in.keyId.end() ? MTB_NONE : k->second;
 }
 // the JSON text of an interned props id's markerId (property set, or op-props list), or nullptr
 const std::string* props_marker_json(const Interner& in, uint32_t props, bool opList) {
@@ -557,8 +564,10 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, H
     auto it = d->markerOrd.find(*key);
     if (it == d->markerOrd.end())
       raise(MTB_E_UNSUPPORTED, "unsupported: relative position names no marker of the document (posFromRelativePos -1)");
-    if (d->markerAmbig[it->second] || d->markerIdsUnstable)
-      raise(MTB_E_UNSUPPORTED, "unsupported: relative position naming a marker id that is reused or set by an annotate");
+    if (d->markerAmbig[it->second]) {
+      if (d->totalLocal) raise(MTB_E_UNSUPPORTED, "unsupported: relative position naming a reused marker id in a live client's document");
+      d->relOnDup = true;
+    }
     const hj::Value* off = member(*rp, u"offset");
     double o = 0;
     if (off && off->kind != hj::Value::kNull) {
@@ -576,6 +585,12 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, H
     return MTB_RELPOS | at;
   }
   raise(MTB_E_UNSUPPORTED, "unsupported: op without numeric position");
+}
+
+// An annotate's props.markerId as the device compares it with an annotated marker's own id (JS ===): 1 = a
+// primitive (equal iff the interned value ids are), 2 = null, an object or an array (equal to nothing).
+uint32_t annot_marker_test(const hj::Value* v) {
+  return (v->kind == hj::Value::kStr || v->kind == hj::Value::kNum || v->kind == hj::Value::kBool) ? 1u : 2u;
 }
 
 // One delta op -> record (client.ts:489-524 insert, :430 remove, :457 annotate)
@@ -639,7 +654,11 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
     r.pos2 = position(op, u"pos2", u"relativePos2", rel, &r);
     if (type == 2) {
       const hj::Value* props = member(op, u"props");
-      if (props && props->kind == hj::Value::kObj && member(*props, u"markerId")) d.markerIdsUnstable = true;
+      if (props && props->kind == hj::Value::kObj)
+        if (const hj::Value* mid = member(*props, u"markerId")) {  // assert 0x5ad's operand (mergeTree.ts:1912-1918)
+          d.markerIdAnnot = true;
+          r.payload = annot_marker_test(mid);
+        }
       hj::Value empty;
       empty.kind = hj::Value::kObj;
       r.props = b->in.props(props && props->kind == hj::Value::kObj ? *props : empty);
@@ -940,8 +959,19 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
     im.mk_map = (uint32_t)im.aux.size();
     im.mk_n = (uint32_t)d.markerAmbig.size();
     im.aux.resize(im.aux.size() + im.mk_n, MTB_NONE);
+    std::vector<uint32_t> all;
     for (size_t i = 0; i < hdr.size(); i++)
-      if (hdr[i].mord && hdr[i].rseq < 0) im.aux[im.mk_map + hdr[i].mord - 1] = (uint32_t)i;
+      if (hdr[i].mord && hdr[i].rseq < 0) {
+        im.aux[im.mk_map + hdr[i].mord - 1] = (uint32_t)i;
+        all.push_back((uint32_t)i);
+        all.push_back(hdr[i].mord - 1);
+      }
+    if (!all.empty()) {  // [n, cap, (segment, ordinal)*] for blockUpdate's re-mapping of reused ids
+      im.mk_all = (uint32_t)im.aux.size();
+      im.aux.push_back((uint32_t)all.size() / 2);
+      im.aux.push_back((uint32_t)all.size() / 2);
+      im.aux.insert(im.aux.end(), all.begin(), all.end());
+    }
   }
   // body: runs of NonCollab/UniversalSeq segments share one insertSegments call; any other segment is
   // inserted alone with its own client and seq (snapshotLoader.ts:201-220)
@@ -1078,6 +1108,7 @@ Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
   }
   // a live client's pending groups: directory entries (8 words, doubling) and member lists
   c.aux += (uint32_t)std::min<uint64_t>(48 * d.totalLocal, 1u << 30);
+  if (!d.markerAmbig.empty()) c.aux += (uint32_t)std::min<uint64_t>(8 * n, 1u << 30);  // the id map and mk_all
   return c;
 }
 bool fits(const DocState& s, const Caps& c) {
@@ -1173,6 +1204,7 @@ void device_init(mtb_dev* b) {
       s.aux_used = (uint32_t)im.aux.size();
       s.mk_map = im.mk_map;
       s.mk_n = im.mk_n;
+      s.mk_all = im.mk_all;
       s.heap_cnt = 0;
       s.text_used = (uint32_t)d.initText.size();
       segc.add(recs.size(), s.seg_base, im.segp.size());
@@ -1399,6 +1431,7 @@ std::string derr_text(int e) {
     case DERR_HOST: return "host post-processing of the replay failed";
     case DERR_REGEN: return "0x033/0x035 regeneratePendingOp: segment group not at the head of the pending queue";
     case DERR_SCHED: return "internal: the document's records did not all run (replay scheduler invariant)";
+    case DERR_ASSERT_MKID: return "0x5ad Cannot change the markerId of an existing marker";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     default: return "device error " + std::to_string(e);
   }
@@ -1406,7 +1439,7 @@ std::string derr_text(int e) {
 int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
   if (e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) return MTB_E_CAPACITY;
-  if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN) return MTB_E_ASSERT;
+  if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN || e == DERR_ASSERT_MKID) return MTB_E_ASSERT;
   if (e == DERR_SCHED) return MTB_E_INTERNAL;
   return MTB_E_UNSUPPORTED;
 }
@@ -1496,7 +1529,8 @@ void launch_main(mtb_dev* b, const Tables& t) {
     // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
     // batches where some document met a marker id
     bool markers = false;
-    for (uint32_t i = 0; i < b->ndocs && !markers; i++) markers = !b->docs[i].markerAmbig.empty();
+    for (uint32_t i = 0; i < b->ndocs && !markers; i++)
+      markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot;
     // more documents than wave slots: the ticket-scheduled kernel (MTB_SCHED=0 turns it off, MTB_CHUNKS sets
     // the tickets per document)
     if (!b->live && !markers && !b->waveSlots) {
@@ -1653,6 +1687,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
     s.op_next = 0;
     mtb_op* out = ops.get() + opOff[i];
     s.mk_cap = (uint32_t)d.markerAmbig.size();
+    if (d.markerDup) s.flags |= DSF_MKDUP;
     for (mtb_op o : d.pending) {
       // text offsets move with the arena; a PermutationSegment's LOADSEG payload is its handle start
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER) && !d.perm) o.payload += base;
@@ -1702,6 +1737,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   t.key_rank = b->dKeyRank.p;
   t.delta = b->dDelta.p;
   t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
+  t.mk_key = marker_key_id(b->in);
   b->residentLoad = anyLoad;
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
@@ -2931,6 +2967,8 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     if (b->opts.flags & MTB_BATCH_CATCHUP) raise(MTB_E_UNSUPPORTED, "unsupported: local ops in a catch-up batch");
     HostDoc& d = docref(b, doc);
     if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    if (d.relOnDup)  // the live kernel keeps idToSegment without blockUpdate's re-mapping
+      raise(MTB_E_UNSUPPORTED, "unsupported: local ops in a document whose relative positions name a reused marker id");
     const hj::Value op = hj::parse(json, len);
     if (op.kind != hj::Value::kObj) raise(MTB_E_PARSE, "op is not an object");
     mtb_op base{};
@@ -3201,8 +3239,13 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
           mp.members.push_back({U16(u"markerId"), hj::parse(js->data(), js->size())});
           o.payload = marker_ord(d, &mp);
         }
-      } else if (o.type == MTB_OP_ANNOTATE && props_marker_json(b->in, o.props, true)) {
-        d.markerIdsUnstable = true;
+      } else if (o.type == MTB_OP_ANNOTATE) {
+        o.payload = 0;
+        if (const std::string* js = props_marker_json(b->in, o.props, true)) {
+          const hj::Value v = hj::parse(js->data(), js->size());
+          d.markerIdAnnot = true;
+          o.payload = annot_marker_test(&v);
+        }
       }
     }
     d.payload.insert(d.payload.end(), payload, payload + payload_len);
@@ -3250,6 +3293,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     t.key_rank = b->dKeyRank.p;
     t.delta = b->dDelta.p;
     t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
+    t.mk_key = marker_key_id(b->in);
     HIPCHK(hipEventRecord(b->ev0, b->stream));
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,

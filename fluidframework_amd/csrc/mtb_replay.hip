@@ -243,6 +243,8 @@ struct Eng {
   int ld_pos;                   // insertSegments' advancing insert position within a LOADSEG batch
   uint32_t cur_k;               // index of the record being applied (catch-up delta entries name it)
   bool delta_on;                // the record asks for its delta ranges (MTB_F_DELTA)
+  bool mkDup;                   // DSF_MKDUP: leaf-block updates re-map marker ids (hasMk modes)
+  uint32_t ann_mk;              // the annotate's markerId test (record payload): 0 none, 1 same value, 2 never
   uint32_t delta_used;          // entries written in this document's delta slice
   static constexpr bool isPerm = MODE == MODE_MATRIX || MODE == MODE_LOADPERM;  // PermutationVectors only
   static constexpr bool isLoad = MODE == MODE_LOAD || MODE == MODE_LOADPERM;  // LOADSEG records only
@@ -1287,6 +1289,7 @@ struct Eng {
           if (!isPerm && (U(V.f[F_TEXT][j]) & MTB_MARKER)) return true;  // markers never split
           split_seg(d, j, pjj);
           if (bad()) return false;
+          mk_remap_view(d);  // blockUpdateLength of the leaf block, or split's updates of its halves
           pending_fix = d;  // (handled by the caller, after the walk)
           return true;
         }
@@ -1316,6 +1319,7 @@ struct Eng {
       if (lane == 0) sh->slot[d] = at;
       wsync();
       insert_slot(d, at);
+      mk_remap_view(d);
       add_len_levels(0, d, d, candLen);
       if constexpr (isLoad) load_entries(d, S, C);
       else append_levels(0, d, S, C, WK_MAIN, candLen);
@@ -2299,7 +2303,13 @@ struct Eng {
         insert_levels_sorted(0, d, rl(rseq, t), C, WK_OVERLAP, rl(len, t));
         if (bad()) return 0;
       }
+      mk_remap_view(d);  // afterMarkRemoved: the leaf block's blockUpdateLength / nodeUpdateLengthNewStructure
     } else {
+      if constexpr (hasMk)
+        if (COLD(ann_mk != 0)) {
+          mk_check_annot(vm, lane < count ? V.f[F_TEXT][lane] : 0u, props, opId);
+          if (bad()) return 0;
+        }
       // annotate: one new property set per distinct old set (memoized per op)
       unsigned long long am = vm, handled = 0;
       if (isLive && S >= MTB_PEND) {  // a local annotate: every annotated segment joins its group, in order
@@ -2837,6 +2847,7 @@ struct Eng {
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
           const int kb = __ballot(kblk) != 0;
+          if (!kb) mk_remap_hold(taken, n);  // nodeUpdateLengthNewStructure(packedBlock) (zamboni.ts:103)
           if (lane == q) {
             nbs = nb;
             lens = len;
@@ -3081,6 +3092,7 @@ struct Eng {
         PROF_ZADD(PH_PLACE, tz);
         tz = PROF_T();
         if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);
+        else mk_remap_hold(0, nh);  // blockUpdatePathLengths(block, .., true) (zamboni.ts:55)
         PROF_ADD(PH_PACK, tz);
       } else {
         PROF_ZADD(PH_PLACE, tz);
@@ -3110,6 +3122,115 @@ struct Eng {
     }
     if (lane == 0) aux[map + ord] = sid;
     wsync();
+  }
+  // Duplicate ids (DSF_MKDUP): every marker inserted with an id is listed as (segment, ordinal) in
+  // DocState.mk_all [n, cap, pairs], so a leaf block's update can name the ids of its markers.
+  __device__ __forceinline__ void mk_record(uint32_t ord, uint32_t sid) {
+    uint32_t h = U(ds->mk_all);
+    const uint32_t n = h ? U(aux[h]) : 0u, cap = h ? U(aux[h + 1]) : 0u;
+    if (n >= cap) {
+      const uint32_t nc = cap ? 2 * cap : 8u;
+      const uint32_t nh = alloc_aux(2 + 2 * nc);
+      if (bad()) return;
+      for (uint32_t i = lane; i < 2 * n; i += 64) aux[nh + 2 + i] = aux[h + 2 + i];
+      if (lane == 0) {
+        aux[nh + 1] = nc;
+        ds->mk_all = nh;
+      }
+      h = nh;
+    }
+    if (lane == 0) {
+      aux[h + 2 + 2 * n] = sid;
+      aux[h + 3 + 2 * n] = ord;
+      aux[h] = n + 1;
+    }
+    wsync();
+  }
+  __device__ __forceinline__ uint32_t mk_ord_of(uint32_t sid) const {
+    const uint32_t h = U(ds->mk_all);
+    if (!h) return MTB_NONE;
+    const uint32_t n = U(aux[h]);
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      const unsigned long long m = __ballot(i < n && aux[h + 2 + 2 * i] == sid);
+      if (m) return U(aux[h + 3 + 2 * (base + (uint32_t)first_set(m))]);
+    }
+    return MTB_NONE;
+  }
+  // the value id of key k in property set h (MTB_NONE: absent); per lane
+  __device__ __forceinline__ uint32_t props_val(uint32_t h, uint32_t k) const {
+    if (!h || k == MTB_NONE) return MTB_NONE;
+    const auto p = props_ptr(h);
+    const uint32_t n = p[0];
+    for (uint32_t i = 0; i < n; i++)
+      if (p[1 + 2 * i] == k) return p[2 + 2 * i];
+    return MTB_NONE;
+  }
+  // blockUpdate (mergeTree.ts:2392-2417) of a block of segments: addNodeReferences (:296-306) maps the id
+  // of every child marker whose localNetLength is positive, in child order (the last one wins).  Lane i
+  // holds child i (i < n).  Only documents with a reused id need it: otherwise an id's one marker is
+  // already mapped by its insert and the map is never pruned.
+  __device__ __forceinline__ void mk_remap(int n, uint32_t id, uint32_t text, uint32_t props, int len, int rseq) {
+    const uint32_t key = U(sh->tab.mk_key);
+    const bool q = lane < n && (id & MTB_LEAF) && (text & MTB_MARKER) && props && key != MTB_NONE &&
+                   local_len(len, rseq) > 0 && props_val(props, key) != MTB_NONE;
+    unsigned long long m = __ballot(q);
+    while (m && !err) {
+      const int t = first_set(m);
+      m &= m - 1;
+      const uint32_t sid = rlu(id, t) & ~MTB_LEAF;
+      const uint32_t ord = mk_ord_of(sid);
+      if (ord != MTB_NONE) mk_set(ord, sid);
+    }
+  }
+  __device__ __forceinline__ void mk_remap_view(int d) {
+    if constexpr (MODE == MODE_MARKERS || MODE == MODE_LOAD) {
+      if (COLD(mkDup)) {
+        const View& V = sh->v[d];
+        const int n = U(V.count);
+        uint32_t id = MTB_NONE, text = 0, props = 0;
+        int len = 0, rseq = -1;
+        if (lane < n) {
+          id = V.f[F_ID][lane];
+          text = V.f[F_TEXT][lane];
+          props = V.f[F_PROPS][lane];
+          len = (int)V.f[F_LEN][lane];
+          rseq = (int)V.f[F_RSEQ][lane];
+        }
+        mk_remap(n, id, text, props, len, rseq);
+      }
+    }
+  }
+  __device__ __forceinline__ void mk_remap_hold(int from, int n) {  // children placed from sh->hold[.][from..)
+    if constexpr (MODE == MODE_MARKERS || MODE == MODE_LOAD) {
+      if (COLD(mkDup)) {
+        uint32_t id = MTB_NONE, text = 0, props = 0;
+        int len = 0, rseq = -1;
+        if (lane < n) {
+          id = sh->hold[F_ID][from + lane];
+          text = sh->hold[F_TEXT][from + lane];
+          props = sh->hold[F_PROPS][from + lane];
+          len = (int)sh->hold[F_LEN][from + lane];
+          rseq = (int)sh->hold[F_RSEQ][from + lane];
+        }
+        mk_remap(n, id, text, props, len, rseq);
+      }
+    }
+  }
+  // assert 0x5ad (annotateRange, mergeTree.ts:1912-1918): an annotate whose props name markerId must carry
+  // each annotated marker's own id (JS ===; the host reduced the op's value to ann_mk: 1 = a primitive,
+  // compared as its value id, 2 = null / object, equal to nothing).  Lanes of `vm` hold the visited children.
+  __device__ __forceinline__ void mk_check_annot(unsigned long long vm, uint32_t text, uint32_t props, uint32_t opId) {
+    const bool mk = ((vm >> lane) & 1) && (text & MTB_MARKER);
+    if (!__ballot(mk)) return;
+    if (ann_mk != 1) { fail(DERR_ASSERT_MKID); return; }
+    const uint32_t key = U(sh->tab.mk_key);
+    const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * opId]);
+    uint32_t vop = MTB_NONE;
+    const uint32_t nop = U(op[0]);
+    for (uint32_t q = 0; q < nop; q++)
+      if (U(op[1 + 2 * q]) == key) vop = U(op[2 + 2 * q]);
+    if (__ballot(mk && props_val(props, key) != vop)) fail(DERR_ASSERT_MKID);
   }
   // posFromRelativePos (mergeTree.ts:1371-1395) of a record position field `v` in the op's (R, C) view:
   // v itself, or for MTB_RELPOS | descriptor offset: getPosition (:768-785) of the mapped marker (0 once
@@ -3208,6 +3329,8 @@ struct Eng {
       n_mod += 1;
       if (COLD(marker && o.payload != 0)) {  // body markers are mapped whatever their removal (:1658-1663)
         mk_set(o.payload - 1, sid);
+        if (bad()) return;
+        mk_record(o.payload - 1, sid);
         if (bad()) return;
       }
       const bool ok = walk(ld_pos, 0, C, S, true, rseq >= 0 ? 0 : len, first);
@@ -3317,6 +3440,8 @@ struct Eng {
             if (COLD(marker && o.payload != 0)) {
               mk_set(o.payload - 1, sid);
               if (bad()) return;
+              mk_record(o.payload - 1, sid);
+              if (bad()) return;
             }
           if (!walk(p1, R, C, S, true, len, true)) {
             fail(DERR_INSERT);
@@ -3340,6 +3465,7 @@ struct Eng {
       case MTB_OP_ANNOTATE: {
         ops_applied++;
         view_clear();
+        if constexpr (hasMk) ann_mk = o.type == MTB_OP_ANNOTATE ? (o.payload & 3u) : 0u;
         uint64_t t0 = PROF_T();
         int p1 = (int)o.pos1, p2 = (int)o.pos2;
         if constexpr (hasMk)
@@ -3456,6 +3582,12 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.pending_fix = -1;
   e.ld_pos = 0;
   e.delta_on = false;
+#ifdef MTB_NO_MKREMAP  // (test builds: shows the reused-id tests depend on the re-mapping)
+  e.mkDup = false;
+#else
+  e.mkDup = (ds->flags & DSF_MKDUP) != 0;
+#endif
+  e.ann_mk = 0;
   e.delta_used = ds->delta_used;
   e.cur_k = 0;
   e.sp_internal = false;

@@ -978,7 +978,19 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
   const int localSeq = seq == UnassignedSeq ? ++window.localSeq : INT32_MIN;  // mergeTree.ts:1909-1910
   SegGroup* group = nullptr;
   if (seq == UnassignedSeq && rewrite) fail_unsupported("local rewrite annotate");
+  // assert 0x5ad (mergeTree.ts:1912-1918): an annotate naming markerId must carry the marker's own id
+  // (JS ===: primitives by value; an object or array value is a fresh object, never equal)
+  const JVal* opId = obj_get(props, u"markerId");
+  auto same_id = [](const JVal* a, const JVal* b) {
+    const JVal::T ta = a ? a->t : JVal::Undef, tb = b ? b->t : JVal::Undef;
+    if (ta != tb || ta == JVal::Obj || ta == JVal::Arr) return false;
+    if (ta == JVal::Num) return a->num == b->num;
+    if (ta == JVal::Str) return a->str == b->str;
+    return true;
+  };
   auto annotate = [&](Seg* s, int, int, int) -> bool {
+    if (opId && s->isMarker && !same_id(opId, s->props ? obj_get(*s->props, u"markerId") : nullptr))
+      fail_assert("0x5ad", "Cannot change the markerId of an existing marker");
     annotated.push_back(s);
     applyProps(s, props, rewrite, seq, window.collaborating);
     counters.segsTouched += 1;

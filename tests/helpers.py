@@ -445,13 +445,26 @@ def load_logbatch(B, lb, docs=None, props_interned=False):
     return docs
 
 
-def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="hello marker world", p_rel=0.5):
+def _marker_ids_ok(gen, a, b, R, cid, mid):
+    """Every marker in [a, b) of the (R, cid) view carries markerId `mid` (annotateRange's assert 0x5ad)."""
+    for e in gen.map_range(a, b, R, cid):
+        seg = e["segment"]
+        if seg.get("type") == "Marker" and (seg.get("properties") or {}).get("markerId") != mid:
+            return False
+    return True
+
+
+def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="hello marker world", p_rel=0.5,
+                    dup_ids=0):
     """A sequenced op log with markers carrying unique `markerId`s and ops whose positions are marker-relative
     (IRelativePosition, ops.ts:77-92): `annotateMarker` ops (opBuilder.ts:25-43, {id, before: true} ..
     {id}) and inserts / removes / annotates with relativePos1/2 (before / offset), next to plain ones.  A
     generator oracle (every message applied as it is made) resolves each candidate relative position in the
     sender's (refSeq, client) view (posFromRelativePos) so that only in-range ops are emitted; markers that
-    were removed, or unlinked by zamboni, stay eligible.  Returns (initial text, messages)."""
+    were removed, or unlinked by zamboni, stay eligible.  With `dup_ids` > 0 marker ids come from a pool of
+    that many (so ids are reused and blockUpdate's re-mapping decides what they name), annotates may name
+    markerId (the marker's own id, as assert 0x5ad requires; text ranges any id) and rewrite annotates drop
+    markers' ids.  Returns (initial text, messages)."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -488,7 +501,7 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
         x = rng.random()
         op = None
         if x < 0.12 or n == 0:
-            mid = f"m{seed}-{seq}"
+            mid = f"d{rng.randrange(dup_ids)}" if dup_ids else f"m{seed}-{seq}"
             p = rng.randint(0, n)
             op = {"type": 0, "pos1": p, "seg": {"marker": {"refType": rng.choice([0, 1, 2])},
                                                  "props": {"markerId": mid, "kind": rng.randint(0, 2)}}}
@@ -499,6 +512,15 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
             if 0 <= p and p + 1 <= n:
                 op = {"type": 2, "relativePos1": {"id": mid, "before": True}, "relativePos2": {"id": mid},
                       "props": {"state": rng.choice(["open", "closed", None])}}
+                if dup_ids and rng.random() < 0.5 and _marker_ids_ok(gen, p, p + 1, R, cid, mid):
+                    op["props"]["markerId"] = mid  # the marker's own id: no assert
+        elif dup_ids and x < 0.31 and n > 0:  # rewrite (drops markerId) or a markerId annotate over text
+            a = rng.randrange(n)
+            b = min(n, a + rng.randint(1, 4))
+            if rng.random() < 0.5:
+                op = {"type": 2, "pos1": a, "pos2": b, "props": {"state": "rw"}, "combiningOp": {"name": "rewrite"}}
+            elif _marker_ids_ok(gen, a, b, R, cid, "t"):
+                op = {"type": 2, "pos1": a, "pos2": b, "props": {"markerId": "t"}}
         if op is None:
             t = rng.choice([0, 0, 1, 2])
             if t == 0:

@@ -240,3 +240,132 @@ def test_test_client_helpers_reference_applymsg_kat():
     assert c.getText(0, 3) == "ab"
     props = [e["segment"].get("properties") for e in B.map_range(0, 0, 2)]
     assert props == [{"x": 1}]
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_reused_marker_ids_follow_block_update(new_mode):
+    """Marker ids reused across markers (make_marker_log(dup_ids=...)): which marker an id names is decided
+    by the last blockUpdate of a leaf block holding one of them (mergeTree.ts:2392 -> addNodeReferences
+    :296-306; insertingWalk :1780-1846, split :1858-1871, markRangeRemoved's post-order :2019-2026,
+    zamboni.ts:55/:103), with annotates naming markerId (assert 0x5ad) and rewrites dropping ids.  The
+    marker kernel's re-mapping (DSF_MKDUP) against the oracle: dumps, text, digests, SnapshotV1."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    logs = [make_marker_log(300 + s, 800, n_clients=3 + s % 3, lag=4 + 5 * s, new_mode=new_mode, dup_ids=2 + s % 4)
+            for s in range(12)]
+    B = MergeTreeBatch(len(logs), new_length_calc=new_mode)
+    orc = []
+    for i, (init, _) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("obs")
+        orc.append(o)
+    for part in (slice(0, 300), slice(300, None)):
+        for i, (_, msgs) in enumerate(logs):
+            for m in msgs[part]:
+                B[i].applyMsg(m)
+                orc[i].apply_msg(m)
+        st = B.replay()
+        assert st["errors"] == 0, st
+        for i, o in enumerate(orc):
+            _same(B, i, o, f"log {i} {part}")
+    for i, o in enumerate(orc):
+        gb, gs = B.summarize_v1(i)
+        assert [list(x) for x in gb] == o.summarize_v1()["blobs"], f"log {i}: SnapshotV1 differs"
+
+
+def test_reused_id_kat_and_marker_id_assert_on_the_engine():
+    """test_relative_positions.py's duplicate-id KAT (the newer marker's insert re-maps the older one too,
+    child order: the last wins) and assert 0x5ad (an annotate changing a marker's id) fail / pass per
+    document on the engine exactly as on the oracle."""
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from pyoracle import OracleDoc, OracleError
+
+    def msg(cid, seq, ref, op):
+        return {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref, "minimumSequenceNumber": 0,
+                "type": "op", "contents": op}
+
+    mk = lambda pos, mid: {"type": 0, "pos1": pos, "seg": {"marker": {"refType": 1}, "props": {"markerId": mid}}}
+    kat = [msg("a", 1, 0, mk(2, "d")), msg("a", 2, 1, mk(9, "d")),
+           msg("b", 3, 2, {"type": 0, "relativePos1": {"id": "d", "before": True}, "seg": "<"})]
+    assert_log = [msg("a", 1, 0, mk(2, "k")), msg("b", 2, 1, {"type": 2, "pos1": 2, "pos2": 3, "props": {"markerId": "z"}})]
+    ok_log = [msg("a", 1, 0, mk(2, "k")), msg("b", 2, 1, {"type": 2, "pos1": 1, "pos2": 4, "props": {"markerId": "k"}}),
+              msg("b", 3, 2, {"type": 0, "relativePos1": {"id": "k"}, "seg": ">"})]
+    B = MergeTreeBatch(3)
+    for i, log in enumerate((kat, assert_log, ok_log)):
+        B[i].insertTextLocal(0, "hello world")
+        B[i].startOrUpdateCollaboration("obs")
+        for m in log:
+            B[i].applyMsg(m)
+    with pytest.raises(MergeTreeError, match="0x5ad"):
+        B.replay()
+    for i, log in ((0, kat), (2, ok_log)):
+        o = OracleDoc()
+        o.insert_text_local(0, "hello world")
+        o.start_collab("obs")
+        for m in log:
+            o.apply_msg(m)
+        _same(B, i, o, f"doc {i}")
+    assert B.text(0) == "hello wo<rld"  # inserted before the newer marker "d" (position 9)
+    o = OracleDoc()
+    o.insert_text_local(0, "hello world")
+    o.start_collab("obs")
+    o.apply_msg(assert_log[0])
+    with pytest.raises(OracleError, match="0x5ad"):
+        o.apply_msg(assert_log[1])
+
+
+def test_loaded_summary_with_reused_marker_ids():
+    """A SnapshotV1 header and body holding several markers per id (reloadFromSegments' blockUpdate maps the
+    last live one; body inserts re-map through insertingWalk), then marker-relative ops naming them."""
+    import random as _r
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    rng = _r.Random(9)
+    src = OracleDoc(chunk_size=40)
+    src.insert_text_local(0, "x" * 120)
+    for k in range(24):
+        src.insert_marker_local(rng.randint(0, src.get_length()), 1, {"markerId": f"d{k % 3}"})
+    src.start_collab("w")
+    blobs = src.summarize_v1()["blobs"]
+    assert any("body_" in p for p, _ in blobs)
+    gen = OracleDoc(chunk_size=40)
+    gen.load_v1(blobs, "gen")
+    msgs, seq = [], 0
+    while len(msgs) < 300:
+        seq += 1
+        cid = rng.choice(["a", "b", "c"])
+        ref = max(0, seq - 1 - rng.randint(0, 6))
+        mid = f"d{rng.randrange(3)}"
+        r = rng.random()
+        if r < 0.3:
+            op = {"type": 0, "pos1": rng.randint(0, gen.remote_length(ref, 0)),
+                  "seg": {"marker": {"refType": 1}, "props": {"markerId": mid}}}
+        elif r < 0.7:
+            op = {"type": 0, "relativePos1": {"id": mid, "before": rng.random() < 0.5}, "seg": rng.choice(["y", "zz"])}
+        else:
+            op = {"type": 1, "relativePos1": {"id": mid, "before": True}, "relativePos2": {"id": mid, "offset": 1}}
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+             "minimumSequenceNumber": max(0, seq - 8), "type": "op", "contents": op}
+        probe = OracleDoc(chunk_size=40)  # keep only ops valid in the sender's view
+        probe.load_v1(blobs, "gen")
+        try:
+            for x in msgs + [m]:
+                probe.apply_msg(x)
+        except Exception:
+            seq -= 1
+            continue
+        gen.apply_msg(m)
+        msgs.append(m)
+    o = OracleDoc(chunk_size=40)
+    o.load_v1(blobs, "obs")
+    B = MergeTreeBatch(1, chunk_size=40)
+    B[0].load([tuple(x) for x in blobs], "obs")
+    for m in msgs:
+        B[0].applyMsg(m)
+        o.apply_msg(m)
+    st = B.replay()
+    assert st["errors"] == 0, st
+    _same(B, 0, o, "loaded reused ids")

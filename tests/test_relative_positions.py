@@ -89,7 +89,7 @@ def test_unlinked_marker_position_is_zero():
 def test_duplicate_ids_follow_block_update():
     """Two markers with one id: insertSegments maps the newer one; any later blockUpdate of the older
     one's block maps the older one back (children in order, last wins) — observable through relative
-    positions.  Oracle-defined (the engine rejects relative ops naming a reused id)."""
+    positions.  Oracle-defined; the engine's marker kernel re-maps the same way (tests/test_gpu_relpos.py)."""
     o = _doc()
     o.apply_msg(_msg("a", 1, 0, 0, {"type": 0, "pos1": 2, "seg": {"marker": {}, "props": {"markerId": "d"}}}))
     o.apply_msg(_msg("a", 2, 1, 0, {"type": 0, "pos1": 9, "seg": {"marker": {}, "props": {"markerId": "d"}}}))
@@ -129,13 +129,58 @@ def test_host_rejects_unresolvable_relative_positions_at_pack_time():
     assert fl & 0x20 and p1 & 0x80000000  # MTB_F_RELPOS: pos1 names a descriptor
     t, fl, c, seq, ref, msn, p1, p2, pay, pr = struct.unpack_from("<BBHIIIIIII", ob, 0)
     assert fl & 0x02 and pay == 1  # the marker carries its id ordinal + 1
-    # a reused id makes relative positions naming it ambiguous (blockUpdate would decide)
+    # a reused id: the observer's marker kernel re-maps it at blockUpdate time, so relative positions naming
+    # it pack; a live client's document (local ops) rejects them, before or after its first local op
     B[0].applyMsg(_msg("B", 3, 2, 0, mk))
-    with pytest.raises(MergeTreeError, match="reused"):
-        B[0].applyMsg(_msg("B", 4, 3, 0, {"type": 1, "relativePos1": {"id": "m1", "before": True}, "relativePos2": {"id": "m1"}}))
+    rm = {"type": 1, "relativePos1": {"id": "m1", "before": True}, "relativePos2": {"id": "m1"}}
+    B[0].applyMsg(_msg("B", 4, 3, 0, rm))
+    with pytest.raises(MergeTreeError, match="reused marker id"):
+        B[0].insertSegmentLocal(0, "x")
+    L = MergeTreeBatch(1)
+    L[0].startOrUpdateCollaboration("A")
+    L[0].applyMsg(_msg("B", 1, 0, 0, mk))
+    L[0].applyMsg(_msg("B", 2, 1, 0, mk))
+    L[0].insertSegmentLocal(0, "x")
+    with pytest.raises(MergeTreeError, match="reused marker id"):
+        L[0].applyMsg(_msg("B", 3, 2, 0, rm))
     # a live client's local ops and catch-up batches take absolute positions only
     C = MergeTreeBatch(1, catch_up=True)
     C[0].startOrUpdateCollaboration("A")
     C[0].applyMsg(_msg("B", 1, 0, 0, mk))
     with pytest.raises(MergeTreeError, match="relative positions here"):
         C[0].applyMsg(_msg("B", 2, 1, 0, {"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
+
+
+def test_annotate_may_not_change_a_marker_id():
+    """annotateRange's assert 0x5ad (mergeTree.ts:1912-1918): props naming markerId must carry each annotated
+    marker's own id (JS ===): the same primitive passes, another value / null / an object fails, a marker
+    without an id fails, text segments are not checked."""
+    from pyoracle import OracleError
+
+    def doc_with_markers():
+        o = _doc()
+        o.apply_msg(_msg("a", 1, 0, 0, {"type": 0, "pos1": 2, "seg": {"marker": {"refType": 1}, "props": {"markerId": "k"}}}))
+        o.apply_msg(_msg("a", 2, 1, 0, {"type": 0, "pos1": 8, "seg": {"marker": {"refType": 1}}}))
+        return o
+
+    o = doc_with_markers()
+    o.apply_msg(_msg("b", 3, 2, 0, {"type": 2, "pos1": 2, "pos2": 3, "props": {"markerId": "k", "x": 1}}))
+    o.apply_msg(_msg("b", 4, 3, 0, {"type": 2, "pos1": 4, "pos2": 7, "props": {"markerId": "text-ok"}}))
+    assert o.pos_from_relative({"id": "k", "before": True}, 4, 0) == 2
+    for props, at in (({"markerId": "z"}, 2), ({"markerId": None}, 2), ({"markerId": {"k": 1}}, 2), ({"markerId": "k"}, 8)):
+        o = doc_with_markers()
+        with pytest.raises(OracleError, match="0x5ad"):
+            o.apply_msg(_msg("b", 3, 2, 0, {"type": 2, "pos1": at, "pos2": at + 1, "props": props}))
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_duplicate_id_log_generator_replays_on_a_fresh_oracle(new_mode):
+    """make_marker_log(dup_ids=...) streams (reused ids, markerId annotates, rewrites dropping ids) replay."""
+    from pyoracle import OracleDoc
+    init, msgs = make_marker_log(21, 500, new_mode=new_mode, dup_ids=3)
+    assert sum(1 for m in msgs if "markerId" in (m["contents"].get("props") or {}) and m["contents"]["type"] == 2) > 10
+    o = OracleDoc(new_length_calc=new_mode, verify=True)
+    o.insert_text_local(0, init)
+    o.start_collab("obs")
+    for m in msgs:
+        o.apply_msg(m)
