@@ -269,6 +269,7 @@ struct Eng {
     return seg_used++;
   }
   __device__ __forceinline__ uint32_t* bw(uint32_t b) const { return reinterpret_cast<uint32_t*>(&blk[b]); }
+  __device__ __forceinline__ u32x4* lst4() const { return reinterpret_cast<u32x4*>(lst); }
   __device__ __forceinline__ uint32_t alloc_blk() {
     uint32_t b;
     if (free_top > 0) {
@@ -599,17 +600,17 @@ struct Eng {
     bool unsorted = false;
     for (uint32_t base = 0; base < cnt; base += 64) {
       const uint32_t i = base + lane;
-      WEnt e;
+      u32x4 e = {0u, 0u, 0u, 0u};  // (entries as vectors: struct copies here went through scratch)
       bool keep = false;
       if (i < cnt) {
-        e = lst[off + i];
-        keep = e.seq > minSeq;
+        e = lst4()[off + i];
+        keep = (int)e.x > minSeq;
       }
       const unsigned long long m = __ballot(keep);
-      if (keep) lst[no + w + rank_below(m)] = e;
+      if (keep) lst4()[no + w + rank_below(m)] = e;
       w += __popcll(m);
       // order check: each kept entry against the largest kept seq before it (prefix max)
-      int pm = keep ? e.seq : MTB_NOKEY;
+      int pm = keep ? (int)e.x : MTB_NOKEY;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const int t = __shfl_up(pm, o, 64);
@@ -618,7 +619,7 @@ struct Eng {
       int prev = __shfl_up(pm, 1, 64);
       if (lane == 0) prev = MTB_NOKEY;
       prev = max(prev, carry);
-      if (keep && e.seq < prev) unsorted = true;
+      if (keep && (int)e.x < prev) unsorted = true;
       carry = max(carry, rl(pm, 63));
     }
     live = w;
@@ -729,12 +730,11 @@ struct Eng {
           const uint32_t n = top < 64 ? top : 64u;
           const uint32_t i = top - n + (uint32_t)lane;
           const bool v = (uint32_t)lane < n;
-          WEnt e;
-          e.seq = MTB_NOKEY;
-          if (v) e = lst[loff + i];
-          const bool gt = v && e.seq > seqv;
+          u32x4 e = {(uint32_t)MTB_NOKEY, 0u, 0u, 0u};
+          if (v) e = lst4()[loff + i];
+          const bool gt = v && (int)e.x > seqv;
           const unsigned long long m = __ballot(gt);
-          if (gt) lst[loff + i + 1] = e;  // (sorted: the lanes above seqv are a suffix of the chunk)
+          if (gt) lst4()[loff + i + 1] = e;  // (sorted: the lanes above seqv are a suffix of the chunk)
           wsync();
           const uint32_t g = (uint32_t)__popcll(m);
           p = top - g;
@@ -881,7 +881,7 @@ struct Eng {
     for (int base = 0; base < ltotal; base += 64) {
       const int t = base + lane;
       bool keep = false;
-      WEnt e;
+      u32x4 e = {0u, 0u, 0u, 0u};
       if (t < ltotal) {
         int j = 0;
 #pragma unroll
@@ -891,12 +891,12 @@ struct Eng {
 #pragma unroll
         for (int q = 0; q < MTB_MAXCH; q++)
           if (q == j) p = off[q] + (t - pre[q]);
-        e = lst[p];
-        keep = e.seq > minSeq;
-        e.ck = (e.ck & 0xFFFFF) | (j << 20);
+        e = lst4()[p];
+        keep = (int)e.x > minSeq;
+        e.y = (e.y & 0xFFFFFu) | ((uint32_t)j << 20);
       }
       const unsigned long long m = __ballot(keep);
-      if (keep) lst[no + wpos + rank_below(m)] = e;
+      if (keep) lst4()[no + wpos + rank_below(m)] = e;
       wpos += __popcll(m);
     }
     wsync();
@@ -952,11 +952,11 @@ struct Eng {
         for (uint32_t base = 0; base < T; base += 64) {
           const uint32_t i = base + (uint32_t)lane;
           if (i < T) {
-            const WEnt e = lst[no + i];
-            const int bk = e.seq - minSeq - 1;
+            const u32x4 e = lst4()[no + i];
+            const int bk = (int)e.x - minSeq - 1;
             const uint32_t sft = (uint32_t)(bk & 1) * 16;
             const uint32_t old = atomicAdd(&hist[bk >> 1], 1u << sft);
-            lst[no2 + ((old >> sft) & 0xFFFF)] = e;
+            lst4()[no2 + ((old >> sft) & 0xFFFF)] = e;
           }
         }
         wsync();
@@ -3741,11 +3741,15 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
 // record fraction of chunk c in 1/4096 (the last one 4096).
 // one ticket: the replay engine as a called function (its register allocation stays the replay kernel's
 // instead of being shaped by the ticket loop around it)
-__device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, DocState* docs, uint32_t ndocs,
-                                                       const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
-                                                       uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
-                                                       const Tables& tables, uint32_t upto) {
-  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables, upto);
+// (the slices are passed as global-address-space pointers: a called function cannot infer that of plain
+// pointer arguments, and its memory accesses would all be flat instructions)
+__device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, gptr<DocState> docs, uint32_t ndocs,
+                                                       gptr<const mtb_op> ops, gptr<uint32_t> segp, gptr<FBlk> blks,
+                                                       gptr<WEnt> lists, gptr<uint16_t> text, gptr<Lru> heap,
+                                                       gptr<uint32_t> aux, gptr<uint32_t> freel, const Tables& tables,
+                                                       uint32_t upto) {
+  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, (DocState*)docs, ndocs, (const mtb_op*)ops, (uint32_t*)segp, (FBlk*)blks,
+                          (WEnt*)lists, (uint16_t*)text, (Lru*)heap, (uint32_t*)aux, (uint32_t*)freel, tables, upto);
 }
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
@@ -3786,8 +3790,9 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
       }
-      sched_ticket(sh, d, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
-                   U(sched[MTB_SCHED_HDR + ndocs + c]));
+      sched_ticket(sh, d, (gptr<DocState>)docs, ndocs, (gptr<const mtb_op>)ops, (gptr<uint32_t>)segp,
+                   (gptr<FBlk>)blks, (gptr<WEnt>)lists, (gptr<uint16_t>)text, (gptr<Lru>)heap, (gptr<uint32_t>)aux,
+                   (gptr<uint32_t>)freel, tables, U(sched[MTB_SCHED_HDR + ndocs + c]));
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X guide: the write-back completes before the flag)
       if (lane == 0) __hip_atomic_store(prog, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
