@@ -41,6 +41,7 @@ hipError_t mtb_launch_rewind(hipStream_t stream, uint32_t ndocs, DocState* docs,
 hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
+int mtb_sched_waves_per_cu();
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
@@ -446,7 +447,7 @@ struct mtb_dev {
   DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
   DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_sched_kernel)
-  uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x 4 SIMDs x 4 waves)
+  uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x the sched kernel's occupancy)
   uint32_t nXcc = 0;                // XCDs of the device (the ticket scheduler's queues)
   mtb_launch_info launch{};         // what the last replay launched (mtb_launch_info)
   uint32_t schedAbortHost = 0;
@@ -1536,7 +1537,7 @@ void launch_main(mtb_dev* b, const Tables& t) {
     if (!b->live && !markers && !b->waveSlots) {
       hipDeviceProp_t prop;
       HIPCHK(hipGetDeviceProperties(&prop, b->device));
-      b->waveSlots = (uint32_t)prop.multiProcessorCount * 16u;
+      b->waveSlots = (uint32_t)prop.multiProcessorCount * (uint32_t)mtb_sched_waves_per_cu();  // (16: 4 per SIMD)
       int nx = 1;
       if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, b->device) != hipSuccess) nx = 1;
       b->nXcc = (uint32_t)std::max(1, std::min(8, nx));

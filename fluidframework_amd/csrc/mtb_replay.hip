@@ -3892,6 +3892,14 @@ hipError_t mtb_launch_observer(KPARAMS) {
     hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
   return hipGetLastError();
 }
+// resident waves of the scheduled kernel per CU (its grid is exactly the device's resident slots)
+int mtb_sched_waves_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(mtb_replay_sched_kernel), 64, 0) !=
+          hipSuccess || n <= 0)
+    return 16;
+  return n;
+}
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
