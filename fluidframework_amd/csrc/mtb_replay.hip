@@ -159,6 +159,12 @@ struct Rec {
 };
 
 template <int HEAPN>
+#ifndef MTB_LSTK
+#define MTB_LSTK 8    // capacity classes with an LDS stack of free lists
+#endif
+#ifndef MTB_LSTK_N
+#define MTB_LSTK_N 4  // lists per stack
+#endif
 struct ScratchT {  // LDS, one per wave
   View v[MTB_VDEPTH];
   uint32_t path[MTB_VDEPTH];   // block at each depth of the current walk
@@ -168,6 +174,10 @@ struct ScratchT {  // LDS, one per wave
   int32_t acc[MTB_VDEPTH];     // node_map accumulated observer-length delta
   uint32_t rmeta[4];           // root window-list metadata (loff, lcnt, lcap)
   uint32_t lfree[MTB_LCLASSES];  // free window lists per capacity class (8 << c entries)
+#ifndef MTB_NO_LSTK
+  uint32_t lstk[MTB_LSTK][MTB_LSTK_N];  // the last lists freed in the small classes, held in LDS: a pop
+  uint32_t lstkn[MTB_LSTK];             // from here needs no dependent read of the next pointer in HBM
+#endif
   int32_t corr[MTB_MAXCH];
   uint32_t nseg[8];            // staged fields of a child being inserted
   uint32_t sp[8];              // split_block results: cachedLength and list metadata of both halves
@@ -527,6 +537,18 @@ struct Eng {
   __device__ __forceinline__ uint32_t list_alloc(uint32_t want, uint32_t& cap) {
     cap = list_class_cap(want);
     const int c = list_class(cap);
+#ifndef MTB_NO_LSTK
+    if (c < MTB_LSTK) {
+      const uint32_t n = U(sh->lstkn[c]);
+      if (n) {
+        const uint32_t h = U(sh->lstk[c][n - 1]);
+        wsync();
+        if (lane == 0) sh->lstkn[c] = n - 1;
+        wsync();
+        return h;
+      }
+    }
+#endif
     if (c < MTB_LCLASSES) {
       const uint32_t head = U(sh->lfree[c]);
       if (head != MTB_NONE) {
@@ -550,6 +572,20 @@ struct Eng {
     if (cap < 8 || (cap & (cap - 1))) return;
     const int c = list_class(cap);
     if (c >= MTB_LCLASSES) return;
+#ifndef MTB_NO_LSTK
+    if (c < MTB_LSTK) {
+      const uint32_t n = U(sh->lstkn[c]);
+      if (n < MTB_LSTK_N) {
+        wsync();
+        if (lane == 0) {
+          sh->lstk[c][n] = off;
+          sh->lstkn[c] = n + 1;
+        }
+        wsync();
+        return;
+      }
+    }
+#endif
     if (lane == 0) {
       reinterpret_cast<uint32_t*>(&lst[off])[0] = U(sh->lfree[c]);
       sh->lfree[c] = off;
@@ -3609,6 +3645,9 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   } else if (e.lane < MTB_LCLASSES) {
     sh.lfree[e.lane] = reinterpret_cast<const uint32_t*>(e.lst)[e.lane];
   }
+#ifndef MTB_NO_LSTK
+  if (e.lane < MTB_LSTK) sh.lstkn[e.lane] = 0;
+#endif
   if (e.lane == 0) sh.path[0] = e.root;
   e.heap_lds = e.heap_cnt + 1 < e.lheap_n;
   if (e.heap_lds)
@@ -3670,6 +3709,20 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
       gheap[i].seg = v.x;
       gheap[i].maxSeq = (int)v.y;
     }
+#ifndef MTB_NO_LSTK
+  // the LDS stacks go back onto the free lists in HBM (lane c: class c)
+  if (e.lane < MTB_LSTK) {
+    uint32_t head = sh.lfree[e.lane];
+    const uint32_t n = sh.lstkn[e.lane];
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t off = sh.lstk[e.lane][i];
+      reinterpret_cast<uint32_t*>(&e.lst[off])[0] = head;
+      head = off;
+    }
+    sh.lfree[e.lane] = head;
+  }
+  __syncthreads();
+#endif
   if (e.lane < MTB_LCLASSES) reinterpret_cast<uint32_t*>(e.lst)[e.lane] = sh.lfree[e.lane];
   __syncthreads();
   if (e.lane == 0) {
