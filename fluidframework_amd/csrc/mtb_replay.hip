@@ -159,6 +159,9 @@ struct Rec {
 };
 
 template <int HEAPN>
+#ifndef MTB_SORT_MIN
+#define MTB_SORT_MIN 64  // rebuilt lists longer than this are counting-sorted (shorter ones are read whole)
+#endif
 #ifndef MTB_LSTK
 #define MTB_LSTK 8    // capacity classes with an LDS stack of free lists
 #endif
@@ -944,7 +947,7 @@ struct Eng {
     uint32_t outOff = no, outCap = cap | MTB_LUNSORTED;
     if (T <= 1) {
       outCap = cap;
-    } else if (T > 64 && T < 65536) {  // (a list of one chunk is read whole anyway: left unsorted)
+    } else if (T > MTB_SORT_MIN && T < 65536) {  // (a list of one chunk is read whole anyway: left unsorted)
       uint32_t* hist = &sh->hold[0][0];
       for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
       wsync();

@@ -60,7 +60,8 @@ typedef struct mtb_op {
   uint32_t msn;      /* minimumSequenceNumber */
   uint32_t pos1;
   uint32_t pos2;
-  uint32_t payload;  /* insert: offset (UTF-16 units) of the text in the payload passed with it */
+  uint32_t payload;  /* insert: offset (UTF-16 units) of the text in the payload passed with it;
+                        annotate: set by the host (assert 0x5ad's markerId test, mergeTree.ts:1912-1918) */
   uint32_t props;    /* insert/annotate: props id from mtb_intern_props (0 = none) */
 } mtb_op;
 
