@@ -2961,7 +2961,7 @@ int mtbx_apply_msg_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) 
 
 // A live client's own op (client.ts:196-247 insertSegmentLocal / removeRangeLocal): the IMergeTreeOp it
 // sends, applied at the document's next replay in its own view with UnassignedSequenceNumber
-// (DESIGN.md section 10).  Local rewrite annotates are not supported.
+// (DESIGN.md section 10).  Local rewrite annotates count as pending rewrites (pendingRewriteCount).
 int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
   return guarded(b, [&] {
     if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: local ops on a matrix batch");
@@ -2979,8 +2979,6 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     try {
       pack_delta(b, d, op, base, recs);
       for (const mtb_op& r : recs) {
-        if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE))
-          raise(MTB_E_UNSUPPORTED, "unsupported: local rewrite annotate (pendingRewriteCount)");
         if (r.type != MTB_OP_INSERT && r.type != MTB_OP_REMOVE && r.type != MTB_OP_ANNOTATE)
           raise(MTB_E_ARG, "local op without an effect");
         if (r.type == MTB_OP_INSERT && !(r.flags & MTB_F_MARKER) && r.pos2 == 0) raise(MTB_E_ARG, "empty local insert");
@@ -3058,6 +3056,10 @@ int mtbx_regenerate_pending_op(mtb_dev* b, uint32_t doc, const char* json, size_
         const Seg& sg = d.segs[sid];
         const hj::Value& reset = *members[g];
         std::string o = "{\"pos1\":" + std::to_string(pos);
+        if (ty == MTB_OP_ANNOTATE) {  // createAnnotateRangeOp(start, end, props, combiningOp) (opBuilder.ts:52-65)
+          const hj::Value* comb = member(reset, u"combiningOp");
+          if (comb && comb->kind != hj::Value::kUndef) o = "{\"combiningOp\":" + hj::dump(*comb) + ",\"pos1\":" + std::to_string(pos);
+        }
         if (ty == MTB_OP_INSERT) {  // createInsertSegmentOp(pos, segment): segment.toJSONObject()
           const hj::Value* rseg = member(reset, u"seg");
           const hj::Value* rprops = rseg && rseg->kind == hj::Value::kObj ? member(*rseg, u"props") : nullptr;

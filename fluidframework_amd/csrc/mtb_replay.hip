@@ -267,6 +267,7 @@ struct Eng {
   int local_seq;                // MODE_LIVE: collabWindow.localSeq
   uint32_t pend_dir, pend_head, pend_n, pend_cap;  // MODE_LIVE: pending segment-group FIFO (DocState)
   bool grp_open;                // MODE_LIVE: the current local op already has its group
+  bool pk_rw;                   // MODE_LIVE: pending_keys found a pending local rewrite on the segment
   int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
   uint64_t prof[NPH];
@@ -1541,9 +1542,29 @@ struct Eng {
     grp_push(pend_n - 1, sid);
   }
   // PropertiesManager.pendingKeyUpdateCount of segment `sid` (segmentPropertiesManager.ts:60-157): the keys
-  // of the pending ANNOTATE groups holding it, collected at sh->hold[2] (at most 64); returns their number
+  // of the pending ANNOTATE groups holding it, collected at sh->hold[2] (at most 64); returns their number.
+  // A group's props word carries MTB_GRP_REWRITE for a local rewrite: its null keys are not pending
+  // (:126-131), and pk_rw reports pendingRewriteCount > 0 (a remote annotate then leaves the segment alone).
+  __device__ __forceinline__ uint32_t pending_keys_of(uint32_t pw, uint32_t nk) {
+    const bool rw = (pw & MTB_GRP_REWRITE) != 0;
+    if (rw) pk_rw = true;
+    const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * (pw & ~MTB_GRP_REWRITE)]);
+    const uint32_t nop = U(op[0]);
+    for (uint32_t q0 = 0; q0 < nop; q0 += 64) {
+      const uint32_t q = q0 + (uint32_t)lane;
+      const bool take = q < nop && !(rw && op[2 + 2 * q] == MTB_NONE);
+      const unsigned long long m = __ballot(take);
+      const uint32_t at = nk + rank_below(m);
+      if (take && at < 64) sh->hold[2][at] = op[1 + 2 * q];
+      nk += (uint32_t)__popcll(m);
+      if (nk > 64) nk = 64;
+    }
+    wsync();
+    return nk;
+  }
   __device__ __forceinline__ uint32_t pending_keys(uint32_t sid) {
     uint32_t nk = 0;
+    pk_rw = false;
     for (uint32_t i = 0; i < pend_n && !err; i++) {
       const auto e = grp_ent(i);
       if (U(e[4]) != MTB_OP_ANNOTATE) continue;
@@ -1551,24 +1572,14 @@ struct Eng {
       bool found = false;
       for (uint32_t q = 0; q < cnt && !found; q += 64) found = __ballot(q + lane < cnt && aux[off + q + lane] == sid) != 0;
       if (!found) continue;
-      const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * U(e[5])]);
-      const uint32_t nop = U(op[0]);
-      for (uint32_t q = lane; q < nop; q += 64)
-        if (nk + q < 64) sh->hold[2][nk + q] = op[1 + 2 * q];
-      nk = nk + nop < 64 ? nk + nop : 64;
-      wsync();
+      nk = pending_keys_of(U(e[5]), nk);
     }
     const uint32_t orp = U(ds->orphans);
     if (COLD(orp != 0)) {  // keys a reconnect left pending without a group
       const uint32_t n = U(aux[orp]);
       for (uint32_t i = 0; i < n && !err; i++) {
         if (U(aux[orp + 3 + 2 * i]) != sid) continue;
-        const auto op = UP(sh->tab.pool) + U(UP(sh->tab.pidx)[2 * U(aux[orp + 2 + 2 * i])]);
-        const uint32_t nop = U(op[0]);
-        for (uint32_t q = lane; q < nop; q += 64)
-          if (nk + q < 64) sh->hold[2][nk + q] = op[1 + 2 * q];
-        nk = nk + nop < 64 ? nk + nop : 64;
-        wsync();
+        nk = pending_keys_of(U(aux[orp + 2 + 2 * i]), nk);
       }
     }
     return nk;
@@ -2356,7 +2367,7 @@ struct Eng {
         while (gm && !err) {
           const int t = first_set(gm);
           gm &= gm - 1;
-          grp_add(rlu(id, t) & ~MTB_LEAF, MTB_OP_ANNOTATE, opId);
+          grp_add(rlu(id, t) & ~MTB_LEAF, MTB_OP_ANNOTATE, opId | (rewrite ? MTB_GRP_REWRITE : 0u));
         }
       } else if (isLive && COLD((U(ds->pend_ann) | U(ds->orphans)) != 0)) {
         // a remote annotate leaves the keys of pending local annotates alone (shouldModifyKey,
@@ -2366,6 +2377,13 @@ struct Eng {
           const int t = first_set(xm);
           xm &= xm - 1;
           const uint32_t nk = pending_keys(rlu(id, t) & ~MTB_LEAF);
+#ifndef MTB_NO_RWBLOCK  // (test builds: shows the rewrite farms depend on it)
+          if (pk_rw) {  // pendingRewriteCount > 0: the remote annotate leaves the segment alone (:75-82)
+            am &= ~(1ull << t);
+            handled |= 1ull << t;
+            continue;
+          }
+#endif
           if (!nk) continue;
           const uint32_t np = props_apply_slow(rlu(props, t), opId, rewrite, nk);
           if (bad()) return 0;
@@ -3402,7 +3420,7 @@ struct Eng {
     }
     if (o.type == MTB_OP_INSERT) {
       if ((int)o.pos1 < 0 || (int)o.pos1 > len) { fail(DERR_RANGE); return; }
-    } else if (o.type == MTB_OP_REMOVE || (o.type == MTB_OP_ANNOTATE && !(o.flags & MTB_F_REWRITE))) {
+    } else if (o.type == MTB_OP_REMOVE || o.type == MTB_OP_ANNOTATE) {
       // getValidOpRange (client.ts:550-585): start in [0, length), end > start (end past the length is
       // not checked; nodeMap stops at the tree's end)
       if ((int)o.pos1 < 0 || (int)o.pos1 >= len || (int)o.pos2 <= (int)o.pos1) { fail(DERR_RANGE); return; }
@@ -3636,6 +3654,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.pend_n = ds->pend_n;
   e.pend_cap = ds->pend_cap;
   e.grp_open = false;
+  e.pk_rw = false;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
   for (int i = 0; i < NPH; i++) e.prof[i] = 0;

@@ -336,7 +336,10 @@ Seg* MergeTree::splitAt(Seg* s, int pos) {
     g->segments.push_back(r);
     r->groups.push_back(g);
   }
-  if (s->hasPropManager && s->props) r->pendingKeys = s->pendingKeys;  // PropertiesManager.copyTo
+  if (s->hasPropManager && s->props) {  // PropertiesManager.copyTo
+    r->pendingKeys = s->pendingKeys;
+    r->pendingRewrite = s->pendingRewrite;
+  }
   counters.segsTouched += 2;  // split: left half modified + right half created
   return r;
 }
@@ -643,7 +646,7 @@ SegGroup* MergeTree::addToPendingList(Seg* s, SegGroup* g, int localSeq) {
 }
 
 // ackPendingSegment (mergeTree.ts:1283-1322) with BaseSegment.ack (mergeTreeNodes.ts:439-480)
-void MergeTree::ackPendingSegment(int opType, const JObj* props, int seq) {
+void MergeTree::ackPendingSegment(int opType, const JObj* props, int seq, bool rewrite) {
   SegGroup* g = nullptr;
   if (!pendingSegments.empty()) {
     g = pendingSegments.front();
@@ -659,8 +662,10 @@ void MergeTree::ackPendingSegment(int opType, const JObj* props, int seq) {
       switch (opType) {
         case 2:  // PropertiesManager.ackPendingProperties (segmentPropertiesManager.ts:31-58)
           if (!s->hasPropManager) fail_assert("0x044", "On annotate ack, missing segment property manager!");
+          if (rewrite) s->pendingRewrite--;  // decrementPendingCounts (segmentPropertiesManager.ts:36-58)
           if (props)
             for (auto& kv : *props) {
+              if (rewrite && kv.second.t == JVal::Null) continue;
               auto it = s->pendingKeys.find(kv.first);
               if (it == s->pendingKeys.end()) continue;
               if (it->second <= 0) fail_assert("0x05c", "Trying to update more annotate props than do exist!");
@@ -943,16 +948,18 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
 
 // PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) combined with
 // BaseSegment.addProperties: a local op (seq Unassigned) while collaborating counts its keys as pending;
-// a sequenced remote op leaves the keys with pending local updates alone (shouldModifyKey).  Local
-// rewrites (pendingRewriteCount) are not restated.
+// a sequenced remote op leaves the keys with pending local updates alone (shouldModifyKey), and leaves a
+// segment with a pending local rewrite (pendingRewriteCount > 0) alone altogether (:75-82).
 static void applyProps(Seg* s, const JObj& newProps, bool rewrite, int seq = UniversalSeq, bool collaborating = false) {
   s->hasPropManager = true;
   if (!s->props) s->props = JObj();
+  if (collaborating && s->pendingRewrite > 0 && seq != UnassignedSeq && seq != UniversalSeq) return;
   JObj& old = *s->props;
   auto shouldModify = [&](const u16str& k) {
     return seq == UnassignedSeq || seq == UniversalSeq || s->pendingKeys.find(k) == s->pendingKeys.end();
   };
   if (rewrite) {
+    if (collaborating && seq == UnassignedSeq) s->pendingRewrite++;
     std::vector<u16str> keys;
     for (auto& kv : old) keys.push_back(kv.first);
     for (auto& k : keys) {
@@ -962,8 +969,12 @@ static void applyProps(Seg* s, const JObj& newProps, bool rewrite, int seq = Uni
   }
   for (auto& kv : newProps) {
     if (collaborating) {
-      if (seq == UnassignedSeq) s->pendingKeys[kv.first]++;
-      else if (!shouldModify(kv.first)) continue;
+      if (seq == UnassignedSeq) {
+        if (rewrite && kv.second.t == JVal::Null) continue;  // (a rewrite's null keys are not counted)
+        s->pendingKeys[kv.first]++;
+      } else if (!shouldModify(kv.first)) {
+        continue;
+      }
     }
     if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
@@ -977,7 +988,6 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
   std::vector<Seg*> annotated;
   const int localSeq = seq == UnassignedSeq ? ++window.localSeq : INT32_MIN;  // mergeTree.ts:1909-1910
   SegGroup* group = nullptr;
-  if (seq == UnassignedSeq && rewrite) fail_unsupported("local rewrite annotate");
   // assert 0x5ad (mergeTree.ts:1912-1918): an annotate naming markerId must carry the marker's own id
   // (JS ===: primitives by value; an object or array value is a fresh object, never equal)
   const JVal* opId = obj_get(props, u"markerId");
@@ -1451,7 +1461,10 @@ void Doc::applyMsgCore(const JVal& msg) {
       auto ackOne = [&](const JVal& op) {
         const JVal* t = obj_get(op.obj, u"type");
         const JVal* pr = obj_get(op.obj, u"props");
-        mt.ackPendingSegment(t && t->t == JVal::Num ? (int)t->num : -1, pr && pr->t == JVal::Obj ? &pr->obj : nullptr, seq);
+        const JVal* comb = obj_get(op.obj, u"combiningOp");
+        const JVal* cname = comb && comb->t == JVal::Obj ? obj_get(comb->obj, u"name") : nullptr;
+        const bool rw = cname && cname->t == JVal::Str && cname->str == u"rewrite";
+        mt.ackPendingSegment(t && t->t == JVal::Num ? (int)t->num : -1, pr && pr->t == JVal::Obj ? &pr->obj : nullptr, seq, rw);
       };
       const JVal* t = obj_get(contents->obj, u"type");
       if (t && t->t == JVal::Num && (int)t->num == 3) {
@@ -1556,15 +1569,21 @@ std::string Doc::removeLocalOp(int start, int end) {
   mt.markRangeRemoved(start, end, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"type\":1}";
 }
-std::string Doc::annotateLocalOp(int start, int end, const JObj& props) {
+std::string Doc::annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp) {
   if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
+  bool rewrite = false;
+  if (combiningOp) {  // annotateRangeLocal(start, end, props, combiningOp): only "rewrite" is restated
+    const JVal* name = combiningOp->t == JVal::Obj ? obj_get(combiningOp->obj, u"name") : nullptr;
+    if (!(name && name->t == JVal::Str && name->str == u"rewrite")) fail_unsupported("combiningOp other than rewrite");
+    rewrite = true;
+  }
   validLocalRange(start, end, mt.length(), false);
-  mt.annotateRange(start, end, props, false, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
+  mt.annotateRange(start, end, props, rewrite, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   JVal pv;
   pv.t = JVal::Obj;
   pv.obj = props;
-  return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"props\":" + json_stringify(pv) +
-         ",\"type\":2}";
+  return std::string(combiningOp ? "{\"combiningOp\":" + json_stringify(*combiningOp) + "," : "{") + "\"pos1\":" +
+         std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"props\":" + json_stringify(pv) + ",\"type\":2}";
 }
 
 std::string Doc::localOpJson(const JVal& op) {
@@ -1590,9 +1609,9 @@ std::string Doc::localOpJson(const JVal& op) {
     out = removeLocalOp(pos(u"pos1", u"relativePos1", false), pos(u"pos2", u"relativePos2", false));
   } else if (type == 2) {
     const JVal* pr = obj_get(op.obj, u"props");
-    if (obj_get(op.obj, u"combiningOp")) fail_unsupported("local annotate with a combiningOp");
+    const JVal* comb = obj_get(op.obj, u"combiningOp");
     out = annotateLocalOp(pos(u"pos1", u"relativePos1", false), pos(u"pos2", u"relativePos2", false),
-                          pr && pr->t == JVal::Obj ? pr->obj : JObj());
+                          pr && pr->t == JVal::Obj ? pr->obj : JObj(), comb && comb->t != JVal::Undef ? comb : nullptr);
   } else {
     throw OracleError(-8, "unsupported local op type");
   }
@@ -1748,7 +1767,10 @@ std::string Doc::regeneratePendingOp(const JVal& op) {
       bool have = false;
       if (t == 2) {
         if (!s->removed || (s->localRemovedSeq != INT32_MIN && s->removedSeq == UnassignedSeq)) {
+          // createAnnotateRangeOp(start, end, props, combiningOp) (opBuilder.ts:52-65)
+          const JVal* comb = obj_get(resetOp->obj, u"combiningOp");
           newOp = jop({{u"pos1", JVal::number(pos)}, {u"pos2", JVal::number(pos + s->cachedLength)}});
+          if (comb && comb->t != JVal::Undef) newOp.obj.insert(newOp.obj.begin(), {u"combiningOp", *comb});
           const JVal* pr = obj_get(resetOp->obj, u"props");
           if (pr) newOp.obj.push_back({u"props", *pr});
           newOp.obj.push_back({u"type", JVal::number(2)});

@@ -64,6 +64,7 @@ struct Seg : Node {
   int localRemovedSeq = INT32_MIN;
   std::vector<struct SegGroup*> groups;  // a queue (front = oldest); a vector allocates nothing when empty
   std::map<u16str, int> pendingKeys;
+  int pendingRewrite = 0;          // PropertiesManager.pendingRewriteCount (segmentPropertiesManager.ts:26)
   Seg() : Node(true) {}
 };
 
@@ -186,7 +187,7 @@ class MergeTree {
   // (type INSERT 0 / REMOVE 1 / ANNOTATE 2, its props for ANNOTATE)
   std::deque<std::unique_ptr<SegGroup>> groupPool;
   std::deque<SegGroup*> pendingSegments;
-  void ackPendingSegment(int opType, const JObj* props, int seq);
+  void ackPendingSegment(int opType, const JObj* props, int seq, bool rewrite = false);
   void zamboniSegments();
   // mergeTreeDeltaCallback (INSERT 0 / REMOVE 1 / ANNOTATE 2 with the annotate's props), fired after the
   // op is applied and before its zamboni, only for non-empty delta segment lists
@@ -283,7 +284,7 @@ class Doc {
   // and returned as the IMergeTreeOp JSON to submit; acked by applyMsg of the sequenced message
   std::string insertLocalOp(int pos, const JVal& segSpec);
   std::string removeLocalOp(int start, int end);
-  std::string annotateLocalOp(int start, int end, const JObj& props);
+  std::string annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp = nullptr);
   // a live client's local op given as the IMergeTreeOp JSON it sends (pos1 / pos2 or marker-relative
   // relativePos1 / relativePos2, resolved in the local view by getValidOpRange, client.ts:527-547); returns
   // the op to send (the input itself when it names relative positions, as Client.annotateMarker does)

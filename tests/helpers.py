@@ -187,7 +187,7 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
 
 
 def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
-                   record=None, reconnect=0.0):
+                   record=None, reconnect=0.0, rewrite=0.0):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
@@ -195,7 +195,9 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     everything.  With `reconnect` > 0 a client disconnects (probability per round) in the style of
     client.reconnectFarm.spec.ts: its ops still in the sequencer's queue are dropped, it catches up on the
     sequenced stream, then regenerates each dropped op (Client.regeneratePendingOp, client.ts:917-960) and
-    resubmits the result at its current seq.  Returns (clients, observer, sequenced messages)."""
+    resubmits the result at its current seq.  With `rewrite` > 0 that fraction of the local annotates are
+    `rewrite` annotates (combiningOp {"name": "rewrite"}: pendingRewriteCount, segmentPropertiesManager.ts).
+    Returns (clients, observer, sequenced messages)."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -223,7 +225,10 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
         b = min(n, a + rng.randint(1, 6))
         if not annotate or r < 0.8:
             return c.remove_local_op(a, b)
-        return c.annotate_local_op(a, b, {"k": rng.choice([1, 2, None]), "w": rng.randint(0, 1)})
+        props = {"k": rng.choice([1, 2, None]), "w": rng.randint(0, 1)}
+        if rewrite and rng.random() < rewrite:
+            return c.local_op_json({"combiningOp": {"name": "rewrite"}, "pos1": a, "pos2": b, "props": props, "type": 2})
+        return c.annotate_local_op(a, b, props)
 
     def sequence(m):
         cid, ref, op = queue.pop(0)

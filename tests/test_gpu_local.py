@@ -15,10 +15,10 @@ from helpers import run_local_farm
 pytestmark = pytest.mark.gpu
 
 
-def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False, reconnect=0.0):
+def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annotate=False, reconnect=0.0, rewrite=0.0):
     rec = {}
     run_local_farm(seed, n_clients=n_clients, n_rounds=n_rounds, new_mode=new_mode, annotate=annotate, record=rec,
-                   reconnect=reconnect)
+                   reconnect=reconnect, rewrite=rewrite)
     return _replay_record(rec, seed, new_mode, rounds_per_replay, "hello world")
 
 
@@ -88,6 +88,20 @@ def test_local_annotate_farm_new_length_calc(seed):
 def test_local_annotate_farm_batched_rounds(seed):
     assert _replay_farm(seed, n_clients=8, n_rounds=120, new_mode=seed % 2 == 0, rounds_per_replay=10,
                         annotate=True) > 0
+
+
+REWRITE_SEEDS = list(range(131, 147))
+
+
+@pytest.mark.parametrize("seed", REWRITE_SEEDS)
+def test_local_rewrite_farm(seed):
+    """Local rewrite annotates (combiningOp "rewrite", segmentPropertiesManager.ts:60-157): pendingRewriteCount
+    makes a remote annotate leave the segment alone until the ack, a rewrite's null keys are not pending, the
+    count follows split-off halves (copyTo) and survives a reconnect (orphaned groups) -- half of the local
+    annotates are rewrites, some farms reconnect; states equal the oracle clients' after every round and
+    regenerated ops (combiningOp first, as createAnnotateRangeOp writes it) equal op for op."""
+    assert _replay_farm(seed, n_clients=3 + seed % 4, n_rounds=40, new_mode=seed % 2 == 0, annotate=True,
+                        reconnect=0.3 if seed % 3 == 0 else 0.0, rewrite=0.5) > 0
 
 
 @pytest.mark.parametrize("seed", list(range(71, 87)))
