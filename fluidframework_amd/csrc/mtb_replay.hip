@@ -177,6 +177,8 @@ struct ScratchT {  // LDS, one per wave
   int32_t acc[MTB_VDEPTH];     // node_map accumulated observer-length delta
   uint32_t rmeta[4];           // root window-list metadata (loff, lcnt, lcap)
   uint32_t lfree[MTB_LCLASSES];  // free window lists per capacity class (8 << c entries)
+  uint32_t capv[8];              // the document's slice capacities (DocState seg, blk, list, text, heap, aux
+                                 // caps, delta_cap): an allocation's bound check reads LDS, not HBM
 #ifndef MTB_NO_LSTK
   uint32_t lstk[MTB_LSTK][MTB_LSTK_N];  // the last lists freed in the small classes, held in LDS: a pop
   uint32_t lstkn[MTB_LSTK];             // from here needs no dependent read of the next pointer in HBM
@@ -279,7 +281,7 @@ struct Eng {
   }
   __device__ __forceinline__ bool bad() const { return COLD(err != 0); }
   __device__ __forceinline__ uint32_t alloc_seg() {
-    if (seg_used >= ds->seg_cap) { fail(DERR_CAP_SEG); return 0; }
+    if (seg_used >= U(sh->capv[0])) { fail(DERR_CAP_SEG); return 0; }
     return seg_used++;
   }
   __device__ __forceinline__ uint32_t* bw(uint32_t b) const { return reinterpret_cast<uint32_t*>(&blk[b]); }
@@ -290,7 +292,7 @@ struct Eng {
       free_top--;
       b = U(UP(sh->gfree)[free_top]);
     } else {
-      if (blk_used >= ds->blk_cap) { fail(DERR_CAP_BLK); return 0; }
+      if (blk_used >= U(sh->capv[1])) { fail(DERR_CAP_BLK); return 0; }
       b = blk_used++;
     }
     uint32_t* w = bw(b);
@@ -310,7 +312,7 @@ struct Eng {
     free_top++;
   }
   __device__ __forceinline__ uint32_t alloc_aux(uint32_t n) {
-    if (aux_used + n > ds->aux_cap) { fail(DERR_CAP_AUX); return 1; }
+    if (aux_used + n > U(sh->capv[5])) { fail(DERR_CAP_AUX); return 1; }
     uint32_t o = aux_used;
     aux_used += n;
     return o;
@@ -563,7 +565,7 @@ struct Eng {
         return head;
       }
     }
-    if (list_used + cap > ds->list_cap) {
+    if (list_used + cap > U(sh->capv[2])) {
       fail(DERR_CAP_LIST);
       return 0;
     }
@@ -1450,7 +1452,7 @@ struct Eng {
     wsync();
   }
   __device__ __forceinline__ void heap_add(uint32_t s, int maxSeq) {
-    if (heap_cnt + 1 >= ds->heap_cap) { fail(DERR_CAP_HEAP); return; }
+    if (heap_cnt + 1 >= U(sh->capv[4])) { fail(DERR_CAP_HEAP); return; }
     if (COLD(heap_lds && heap_cnt + 1 >= lheap_n)) heap_spill();
     uint32_t k = ++heap_cnt;
     Lru x;
@@ -1923,7 +1925,7 @@ struct Eng {
   // unacked insert and a remotely removed segment are normalized
   __device__ __forceinline__ void normalize() {
     const uint32_t save = aux_used;
-    const uint32_t room = ds->aux_cap > aux_used ? ds->aux_cap - aux_used : 0;
+    const uint32_t room = U(sh->capv[5]) > aux_used ? U(sh->capv[5]) - aux_used : 0;
     const uint32_t cap = room / 16 < 4096 ? room / 16 : 4096;  // run entries the scratch holds
     if (cap < 2) return;
     const uint32_t sc = alloc_aux(16 * cap);
@@ -2032,7 +2034,7 @@ struct Eng {
             emit = rsk < 0 || rsk >= MTB_PEND;
           }
           if (emit) {
-            if (delta_used + 1 > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+            if (delta_used + 1 > U(sh->capv[6])) { fail(DERR_CAP_DELTA); return; }
             if (lane == 0) {
               const auto o = dslice() + 4 * delta_used;
               o[0] = cur_k;
@@ -2201,7 +2203,7 @@ struct Eng {
     const unsigned long long m = __ballot(sel);
     if (!m) return;
     const uint32_t n = (uint32_t)__popcll(m);
-    if (delta_used + n > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+    if (delta_used + n > U(sh->capv[6])) { fail(DERR_CAP_DELTA); return; }
     if (sel) {
       const auto e = dslice() + 4 * (delta_used + rank_below(m));
       e[0] = cur_k;
@@ -2774,7 +2776,7 @@ struct Eng {
       if (!contiguous) {
         const bool atEnd = ttext + (uint32_t)tlen == text_used;
         const uint32_t need = atEnd ? (uint32_t)(total - tlen) : (uint32_t)total;
-        if (text_used + need > ds->text_cap) { fail(DERR_CAP_TEXT); return nh; }
+        if (text_used + need > U(sh->capv[3])) { fail(DERR_CAP_TEXT); return nh; }
         uint32_t w = text_used;
         if (!atEnd) {
           copy_text(w, ttext, (uint32_t)tlen);
@@ -2990,7 +2992,7 @@ struct Eng {
     const uint32_t L = U(ht[0]);
     const uint32_t fr = U(ht[1]);
     const uint32_t next = fr < L ? U(ht[1 + fr]) : fr + 1;  // handles[free] ?? free + 1
-    if (fr >= L && 2u * (L + 2u) > ds->text_cap) {
+    if (fr >= L && 2u * (L + 2u) > U(sh->capv[3])) {
       fail(DERR_CAP_TEXT);
       return 0;
     }
@@ -3093,7 +3095,7 @@ struct Eng {
   // handle or first recycled handle, count].  The host replays them, with the setCell values, into the
   // matrix's SparseArray2D (matrix.ts:668-690 sets, :721-733 clears of recycled handles).
   __device__ __forceinline__ void cell_event(uint32_t kind, uint32_t a, uint32_t n) {
-    if (delta_used + 1 > ds->delta_cap) { fail(DERR_CAP_DELTA); return; }
+    if (delta_used + 1 > U(sh->capv[6])) { fail(DERR_CAP_DELTA); return; }
     if (lane == 0) {
       const auto e = dslice() + 4 * delta_used;
       e[0] = cur_k;
@@ -3655,6 +3657,8 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.pend_cap = ds->pend_cap;
   e.grp_open = false;
   e.pk_rw = false;
+  if (e.lane < 6) sh.capv[e.lane] = (&ds->seg_cap)[e.lane];
+  if (e.lane == 6) sh.capv[6] = ds->delta_cap;
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
   for (int i = 0; i < NPH; i++) e.prof[i] = 0;
