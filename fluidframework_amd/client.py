@@ -394,17 +394,16 @@ class Client:
     def annotateMarker(self, markerId, props, combiningOp=None):
         """Client.annotateMarker (client.ts:190-197, createAnnotateMarkerOp opBuilder.ts:25-43) for the marker
         carrying `markerId`: a local annotate with marker-relative positions; returns the op to send."""
-        if combiningOp is not None:
-            raise MergeTreeError(-6, "unsupported: local annotate with a combiningOp")
-        return self.applyLocalOp({"props": props, "relativePos1": {"id": markerId, "before": True},
-                                  "relativePos2": {"id": markerId}, "type": 2})
+        op = {"props": props, "relativePos1": {"id": markerId, "before": True}, "relativePos2": {"id": markerId},
+              "type": 2}
+        return self.applyLocalOp(op if combiningOp is None else {"combiningOp": combiningOp, **op})
 
     def annotateRangeLocal(self, start, end, props, combiningOp=None):
         """annotateRangeLocal (client.ts:206): the keys stay pending on the annotated segments until the
-        op's ack; returns the IMergeTreeAnnotateMsg to send."""
-        if combiningOp is not None:
-            raise MergeTreeError(-6, "unsupported: local annotate with a combiningOp")
-        return self.applyLocalOp({"pos1": start, "pos2": end, "props": props, "type": 2})
+        op's ack (a "rewrite" combiningOp: pendingRewriteCount; other combiningOps are rejected by the
+        engine); returns the IMergeTreeAnnotateMsg to send."""
+        op = {"pos1": start, "pos2": end, "props": props, "type": 2}
+        return self.applyLocalOp(op if combiningOp is None else {"combiningOp": combiningOp, **op})
 
     def getText(self, start=None, end=None):
         """TestClient.getText (testClient.ts:185): the local view's text, or of [start, end) in positions that

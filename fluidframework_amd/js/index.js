@@ -221,14 +221,16 @@ class Client {
 
   /** Client.annotateMarker (client.ts:190) for the marker carrying `markerId`: returns the op to send. */
   annotateMarker(markerId, props, combiningOp) {
-    if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");
-    return this.applyLocalOp({ props, relativePos1: { id: markerId, before: true }, relativePos2: { id: markerId }, type: 2 });
+    // createAnnotateMarkerOp (opBuilder.ts:25-43); a combiningOp other than "rewrite" is rejected by the engine
+    const op = { props, relativePos1: { id: markerId, before: true }, relativePos2: { id: markerId }, type: 2 };
+    return this.applyLocalOp(combiningOp === undefined ? op : { combiningOp, ...op });
   }
 
   /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
   annotateRangeLocal(start, end, props, combiningOp) {
-    if (combiningOp !== undefined) throw unsupported("local annotate with a combiningOp");
-    return this.applyLocalOp({ pos1: start, pos2: end, props, type: 2 });
+    // createAnnotateRangeOp (opBuilder.ts:52-65): a local "rewrite" is pending (pendingRewriteCount) until its ack
+    const op = { pos1: start, pos2: end, props, type: 2 };
+    return this.applyLocalOp(combiningOp === undefined ? op : { combiningOp, ...op });
   }
 
   /** Client.startOrUpdateCollaboration (client.ts:1133). */
