@@ -25,7 +25,7 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
            "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
            "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op",
-           "mtb_get_launch_info"]
+           "mtb_get_launch_info", "mtb_detached_op_json", "mtb_maintenance"]
 
 
 class MtbLaunchInfo(ctypes.Structure):
@@ -94,6 +94,8 @@ def lib():
     L.mtb_matrix_get_cell.argtypes = [vp, u32, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.mtb_apply_msg_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
     L.mtb_local_op_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    L.mtb_detached_op_json.argtypes = [vp, u32, ctypes.c_char_p, sz]
+    L.mtb_maintenance.argtypes = [vp, u32, u32]
     L.mtb_regenerate_pending_op.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(sz)]
     L.mtb_append_ops.argtypes = [vp, u32, vp, u32, vp, sz]

@@ -323,30 +323,53 @@ class Client:
     def __init__(self, batch, doc):
         self._b = batch
         self._doc = doc
-        self._initial = []
+        self._detached = []  # edits made before collaboration (IMergeTreeOps)
         self.longClientId = None
 
-    # local edits: detached before collaboration (client.replay.spec.ts:27), afterwards a live client's
-    # pending ops (client.ts:196, see insertSegmentLocal)
+    # local edits: detached before collaboration (client.replay.spec.ts:27, createClientsAtInitialState
+    # testClientLogger.ts:51-78), afterwards a live client's pending ops (client.ts:196, see insertSegmentLocal)
     def insertTextLocal(self, pos, text, props=None):
+        seg = text if props is None else {"text": text, "props": props}
         if self.longClientId is not None:
-            return self.insertSegmentLocal(pos, text if props is None else {"text": text, "props": props})
-        if props is not None:
-            raise MergeTreeError(-6, "unsupported: detached text with properties")
-        cur = "".join(self._initial)
-        self._initial = [cur[:pos] + text + cur[pos:]]
+            return self.insertSegmentLocal(pos, seg)
+        return self._detach({"pos1": pos, "seg": seg, "type": 0})
+
+    def _detach(self, op):
+        if self.longClientId is not None:
+            return None
+        self._detached.append(op)
+        return op
 
     def startOrUpdateCollaboration(self, longClientId, minSeq=0, currentSeq=0):
         if self.longClientId is not None:
             raise MergeTreeError(-6, "unsupported: re-keying the observer id")
-        self._b.init_doc(self._doc, "".join(self._initial), longClientId, minSeq, currentSeq)
+        ops = self._detached
+        # one detached text insert into the empty document is the document's initial segment; any other
+        # detached edits are replayed as such (seq 0, LocalClientId) before the first message
+        first = ops[0] if ops and ops[0]["type"] == 0 and ops[0]["pos1"] == 0 and isinstance(ops[0]["seg"], str) else None
+        self._b.init_doc(self._doc, first["seg"] if first else "", longClientId, minSeq, currentSeq)
+        for op in ops[1:] if first else ops:
+            s = json.dumps(op).encode()
+            self._b._chk(self._b._L.mtb_detached_op_json(self._b._h, self._doc, s, len(s)))
+        self._detached = []
         self.longClientId = longClientId
+
+    def zamboniSegments(self):
+        """zamboniSegments(mergeTree) (zamboni.ts:19-60) as the reference's unit tests call it; applied at the
+        next replay."""
+        self._b._chk(self._b._L.mtb_maintenance(self._b._h, self._doc, 0))
+        self._b._dirty = True
+
+    def packParentRoot(self):
+        """packParent(mergeTree.root, mergeTree) (zamboni.ts:63-120) as mergeTree.zamboni.spec.ts calls it."""
+        self._b._chk(self._b._L.mtb_maintenance(self._b._h, self._doc, 1))
+        self._b._dirty = True
 
     def load(self, storage, clientId=None):
         """Client.load (client.ts:1007) from a SnapshotV1 summary.  `storage` maps blob path -> content (a
         dict, or [(path, content), ...]); `clientId` is the runtime's client id (the reference falls back
         to "snapshot", snapshotLoader.ts:154).  The body is appended by the next replay."""
-        if self.longClientId is not None or self._initial:
+        if self.longClientId is not None or self._detached:
             raise MergeTreeError(-1, "document already initialised")
         blobs = list(storage.items()) if isinstance(storage, dict) else list(storage)
         longId = clientId if clientId is not None else "snapshot"
@@ -373,8 +396,10 @@ class Client:
         return self.applyLocalOp({"pos1": pos, "seg": seg, "type": 0})
 
     def removeRangeLocal(self, start, end):
-        """removeRangeLocal (client.ts:230): returns the IMergeTreeRemoveMsg to send."""
-        return self.applyLocalOp({"pos1": start, "pos2": end, "type": 1})
+        """removeRangeLocal (client.ts:230): returns the IMergeTreeRemoveMsg to send (before collaboration a
+        detached remove: the segments stay as tombstones with removedSeq UniversalSequenceNumber)."""
+        op = {"pos1": start, "pos2": end, "type": 1}
+        return self._detach(op) if self.longClientId is None else self.applyLocalOp(op)
 
     def regeneratePendingOp(self, resetOp, segmentGroup=None):
         """Client.regeneratePendingOp (client.ts:917-960) after a reconnect: `resetOp` is the oldest pending op
@@ -403,7 +428,8 @@ class Client:
         op's ack (a "rewrite" combiningOp: pendingRewriteCount; other combiningOps are rejected by the
         engine); returns the IMergeTreeAnnotateMsg to send."""
         op = {"pos1": start, "pos2": end, "props": props, "type": 2}
-        return self.applyLocalOp(op if combiningOp is None else {"combiningOp": combiningOp, **op})
+        op = op if combiningOp is None else {"combiningOp": combiningOp, **op}
+        return self._detach(op) if self.longClientId is None else self.applyLocalOp(op)
 
     def getText(self, start=None, end=None):
         """TestClient.getText (testClient.ts:185): the local view's text, or of [start, end) in positions that
@@ -453,6 +479,8 @@ class Client:
         seg = {"marker": {"refType": behaviors}}
         if props:
             seg["props"] = props
+        if self.longClientId is None:
+            return self._detach({"pos1": pos, "seg": seg, "type": 0})
         return self.insertSegmentLocal(pos, seg)
 
     def getContainingSegment(self, pos, sequenceArgs=None):

@@ -20,6 +20,8 @@ int mtbx_docs_load_v1(mtb_dev* b, uint32_t n, const uint32_t* docs, const mtb_bl
                      const uint32_t* nblobs, const char* const* observer_long_ids, uint32_t threads);
 int mtbx_apply_msg_json(mtb_dev* b, uint32_t doc, const char* json_utf8, size_t len);
 int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json_utf8, size_t len);
+int mtbx_detached_op_json(mtb_dev* b, uint32_t doc, const char* json_utf8, size_t len);
+int mtbx_maintenance(mtb_dev* b, uint32_t doc, uint32_t kind);
 int mtbx_regenerate_pending_op(mtb_dev* b, uint32_t doc, const char* json, size_t len, char** out, size_t* out_len);
 int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n,
                    const uint16_t* payload, size_t payload_len);

@@ -50,6 +50,11 @@
 // normalizeSegmentsOnRebase when currentSeq moved, then per member group the regenerated ops' entries
 // [record, op type | group index << 8, segment, position] in the document's delta slice.
 #define MTB_OP_REGEN 7
+// The merge tree's maintenance calls made directly by the reference's unit tests (mtb_maintenance, MODE_LIVE):
+// pos1 = 0 zamboniSegments(mergeTree) (zamboni.ts:19-60), 1 packParent(root, mergeTree) (zamboni.ts:63-120).
+#define MTB_OP_MAINT 8
+// LocalClientId (-1): the client of a detached client's segments and removals (mtb_detached_op_json)
+#define MTB_LOCAL_CLIENT 0xFFFFu
 // A pending (unacked) local insert / remove stores MTB_PEND + localSeq in the segment's F_SEQ / F_RSEQ:
 // larger than every sequence number, so every remote perspective sees it as "not yet" and breakTie orders
 // it after sequenced segments (UnassignedSequenceNumber -> Number.MAX_SAFE_INTEGER - 1, mergeTree.ts:1719).

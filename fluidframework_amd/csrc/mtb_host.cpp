@@ -334,6 +334,7 @@ struct HostDoc {
   int64_t lastSeq = 0;            // last appended message seq (host-side 0x038 check)
   uint64_t totalOps = 0;          // all records ever appended (capacity sizing)
   uint64_t totalLocal = 0;        // local-op records, and groups a REGEN may re-queue (aux sizing)
+  uint64_t totalDetached = 0;     // records of detached edits (mtb_detached_op_json), all before the first message
   uint64_t totalPayload = 0;
   // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
   bool loaded = false;
@@ -352,12 +353,11 @@ struct HostDoc {
   LoadImage img;
   // idToSegment keys (mergeTree.ts:549): marker id -> per-document ordinal (first-seen order).  An id met on
   // a second marker is reused: blockUpdate's re-mapping (:296-306) decides which marker it names, which the
-  // marker kernel reproduces (DSF_MKDUP); a live client's batch rejects relative positions naming one.
+  // marker and live kernels reproduce (DSF_MKDUP).
   std::unordered_map<std::string, uint32_t> markerOrd;
   std::vector<uint8_t> markerAmbig;
   bool markerDup = false;      // some id is reused
   bool markerIdAnnot = false;  // an annotate names markerId (assert 0x5ad is checked on the device)
-  bool relOnDup = false;       // a relative position named a reused id
   // device mirror
   DocState st{};
   bool onDevice = false;
@@ -565,10 +565,6 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, H
     auto it = d->markerOrd.find(*key);
     if (it == d->markerOrd.end())
       raise(MTB_E_UNSUPPORTED, "unsupported: relative position names no marker of the document (posFromRelativePos -1)");
-    if (d->markerAmbig[it->second]) {
-      if (d->totalLocal) raise(MTB_E_UNSUPPORTED, "unsupported: relative position naming a reused marker id in a live client's document");
-      d->relOnDup = true;
-    }
     const hj::Value* off = member(*rp, u"offset");
     double o = 0;
     if (off && off->kind != hj::Value::kNull) {
@@ -1839,6 +1835,18 @@ void replay(mtb_dev* b, mtb_stats* out) {
             (unsigned long long)mx[0], (unsigned long long)mx[1], (unsigned long long)mx[2], (unsigned long long)mx[3],
             (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mxo);
   }
+  if (getenv("MTB_CHECK_OUT")) {  // MTB_CHECK builds: slice-bound violations per document (DocState.pad3)
+    static const char* pools[4] = {"segp", "blk", "lst", "aux"};
+    uint32_t nbad = 0;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      const uint32_t* r = b->hst[i].pad3;
+      if (!r[0]) continue;
+      if (nbad++ < 16)
+        fprintf(stderr, "mtb_check doc %u: %u out-of-slice accesses, first %s[%u] (capacity %u), op_next %u\n", i, r[0],
+                pools[r[3] & 3], r[1], r[2], b->hst[i].op_next);
+    }
+    fprintf(stderr, "mtb_check: %u of %u documents with out-of-slice accesses\n", nbad, b->ndocs);
+  }
   if (out) *out = st;
   if (firstErr == DERR_HOST) raise(MTB_E_ARG, "document " + std::to_string(errDoc) + ": " + b->docs[errDoc].hostErr);
   if (firstErr)
@@ -2968,8 +2976,6 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     if (b->opts.flags & MTB_BATCH_CATCHUP) raise(MTB_E_UNSUPPORTED, "unsupported: local ops in a catch-up batch");
     HostDoc& d = docref(b, doc);
     if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
-    if (d.relOnDup)  // the live kernel keeps idToSegment without blockUpdate's re-mapping
-      raise(MTB_E_UNSUPPORTED, "unsupported: local ops in a document whose relative positions name a reused marker id");
     const hj::Value op = hj::parse(json, len);
     if (op.kind != hj::Value::kObj) raise(MTB_E_PARSE, "op is not an object");
     mtb_op base{};
@@ -2992,6 +2998,56 @@ int mtbx_local_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
     d.pending.insert(d.pending.end(), recs.begin(), recs.end());
     d.totalOps += recs.size();
     d.totalLocal += recs.size();
+  });
+}
+
+// A detached client's edit before collaboration (client.ts:196-247 while not collaborating: seq
+// UniversalSequenceNumber, clientId LocalClientId, refSeq 0): applied by the next replay like a sequenced op of
+// client -1 at seq 0 -- every perspective it meets is the local one (everything is at seq 0), no LRU entry
+// (seq 0 is not above the window), no zamboni (empty heap), no updateSeqNumbers.
+int mtbx_detached_op_json(mtb_dev* b, uint32_t doc, const char* json, size_t len) {
+  return guarded(b, [&] {
+    if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: detached ops on a matrix batch");
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    if (d.totalOps != d.totalDetached || d.min0 != 0 || d.cur0 != 0 || d.loaded)
+      raise(MTB_E_ARG, "detached ops come before the document's first message or local op");
+    const hj::Value op = hj::parse(json, len);
+    if (op.kind != hj::Value::kObj) raise(MTB_E_PARSE, "op is not an object");
+    mtb_op base{};
+    base.client = (uint16_t)MTB_LOCAL_CLIENT;
+    std::vector<mtb_op> recs;
+    const size_t payloadBefore = d.payload.size();
+    try {
+      pack_delta(b, d, op, base, recs);
+      for (const mtb_op& r : recs)
+        if (r.flags & MTB_F_RELPOS) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions in a detached op");
+    } catch (...) {
+      d.payload.resize(payloadBefore);
+      throw;
+    }
+    d.totalPayload += d.payload.size() - payloadBefore;
+    d.pending.insert(d.pending.end(), recs.begin(), recs.end());
+    d.totalOps += recs.size();
+    d.totalDetached += recs.size();
+  });
+}
+
+// zamboniSegments / packParent(root) as the reference's unit tests call them (an internal record; the live
+// kernel, which carries every engine path, applies it)
+int mtbx_maintenance(mtb_dev* b, uint32_t doc, uint32_t kind) {
+  return guarded(b, [&] {
+    if (b->matrix) raise(MTB_E_UNSUPPORTED, "unsupported: maintenance calls on a matrix batch");
+    if (kind > 1) raise(MTB_E_ARG, "maintenance kind: 0 zamboniSegments, 1 packParent(root)");
+    HostDoc& d = docref(b, doc);
+    if (!d.inited) raise(MTB_E_ARG, "mtb_doc_init must be called first");
+    mtb_op r{};
+    r.type = MTB_OP_MAINT;
+    r.pos1 = kind;
+    d.pending.push_back(r);
+    d.totalOps++;
+    d.totalLocal++;
+    b->live = true;
   });
 }
 

@@ -279,6 +279,12 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len) {
   DOC_CALL(doc, mtbx_local_op_json(d_, l_, json_utf8, len));
 }
+int mtb_detached_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len) {
+  DOC_CALL(doc, mtbx_detached_op_json(d_, l_, json_utf8, len));
+}
+int mtb_maintenance(mtb_batch* b, uint32_t doc, uint32_t kind) {
+  DOC_CALL(doc, mtbx_maintenance(d_, l_, kind));
+}
 int mtb_regenerate_pending_op(mtb_batch* b, uint32_t doc, const char* op_json, size_t len, char** out, size_t* out_len) {
   DOC_CALL(doc, mtbx_regenerate_pending_op(d_, l_, op_json, len, out, out_len));
 }

@@ -223,6 +223,38 @@ using ScratchBig = ScratchT<MTB_LDS_HEAP_LONG>;
 #define memo_old sh->memo[0]
 #define memo_new sh->memo[1]
 
+// MTB_CHECK builds (diagnostic only): the engine's slice pointers are bounds-checked against the document's
+// capacities (sh->capv); an index past its slice is replaced by 0 and reported in DocState.pad3 [count, index,
+// capacity, pool (0 segp, 1 blk, 2 lst, 3 aux)], which the host prints with MTB_CHECK_OUT=1.
+#ifdef MTB_CHECK
+template <class T>
+struct CP {
+  T* p;
+  const uint32_t* cap;  // LDS
+  uint32_t* rep;        // DocState.pad3
+  uint32_t pool;
+  __device__ CP() : p(nullptr), cap(nullptr), rep(nullptr), pool(0) {}
+  __device__ T& operator[](uint32_t i) const {
+    const uint32_t c = *cap;
+    if (COLD(i >= c)) {
+      if (atomicAdd(rep, 1u) == 0) {
+        rep[1] = i;
+        rep[2] = c;
+        rep[3] = pool;
+      }
+      i = 0;
+    }
+    return p[i];
+  }
+  __device__ operator T*() const { return p; }
+};
+#define SLICE(T) CP<T>
+#define RAW(x) ((x).p)
+#else
+#define SLICE(T) T*
+#define RAW(x) (x)
+#endif
+
 // Engine variants: MODE_REPLAY (mtb_replay_kernel); MODE_LOAD applies only the LOADSEG records at
 // the head of each document's records (mtb_load_kernel); MODE_MATRIX replays SharedMatrix vector pairs
 // with setCell handle allocation (mtb_matrix_kernel); MODE_LIVE is MODE_REPLAY plus the local ops, acks and
@@ -234,10 +266,10 @@ enum { MODE_REPLAY = 0, MODE_LOAD = 1, MODE_MATRIX = 2, MODE_LIVE = 3, MODE_MARK
 template <int MODE, class SCR>
 struct Eng {
   DocState* ds;
-  uint32_t* segp;  // parent block of each segment
-  FBlk* blk;
-  WEnt* lst;
-  uint32_t* aux;
+  SLICE(uint32_t) segp;  // parent block of each segment
+  SLICE(FBlk) blk;
+  SLICE(WEnt) lst;
+  SLICE(uint32_t) aux;
   SCR* sh;
   static constexpr uint32_t lheap_n = sizeof(SCR::heap) / sizeof(Lru);  // LDS heap capacity
   int lane;
@@ -285,7 +317,15 @@ struct Eng {
     return seg_used++;
   }
   __device__ __forceinline__ uint32_t* bw(uint32_t b) const { return reinterpret_cast<uint32_t*>(&blk[b]); }
+#ifdef MTB_CHECK
+  __device__ __forceinline__ CP<u32x4> lst4() const {
+    CP<u32x4> c;
+    c.p = reinterpret_cast<u32x4*>(lst.p), c.cap = lst.cap, c.rep = lst.rep, c.pool = 2;
+    return c;
+  }
+#else
   __device__ __forceinline__ u32x4* lst4() const { return reinterpret_cast<u32x4*>(lst); }
+#endif
   __device__ __forceinline__ uint32_t alloc_blk() {
     uint32_t b;
     if (free_top > 0) {
@@ -1502,7 +1542,7 @@ struct Eng {
   // The FIFO of SegmentGroups (pendingSegments, mergeTree.ts:532): directory entry i (0 = oldest) is
   // [localSeq, member list offset, count, capacity, op type, op props id] in the aux arena.
   __device__ __forceinline__ gptr<uint32_t> grp_ent(uint32_t i) const {
-    return UP(aux) + pend_dir + MTB_PEND_ENT * ((pend_head + i) & (pend_cap - 1));
+    return UP(RAW(aux)) + pend_dir + MTB_PEND_ENT * ((pend_head + i) & (pend_cap - 1));
   }
   // room for one more group at the FIFO's tail: the directory starts at MTB_PEND_GROUPS entries and doubles
   // when full (the pending entries move to the front of the new one, oldest first)
@@ -1512,7 +1552,7 @@ struct Eng {
     if (ncap > MTB_PEND_MAX) { fail(DERR_CAP_PEND); return false; }
     const uint32_t nd = alloc_aux(MTB_PEND_ENT * ncap);
     if (bad()) return false;
-    const auto dst = UP(aux) + nd;
+    const auto dst = UP(RAW(aux)) + nd;
     for (uint32_t w = (uint32_t)lane; w < MTB_PEND_ENT * pend_n; w += 64) dst[w] = grp_ent(w / MTB_PEND_ENT)[w % MTB_PEND_ENT];  // (per lane)
     wsync();
     pend_dir = nd;
@@ -1707,6 +1747,18 @@ struct Eng {
       n_mod += 1;
       wsync();
       lru_add(sid, b, sc, S);  // addToLRUSet(segment, seq)
+    }
+    // nodesToUpdate (distinct parents in first-appearance order): blockUpdate re-maps marker ids
+    // (mergeTree.ts:1316 -> :2392), annotate acks included
+    if constexpr (hasMk) {
+      if (COLD(mkDup)) {
+        for (uint32_t i = 0; i < cnt && !err; i++) {
+          const uint32_t b = U(segp[U(aux[off + i])]);
+          bool seen = false;
+          for (uint32_t q = 0; q < i; q += 64) seen |= __ballot(q + lane < i && segp[aux[off + q + lane]] == b) != 0;
+          if (!seen) mk_remap_blk(b);
+        }
+      }
     }
     // nodesToUpdate: the distinct parents, in order (a repeat only rebuilds again)
     uint32_t prev = MTB_NONE;
@@ -1907,11 +1959,15 @@ struct Eng {
     }
     wsync();
     n_mod += n;
-    // nodeUpdateLengthNewStructure of the ancestors: block lengths, then the window lists
+    // nodeUpdateLengthNewStructure of the ancestors: block lengths (and the leaf blocks' marker ids,
+    // deepest first, in run order, mergeTree.ts:2320-2331), then the window lists
     uint32_t prev = MTB_NONE;
     for (uint32_t i = 0; i < n && !err; i++) {
       const uint32_t b = E(i, 1);
-      if (b != prev) fix_len(b);
+      if (b != prev) {
+        fix_len(b);
+        mk_remap_blk(b);
+      }
       prev = b;
     }
     prev = MTB_NONE;
@@ -2058,7 +2114,7 @@ struct Eng {
 
   // ------------------------------------------------------------------ properties
   __device__ __forceinline__ gptr<const uint32_t> props_ptr(uint32_t h) const {
-    return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : GP((const uint32_t*)aux + h);
+    return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : GP((const uint32_t*)RAW(aux) + h);
   }
   // matchProperties (properties.ts:71-96) on interned property sets
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
@@ -3243,7 +3299,7 @@ struct Eng {
     }
   }
   __device__ __forceinline__ void mk_remap_view(int d) {
-    if constexpr (MODE == MODE_MARKERS || MODE == MODE_LOAD) {
+    if constexpr (hasMk) {
       if (COLD(mkDup)) {
         const View& V = sh->v[d];
         const int n = U(V.count);
@@ -3260,8 +3316,27 @@ struct Eng {
       }
     }
   }
+  // blockUpdate of leaf-level block b read from its record (MODE_LIVE: acks, normalizeAdjacentSegments)
+  __device__ __forceinline__ void mk_remap_blk(uint32_t b) {
+    if constexpr (hasMk) {
+      if (COLD(mkDup)) {
+        const uint32_t* r = bw(b);
+        const int n = (int)U(r[FB_HDR]);
+        uint32_t id = MTB_NONE, text = 0, props = 0;
+        int len = 0, rseq = -1;
+        if (lane < n) {
+          id = r[F_ID * 8 + lane];
+          text = r[F_TEXT * 8 + lane];
+          props = r[F_PROPS * 8 + lane];
+          len = (int)r[F_LEN * 8 + lane];
+          rseq = (int)r[F_RSEQ * 8 + lane];
+        }
+        mk_remap(n, id, text, props, len, rseq);
+      }
+    }
+  }
   __device__ __forceinline__ void mk_remap_hold(int from, int n) {  // children placed from sh->hold[.][from..)
-    if constexpr (MODE == MODE_MARKERS || MODE == MODE_LOAD) {
+    if constexpr (hasMk) {
       if (COLD(mkDup)) {
         uint32_t id = MTB_NONE, text = 0, props = 0;
         int len = 0, rseq = -1;
@@ -3567,6 +3642,19 @@ struct Eng {
       case MTB_OP_REGEN:
         if constexpr (isLive) regen(o.pos1);
         break;
+      case MTB_OP_MAINT:  // zamboniSegments / packParent(root) called directly (mergeTree.zamboni.spec.ts)
+        if constexpr (isLive) {
+          view_clear();
+          if (o.pos1 == 0) {
+            zamboni();
+          } else {
+            const uint32_t rc = U(blk[root].count);
+            if (rc > 0 && (U(blk[root].f[F_ID][0]) & MTB_LEAF)) { fail(DERR_SHAPE); return; }  // children must be blocks
+            pack_parent(root);
+          }
+          view_clear();
+        }
+        break;
       default:
         break;
     }
@@ -3602,10 +3690,20 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.xch = xch;
   e.wv = wv;
   e.ds = ds;
+#ifdef MTB_CHECK
+  {
+    uint32_t* rep = &ds->pad3[0];
+    e.segp.p = segp + ds->seg_base, e.segp.cap = &sh.capv[0], e.segp.rep = rep, e.segp.pool = 0;
+    e.blk.p = blks + ds->blk_base, e.blk.cap = &sh.capv[1], e.blk.rep = rep, e.blk.pool = 1;
+    e.lst.p = lists + ds->list_base, e.lst.cap = &sh.capv[2], e.lst.rep = rep, e.lst.pool = 2;
+    e.aux.p = aux + ds->aux_base, e.aux.cap = &sh.capv[5], e.aux.rep = rep, e.aux.pool = 3;
+  }
+#else
   e.segp = segp + ds->seg_base;
   e.blk = blks + ds->blk_base;
   e.lst = lists + ds->list_base;
   e.aux = aux + ds->aux_base;
+#endif
   Lru* const gheap = heap + ds->heap_base;
   const mtb_op* const dops = ops + ds->op_base;
   sh.tab = tables;  // (every lane stores the same values)
@@ -3669,7 +3767,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
     if (e.lane < MTB_LCLASSES) sh.lfree[e.lane] = MTB_NONE;
     e.list_used = MTB_LIST_RESERVED;
   } else if (e.lane < MTB_LCLASSES) {
-    sh.lfree[e.lane] = reinterpret_cast<const uint32_t*>(e.lst)[e.lane];
+    sh.lfree[e.lane] = reinterpret_cast<const uint32_t*>(RAW(e.lst))[e.lane];
   }
 #ifndef MTB_NO_LSTK
   if (e.lane < MTB_LSTK) sh.lstkn[e.lane] = 0;
@@ -3749,7 +3847,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   }
   __syncthreads();
 #endif
-  if (e.lane < MTB_LCLASSES) reinterpret_cast<uint32_t*>(e.lst)[e.lane] = sh.lfree[e.lane];
+  if (e.lane < MTB_LCLASSES) reinterpret_cast<uint32_t*>(RAW(e.lst))[e.lane] = sh.lfree[e.lane];
   __syncthreads();
   if (e.lane == 0) {
     ds->min_seq = e.minSeq;
@@ -3862,6 +3960,10 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
         while (!(ready = U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= c) && n < spins) {
           n++;
           __builtin_amdgcn_s_sleep(16);
+          // another wave gave up: leave now (this ticket's chunk is replayed by the finish kernel)
+          if (COLD((n & 1023) == 0) &&
+              U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+            return;
         }
         if (!ready) {
           if (lane == 0) __hip_atomic_store(&sched[MTB_SCHED_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4290,7 +4392,10 @@ extern "C" __global__ void __launch_bounds__(64)
     }
     __syncthreads();
   };
-  const bool bad = s.err != 0 || s.root >= s.blk_used;
+  // a tree the walk cannot trust (too deep, a child id outside the slice, a cycle: the digest kernel's
+  // conditions) reports MTB_NONE and the host serializes the document from its downloaded slices instead
+  bool bad = s.err != 0 || s.root >= s.blk_used;
+  uint32_t entered = 0;
   if (!bad) enter(s.root, 0);
   while (!bad) {
     const int c = bc[d], kk = nxt[d];
@@ -4303,7 +4408,10 @@ extern "C" __global__ void __launch_bounds__(64)
     if (!(child & MTB_LEAF)) {
       if (lane == 0) nxt[d] = kk + 1;
       __syncthreads();
-      if (d + 1 >= MTB_DG_DEPTH) break;
+      if (d + 1 >= MTB_DG_DEPTH || child >= s.blk_used || ++entered > s.blk_used) {
+        bad = true;
+        break;
+      }
       d++;
       enter(child, d);
       continue;

@@ -175,7 +175,7 @@ class Client {
   constructor(batch, doc) {
     this.batch = batch;
     this.doc = doc;
-    this.initial = "";
+    this.detached = [];  // edits before collaboration (IMergeTreeOps)
     this.longClientId = undefined;
   }
 
@@ -185,9 +185,30 @@ class Client {
    * collaborating, a live client's local insert (insertSegmentLocal) whose op is returned.
    */
   insertTextLocal(pos, text, props) {
-    if (this.longClientId !== undefined) return this.insertSegmentLocal(pos, props === undefined ? text : { text, props });
-    if (props !== undefined) throw unsupported("detached text with properties");
-    this.initial = this.initial.slice(0, pos) + text + this.initial.slice(pos);
+    const seg = props === undefined ? text : { text, props };
+    if (this.longClientId !== undefined) return this.insertSegmentLocal(pos, seg);
+    return this.detach({ pos1: pos, seg, type: 0 });
+  }
+
+  /** An edit before collaboration (createClientsAtInitialState, testClientLogger.ts:51-78): kept until
+   * startOrUpdateCollaboration, then applied at seq 0 by LocalClientId (segments and tombstones). */
+  detach(op) {
+    this.detached.push(op);
+    return op;
+  }
+
+  /** zamboniSegments(mergeTree) (zamboni.ts:19-60), as the reference's unit tests call it. */
+  zamboniSegments() {
+    this.batch.checkIdle();
+    native.maintenance(this.batch.handle, this.doc, 0);
+    this.batch.dirty = true;
+  }
+
+  /** packParent(mergeTree.root, mergeTree) (zamboni.ts:63-120), as mergeTree.zamboni.spec.ts calls it. */
+  packParentRoot() {
+    this.batch.checkIdle();
+    native.maintenance(this.batch.handle, this.doc, 1);
+    this.batch.dirty = true;
   }
 
   // ---- a live client's own ops (client.ts:196-247): applied at the next flush in this client's view,
@@ -207,7 +228,8 @@ class Client {
 
   /** Client.removeRangeLocal (client.ts:230): returns the remove op to send. */
   removeRangeLocal(start, end) {
-    return this.applyLocalOp({ pos1: start, pos2: end, type: 1 });
+    const op = { pos1: start, pos2: end, type: 1 };
+    return this.longClientId === undefined ? this.detach(op) : this.applyLocalOp(op);
   }
 
   /** Client.regeneratePendingOp (client.ts:917-960): the op to resubmit after a reconnect for the oldest
@@ -229,14 +251,20 @@ class Client {
   /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
   annotateRangeLocal(start, end, props, combiningOp) {
     // createAnnotateRangeOp (opBuilder.ts:52-65): a local "rewrite" is pending (pendingRewriteCount) until its ack
-    const op = { pos1: start, pos2: end, props, type: 2 };
-    return this.applyLocalOp(combiningOp === undefined ? op : { combiningOp, ...op });
+    const op0 = { pos1: start, pos2: end, props, type: 2 };
+    const op = combiningOp === undefined ? op0 : { combiningOp, ...op0 };
+    return this.longClientId === undefined ? this.detach(op) : this.applyLocalOp(op);
   }
 
-  /** Client.startOrUpdateCollaboration (client.ts:1133). */
+  /** Client.startOrUpdateCollaboration (client.ts:1133).  One detached text insert into the empty document
+   * is its initial segment; other detached edits are applied (seq 0, LocalClientId) before the first message. */
   startOrUpdateCollaboration(longClientId, minSeq = 0, currentSeq = 0) {
     if (this.longClientId !== undefined) throw unsupported("re-keying the observer id");
-    native.docInit(this.batch.handle, this.doc, this.initial, longClientId, minSeq, currentSeq);
+    const ops = this.detached;
+    const first = ops.length && ops[0].type === 0 && ops[0].pos1 === 0 && typeof ops[0].seg === "string" ? ops[0] : undefined;
+    native.docInit(this.batch.handle, this.doc, first ? first.seg : "", longClientId, minSeq, currentSeq);
+    for (const op of first ? ops.slice(1) : ops) native.detachedOp(this.batch.handle, this.doc, JSON.stringify(op));
+    this.detached = [];
     this.longClientId = longClientId;
   }
 
@@ -248,7 +276,7 @@ class Client {
    * exist in the V1 format, so `catchupOpsP` resolves to [].
    */
   async load(runtime, storage) {
-    if (this.longClientId !== undefined || this.initial) throw new Error("document already initialised");
+    if (this.longClientId !== undefined || this.detached.length) throw new Error("document already initialised");
     const text = (x) => (typeof x === "string" ? x : Buffer.from(x instanceof ArrayBuffer ? new Uint8Array(x) : x).toString("utf8"));
     const header = text(await storage.readBlob("header"));
     const blobs = [["header", header]];

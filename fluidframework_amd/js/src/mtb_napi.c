@@ -293,6 +293,34 @@ static napi_value js_local_op(napi_env env, napi_callback_info info) {
   return undef(env);
 }
 
+/* detachedOp(h, doc, JSON.stringify(IMergeTreeOp)): an edit before collaboration (seq 0, LocalClientId) */
+static napi_value js_detached_op(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc;
+  if (!b || !get_u32(env, argv[1], &doc)) return NULL;
+  size_t n = 0;
+  char* s = get_utf8(env, argv[2], &n);
+  if (!s) return NULL;
+  int rc = mtb_detached_op_json(b, doc, s, n);
+  free(s);
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
+/* maintenance(h, doc, kind): 0 zamboniSegments, 1 packParent(root)              zamboni.ts:19-120 */
+static napi_value js_maintenance(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return NULL;
+  mtb_batch* b = get_batch(env, argv[0]);
+  uint32_t doc, kind;
+  if (!b || !get_u32(env, argv[1], &doc) || !get_u32(env, argv[2], &kind)) return NULL;
+  int rc = mtb_maintenance(b, doc, kind);
+  if (rc) return throw_rc(env, b, rc);
+  return undef(env);
+}
+
 /* regeneratePendingOp(h, doc, JSON.stringify(resetOp)) -> JSON of the op(s) to resubmit   client.ts:917-960 */
 static napi_value js_regenerate(napi_env env, napi_callback_info info) {
   napi_value argv[3];
@@ -762,6 +790,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"matrixLoad", js_matrix_load},  {"summarizeLegacy", js_summarize_legacy},
       {"applyMsg", js_apply_msg},      {"appendOps", js_append_ops},
       {"localOp", js_local_op},        {"summarizeV1Many", js_summarize_v1_many},
+      {"detachedOp", js_detached_op},  {"maintenance", js_maintenance},
       {"digests", js_digests},
       {"addClient", js_add_client},    {"internProps", js_intern_props},
       {"replay", js_replay},           {"replayAsync", js_replay_async},

@@ -179,9 +179,22 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
  * view with UnassignedSequenceNumber, after getValidOpRange's bounds check (a failure is reported by that
  * replay).  Its sequenced message, passed to mtb_apply_msg_json, is the ack (ackPendingSegment,
  * client.ts:641-662).  A local annotate's keys stay pending on its segments until its ack (remote annotates
- * leave them alone, segmentPropertiesManager.ts:60-157).  Local rewrite annotates, marker-relative
- * positions, matrix and catch-up batches are MTB_E_UNSUPPORTED. */
+ * leave them alone, segmentPropertiesManager.ts:60-157; a local rewrite annotate counts as a pending rewrite).
+ * Marker-relative positions resolve in the client's own view.  Matrix and catch-up batches are
+ * MTB_E_UNSUPPORTED. */
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
+/* A detached edit before collaboration (TestClient.insertTextLocal / removeRangeLocal / annotateRangeLocal
+ * while the collab window is not collaborating, client.ts:196-247 with getLocalSequenceNumber() =
+ * UniversalSequenceNumber and clientId = LocalClientId; createClientsAtInitialState, testClientLogger.ts:51-78):
+ * the op (JSON IMergeTreeOp) is applied at the next replay with seq 0, refSeq 0 and LocalClientId, no LRU entry
+ * and no zamboni -- the segments and tombstones a detached client builds.  Only after mtb_doc_init(min_seq 0,
+ * cur_seq 0) and before the document's first message or local op. */
+int mtb_detached_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
+/* The merge tree's maintenance functions that the reference's own unit tests call directly
+ * (mergeTree.zamboni.spec.ts: zamboni.ts exports): kind 0 = zamboniSegments(mergeTree) (zamboni.ts:19-60),
+ * kind 1 = packParent(root, mergeTree) (zamboni.ts:63-120; the root's children must be blocks, else
+ * MTB_E_INTERNAL at replay).  Queued as an internal record, applied at the next replay. */
+int mtb_maintenance(mtb_batch* b, uint32_t doc, uint32_t kind);
 /* Client.regeneratePendingOp (client.ts:917-960) after a reconnect: `op_json` is the live client's oldest
  * pending op (as submitted; a GROUP names one pending op per member).  Replays the batch, then on the GPU
  * normalizes the segment order around pending segments (normalizeSegmentsOnRebase, mergeTree.ts:2357-2390)

@@ -187,7 +187,7 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
 
 
 def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
-                   record=None, reconnect=0.0, rewrite=0.0):
+                   record=None, reconnect=0.0, rewrite=0.0, marker_ids=0):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
@@ -197,9 +197,12 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     sequenced stream, then regenerates each dropped op (Client.regeneratePendingOp, client.ts:917-960) and
     resubmits the result at its current seq.  With `rewrite` > 0 that fraction of the local annotates are
     `rewrite` annotates (combiningOp {"name": "rewrite"}: pendingRewriteCount, segmentPropertiesManager.ts).
-    Returns (clients, observer, sequenced messages)."""
+    With `marker_ids` > 0 clients also insert markers whose `markerId` comes from a pool of that many (ids are
+    reused, so blockUpdate's re-mapping decides what an id names, mergeTree.ts:2392 -> :296-306) and send
+    marker-relative inserts and annotateMarker ops (relativePos1 {id, before}, relativePos2 {id}) for ids
+    their own view resolves.  Returns (clients, observer, sequenced messages)."""
     import random
-    from pyoracle import OracleDoc
+    from pyoracle import OracleDoc, OracleError
     rng = random.Random(seed)
     ids = [f"c{k}" for k in range(n_clients)]
     clients = []
@@ -217,6 +220,19 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     def local_op(c):
         n = c.get_length()
         r = rng.random()
+        if marker_ids:
+            mid = f"d{rng.randrange(marker_ids)}"
+            if r < 0.12:
+                return c.insert_local_op(rng.randint(0, n), {"marker": {"refType": 1}, "props": {"markerId": mid}})
+            if r < 0.26 and n > 0:
+                p = c.pos_from_relative({"id": mid, "before": True}, c.current_seq, 0)
+                if 0 <= p < n:
+                    if rng.random() < 0.5:
+                        return c.local_op_json({"type": 0, "relativePos1": {"id": mid, "before": True},
+                                                "seg": rng.choice(words)})
+                    return c.local_op_json({"type": 2, "relativePos1": {"id": mid, "before": True},
+                                            "relativePos2": {"id": mid}, "props": {"seen": rng.randint(0, 3)}})
+            r = rng.random()
         if n == 0 or r < 0.5:
             t = rng.choice(words)
             seg = {"text": t, "props": {"k": rng.randint(0, 2)}} if rng.random() < 0.2 else t
@@ -258,6 +274,36 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
         if rounds is not None:
             rounds[-1] = [(ev, clients[k].digest(), clients[k].get_text()) for k, ev in enumerate(rounds[-1])]
 
+    try:
+        _farm_rounds(n_rounds, rounds, reconnect, rng, queue, ids, clients, deliver, n_clients, local_op, sequence,
+                     end_round, log, seen)
+    except OracleError:
+        # reused marker ids: clients' idToSegment maps diverge (the reference's own behaviour), so a later op
+        # can be invalid on a receiver; the farm ends at the last complete round
+        if not marker_ids:
+            raise
+        if rounds is not None:
+            rounds.pop()
+            record["stopped"] = True
+        obs_log = []
+        for m in log:
+            try:
+                obs.apply_msg(m)
+            except OracleError:
+                break
+            obs_log.append(m)
+        if record is not None:
+            record["obs_log"] = obs_log
+        return clients, obs, log
+    for m in log:
+        obs.apply_msg(m)
+    if record is not None:
+        record["obs_log"] = log
+    return clients, obs, log
+
+
+def _farm_rounds(n_rounds, rounds, reconnect, rng, queue, ids, clients, deliver, n_clients, local_op, sequence,
+                 end_round, log, seen):
     for _ in range(n_rounds):
         if rounds is not None:
             rounds.append([[] for _ in range(n_clients)])
@@ -293,9 +339,6 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     for k in range(n_clients):
         deliver(k, len(log))
     end_round()
-    for m in log:
-        obs.apply_msg(m)
-    return clients, obs, log
 
 
 def _doover(lo, hi, grow):

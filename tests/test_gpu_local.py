@@ -22,16 +22,24 @@ def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annot
     return _replay_record(rec, seed, new_mode, rounds_per_replay, "hello world")
 
 
-def _replay_record(rec, seed, new_mode, rounds_per_replay, initial):
+def _replay_record(rec, seed, new_mode, rounds_per_replay, initial, observer=None):
+    """observer: an OracleDoc that applied rec["obs_log"]; it becomes one more document of the (live) batch,
+    fed its messages in four parts across the replays, and is compared at the end."""
     import json
     from fluidframework_amd import MergeTreeBatch
     ids = rec["ids"]
     n_clients = len(ids)
-    B = MergeTreeBatch(n_clients, new_length_calc=new_mode)
+    B = MergeTreeBatch(n_clients + (observer is not None), new_length_calc=new_mode)
     for k, cid in enumerate(ids):
         if initial:
             B[k].insertTextLocal(0, initial)
         B[k].startOrUpdateCollaboration(cid)
+    if observer is not None:
+        if initial:
+            B[n_clients].insertTextLocal(0, initial)
+        B[n_clients].startOrUpdateCollaboration("obs")
+        obs_log = rec["obs_log"]
+        obs_parts = [obs_log[len(obs_log) * q // 4: len(obs_log) * (q + 1) // 4] for q in range(4)]
     checked = 0
     for r, rnd in enumerate(rec["rounds"]):
         for k, (events, _, _) in enumerate(rnd):
@@ -46,12 +54,23 @@ def _replay_record(rec, seed, new_mode, rounds_per_replay, initial):
                     B[k].applyMsg(x)
         if (r + 1) % rounds_per_replay and r + 1 < len(rec["rounds"]):
             continue
+        if observer is not None and obs_parts and (r + 1) * 4 >= len(rec["rounds"]) * (5 - len(obs_parts)):
+            for m in obs_parts.pop(0):
+                B[n_clients].applyMsg(m)
         B.replay()
         dig = B.digests()
         for k, (_, odig, otext) in enumerate(rnd):
             assert B.text(k) == otext, f"seed {seed} round {r} client {k}: text"
             assert dig[k] == odig, f"seed {seed} round {r} client {k}: digest"
             checked += 1
+    if observer is not None:
+        for part in obs_parts:
+            for m in part:
+                B[n_clients].applyMsg(m)
+        B.replay()
+        assert B.text(n_clients) == observer.get_text(), f"seed {seed}: observer text"
+        assert B.digests(n_clients, 1)[0] == observer.digest(), f"seed {seed}: observer digest"
+        assert B.dump_segments(n_clients) == observer.dump_segments(), f"seed {seed}: observer dump"
     return checked
 
 
@@ -210,6 +229,20 @@ def test_reconnect_farm_reference_divergence(seed, n_clients):
     (tests/test_reference_kats.py::test_reconnect_normalization_reorders_sequenced_segments): the engine
     still equals each oracle client after every round, diverged state included."""
     assert _replay_farm(seed, n_clients=n_clients, n_rounds=60, new_mode=True, annotate=True, reconnect=0.2) > 0
+
+
+@pytest.mark.parametrize("seed", list(range(301, 317)))
+def test_live_farm_reused_marker_ids(seed):
+    """Live clients inserting markers whose ids come from a pool of 2-5 (reused: blockUpdate's re-mapping,
+    mergeTree.ts:2392 -> addNodeReferences :296-306, decides what an id names) and sending marker-relative
+    inserts / annotateMarker ops; acks (ackPendingSegment's nodesToUpdate, :1283-1322) and reconnects
+    (normalizeAdjacentSegments, :2320-2331) re-map too.  Every client's digest and text equal its oracle
+    client's after every round, and an observer document in the same live batch (relative positions naming
+    reused ids, replayed by the live kernel) equals the oracle observer."""
+    rec = {}
+    _, obs, _ = run_local_farm(seed, n_clients=3 + seed % 3, n_rounds=40, new_mode=seed % 2 == 0, annotate=True,
+                               record=rec, marker_ids=2 + seed % 4, reconnect=0.25 if seed % 3 == 0 else 0.0)
+    assert _replay_record(rec, seed, seed % 2 == 0, 1, "hello world", observer=obs) > 0
 
 
 @pytest.mark.parametrize("seed,reconnect", [(101, 0.0), (102, 0.0), (103, 0.3), (104, 0.3)])

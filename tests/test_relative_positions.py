@@ -129,20 +129,18 @@ def test_host_rejects_unresolvable_relative_positions_at_pack_time():
     assert fl & 0x20 and p1 & 0x80000000  # MTB_F_RELPOS: pos1 names a descriptor
     t, fl, c, seq, ref, msn, p1, p2, pay, pr = struct.unpack_from("<BBHIIIIIII", ob, 0)
     assert fl & 0x02 and pay == 1  # the marker carries its id ordinal + 1
-    # a reused id: the observer's marker kernel re-maps it at blockUpdate time, so relative positions naming
-    # it pack; a live client's document (local ops) rejects them, before or after its first local op
+    # a reused id: the marker and live kernels re-map it at blockUpdate time, so relative positions naming
+    # it pack, in an observer's document and in a live client's, before or after its first local op
     B[0].applyMsg(_msg("B", 3, 2, 0, mk))
     rm = {"type": 1, "relativePos1": {"id": "m1", "before": True}, "relativePos2": {"id": "m1"}}
     B[0].applyMsg(_msg("B", 4, 3, 0, rm))
-    with pytest.raises(MergeTreeError, match="reused marker id"):
-        B[0].insertSegmentLocal(0, "x")
+    B[0].insertSegmentLocal(0, "x")
     L = MergeTreeBatch(1)
     L[0].startOrUpdateCollaboration("A")
     L[0].applyMsg(_msg("B", 1, 0, 0, mk))
     L[0].applyMsg(_msg("B", 2, 1, 0, mk))
     L[0].insertSegmentLocal(0, "x")
-    with pytest.raises(MergeTreeError, match="reused marker id"):
-        L[0].applyMsg(_msg("B", 3, 2, 0, rm))
+    L[0].applyMsg(_msg("B", 3, 2, 0, rm))
     # a live client's local ops and catch-up batches take absolute positions only
     C = MergeTreeBatch(1, catch_up=True)
     C[0].startOrUpdateCollaboration("A")
