@@ -22,6 +22,8 @@
 #define MTB_UNDEF (-1)
 #define MTB_MARKER 0x80000000u  // Seg.text flag: marker, low bits = refType + 1 (0 = undefined)
 #define MTB_GPROPS 0x80000000u  // props handle flag: batch-global table (else per-doc aux arena)
+#define MTB_PNAN 0x40000000u    // props handle flag of a per-doc set holding NaN (an incr annotate): such a set
+                                // matches no set, itself included (matchProperties: NaN !== NaN)
 #define MTB_NOKEY ((int32_t)0x80000000)
 // Window lists are allocated in power-of-two capacities (8 << class) from the document's list slice;
 // released lists go to a per-class free stack whose heads live in the slice's first 16 words.
@@ -207,6 +209,8 @@ struct Tables {
   uint32_t* delta;           // catch-up delta pool (per-document slices at DocState.delta_base, 4 words/entry)
   uint32_t class_trivial;    // every matchProperties class holds one value id: classes compare as value ids
   uint32_t mk_key;           // key id of "markerId" (MTB_NONE: no property set names it)
+  uint32_t nan_val;          // value id of NaN (incr annotates; MTB_NONE: none packed); val_falsy bit 1 marks
+                             // the values that incr turns into NaN (numbers, booleans, NaN)
 };
 
 // device error codes (DocState.err)
@@ -235,6 +239,7 @@ struct Tables {
 #define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
 #define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
 #define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
+#define DERR_INCR 24         // an incr annotate over a string / object value (not NaN: unsupported on the device)
 // ticket scheduler words (mtb_replay_sched_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32

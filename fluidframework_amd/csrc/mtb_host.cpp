@@ -172,9 +172,24 @@ struct Interner {
     valJson.push_back(js);
     valId[js] = id;
     valClass.push_back(cls);
-    valFalsy.push_back(v.truthy() ? 0 : 1);
+    // bit 0: JS falsy; bit 1: incr makes it NaN (number / boolean + undefined, properties.ts:38-45)
+    valFalsy.push_back((v.truthy() ? 0 : 1) | (v.kind == hj::Value::kNum || v.kind == hj::Value::kBool ? 2 : 0));
     dirty = true;
     return id;
+  }
+  // NaN, the value an incr annotate gives a numeric key: JSON null (JSON.stringify), its own matchProperties
+  // class; a set holding it is flagged MTB_PNAN by the device and matches nothing (NaN !== NaN)
+  uint32_t nanVal = MTB_NONE;
+  uint32_t nan() {
+    if (nanVal != MTB_NONE) return nanVal;
+    nanVal = (uint32_t)valJson.size();
+    valJson.push_back("null");  // (null itself is never a stored value: it deletes)
+    const uint32_t cls = (uint32_t)classId.size();
+    classId["\x01NaN"] = cls;
+    valClass.push_back(cls);
+    valFalsy.push_back(1 | 2);
+    dirty = true;
+    return nanVal;
   }
   // props object -> id with (a) op-props list for annotate, (b) property set for insert specs.
   uint32_t props(const hj::Value& obj) {
@@ -662,8 +677,21 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
       const hj::Value* comb = member(op, u"combiningOp");
       if (comb && comb->kind == hj::Value::kObj) {
         const hj::Value* name = member(*comb, u"name");
-        if (name && name->kind == hj::Value::kStr && name->s == u"rewrite") r.flags |= MTB_F_REWRITE;
-        else raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite");
+        if (name && name->kind == hj::Value::kStr && name->s == u"rewrite") {
+          r.flags |= MTB_F_REWRITE;
+        } else if (name && name->kind == hj::Value::kStr && name->s == u"incr") {
+          // combine(op, previous, undefined) (segmentPropertiesManager.ts:145-147, properties.ts:24-69): NaN for a
+          // number / boolean / absent previous value when defaultValue is absent or numeric; a string previous
+          // value (string concatenation) fails the document at replay (DERR_INCR)
+          const hj::Value* dv = member(*comb, u"defaultValue");
+          if (dv && dv->kind != hj::Value::kUndef && dv->kind != hj::Value::kNull && dv->kind != hj::Value::kNum &&
+              dv->kind != hj::Value::kBool)
+            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with a non-numeric defaultValue (string concatenation)");
+          r.flags |= MTB_F_INCR;
+          b->in.nan();
+        } else {
+          raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite / incr (consensus mutates shared value objects)");
+        }
       }
     }
     out.push_back(r);
@@ -1430,6 +1458,7 @@ std::string derr_text(int e) {
     case DERR_SCHED: return "internal: the document's records did not all run (replay scheduler invariant)";
     case DERR_ASSERT_MKID: return "0x5ad Cannot change the markerId of an existing marker";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
+    case DERR_INCR: return "unsupported: incr combiningOp over a string or object property value (string concatenation)";
     default: return "device error " + std::to_string(e);
   }
 }
@@ -1731,6 +1760,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   t.pidx = b->dPidx.p;
   t.val_class = b->dValClass.p;
   t.val_falsy = b->dValFalsy.p;
+  t.nan_val = b->in.nanVal;
   t.key_rank = b->dKeyRank.p;
   t.delta = b->dDelta.p;
   t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
@@ -1902,7 +1932,7 @@ PropView props_of(mtb_dev* b, const HostDoc& d, uint32_t h) {
   PropView v;
   if (!h) return v;
   if (h & MTB_GPROPS) v.p = b->in.pool.data() + (h & ~MTB_GPROPS);
-  else v.p = d.aux.data() + h;
+  else v.p = d.aux.data() + (h & ~MTB_PNAN);
   return v;
 }
 void props_json(mtb_dev* b, std::string& o, PropView v) {
@@ -1917,6 +1947,9 @@ void props_json(mtb_dev* b, std::string& o, PropView v) {
 }
 bool props_match(mtb_dev* b, PropView a, PropView c) {
   if (a.n() != c.n()) return false;
+  if (b->in.nanVal != MTB_NONE)  // NaN !== NaN: a set holding NaN matches nothing
+    for (uint32_t i = 0; i < a.n(); i++)
+      if (a.p[2 + 2 * i] == b->in.nanVal || c.p[2 + 2 * i] == b->in.nanVal) return false;
   for (uint32_t i = 0; i < a.n(); i++) {
     bool found = false;
     for (uint32_t q = 0; q < c.n(); q++) {
@@ -2460,6 +2493,8 @@ void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
         for (mtb_op& r : recs) {
           if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE))
             raise(MTB_E_UNSUPPORTED, "unsupported: catch-up rewriting of a lagging rewrite annotate");
+          if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_INCR))
+            raise(MTB_E_UNSUPPORTED, "unsupported: catch-up rewriting of a lagging incr annotate");
           if (r.type == MTB_OP_INSERT || r.type == MTB_OP_REMOVE || r.type == MTB_OP_ANNOTATE) r.flags |= MTB_F_DELTA;
         }
       }
@@ -3349,6 +3384,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     t.pidx = b->dPidx.p;
     t.val_class = b->dValClass.p;
     t.val_falsy = b->dValFalsy.p;
+  t.nan_val = b->in.nanVal;
     t.key_rank = b->dKeyRank.p;
     t.delta = b->dDelta.p;
     t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;

@@ -2114,10 +2114,12 @@ struct Eng {
 
   // ------------------------------------------------------------------ properties
   __device__ __forceinline__ gptr<const uint32_t> props_ptr(uint32_t h) const {
-    return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS)) : GP((const uint32_t*)RAW(aux) + h);
+    return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS))
+                            : GP((const uint32_t*)RAW(aux) + (h & ~MTB_PNAN));
   }
   // matchProperties (properties.ts:71-96) on interned property sets
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
+    if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
     if (a == b) return true;
     const gptr<const uint32_t> pa = a ? props_ptr(a) : nullptr;
     const gptr<const uint32_t> pb = b ? props_ptr(b) : nullptr;
@@ -2144,13 +2146,15 @@ struct Eng {
   }
   // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157).
   // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
-  __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, bool rewrite) {
+  // comb: 0 none, 1 rewrite, 2 incr (the annotate's combiningOp)
+  __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, int comb) {
     const uint32_t mo = U(memo_old), mn = U(memo_new);
     if (HOT(old == mo && mn)) return mn;
-    return props_apply_slow(old, opId, rewrite);
+    return props_apply_slow(old, opId, comb);
   }
   // nex > 0: the first nex words of sh->hold[2] are keys this edit leaves alone (pending local keys)
-  __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, bool rewrite, uint32_t nex = 0) {
+  __device__ __forceinline__ uint32_t props_apply_slow(uint32_t old, uint32_t opId, int comb, uint32_t nex = 0) {
+    const bool rewrite = comb == 1;
     auto excluded = [&](uint32_t k) {
       bool x = false;
       for (uint32_t i = 0; i < nex; i++) x |= sh->hold[2][i] == k;
@@ -2178,7 +2182,7 @@ struct Eng {
         for (uint32_t q = 0; q < nop; q++) {
           if (op[1 + 2 * q] == k) {
             const uint32_t v = op[2 + 2 * q];
-            keep = v != MTB_NONE && !sh->tab.val_falsy[v];
+            keep = v != MTB_NONE && !(sh->tab.val_falsy[v] & 1);
           }
         }
         if (!keep && nex && excluded(k)) keep = true;
@@ -2194,11 +2198,17 @@ struct Eng {
     }
     for (uint32_t q = 0; q < nop; q++) {
       const uint32_t k = op[1 + 2 * q];
-      const uint32_t v = op[2 + 2 * q];
+      uint32_t v = op[2 + 2 * q];
       if (nex && excluded(k)) continue;
       int at = -1;
       for (uint32_t i = 0; i < n; i++)
         if (sh->pk[i] == k) at = (int)i;
+      if (COLD(comb == 2)) {
+        // incr: combine(op, previous, undefined) (properties.ts:24-69) -- previous (or the host-checked numeric
+        // defaultValue) + undefined is NaN for numbers / booleans / NaN; strings and objects are not restated
+        if (at >= 0 && !(sh->tab.val_falsy[sh->pv[at]] & 2)) { fail(DERR_INCR); return 0; }
+        v = U(sh->tab.nan_val);
+      }
       if (v == MTB_NONE) {
         if (at >= 0) {
           for (uint32_t i = (uint32_t)at; i + 1 < n; i++) {
@@ -2237,12 +2247,18 @@ struct Eng {
         n++;
       }
     }
-    const uint32_t h = alloc_aux(1 + 2 * n);
+    uint32_t h = alloc_aux(1 + 2 * n);
     if (bad()) return 0;
     aux[h] = n;
     for (uint32_t i = lane; i < n; i += 64) {
       aux[h + 1 + 2 * i] = sh->pk[i];
       aux[h + 2 + 2 * i] = sh->pv[i];
+    }
+    const uint32_t nanv = U(sh->tab.nan_val);
+    if (COLD(nanv != MTB_NONE)) {  // a set holding NaN matches nothing: its handle says so
+      bool hasNan = false;
+      for (uint32_t i = lane; i < n; i += 64) hasNan |= sh->pv[i] == nanv;
+      if (__ballot(hasNan)) h |= MTB_PNAN;
     }
     wsync();
     memo_old = old;
@@ -2305,7 +2321,8 @@ struct Eng {
   // boundaries were split beforehand, so each segment is wholly in or out of the range).  `pos` is the
   // position at the start of the block; returns the block's total visible length.
   __device__ __forceinline__ int map_leaf_block(int d, int pos, int start, int end, int S, int C, bool remove, uint32_t opId,
-                                bool rewrite) {
+                                int comb) {
+    const bool rewrite = comb == 1;
     View& V = sh->v[d];
     const uint32_t b = U(V.b);
     const int count = U(V.count);
@@ -2442,8 +2459,8 @@ struct Eng {
             continue;
           }
 #endif
-          if (!nk) continue;
-          const uint32_t np = props_apply_slow(rlu(props, t), opId, rewrite, nk);
+          if (!nk || comb == 2) continue;  // (a combiningOp modifies pending keys too, shouldModifyKey :95-106)
+          const uint32_t np = props_apply_slow(rlu(props, t), opId, comb, nk);
           if (bad()) return 0;
           memo_old = MTB_NONE;  // (an edit with exclusions is never reused)
           if (lane == t) {
@@ -2458,7 +2475,7 @@ struct Eng {
       while (am) {
         const int t = first_set(am);
         const uint32_t old = rlu(props, t);
-        const uint32_t np = props_apply(old, opId, rewrite);
+        const uint32_t np = props_apply(old, opId, comb);
         if (bad()) return 0;
         const bool mine = visit && props == old && !((handled >> lane) & 1);
         if (mine) {
@@ -2491,7 +2508,7 @@ struct Eng {
   // parent's slot and list.  The walk's per-child loop (skip children of undefined / zero length or
   // wholly before `start`, stop at the first one at or after `end`) is one scan over the block's slots:
   // the next child descended into is the first slot at or after the cursor that overlaps the range.
-  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, bool rewrite) {
+  __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, int comb) {
     if (end == start) return;
     int d = 0;
     bool exiting = false;  // a leaf block reached `end`: every open block is only flushed from here on
@@ -2512,7 +2529,7 @@ struct Eng {
       if (!exiting) {
         if (idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
           // a block of segments: every touched segment at once
-          const int tot = map_leaf_block(d, bpos, start, end, S, C, remove, opId, rewrite);
+          const int tot = map_leaf_block(d, bpos, start, end, S, C, remove, opId, comb);
           if (bad()) return;
           if (bpos + tot >= end) exiting = true;
         } else {
@@ -2721,7 +2738,9 @@ struct Eng {
         const int lmkv = dpp_shr_t<0x111>((int)mk);
         const int llastv = dpp_shr_t<0x111>((int)last);
         const bool base = cand & lcand & !mk & (lmkv == 0) & ((uint16_t)llastv != (uint16_t)'\n');
-        const bool sameH = f[F_PROPS] == (uint32_t)dpp_shr_t<0x111>((int)f[F_PROPS]);
+        const uint32_t lprops = (uint32_t)dpp_shr_t<0x111>((int)f[F_PROPS]);
+        const bool sameH = f[F_PROPS] == lprops;
+        const bool nanPair = ((f[F_PROPS] | lprops) & MTB_PNAN) != 0;  // a set holding NaN matches nothing
         const bool sameN = g.n == (uint32_t)dpp_shr_t<0x111>((int)g.n);
         const bool k0k0 = g.k0 == (uint32_t)dpp_shr_t<0x111>((int)g.k0);
         const bool c0c0 = g.c0 == (uint32_t)dpp_shr_t<0x111>((int)g.c0);
@@ -2731,10 +2750,10 @@ struct Eng {
         const bool c0c1 = g.c0 == (uint32_t)dpp_shr_t<0x111>((int)g.c1);
         const bool k1k0 = g.k1 == (uint32_t)dpp_shr_t<0x111>((int)g.k0);
         const bool c1c0 = g.c1 == (uint32_t)dpp_shr_t<0x111>((int)g.c0);
-        bool eq = sameH || (sameN && (g.n == 0 || (g.n == 1 && k0k0 && c0c0) ||
-                                      (g.n == 2 && ((k0k0 && c0c0 && k1k1 && c1c1) || (k0k1 && c0c1 && k1k0 && c1c0)))));
+        bool eq = !nanPair && (sameH || (sameN && (g.n == 0 || (g.n == 1 && k0k0 && c0c0) ||
+                                                   (g.n == 2 && ((k0k0 && c0c0 && k1k1 && c1c1) || (k0k1 && c0c1 && k1k0 && c1c0))))));
         // more than two keys: a full matchProperties, one neighbour pair at a time (rare)
-        unsigned long long nf = __ballot(base && !sameH && sameN && g.n > 2);
+        unsigned long long nf = __ballot(base && !sameH && !nanPair && sameN && g.n > 2);
         if (COLD(nf)) {
           while (nf) {
             const int t = first_set(nf);
@@ -3618,7 +3637,8 @@ struct Eng {
         t0 = PROF_T();
         const uint32_t dfrom = delta_used;
         if (isLive) sh->memo[2] = 0;
-        node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props, (o.flags & MTB_F_REWRITE) != 0);
+        node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props,
+                 o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_REWRITE) ? 1 : (o.flags & MTB_F_INCR) ? 2 : 0);
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);
@@ -4236,7 +4256,7 @@ extern "C" __global__ void __launch_bounds__(64)
         }
         uint64_t Ph = 0;
         if (props) {
-          const uint32_t* ps = (props & MTB_GPROPS) ? pool + (props & ~MTB_GPROPS) : A + props;
+          const uint32_t* ps = (props & MTB_GPROPS) ? pool + (props & ~MTB_GPROPS) : A + (props & ~MTB_PNAN);
           const uint32_t n = ps[0];
           for (uint32_t i = 0; i < n; i++) Ph += dg_mix(dg_mix(i + 1, khash[ps[1 + 2 * i]]), vhash[ps[2 + 2 * i]]);
         }
@@ -4315,6 +4335,7 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
 namespace mtbk {
 __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uint32_t* pool, const uint32_t* A,
                                                const uint32_t* vcl) {
+  if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
   if (a == b) return true;
   const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + a) : nullptr;
   const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + b) : nullptr;
@@ -4363,6 +4384,7 @@ extern "C" __global__ void __launch_bounds__(64)
   // inline a per-document property set (global ones are referenced by pool offset)
   auto props_out = [&](uint32_t h) -> uint32_t {
     if (!h || (h & MTB_GPROPS)) return h;
+    h &= ~MTB_PNAN;  // (the host serializes the copy; NaN is JSON null)
     const uint32_t m = 1 + 2 * U(A[h]);
     if (emit)
       for (uint32_t i = (uint32_t)lane; i < m; i += 64) OW[nw + i] = A[h + i];

@@ -48,6 +48,8 @@ enum {
   MTB_F_MARKER = 0x02,  /* insert: Marker segment, pos2 = refType (0xFFFFFFFF = undefined) */
   MTB_F_REWRITE = 0x04, /* annotate: combiningOp {name:"rewrite"} */
   MTB_F_SEGOBJ = 0x08,  /* insert: seg given as {text, props?} object (props id may be 0) */
+  MTB_F_INCR = 0x08,    /* annotate: combiningOp {name:"incr"} -- every key of props becomes combine(op, previous,
+                           undefined) (properties.ts:24-69), NaN for numeric / boolean / absent previous values */
   MTB_F_PERMSEG = 0x40, /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
   MTB_F_DELTA = 0x80    /* record the op's delta ranges (catch-up rewriting, MTB_BATCH_CATCHUP) */
 };

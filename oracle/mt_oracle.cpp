@@ -950,13 +950,49 @@ void MergeTree::markRangeRemoved(int start, int end, int refSeq, int clientId, i
 // BaseSegment.addProperties: a local op (seq Unassigned) while collaborating counts its keys as pending;
 // a sequenced remote op leaves the keys with pending local updates alone (shouldModifyKey), and leaves a
 // segment with a pending local rewrite (pendingRewriteCount > 0) alone altogether (:75-82).
-static void applyProps(Seg* s, const JObj& newProps, bool rewrite, int seq = UniversalSeq, bool collaborating = false) {
+Comb parse_comb(const JVal* comb) {
+  Comb c;
+  if (!comb || comb->t != JVal::Obj) return c;
+  const JVal* name = obj_get(comb->obj, u"name");
+  if (name && name->t == JVal::Str && name->str == u"rewrite") {
+    c.kind = Comb::Rewrite;
+  } else if (name && name->t == JVal::Str && name->str == u"incr") {
+    c.kind = Comb::Incr;
+    if (const JVal* d = obj_get(comb->obj, u"defaultValue")) c.defaultValue = *d;
+    if (const JVal* m = obj_get(comb->obj, u"minValue")) c.minValue = *m;
+  } else {
+    fail_unsupported("combiningOp other than rewrite / incr");
+  }
+  return c;
+}
+// combine(combiningOp, previousValue, undefined, seq) for "incr" (properties.ts:24-69)
+static JVal combine_incr(const Comb& c, const JVal* prev) {
+  JVal cur = prev ? *prev : JVal::undef();
+  if (cur.t == JVal::Undef) cur = c.defaultValue;
+  switch (cur.t) {  // _currentValue += undefined
+    case JVal::Str: cur.str += u"undefined"; break;
+    case JVal::Undef:
+    case JVal::Null:
+    case JVal::False:
+    case JVal::True:
+    case JVal::Num: cur = JVal::number(std::nan("")); break;
+    default: fail_unsupported("incr of an object or array property value");
+  }
+  if (!js_falsy(&c.minValue)) {  // if (_currentValue < minValue) _currentValue = minValue
+    if (c.minValue.t == JVal::Obj || c.minValue.t == JVal::Arr) fail_unsupported("incr with an object minValue");
+    // NaN < x is false; "...undefined" < a number compares NaN; two strings compare by UTF-16 code units
+    if (cur.t == JVal::Str && c.minValue.t == JVal::Str && cur.str < c.minValue.str) cur = c.minValue;
+  }
+  return cur;
+}
+static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq = UniversalSeq, bool collaborating = false) {
   s->hasPropManager = true;
   if (!s->props) s->props = JObj();
   if (collaborating && s->pendingRewrite > 0 && seq != UnassignedSeq && seq != UniversalSeq) return;
   JObj& old = *s->props;
+  const bool rewrite = comb.kind == Comb::Rewrite, combining = comb.kind == Comb::Incr;
   auto shouldModify = [&](const u16str& k) {
-    return seq == UnassignedSeq || seq == UniversalSeq || s->pendingKeys.find(k) == s->pendingKeys.end();
+    return seq == UnassignedSeq || seq == UniversalSeq || s->pendingKeys.find(k) == s->pendingKeys.end() || combining;
   };
   if (rewrite) {
     if (collaborating && seq == UnassignedSeq) s->pendingRewrite++;
@@ -976,13 +1012,15 @@ static void applyProps(Seg* s, const JObj& newProps, bool rewrite, int seq = Uni
         continue;
       }
     }
-    if (kv.second.t == JVal::Null) obj_del(old, kv.first);
+    if (combining) obj_set(old, kv.first, combine_incr(comb, obj_get(old, kv.first)));
+    else if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
   }
 }
 
 // annotateRange (mergeTree.ts:1895-1958)
-void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq) {
+void MergeTree::annotateRange(int start, int end, const JObj& props, const Comb& comb, int refSeq, int clientId, int seq) {
+  const bool rewrite = comb.kind == Comb::Rewrite;
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
   std::vector<Seg*> annotated;
@@ -1002,7 +1040,7 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
     if (opId && s->isMarker && !same_id(opId, s->props ? obj_get(*s->props, u"markerId") : nullptr))
       fail_assert("0x5ad", "Cannot change the markerId of an existing marker");
     annotated.push_back(s);
-    applyProps(s, props, rewrite, seq, window.collaborating);
+    applyProps(s, props, comb, seq, window.collaborating);
     counters.segsTouched += 1;
     if (window.collaborating) {
       if (seq == UnassignedSeq) group = addToPendingList(s, group, localSeq);
@@ -1014,6 +1052,7 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, bool rewrit
   nodeMap(refSeq, clientId, annotate, post, start, end);
   if (onDelta && !annotated.empty()) {
     if (rewrite) fail_unsupported("catch-up rewriting of a rewrite annotate");
+    if (comb.kind == Comb::Incr) fail_unsupported("catch-up rewriting of an incr annotate");
     onDelta(2, annotated, &props);
   }
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
@@ -1309,16 +1348,10 @@ void Doc::applyRemoteDelta(const JVal& op, int client, int refSeq, int seq) {
       int a = getPos(mt, op, u"pos1", u"relativePos1", refSeq, client);
       int b = getPos(mt, op, u"pos2", u"relativePos2", refSeq, client);
       const JVal* props = obj_get(op.obj, u"props");
-      const JVal* comb = obj_get(op.obj, u"combiningOp");
-      bool rewrite = false;
-      if (comb && comb->t == JVal::Obj) {
-        const JVal* name = obj_get(comb->obj, u"name");
-        if (name && name->t == JVal::Str && name->str == u"rewrite") rewrite = true;
-        else fail_unsupported("combiningOp other than rewrite");
-      }
+      const Comb comb = parse_comb(obj_get(op.obj, u"combiningOp"));
       JObj p;
       if (props && props->t == JVal::Obj) p = props->obj;
-      mt.annotateRange(a, b, p, rewrite, refSeq, client, seq);
+      mt.annotateRange(a, b, p, comb, refSeq, client, seq);
       break;
     }
     case 3: {  // GROUP (client.ts:816-824)
@@ -1528,7 +1561,9 @@ void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::ve
       const JVal* p = propsOf(r.props);
       static const JObj empty;
       const JObj& o = (p && p->t == JVal::Obj) ? p->obj : empty;
-      mt.annotateRange((int)r.pos1, (int)r.pos2, o, (r.flags & 0x04) != 0, (int)r.refSeq, r.client, (int)r.seq);
+      Comb comb;  // MTB_F_REWRITE 0x04, MTB_F_INCR 0x08 (annotate records)
+      comb.kind = (r.flags & 0x04) ? Comb::Rewrite : (r.flags & 0x08) ? Comb::Incr : Comb::None;
+      mt.annotateRange((int)r.pos1, (int)r.pos2, o, comb, (int)r.refSeq, r.client, (int)r.seq);
       break;
     }
     case 4:
@@ -1571,14 +1606,9 @@ std::string Doc::removeLocalOp(int start, int end) {
 }
 std::string Doc::annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp) {
   if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
-  bool rewrite = false;
-  if (combiningOp) {  // annotateRangeLocal(start, end, props, combiningOp): only "rewrite" is restated
-    const JVal* name = combiningOp->t == JVal::Obj ? obj_get(combiningOp->obj, u"name") : nullptr;
-    if (!(name && name->t == JVal::Str && name->str == u"rewrite")) fail_unsupported("combiningOp other than rewrite");
-    rewrite = true;
-  }
+  const Comb comb = parse_comb(combiningOp);  // annotateRangeLocal(start, end, props, combiningOp)
   validLocalRange(start, end, mt.length(), false);
-  mt.annotateRange(start, end, props, rewrite, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
+  mt.annotateRange(start, end, props, comb, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   JVal pv;
   pv.t = JVal::Obj;
   pv.obj = props;
@@ -1837,7 +1867,7 @@ void Doc::insertMarkerLocal(int pos, int refType, const std::optional<JObj>& pro
 }
 void Doc::annotateRangeLocal(int start, int end, const JObj& props) {
   if (mt.window.collaborating) fail_unsupported("local edits while collaborating");
-  mt.annotateRange(start, end, props, false, mt.window.currentSeq, mt.window.clientId, UniversalSeq);
+  mt.annotateRange(start, end, props, Comb(), mt.window.currentSeq, mt.window.clientId, UniversalSeq);
 }
 void Doc::removeRangeLocal(int start, int end) {
   if (mt.window.collaborating) fail_unsupported("local edits while collaborating");

@@ -33,6 +33,17 @@ constexpr int TextSegmentGranularity = 256;// MT/textSegment.ts:20
 constexpr int ZamboniSegmentsMax = 2;      // MT/zamboni.ts:14
 constexpr int UNDEF_LEN = -1;              // `undefined` result of nodeLength
 
+// ICombiningOp of an annotate (ops.ts): none, "rewrite" (segmentPropertiesManager.ts:109-123) or "incr"
+// (properties.ts:24-69: each key becomes combine(op, previousValue, undefined, seq), the previous value or
+// defaultValue plus undefined -- NaN for numbers, booleans, null and undefined; a string gets "undefined"
+// appended; then minValue when truthy and larger).  "consensus" and other names are not restated.
+struct Comb {
+  enum Kind { None, Rewrite, Incr } kind = None;
+  JVal defaultValue;  // Undef when absent
+  JVal minValue;
+};
+Comb parse_comb(const JVal* comb);  // (throws OracleError unsupported for other names)
+
 struct Block;
 
 struct Node {
@@ -182,7 +193,7 @@ class MergeTree {
   // reloadFromSegments (mergeTree.ts:678-721): bottom-up B-tree, MaxNodesInBlock - 1 children per block
   void reloadFromSegments(const std::vector<Seg*>& segs);
   void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq);
-  void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq);
+  void annotateRange(int start, int end, const JObj& props, const Comb& comb, int refSeq, int clientId, int seq);
   // pendingSegments (mergeTree.ts:532) and ackPendingSegment (:1283-1322) for one acked delta op
   // (type INSERT 0 / REMOVE 1 / ANNOTATE 2, its props for ANNOTATE)
   std::deque<std::unique_ptr<SegGroup>> groupPool;

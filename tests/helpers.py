@@ -187,7 +187,7 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
 
 
 def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
-                   record=None, reconnect=0.0, rewrite=0.0, marker_ids=0):
+                   record=None, reconnect=0.0, rewrite=0.0, marker_ids=0, incr=0.0):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
@@ -200,7 +200,9 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     With `marker_ids` > 0 clients also insert markers whose `markerId` comes from a pool of that many (ids are
     reused, so blockUpdate's re-mapping decides what an id names, mergeTree.ts:2392 -> :296-306) and send
     marker-relative inserts and annotateMarker ops (relativePos1 {id, before}, relativePos2 {id}) for ids
-    their own view resolves.  Returns (clients, observer, sequenced messages)."""
+    their own view resolves.  With `incr` > 0 that fraction of the local annotates are combiningOp "incr"
+    annotates (their numeric keys become NaN; a remote incr modifies pending keys too, shouldModifyKey).
+    Returns (clients, observer, sequenced messages)."""
     import random
     from pyoracle import OracleDoc, OracleError
     rng = random.Random(seed)
@@ -242,6 +244,8 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
         if not annotate or r < 0.8:
             return c.remove_local_op(a, b)
         props = {"k": rng.choice([1, 2, None]), "w": rng.randint(0, 1)}
+        if incr and rng.random() < incr:  # combiningOp incr: the numeric keys become NaN (properties.ts:24-69)
+            return c.local_op_json({"combiningOp": {"name": "incr"}, "pos1": a, "pos2": b, "props": props, "type": 2})
         if rewrite and rng.random() < rewrite:
             return c.local_op_json({"combiningOp": {"name": "rewrite"}, "pos1": a, "pos2": b, "props": props, "type": 2})
         return c.annotate_local_op(a, b, props)
@@ -601,6 +605,64 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
                 op = {"type": 0, "pos1": 0, "seg": "seed"}
         msn = min(ref)
         m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": msn,
+             "type": "op", "contents": op}
+        gen.apply_msg(m)
+        msgs.append(m)
+    gen.close()
+    return initial, msgs
+
+
+def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello incr world", p_incr=0.15):
+    """A sequenced op log whose annotates are partly combiningOp "incr" annotates (segmentPropertiesManager.ts:
+    145-147 -> combine(op, previous, undefined) of properties.ts:24-69): numeric keys "n" / "m" (incr makes
+    them NaN, JSON null, never matchProperties-equal), a string key "s" that incr never names, null deletes,
+    some incr ops with a numeric defaultValue / minValue; inserts with props, removes.  Every message is
+    applied to a generator oracle as it is made.  Returns (initial text, messages)."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed)
+    ids = [f"client-{k}" for k in range(n_clients)]
+    gen = OracleDoc(new_length_calc=new_mode)
+    if initial:
+        gen.insert_text_local(0, initial)
+    gen.start_collab("gen-observer")
+    short = {}
+    for cid in ids:
+        gen.add_client(cid)
+        short[cid] = len(short) + 1
+    ref = [0] * n_clients
+    msgs = []
+    words = ["ab", "c", "xyz", "\n", "more text "]
+    for seq in range(1, n_msgs + 1):
+        k = rng.randrange(n_clients)
+        ref[k] = max(ref[k], seq - 1 - rng.randint(0, lag))
+        R, C, cid = ref[k], short[ids[k]], ids[k]
+        n = gen.remote_length(R, C)
+        x = rng.random()
+        if x < 0.4 or n == 0:
+            seg = rng.choice(words)
+            if rng.random() < 0.3:
+                seg = {"text": seg, "props": {"n": rng.randint(0, 2)} if rng.random() < 0.7 else {"s": "v"}}
+            op = {"type": 0, "pos1": rng.randint(0, n), "seg": seg}
+        else:
+            a = rng.randrange(n)
+            b = min(n, a + rng.randint(1, 6))
+            if x < 0.6:
+                op = {"type": 1, "pos1": a, "pos2": b}
+            elif x < 0.6 + p_incr:
+                comb = {"name": "incr"}
+                r = rng.random()
+                if r < 0.2:
+                    comb["defaultValue"] = rng.randint(0, 3)
+                elif r < 0.3:
+                    comb["minValue"] = 1
+                op = {"type": 2, "pos1": a, "pos2": b, "props": {rng.choice(["n", "m"]): rng.randint(1, 3)},
+                      "combiningOp": comb}
+            else:
+                props = rng.choice([{"n": rng.randint(0, 2)}, {"m": rng.randint(0, 2), "s": "w"}, {"n": None},
+                                    {"s": rng.choice(["a", "b"])}, {"m": None, "n": 1}])
+                op = {"type": 2, "pos1": a, "pos2": b, "props": props}
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": min(ref),
              "type": "op", "contents": op}
         gen.apply_msg(m)
         msgs.append(m)

@@ -1,0 +1,86 @@
+"""GPU parity of combiningOp "incr" annotates (segmentPropertiesManager.ts:145-147, properties.ts:24-69;
+CPU known answers in tests/test_incr.py): the engine turns the named numeric keys into its NaN value, whose
+property sets never match (MTB_PNAN handles), against the oracle's JS-semantics restatement.
+
+Bar: bit-exact against the oracle (canonical dump, text, state digest, SnapshotV1) on
+* generated logs (helpers.make_incr_log): remote incr annotates with and without defaultValue / minValue,
+  plain annotates / null deletes of the same keys, inserts with props, removes; both length modes, two
+  flushes, zamboni coalescing around NaN sets;
+* live-client farms (helpers.run_local_farm(incr=...)) with local incr annotates, acks and reconnects (a
+  remote incr also modifies pending local keys, shouldModifyKey);
+* an incr over a string value (JS string concatenation): the engine fails that document loudly
+  (MTB_E_UNSUPPORTED), the other documents of the batch replay.
+"""
+import pytest
+
+from helpers import first_diff, make_incr_log, run_local_farm
+from test_reference_kats import msg
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(B, i, o, what):
+    gd, od = B.dump_segments(i), o.dump_segments()
+    assert gd == od, f"{what}: segment dump differs: {first_diff(gd, od)}"
+    assert B.text(i) == o.get_text(), f"{what}: text differs"
+    assert B.digests(i, 1)[0] == o.digest(), f"{what}: digest differs"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_incr_logs(new_mode):
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    logs = [make_incr_log(500 + s, 1200, n_clients=3 + s % 4, lag=4 + 6 * s, new_mode=new_mode) for s in range(10)]
+    B = MergeTreeBatch(len(logs), new_length_calc=new_mode)
+    orc = []
+    for i, (init, _) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("obs")
+        orc.append(o)
+    for part in (slice(0, 600), slice(600, None)):
+        for i, (_, msgs) in enumerate(logs):
+            for m in msgs[part]:
+                B[i].applyMsg(m)
+                orc[i].apply_msg(m)
+        st = B.replay()
+        assert st["errors"] == 0, st
+        for i, o in enumerate(orc):
+            _same(B, i, o, f"log {i} {part}")
+    for i, o in enumerate(orc):
+        gb, gs = B.summarize_v1(i)
+        assert [list(x) for x in gb] == o.summarize_v1()["blobs"], f"log {i}: SnapshotV1 differs"
+        assert gs == o.summarize_v1()["summary"]
+
+
+@pytest.mark.parametrize("seed", list(range(400, 412)))
+def test_local_incr_farm(seed):
+    from test_gpu_local import _replay_record
+    rec = {}
+    run_local_farm(seed, n_clients=3 + seed % 3, n_rounds=40, new_mode=seed % 2 == 0, annotate=True, record=rec,
+                   incr=0.4, reconnect=0.3 if seed % 3 == 0 else 0.0)
+    assert _replay_record(rec, seed, seed % 2 == 0, 1, "hello world") > 0
+
+
+def test_incr_over_a_string_fails_its_document_only():
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from pyoracle import OracleDoc
+    B = MergeTreeBatch(2)
+    msgs = [msg("a", 1, 0, {"type": 2, "pos1": 0, "pos2": 2, "props": {"s": "abc", "n": 2}})]
+    bad = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"s": 1}, "combiningOp": {"name": "incr"}})]
+    good = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"n": 1}, "combiningOp": {"name": "incr"}})]
+    for i, ms in enumerate((bad, good)):
+        B[i].insertTextLocal(0, "hello")
+        B[i].startOrUpdateCollaboration("obs")
+        for m in ms:
+            B[i].applyMsg(m)
+    with pytest.raises(MergeTreeError, match="incr"):
+        B.replay()
+    o = OracleDoc()
+    o.insert_text_local(0, "hello")
+    o.start_collab("obs")
+    for m in good:
+        o.apply_msg(m)
+    _same(B, 1, o, "good document")
