@@ -38,6 +38,28 @@ def _check(L, h, rc):
         raise MergeTreeError(rc, msg)
 
 
+def catch_up_ops(blobs):
+    """SnapshotLoader.loadBodyAndCatchupOps (snapshotLoader.ts:60-86): the one blob beyond the summary's ordered
+    chunks holds the catch-up messages ([] when there is none).  A legacy header (no "version") lists "header",
+    and "body" when chunkLengthChars < totalLengthChars (buildHeaderMetadataForLegacyChunk,
+    snapshotChunks.ts:178-199)."""
+    paths = [p for p, _ in blobs]
+    hdr = json.loads(dict(blobs)["header"])
+    if hdr.get("version") is None and "headerMetadata" not in hdr:
+        ids = ["header"] + (["body"] if hdr.get("chunkLengthChars", 0) < hdr.get("totalLengthChars", 0) else [])
+    else:
+        ids = [c["id"] for c in hdr["headerMetadata"]["orderedChunkMetadata"]]
+    if len(paths) == len(ids) + 1:
+        rest = [c for p, c in blobs if p not in ids]
+        if len(rest) != 1:
+            raise MergeTreeError(-4, "0x060 There should be only one blob with catch up ops")
+        c = rest[0]
+        return json.loads(c if isinstance(c, str) else bytes(c).decode("utf-8"))
+    if len(paths) != len(ids):
+        raise MergeTreeError(-1, "Unexpected blobs in snapshot")
+    return []
+
+
 class MergeTreeBatch:
     """A batch of independent merge-tree documents replayed together on one MI355X, or spread over several
     (`devices`: documents by hash, each device replaying its share at the same time)."""
@@ -366,15 +388,37 @@ class Client:
         self._b._dirty = True
 
     def load(self, storage, clientId=None):
-        """Client.load (client.ts:1007) from a SnapshotV1 summary.  `storage` maps blob path -> content (a
-        dict, or [(path, content), ...]); `clientId` is the runtime's client id (the reference falls back
-        to "snapshot", snapshotLoader.ts:154).  The body is appended by the next replay."""
+        """Client.load (client.ts:1007) from a SnapshotV1 or SnapshotLegacy summary.  `storage` maps blob path
+        -> content (a dict, or [(path, content), ...]); `clientId` is the runtime's client id (the reference
+        falls back to "snapshot", snapshotLoader.ts:154).  The body is appended by the next replay.  Returns
+        {"catchupOps": [...]}: the summary's catch-up messages (snapshotLoader.ts:60-86), which
+        SharedSegmentSequence applies next (load_sequence)."""
         if self.longClientId is not None or self._detached:
             raise MergeTreeError(-1, "document already initialised")
         blobs = list(storage.items()) if isinstance(storage, dict) else list(storage)
         longId = clientId if clientId is not None else "snapshot"
         self._b.load_v1(self._doc, blobs, longId)
         self.longClientId = longId
+        return {"catchupOps": catch_up_ops(blobs)}
+
+    def loadSequence(self, storage, clientId=None):
+        """SharedSegmentSequence.loadCore (sequence.ts:568-610): Client.load, then every catch-up message
+        checked against the collab window (above minSeq and currentSeq, else "Invalid catchup operations in
+        snapshot") and applied.  Returns the catch-up messages."""
+        msgs = self.load(storage, clientId)["catchupOps"]
+        if msgs:
+            cw = self.getCollabWindow()
+            cur = cw["currentSeq"]
+            for m in msgs:
+                if (m["minimumSequenceNumber"] < cw["minSeq"] or m["referenceSequenceNumber"] < cw["minSeq"] or
+                        m["sequenceNumber"] <= cw["minSeq"] or m["sequenceNumber"] <= cur):
+                    raise MergeTreeError(-1, "Invalid catchup operations in snapshot: " + json.dumps(
+                        {"op": {"seq": m["sequenceNumber"], "minSeq": m["minimumSequenceNumber"],
+                                "refSeq": m["referenceSequenceNumber"]},
+                         "collabWindow": {"seq": cur, "minSeq": cw["minSeq"]}}))
+                self.applyMsg(m)
+                cur = m["sequenceNumber"]
+        return msgs
 
     def applyMsg(self, msg, local=False):
         """client.ts:858-887.  A message from this client's own id (`local`) acks its oldest pending op."""

@@ -926,8 +926,61 @@ void resolve_load_props(mtb_dev* b, HostDoc& d) {
       if ((f.f[F_ID][k] & MTB_LEAF) && f.f[F_PROPS][k]) f.f[F_PROPS][k] = MTB_GPROPS | b->in.pidx[2 * f.f[F_PROPS][k] + 1];
 }
 
-// Client.load of one SnapshotV1 summary into the fresh document d (client.ts:1007 -> SnapshotLoader,
-// snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in parallel.
+// toLatestVersion (snapshotChunks.ts:151-175): a SnapshotLegacy chunk (no "version"; MergeTreeChunkLegacy)
+// read as the V1 chunk the loader expects -- segments = segmentTexts, segmentCount = chunkSegmentCount -- and a
+// legacy header's metadata from buildHeaderMetadataForLegacyChunk (:178-199): [header] + [body] when
+// chunkLengthChars < totalLengthChars, minSequenceNumber = chunkMinSequenceNumber (absent in SnapshotLegacy's
+// output: the loader then takes sequenceNumber), sequenceNumber = chunkSequenceNumber.
+hj::Value to_latest_version(const std::string& path, hj::Value chunk) {
+  if (chunk.kind != hj::Value::kObj) raise(MTB_E_PARSE, "summary chunk is not an object");
+  const hj::Value* ver = member(chunk, u"version");
+  if (ver && ver->kind == hj::Value::kStr && ver->s == u"1") return chunk;
+  if (ver && ver->kind != hj::Value::kUndef) raise(MTB_E_PARSE, "Unsupported chunk path: " + path);
+  hj::Value v;
+  v.kind = hj::Value::kObj;
+  auto put = [&](hj::Value& o, const char16_t* k, const hj::Value* x) {
+    if (x) o.members.push_back({k, *x});
+  };
+  hj::Value one;
+  one.kind = hj::Value::kStr;
+  one.s = u"1";
+  v.members.push_back({u"version", one});
+  put(v, u"segmentCount", member(chunk, u"chunkSegmentCount"));
+  if (path == "header") {
+    if (const hj::Value* hm = member(chunk, u"headerMetadata")) {
+      put(v, u"headerMetadata", hm);
+    } else {
+      hj::Value md, ids;
+      md.kind = hj::Value::kObj;
+      ids.kind = hj::Value::kArr;
+      auto idv = [](const char16_t* id) {
+        hj::Value o, sv;
+        o.kind = hj::Value::kObj;
+        sv.kind = hj::Value::kStr;
+        sv.s = id;
+        o.members.push_back({u"id", sv});
+        return o;
+      };
+      ids.items.push_back(idv(u"header"));
+      const hj::Value* cl = member(chunk, u"chunkLengthChars");
+      const hj::Value* tl = member(chunk, u"totalLengthChars");
+      if (cl && tl && cl->kind == hj::Value::kNum && tl->kind == hj::Value::kNum && cl->n < tl->n)
+        ids.items.push_back(idv(u"body"));
+      md.members.push_back({u"orderedChunkMetadata", ids});
+      put(md, u"minSequenceNumber", member(chunk, u"chunkMinSequenceNumber"));
+      put(md, u"sequenceNumber", member(chunk, u"chunkSequenceNumber"));
+      put(md, u"totalSegmentCount", member(chunk, u"totalSegmentCount"));
+      v.members.push_back({u"headerMetadata", md});
+    }
+  }
+  put(v, u"segments", member(chunk, u"segmentTexts"));
+  return v;
+}
+
+// Client.load of one SnapshotV1 (or SnapshotLegacy) summary into the fresh document d (client.ts:1007 ->
+// SnapshotLoader, snapshotLoader.ts:41-257).  `mu` guards the batch's props table when documents load in
+// parallel.  The catch-up messages blob of a legacy summary is the caller's (SharedSegmentSequence.loadCore
+// applies it, sequence.ts:568-610).
 void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, const char* observer_long_id,
               PropsCache* pc, const std::string& prefix = std::string()) {
   if (b->matrix && !d.perm) raise(MTB_E_ARG, "matrix batch: use mtb_matrix_load");
@@ -943,7 +996,7 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
     raise(MTB_E_ARG, "summary blob not found: " + prefix + path);
   };
   // loadHeader (snapshotLoader.ts:133-167)
-  const hj::Value header = blob("header");
+  const hj::Value header = to_latest_version("header", blob("header"));
   const hj::Value* hsegs = member(header, u"segments");
   const hj::Value* md = member(header, u"headerMetadata");
   if (!hsegs || hsegs->kind != hj::Value::kArr || !md || md->kind != hj::Value::kObj)
@@ -968,11 +1021,16 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
   // loadBody (snapshotLoader.ts:169-220): chunks 1.. of orderedChunkMetadata, appended at the end
   std::vector<LoadSeg> body;
   const hj::Value* ocm = member(*md, u"orderedChunkMetadata");
-  if (ocm && ocm->kind == hj::Value::kArr)
+  // (chunk1.segmentCount === headerMetadata.totalSegmentCount: nothing more to load, snapshotLoader.ts:180)
+  const hj::Value* hsc = member(header, u"segmentCount");
+  const hj::Value* tsc = member(*md, u"totalSegmentCount");
+  const bool complete = hsc && tsc && hsc->kind == hj::Value::kNum && tsc->kind == hj::Value::kNum && hsc->n == tsc->n;
+  if (ocm && ocm->kind == hj::Value::kArr && !complete)
     for (size_t ci = 1; ci < ocm->items.size(); ci++) {
       const hj::Value* id = member(ocm->items[ci], u"id");
       if (!id || id->kind != hj::Value::kStr) raise(MTB_E_PARSE, "chunk metadata without an id");
-      const hj::Value chunk = blob(hj::to_utf8(id->s.data(), id->s.size()));
+      const std::string path = hj::to_utf8(id->s.data(), id->s.size());
+      const hj::Value chunk = to_latest_version(path, blob(path));
       const hj::Value* cs = member(chunk, u"segments");
       if (cs && cs->kind == hj::Value::kArr)
         for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload, pc));

@@ -280,14 +280,54 @@ class Client {
     const text = (x) => (typeof x === "string" ? x : Buffer.from(x instanceof ArrayBuffer ? new Uint8Array(x) : x).toString("utf8"));
     const header = text(await storage.readBlob("header"));
     const blobs = [["header", header]];
-    const md = JSON.parse(header).headerMetadata;
-    const ids = md && Array.isArray(md.orderedChunkMetadata) ? md.orderedChunkMetadata.slice(1).map((c) => c.id) : [];
-    for (const id of ids) blobs.push([id, text(await storage.readBlob(id))]);
+    const h = JSON.parse(header);
+    // toLatestVersion (snapshotChunks.ts:151-199): a legacy header (no "version") lists "body" when
+    // chunkLengthChars < totalLengthChars
+    const md = h.headerMetadata;
+    const ids = md && Array.isArray(md.orderedChunkMetadata) ? md.orderedChunkMetadata.map((c) => c.id)
+      : ["header"].concat(h.version === undefined && h.chunkLengthChars < h.totalLengthChars ? ["body"] : []);
+    for (const id of ids.slice(1)) blobs.push([id, text(await storage.readBlob(id))]);
     const longId = runtime && runtime.clientId !== undefined ? runtime.clientId : "snapshot";
     native.loadV1(this.batch.handle, this.doc, blobs, longId);
     this.longClientId = longId;
     this.batch.dirty = true;
-    return { catchupOpsP: Promise.resolve([]) };
+    // loadBodyAndCatchupOps (snapshotLoader.ts:60-86): the one blob beyond the ordered chunks
+    let catchup = [];
+    if (typeof storage.list === "function") {
+      const all = await storage.list("");
+      if (all.length === ids.length + 1) {
+        const rest = all.filter((p) => !ids.includes(p));
+        if (rest.length !== 1) throw new Error("0x060 There should be only one blob with catch up ops");
+        catchup = JSON.parse(text(await storage.readBlob(rest[0])));
+      } else if (all.length !== ids.length) {
+        throw new Error("Unexpected blobs in snapshot");
+      }
+    }
+    return { catchupOpsP: Promise.resolve(catchup) };
+  }
+
+  /**
+   * SharedSegmentSequence.loadCore (sequence.ts:568-610): Client.load, then each catch-up message checked
+   * against the collab window and applied.  Resolves to the catch-up messages.
+   */
+  async loadSequence(runtime, storage) {
+    const { catchupOpsP } = await this.load(runtime, storage);
+    const msgs = await catchupOpsP;
+    if (msgs.length) {
+      const cw = this.getCollabWindow();
+      let cur = cw.currentSeq;
+      for (const m of msgs) {
+        if (m.minimumSequenceNumber < cw.minSeq || m.referenceSequenceNumber < cw.minSeq ||
+            m.sequenceNumber <= cw.minSeq || m.sequenceNumber <= cur) {
+          throw new Error(`Invalid catchup operations in snapshot: ${JSON.stringify({
+            op: { seq: m.sequenceNumber, minSeq: m.minimumSequenceNumber, refSeq: m.referenceSequenceNumber },
+            collabWindow: { seq: cur, minSeq: cw.minSeq } })}`);
+        }
+        this.applyMsg(m);
+        cur = m.sequenceNumber;
+      }
+    }
+    return msgs;
   }
 
   // ---- op application ---------------------------------------------------------------------------

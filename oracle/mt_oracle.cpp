@@ -2266,6 +2266,85 @@ uint64_t Doc::digest() {
 }
 
 // Client.load -> SnapshotLoader (snapshotLoader.ts:41-257) for SnapshotV1 chunks.
+// toLatestVersion (snapshotChunks.ts:151-175): a legacy chunk (no "version", SnapshotLegacy's MergeTreeChunkLegacy)
+// becomes the V1 shape the loader reads -- segments = segmentTexts, segmentCount = chunkSegmentCount, length =
+// chunkLengthChars -- and a legacy header gets buildHeaderMetadataForLegacyChunk's metadata (:178-199): its own
+// headerMetadata if present, else [header] + [body] when chunkLengthChars < totalLengthChars, minSequenceNumber
+// = chunkMinSequenceNumber (absent in SnapshotLegacy's output), sequenceNumber = chunkSequenceNumber.
+static JVal to_latest_version(const std::string& path, const JVal& chunk) {
+  if (chunk.t != JVal::Obj) throw OracleError(-8, "chunk is not an object");
+  const JVal* ver = obj_get(chunk.obj, u"version");
+  if (ver && ver->t == JVal::Str && ver->str == u"1") return chunk;
+  if (ver && ver->t != JVal::Undef) throw OracleError(-8, "Unsupported chunk path: " + path);
+  JVal v;
+  v.t = JVal::Obj;
+  auto put = [&](const char16_t* k, const JVal* x) {
+    if (x) v.obj.push_back({k, *x});
+  };
+  v.obj.push_back({u"version", JVal::string(u"1")});
+  put(u"length", obj_get(chunk.obj, u"chunkLengthChars"));
+  put(u"segmentCount", obj_get(chunk.obj, u"chunkSegmentCount"));
+  if (path == "header") {
+    if (const JVal* hm = obj_get(chunk.obj, u"headerMetadata")) {
+      put(u"headerMetadata", hm);
+    } else {
+      JVal md;
+      md.t = JVal::Obj;
+      JVal ids;
+      ids.t = JVal::Arr;
+      JVal h;
+      h.t = JVal::Obj;
+      h.obj.push_back({u"id", JVal::string(u"header")});
+      ids.arr.push_back(h);
+      const JVal* cl = obj_get(chunk.obj, u"chunkLengthChars");
+      const JVal* tl = obj_get(chunk.obj, u"totalLengthChars");
+      if (cl && tl && cl->t == JVal::Num && tl->t == JVal::Num && cl->num < tl->num) {
+        JVal bd;
+        bd.t = JVal::Obj;
+        bd.obj.push_back({u"id", JVal::string(u"body")});
+        ids.arr.push_back(bd);
+      }
+      md.obj.push_back({u"orderedChunkMetadata", ids});
+      if (const JVal* m = obj_get(chunk.obj, u"chunkMinSequenceNumber")) md.obj.push_back({u"minSequenceNumber", *m});
+      if (const JVal* q = obj_get(chunk.obj, u"chunkSequenceNumber")) md.obj.push_back({u"sequenceNumber", *q});
+      if (tl) md.obj.push_back({u"totalLength", *tl});
+      if (const JVal* ts = obj_get(chunk.obj, u"totalSegmentCount")) md.obj.push_back({u"totalSegmentCount", *ts});
+      v.obj.push_back({u"headerMetadata", md});
+    }
+  }
+  put(u"segments", obj_get(chunk.obj, u"segmentTexts"));
+  put(u"startIndex", obj_get(chunk.obj, u"chunkStartSegmentIndex"));
+  return v;
+}
+
+std::string Doc::catchUpOps(const std::vector<std::pair<std::string, std::string>>& blobs) {
+  // SnapshotLoader.loadBodyAndCatchupOps (snapshotLoader.ts:60-86): one blob beyond the ordered chunks holds
+  // the catch-up messages (any name: mergeTree options.catchUpBlobName ?? "catchupOps")
+  const JVal header = to_latest_version("header", json_parse(blobs.empty() ? std::string("{}") : [&]() {
+    for (auto& b : blobs)
+      if (b.first == "header") return b.second;
+    throw OracleError(-1, "missing blob header");
+  }()));
+  const JVal* md = obj_get(header.obj, u"headerMetadata");
+  const JVal* ocm = md ? obj_get(md->obj, u"orderedChunkMetadata") : nullptr;
+  const size_t n = ocm && ocm->t == JVal::Arr ? ocm->arr.size() : 1;
+  if (blobs.size() == n + 1) {
+    std::vector<std::string> rest;
+    for (auto& b : blobs) {
+      bool listed = false;
+      for (size_t i = 0; i < n && ocm; i++) {
+        const JVal* id = obj_get(ocm->arr[i].obj, u"id");
+        if (id && id->t == JVal::Str && u16_to_utf8(id->str) == b.first) listed = true;
+      }
+      if (!listed) rest.push_back(b.second);
+    }
+    if (rest.size() != 1) throw OracleError(-4, "0x060 There should be only one blob with catch up ops");
+    return rest[0];
+  }
+  if (blobs.size() != n) throw OracleError(-8, "Unexpected blobs in snapshot");
+  return "[]";
+}
+
 void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId) {
   auto findBlob = [&](const std::string& id) -> const std::string& {
     for (auto& b : blobs)
@@ -2302,8 +2381,7 @@ void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, 
     return s;
   };
   // loadHeader (snapshotLoader.ts:133-167)
-  const JVal header = json_parse(findBlob("header"));
-  if (header.t != JVal::Obj) throw OracleError(-8, "header chunk is not an object");
+  const JVal header = to_latest_version("header", json_parse(findBlob("header")));
   const JVal* hsegs = obj_get(header.obj, u"segments");
   const JVal* md = obj_get(header.obj, u"headerMetadata");
   if (!hsegs || hsegs->t != JVal::Arr || !md || md->t != JVal::Obj) throw OracleError(-8, "header metadata not available");
@@ -2316,10 +2394,13 @@ void Doc::loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, 
   // loadBody (snapshotLoader.ts:169-248)
   const JVal* ocm = obj_get(md->obj, u"orderedChunkMetadata");
   std::vector<Seg*> body;
-  if (ocm && ocm->t == JVal::Arr) {
+  // (chunk1.segmentCount === headerMetadata.totalSegmentCount: nothing more to load, snapshotLoader.ts:180)
+  const bool complete = num(obj_get(header.obj, u"segmentCount"), -1) == num(obj_get(md->obj, u"totalSegmentCount"), -2);
+  if (ocm && ocm->t == JVal::Arr && !complete) {
     for (size_t ci = 1; ci < ocm->arr.size(); ci++) {
       const JVal* id = obj_get(ocm->arr[ci].obj, u"id");
-      const JVal chunk = json_parse(findBlob(u16_to_utf8(id->str)));
+      const std::string path = u16_to_utf8(id->str);
+      const JVal chunk = to_latest_version(path, json_parse(findBlob(path)));
       const JVal* cs = obj_get(chunk.obj, u"segments");
       if (cs && cs->t == JVal::Arr)
         for (auto& sp : cs->arr) body.push_back(specToSegment(sp));

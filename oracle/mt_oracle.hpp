@@ -327,6 +327,8 @@ class Doc {
   // Client.load of a SnapshotV1 summary (snapshotLoader.ts:41-257): header -> reloadFromSegments ->
   // startOrUpdateCollaboration(observer, minSeq, seq) -> body chunks appended through insertSegments.
   void loadV1(const std::vector<std::pair<std::string, std::string>>& blobs, const std::string& observerId);
+  // the catch-up messages blob of a (legacy) summary's blob list, "[]" when there is none (snapshotLoader.ts:60-86)
+  static std::string catchUpOps(const std::vector<std::pair<std::string, std::string>>& blobs);
   // SnapshotV1 (snapshotV1.ts:46-312) -> (blob path, content) list + ISummaryTreeWithStats JSON
   std::vector<std::pair<std::string, std::string>> summarizeV1(std::string* summaryJson);
   // SnapshotLegacy (snapshotlegacy.ts:122-259): header / body chunks at the MSN, plus the catch-up

@@ -342,13 +342,15 @@ int orc_zamboni(orc_doc* d) {
 int orc_pack_parent_root(orc_doc* d) {
   return guard(d, [&] { d->doc.mt.packParentRoot(); });
 }
-// Client.load of a SnapshotV1 summary: blobs_json = [[path, content], ...] (as orc_summarize_v1 returns)
-int orc_load_v1(orc_doc* d, const char* blobs_json, size_t len, const char* observer_id) {
+// Client.load of a SnapshotV1 or SnapshotLegacy summary: blobs_json = [[path, content], ...] (as
+// orc_summarize_v1 / orc_summarize_legacy return); *out = the catch-up messages blob ("[]" when none)
+int orc_load_v1(orc_doc* d, const char* blobs_json, size_t len, const char* observer_id, char** out, size_t* out_len) {
   return guard(d, [&] {
     JVal v = json_parse(blobs_json, len);
     std::vector<std::pair<std::string, std::string>> blobs;
     for (auto& p : v.arr) blobs.push_back({u16_to_utf8(p.arr[0].str), u16_to_utf8(p.arr[1].str)});
     d->doc.loadV1(blobs, observer_id);
+    *out = dupstr(Doc::catchUpOps(blobs), out_len);
   });
 }
 

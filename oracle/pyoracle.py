@@ -55,7 +55,7 @@ def lib():
         L.orc_digest.argtypes = [vp]
         L.orc_zamboni.argtypes = [vp]
         L.orc_pack_parent_root.argtypes = [vp]
-        L.orc_load_v1.argtypes = [vp, cp, sz, cp]
+        L.orc_load_v1.argtypes = [vp, cp, sz, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_enable_catch_up.argtypes = [vp]
         L.orc_summarize_legacy.argtypes = [vp, i, i, cp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_matrix_create.restype = vp
@@ -325,9 +325,28 @@ class OracleDoc:
         return self._L.orc_digest(self._h)
 
     def load_v1(self, blobs, observer_id):
-        """Client.load of a SnapshotV1 summary given as [(path, content), ...] (snapshotLoader.ts:41)."""
+        """Client.load of a SnapshotV1 or SnapshotLegacy summary given as [(path, content), ...]
+        (snapshotLoader.ts:41; legacy chunks through toLatestVersion, snapshotChunks.ts:151-175).  Returns the
+        summary's catch-up messages (snapshotLoader.ts:60-86; [] when it has none)."""
         raw = json.dumps([list(b) for b in blobs]).encode()
-        self._chk(self._L.orc_load_v1(self._h, raw, len(raw), observer_id.encode()))
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_load_v1(self._h, raw, len(raw), observer_id.encode(), ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return json.loads(ctypes.string_at(p, n.value).decode("utf-8"))
+        finally:
+            self._L.orc_free(p)
+
+    load = load_v1
+
+    def apply_catch_up(self, msgs):
+        """SharedSegmentSequence.loadCore's catch-up loop (sequence.ts:576-600): each message must lie above the
+        collab window (else "Invalid catchup operations in snapshot"), then it is applied."""
+        for m in msgs:
+            if (m["minimumSequenceNumber"] < self.min_seq or m["referenceSequenceNumber"] < self.min_seq or
+                    m["sequenceNumber"] <= self.min_seq or m["sequenceNumber"] <= self.current_seq):
+                raise OracleError(-1, "Invalid catchup operations in snapshot")
+            self.apply_msg(m)
 
 
 def msg_from_compact(m):

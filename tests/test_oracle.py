@@ -10,7 +10,7 @@
 * known-answer tests restated from client.applyMsg.spec.ts on the observer path.
 """
 import pytest
-from pyoracle import OracleDoc
+from pyoracle import OracleDoc, OracleError
 
 from helpers import msg_from_compact, replay_fixtures, snapshot_fixture
 
@@ -224,6 +224,62 @@ def test_snapshot_legacy_fixture_bytes(name):
     expected = snapshot_fixture(name, "legacy")
     got = _build_detached(name).summarize_legacy(0, 0)
     assert [list(b) for b in got["blobs"]] == expected
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations",
+                                  "withIntervals"])
+def test_snapshot_legacy_fixture_loads_and_resummarizes(name):
+    """Client.load of the reference's snapshots/legacy files (legacy chunks through toLatestVersion,
+    snapshotChunks.ts:151-199; header, then the "body" chunk when chunkLengthChars < totalLengthChars,
+    snapshotLoader.ts:133-220): the generating recipe's text, and SnapshotLegacy of the loaded string gives the
+    fixture's bytes again."""
+    blobs = snapshot_fixture(name, "legacy")
+    o = OracleDoc()
+    assert o.load_v1(blobs, "loader") == []  # no catch-up blob
+    assert o.get_text() == _build_detached(name).get_text()
+    assert [list(b) for b in o.summarize_legacy(0, 0)["blobs"]] == blobs
+
+
+def _legacy_midstream(d, g, chunk=0):
+    """Replay groups [0, g) with catch-up tracking, then SnapshotLegacy at the MSN (with the catch-up blob)."""
+    o = OracleDoc(chunk_size=chunk)
+    o.insert_text_local(0, d["initialText"])
+    o.start_collab("A")
+    o.enable_catch_up()
+    for grp in d["groups"][:g]:
+        for m in grp["msgs"]:
+            o.apply_msg(msg_from_compact(m))
+    return o, o.summarize_legacy()["blobs"]
+
+
+@pytest.mark.parametrize("idx", [0, 5, 11, 17, 23, 29])
+@pytest.mark.parametrize("g", [16, 40])
+def test_legacy_load_with_catch_up_continues_the_reference_logs(idx, g):
+    """SharedSegmentSequence.loadCore over a SnapshotLegacy summary taken mid-log (sequence.ts:568-610): load
+    the MSN state, replay the catch-up blob with the collab-window validation (lagging messages were rewritten
+    to refSeq = seq - 1, sequence.ts:697-748), then the rest of the log: the golden text after every later
+    group, and a legacy summary of the loaded string at the end equal to the never-stopped one's text."""
+    name, d = FIXTURES[idx]
+    o, blobs = _legacy_midstream(d, g, chunk=300 if idx % 2 else 0)
+    r = OracleDoc(chunk_size=300 if idx % 2 else 0)
+    msgs = r.load_v1(blobs, "loader")
+    assert msgs and all(m["minimumSequenceNumber"] == r.min_seq for m in msgs)
+    r.apply_catch_up(msgs)
+    assert r.get_text() == o.get_text() and r.current_seq == o.current_seq
+    for grp in d["groups"][g:]:
+        for m in grp["msgs"]:
+            r.apply_msg(msg_from_compact(m))
+        assert r.get_text() == grp["resultText"], name
+
+
+def test_catch_up_validation_rejects_stale_messages():
+    """sequence.ts:580-596: a catch-up message at or below the loaded collab window throws."""
+    name, d = FIXTURES[3]
+    _, blobs = _legacy_midstream(d, 20)
+    r = OracleDoc()
+    msgs = r.load_v1(blobs, "loader")
+    with pytest.raises(OracleError, match="Invalid catchup"):
+        r.apply_catch_up([dict(msgs[0], sequenceNumber=r.current_seq)])
 
 
 @pytest.mark.parametrize("idx", [0, 3, 9, 17, 26])
