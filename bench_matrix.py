@@ -8,7 +8,12 @@ of mtb_matrix_kernel.  One step = rewind + replay of every matrix with records r
 
 value = sequenced messages applied per second (vector ops + setCells).  The roofline line is for
 mtb_matrix_kernel with the same algorithmic-bytes rule as bench.py (32 B per record + 24 B per segment
-record created or modified).  cpu_baseline: the C++ oracle replays a bounded sample on the host cores.
+record created or modified); `traffic` = FETCH_SIZE x 2 + WRITE_SIZE of one launch from two rocprofv3 --pmc
+child runs (as bench.py).  cpu_baseline: the C++ oracle replays a bounded sample on the host cores.
+
+parity (every matrix, one unique log each by default): both vectors' GPU state digests against the
+generator oracle's (Doc::digest), and the FNV-1a of every matrix's SharedMatrix summary blobs (rows / cols
+PermutationVector summaries, handle tables, cells) against the oracle's summary of the same log.
 """
 import argparse
 import json
@@ -23,10 +28,50 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBPS = 8000.0
 
 
+def _traffic(args):
+    """HBM bytes of one mtb_matrix_kernel launch: FETCH_SIZE (x2, the gfx950 correction) and WRITE_SIZE from
+    two separate rocprofv3 --pmc child runs of this benchmark (1 step), as bench.py measures the string kernel."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, None
+    vals = {}
+    with tempfile.TemporaryDirectory(prefix="mtb_pmc_") as td:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(td, counter.lower())
+            cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", counter.lower(), "--",
+                   sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-parity", "--traffic", "off", "--steps",
+                   "1", "--warmup", "0", "--matrices", str(args.matrices), "--replicas", str(args.replicas), "--msgs",
+                   str(args.msgs), "--clients", str(args.clients), "--lag", str(args.lag), "--pct-set",
+                   str(args.pct_set), "--seed", str(args.seed)]
+            try:
+                subprocess.run(cmd, env=dict(os.environ, MTB_IN_PMC="1"), stdout=subprocess.DEVNULL, timeout=900,
+                               check=True)
+            except Exception:
+                return None, None
+            per = {}
+            for root, _, files in os.walk(out):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        for r in csv.DictReader(open(os.path.join(root, f))):
+                            if "mtb_matrix_kernel" in r["Kernel_Name"]:
+                                per[int(r["Dispatch_Id"])] = per.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+            if not per:
+                return None, None
+            vals[counter] = per[max(per)]
+    fetch_b, write_b = 2.0 * vals["FETCH_SIZE"] * 1024.0, vals["WRITE_SIZE"] * 1024.0
+    return round(fetch_b + write_b), {"fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"],
+                                      "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
+                                      "note": "last mtb_matrix_kernel launch; FETCH_SIZE doubled per the gfx950 correction"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--matrices", type=int, default=10000)
-    ap.add_argument("--replicas", type=int, default=10)
+    ap.add_argument("--replicas", type=int, default=1)
     ap.add_argument("--msgs", type=int, default=5000)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--lag", type=int, default=64)
@@ -36,6 +81,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=400)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20260303)
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--traffic", choices=["auto", "off"], default="auto")
     args = ap.parse_args()
 
     from fluidframework_amd import MatrixBatch
@@ -78,11 +125,15 @@ def main():
         kms.append(last["kernel_ms"])
     el = sum(times) / len(times)
     km = sum(kms) / len(kms)
-    bad = 0
-    sample = list(range(0, args.matrices, max(1, args.matrices // 32)))[:32]
-    for j in sample:
-        u = j // reps
-        bad += sum(B.checksum(2 * j + v) != lb.mats[u].checksum[v] for v in (0, 1))
+    bad_dig = bad_sum = 0
+    t_par = time.time()
+    if not args.no_parity:
+        dig = B.digests()
+        for j in range(args.matrices):
+            u = j // reps
+            bad_dig += (dig[2 * j] != lb.mats[u].digest[0]) or (dig[2 * j + 1] != lb.mats[u].digest[1])
+            bad_sum += B.matrix_summary_fnv(j) != lb.mats[u].summary_fnv
+    t_par = time.time() - t_par
     msgs = sum(lb.mats[j // reps].n_msgs for j in range(args.matrices))
     sets = sum(lb.mats[j // reps].n_sets for j in range(args.matrices))
     records = sum(lb.mats[j // reps].n_ops[v] for j in range(args.matrices) for v in (0, 1))
@@ -96,6 +147,9 @@ def main():
         cpu = {"value": round(cm / secs, 1), "unit": "msgs/s", "cores": thr, "kind": "port",
                "sample": f"{k} matrices x {args.msgs} msgs ({cm} msgs) of the same logs, C++ oracle (oracle/), "
                          f"{thr} threads, {secs:.2f}s, {cbad} mismatches"}
+    traffic, traffic_info = None, None
+    if args.traffic == "auto" and os.environ.get("MTB_IN_PMC") != "1":
+        traffic, traffic_info = _traffic(args)
     out = {
         "metric": "SharedMatrix sequenced messages applied/sec (rows+cols PermutationVectors + setCell handles)",
         "value": round(msgs / el, 1),
@@ -113,10 +167,15 @@ def main():
                                f"{args.msgs} msgs, {args.pct_set}% setCell, row/col counts 1..8, lag {args.lag}",
                    "msgs_per_step": msgs, "setcells_per_step": sets, "records_per_step": records},
         "roofline": {"bound": "hbm", "achieved": round(alg / (km * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBPS, 6), "traffic": None,
+                     "unit": "GB/s", "frac": round(alg / (km * 1e-3) / 1e9 / HBM_PEAK_GBPS, 6), "traffic": traffic,
                      "kernel": "mtb_matrix_kernel", "kernel_ms": round(km, 3), "alg_bytes_per_launch": alg},
         "cpu_baseline": cpu,
-        "parity": {"sampled_vectors": 2 * len(sample), "mismatches": bad},
+        "parity": None if args.no_parity else {
+            "matrices": args.matrices, "digest_mismatches": bad_dig, "summary_mismatches": bad_sum,
+            "seconds": round(t_par, 2),
+            "what": "every matrix: both vectors' GPU state digests vs the oracle's, and the FNV-1a of its SharedMatrix "
+                    "summary blobs (rows / cols / handle tables / cells) vs the oracle's summary of the same log"},
+        "traffic_pmc": traffic_info,
         "timing": {"generate_s": round(t_gen, 2), "load_and_first_replay_s": round(t_load, 2)},
     }
     print(json.dumps(out), flush=True)

@@ -619,6 +619,19 @@ class MatrixBatch(MergeTreeBatch):
         self._chk(self._L.mtb_matrix_summarize(self._h, m, ctypes.byref(lst)))
         return _blob_list(self._L, lst)
 
+    def matrix_summary_fnv(self, m):
+        """FNV-1a 64 of matrix m's SharedMatrix summary (mtb_blob_list_fnv: blob paths, contents, the
+        ISummaryTreeWithStats JSON) without copying it out (parity checks at scale)."""
+        self._ensure_flushed()
+        lst = _lib.MtbBlobList()
+        self._chk(self._L.mtb_matrix_summarize(self._h, m, ctypes.byref(lst)))
+        h = ctypes.c_uint64()
+        try:
+            self._chk(self._L.mtb_blob_list_fnv(ctypes.byref(lst), ctypes.byref(h)))
+        finally:
+            self._L.mtb_blob_list_free(ctypes.byref(lst))
+        return h.value
+
     def get_cell(self, m, row, col):
         """SharedMatrix.getCell (matrix.ts:173): the value's JSON text, or None when undefined."""
         self._ensure_flushed()

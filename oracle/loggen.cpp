@@ -65,6 +65,9 @@ struct loggen_matrix {
   uint32_t n_short[2];
   uint64_t checksum[2];            // oracle's final canonical dump checksums
   int32_t error;
+  uint64_t digest[2];              // oracle's final state digests v1 of the two vectors (Doc::digest)
+  uint64_t summary_fnv;            // FNV-1a 64 of SharedMatrix.summarizeCore (each blob's path, 0, content, 0; then
+                                   // the ISummaryTreeWithStats JSON): the engine's mtb_blob_list_fnv definition
 };
 
 // Per-document output.  All arrays are malloc'd; free with loggen_free.
@@ -412,6 +415,28 @@ static int gen_matrix_one(const loggen_cfg& cfg, uint32_t index, loggen_matrix* 
   }
   out->checksum[0] = fnv1a64(rowsDoc.dumpSegments());
   out->checksum[1] = fnv1a64(colsDoc.dumpSegments());
+  out->digest[0] = rowsDoc.digest();
+  out->digest[1] = colsDoc.digest();
+  {
+    std::string summary;
+    uint64_t h = 1469598103934665603ull;
+    auto add = [&](const std::string& x) {
+      for (unsigned char c : x) {
+        h ^= c;
+        h *= 1099511628211ull;
+      }
+      h *= 1099511628211ull;  // (a 0 byte)
+    };
+    for (auto& bl : mat.summarize(&summary)) {
+      add(bl.first);
+      add(bl.second);
+    }
+    for (unsigned char c : summary) {
+      h ^= c;
+      h *= 1099511628211ull;
+    }
+    out->summary_fnv = h;
+  }
   return 0;
 }
 

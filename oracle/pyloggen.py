@@ -30,7 +30,8 @@ class LoggenDoc(ctypes.Structure):
 class LoggenMatrix(ctypes.Structure):
     _fields_ = [("ops", ctypes.c_void_p * 2), ("n_ops", ctypes.c_uint32 * 2), ("n_msgs", ctypes.c_uint32),
                 ("n_sets", ctypes.c_uint32), ("client_writer", (ctypes.c_uint16 * 256) * 2),
-                ("n_short", ctypes.c_uint32 * 2), ("checksum", ctypes.c_uint64 * 2), ("error", ctypes.c_int32)]
+                ("n_short", ctypes.c_uint32 * 2), ("checksum", ctypes.c_uint64 * 2), ("error", ctypes.c_int32),
+                ("digest", ctypes.c_uint64 * 2), ("summary_fnv", ctypes.c_uint64)]
 
 
 def _lib():

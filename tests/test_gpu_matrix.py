@@ -215,3 +215,26 @@ def test_reference_conflict_kats_gpu(new_mode):
         if expected is not None:
             assert gg == expected, f"matrix.spec.ts:{line} {name!r}"
         _check(B, i, o, name)
+
+
+def test_matrix_bench_parity_definition():
+    """bench_matrix.py's total parity on a small batch: every vector's GPU state digest equals the generator
+    oracle's Doc::digest and every matrix's summary fingerprint (mtb_blob_list_fnv of
+    SharedMatrix.summarizeCore) equals the oracle's (oracle/loggen.cpp summary_fnv)."""
+    from fluidframework_amd import MatrixBatch
+    from pyloggen import MatrixLogBatch, make_cfg
+    cfg = make_cfg(seed=77, n_clients=6, n_ops=1500, lag=32, pct_set=40)
+    lb = MatrixLogBatch(cfg, 0, 24)
+    B = MatrixBatch(lb.n)
+    for j in range(lb.n):
+        B.init_matrix(j, "obs")
+        for v in (0, 1):
+            for cid in lb.client_ids(j, v)[1:]:
+                B.add_client(2 * j + v, cid)
+            B.append_records(2 * j + v, lb.ops_bytes(j, v), lb.mats[j].n_ops[v], b"")
+    st = B.replay()
+    assert st["errors"] == 0
+    dig = B.digests()
+    for j in range(lb.n):
+        assert (dig[2 * j], dig[2 * j + 1]) == (lb.mats[j].digest[0], lb.mats[j].digest[1]), j
+        assert B.matrix_summary_fnv(j) == lb.mats[j].summary_fnv, j
