@@ -60,6 +60,19 @@ def catch_up_ops(blobs):
     return []
 
 
+def _loaded_window(blobs):
+    """The collab window Client.load starts (snapshotLoader.ts:150-165): minSeq = the header's
+    minSequenceNumber ?? sequenceNumber, currentSeq = sequenceNumber (a legacy header: chunkMinSequenceNumber /
+    chunkSequenceNumber, snapshotChunks.ts:178-199)."""
+    hdr = json.loads(dict(blobs)["header"])
+    md = hdr.get("headerMetadata")
+    if md is not None:
+        seq, mn = md.get("sequenceNumber", 0), md.get("minSequenceNumber")
+    else:
+        seq, mn = hdr.get("chunkSequenceNumber", 0), hdr.get("chunkMinSequenceNumber")
+    return {"minSeq": seq if mn is None else mn, "currentSeq": seq}
+
+
 class MergeTreeBatch:
     """A batch of independent merge-tree documents replayed together on one MI355X, or spread over several
     (`devices`: documents by hash, each device replaying its share at the same time)."""
@@ -399,15 +412,16 @@ class Client:
         longId = clientId if clientId is not None else "snapshot"
         self._b.load_v1(self._doc, blobs, longId)
         self.longClientId = longId
-        return {"catchupOps": catch_up_ops(blobs)}
+        return {"catchupOps": catch_up_ops(blobs), "collabWindow": _loaded_window(blobs)}
 
     def loadSequence(self, storage, clientId=None):
         """SharedSegmentSequence.loadCore (sequence.ts:568-610): Client.load, then every catch-up message
         checked against the collab window (above minSeq and currentSeq, else "Invalid catchup operations in
         snapshot") and applied.  Returns the catch-up messages."""
-        msgs = self.load(storage, clientId)["catchupOps"]
+        r = self.load(storage, clientId)
+        msgs = r["catchupOps"]
         if msgs:
-            cw = self.getCollabWindow()
+            cw = r["collabWindow"]  # (from the header: the batch need not replay before the other loads)
             cur = cw["currentSeq"]
             for m in msgs:
                 if (m["minimumSequenceNumber"] < cw["minSeq"] or m["referenceSequenceNumber"] < cw["minSeq"] or

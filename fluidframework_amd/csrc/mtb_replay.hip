@@ -877,6 +877,25 @@ struct Eng {
     uint32_t scli = 0, srcx = 0;
     if (kblk) {
       const uint32_t* c = bw(ck);
+#ifdef MTB_RB_LOADS
+      // the child's count, slot id and fields in one round trip (the record is always readable)
+      const int ccount = (int)c[FB_HDR];
+      const uint32_t sid = c[F_ID * 8 + s];
+      const int l0 = (int)c[F_LEN * 8 + s], q0 = (int)c[F_SEQ * 8 + s], r0 = (int)c[F_RSEQ * 8 + s];
+      const uint32_t c0 = c[F_CLI * 8 + s], x0 = c[F_RCX * 8 + s];
+      if (s < ccount && (sid & MTB_LEAF)) {
+        slen = l0;
+        sseq = q0;
+        srseq = r0;
+        scli = c0;
+        srcx = x0;
+        if (sseq > minSeq) ne++;
+        if (srseq >= 0 && srseq > minSeq) {
+          ne++;
+          if (srcx) nov = (int)aux[srcx];
+        }
+      }
+#else
       const int ccount = (int)c[FB_HDR];
       if (s < ccount) {
         const uint32_t sid = c[F_ID * 8 + s];
@@ -893,6 +912,7 @@ struct Eng {
           }
         }
       }
+#endif
     }
     // the block children's own lists (metadata in P's slots), concatenated
     uint32_t lc = 0, lo = 0;
@@ -918,6 +938,66 @@ struct Eng {
       for (int o = 32; o > 0; o >>= 1) novt += __shfl_xor(novt, o, 64);
     }
     const uint32_t total = (uint32_t)(nder + novt + ltotal);
+#ifdef MTB_RB_REGSORT
+    // Only derived entries (the children are leaf-level blocks, no overlapping removers): counting-sort them
+    // straight from registers into the final list (no unsorted copy to write, re-read and free).
+    if (ltotal == 0 && novt == 0 && total > MTB_SORT_MIN) {
+      const bool insv = ne >= 1 && sseq > minSeq, remv = srseq >= 0 && srseq > minSeq && ne >= 1;
+      const int bi = sseq - minSeq - 1, br = srseq - minSeq - 1;
+      const bool over = (insv && (bi < 0 || bi >= MTB_SORT_BUCKETS)) || (remv && (br < 0 || br >= MTB_SORT_BUCKETS));
+      if (!__ballot(over)) {
+        list_free(old_loff, old_lcap);
+        uint32_t* hist = &sh->hold[0][0];
+        for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
+        wsync();
+        if (insv) atomicAdd(&hist[bi >> 1], 1u << ((bi & 1) * 16));
+        if (remv) atomicAdd(&hist[br >> 1], 1u << ((br & 1) * 16));
+        wsync();
+        uint32_t wv[8];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          wv[q] = hist[8 * lane + q];
+          tot += (wv[q] & 0xFFFF) + (wv[q] >> 16);
+        }
+        int incl = (int)tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += t;
+        }
+        uint32_t run = (uint32_t)incl - tot;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t c0 = run;
+          run += wv[q] & 0xFFFF;
+          hist[8 * lane + q] = c0 | (run << 16);
+          run += wv[q] >> 16;
+        }
+        wsync();
+        uint32_t cap2;
+        const uint32_t no2 = list_alloc(total + total / 2 + 4, cap2);
+        if (bad()) return;
+        if (insv) {
+          const uint32_t sft = (uint32_t)(bi & 1) * 16;
+          const uint32_t old = atomicAdd(&hist[bi >> 1], 1u << sft);
+          u32x4 e = {(uint32_t)sseq, (uint32_t)WE_KEY(cli_client(scli), WK_MAIN, k), (uint32_t)slen, 0u};
+          lst4()[no2 + ((old >> sft) & 0xFFFF)] = e;
+        }
+        if (remv) {
+          const uint32_t sft = (uint32_t)(br & 1) * 16;
+          const uint32_t old = atomicAdd(&hist[br >> 1], 1u << sft);
+          u32x4 e = {(uint32_t)srseq, (uint32_t)WE_KEY(cli_rc0(scli), WK_MAIN, k), (uint32_t)(-slen), 0u};
+          lst4()[no2 + ((old >> sft) & 0xFFFF)] = e;
+        }
+        wsync();
+        loff_out = no2;
+        lcnt_out = total;
+        lcap_out = cap2;
+        return;
+      }
+    }
+#endif
     uint32_t cap;
     const uint32_t no = list_alloc(total + total / 2 + 4, cap);
     if (bad()) return;

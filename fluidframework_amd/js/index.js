@@ -291,6 +291,10 @@ class Client {
     native.loadV1(this.batch.handle, this.doc, blobs, longId);
     this.longClientId = longId;
     this.batch.dirty = true;
+    // the window startOrUpdateCollaboration opened (snapshotLoader.ts:150-165)
+    const seq = md ? md.sequenceNumber : h.chunkSequenceNumber;
+    const mn = md ? md.minSequenceNumber : h.chunkMinSequenceNumber;
+    this.loadedWindow = { minSeq: mn === undefined ? seq : mn, currentSeq: seq };
     // loadBodyAndCatchupOps (snapshotLoader.ts:60-86): the one blob beyond the ordered chunks
     let catchup = [];
     if (typeof storage.list === "function") {
@@ -314,7 +318,7 @@ class Client {
     const { catchupOpsP } = await this.load(runtime, storage);
     const msgs = await catchupOpsP;
     if (msgs.length) {
-      const cw = this.getCollabWindow();
+      const cw = this.loadedWindow;  // (from the header: no flush before the batch's other loads)
       let cur = cw.currentSeq;
       for (const m of msgs) {
         if (m.minimumSequenceNumber < cw.minSeq || m.referenceSequenceNumber < cw.minSeq ||
