@@ -858,15 +858,22 @@ struct Eng {
   // each block child k, the entries of k's own list plus entries derived from k's segment children
   // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
   // where P's metadata lives.
+  // zready: the caller already staged P's slots and count in sh->zr (from the LDS view or registers), which
+  // saves the dependent fetch of P's record
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out, bool zready = false) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
-    const uint32_t* src = bw(P);
-    const uint32_t w = src[lane];
-    const int count = U((int)src[FB_HDR]);
-    (&Z.f[0][0])[lane] = w;
-    wsync();
+    int count;
+    if (zready) {
+      count = U(Z.count);
+    } else {
+      const uint32_t* src = bw(P);
+      const uint32_t w = src[lane];
+      count = U((int)src[FB_HDR]);
+      (&Z.f[0][0])[lane] = w;
+      wsync();
+    }
     // lane (k, s): segment child s of block child k
     const int k = lane >> 3, s = lane & 7;
     uint32_t ck = MTB_NONE;
@@ -1305,9 +1312,19 @@ struct Eng {
         X = U(P.b);
         meta_of(L, ooff, ocnt, ocap);
         phase = 4;
+#ifdef MTB_RB_LDS
+        // P's record is the LDS view of depth L (insert_slot kept it in step with HBM)
+        (&sh->zr.f[0][0])[lane] = (&P.f[0][0])[lane];
+        if (lane == 0) sh->zr.count = P.count;
+        wsync();
+#endif
       }
       uint32_t a, c2, e;
+#ifdef MTB_RB_LDS
+      rebuild(X, ooff, ocap, a, c2, e, phase == 4);
+#else
       rebuild(X, ooff, ocap, a, c2, e);
+#endif
       if (err) break;
       if (phase == 2) {
         sp_loffL = a;
@@ -3087,15 +3104,43 @@ struct Eng {
       // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
       // site; rebuild uses the union as scratch)
       uint32_t a = 0, c2 = 0, e = 0;
+#ifdef MTB_RB_LDS
+      uint32_t za = 0, zc = 0, ze = 0;  // lane q: new block q's list metadata (P's slot q)
+#endif
       for (int q = 0; q <= cc; q++) {
         const bool isP = q == cc;
         const uint32_t nb = isP ? parent : rlu(nbs, q);
         a = c2 = e = 0;
+#ifdef MTB_RB_LDS
+        if (isP) {  // P's new slots, staged from registers (no dependent fetch of the record just written)
+          const int fld = lane >> 3, s = lane & 7;
+          // (lane-varying sources: ds_bpermute with every lane active)
+          const uint32_t x0 = (uint32_t)__shfl((int)nbs, s, 64), x1 = (uint32_t)__shfl(lens, s, 64);
+          const uint32_t x2 = (uint32_t)__shfl((int)za, s, 64), x3 = (uint32_t)__shfl((int)zc, s, 64);
+          const uint32_t x4 = (uint32_t)__shfl((int)ze, s, 64);
+          uint32_t v = fld == F_ID ? MTB_NONE : 0u;
+          if (s < cc) v = fld == F_ID ? x0 : fld == F_LEN ? x1 : fld == F_SEQ ? x2 : fld == F_RSEQ ? x3 : fld == F_CLI ? x4 : 0u;
+          (&sh->zr.f[0][0])[lane] = v;
+          if (lane == 0) sh->zr.count = cc;
+          wsync();
+        }
+#endif
         if (isP || rl(kbs, q)) {
+#ifdef MTB_RB_LDS
+          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e, isP);
+#else
           rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e);
+#endif
           if (bad()) return;
         }
         if (isP) break;
+#ifdef MTB_RB_LDS
+        if (lane == q) {
+          za = a;
+          zc = c2;
+          ze = e;
+        }
+#endif
         const int len = rl(lens, q);
         if (lane == 0) {
           FBlk& P = blk[parent];
