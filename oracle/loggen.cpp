@@ -347,6 +347,9 @@ static int gen_matrix_one(const loggen_cfg& cfg, uint32_t index, loggen_matrix* 
       const uint32_t r = refSeq[w], seq = cur + 1;
       uint32_t msn = UINT32_MAX;
       for (int k = 1; k <= K; k++) msn = std::min(msn, refSeq[k]);
+      // (the records' short ids follow the documents' own interning order, so state digests agree)
+      shortIn(0, w);
+      shortIn(1, w);
       const int rl = rowsDoc.mt.getLength((int)r, rowsDoc.getOrAddShortClientId(name));
       const int cl = colsDoc.mt.getLength((int)r, colsDoc.getOrAddShortClientId(name));
       JVal contents;
