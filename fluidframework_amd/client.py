@@ -634,15 +634,18 @@ class MatrixBatch(MergeTreeBatch):
         return _blob_list(self._L, lst)
 
     def matrix_summary_fnv(self, m):
-        """FNV-1a 64 of matrix m's SharedMatrix summary (mtb_blob_list_fnv: blob paths, contents, the
-        ISummaryTreeWithStats JSON) without copying it out (parity checks at scale)."""
+        """FNV-1a 64 of matrix m's SharedMatrix summary blobs (mtb_blob_list_fnv over the blob paths and
+        contents; the ISummaryTreeWithStats JSON left out) without copying them out (parity checks at scale)."""
         self._ensure_flushed()
         lst = _lib.MtbBlobList()
         self._chk(self._L.mtb_matrix_summarize(self._h, m, ctypes.byref(lst)))
         h = ctypes.c_uint64()
+        js = lst.summary_json
         try:
+            lst.summary_json = None
             self._chk(self._L.mtb_blob_list_fnv(ctypes.byref(lst), ctypes.byref(h)))
         finally:
+            lst.summary_json = js
             self._L.mtb_blob_list_free(ctypes.byref(lst))
         return h.value
 

@@ -66,8 +66,9 @@ struct loggen_matrix {
   uint64_t checksum[2];            // oracle's final canonical dump checksums
   int32_t error;
   uint64_t digest[2];              // oracle's final state digests v1 of the two vectors (Doc::digest)
-  uint64_t summary_fnv;            // FNV-1a 64 of SharedMatrix.summarizeCore (each blob's path, 0, content, 0; then
-                                   // the ISummaryTreeWithStats JSON): the engine's mtb_blob_list_fnv definition
+  uint64_t summary_fnv;            // FNV-1a 64 of SharedMatrix.summarizeCore's blobs (each blob's path, 0, content,
+                                   // 0): mtb_blob_list_fnv without the ISummaryTreeWithStats JSON (whose stats the
+                                   // GPU tests compare as parsed objects)
 };
 
 // Per-document output.  All arrays are malloc'd; free with loggen_free.
@@ -433,10 +434,6 @@ static int gen_matrix_one(const loggen_cfg& cfg, uint32_t index, loggen_matrix* 
     for (auto& bl : mat.summarize(&summary)) {
       add(bl.first);
       add(bl.second);
-    }
-    for (unsigned char c : summary) {
-      h ^= c;
-      h *= 1099511628211ull;
     }
     out->summary_fnv = h;
   }

@@ -7,8 +7,6 @@ mkdir -p $O
 export TMPDIR=/tmp MTB_LOG_CACHE=/tmp/mtb_logs MTB_NO_TORCH=1
 (while sleep 50; do echo "hb $(date +%T)" >> $O/heartbeat; done) & HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 B="bench.py --no-cpu --no-summary --steps 1 --warmup 0 --parity-sample 4 --traffic off"
 for v in check profpack prof; do
   MTB_LIB=fluidframework_amd/libmtb_$v.so MTB_PROFILE_OUT=1 MTB_CHECK_OUT=1 timeout -k 10 600 python3 $B > $O/bench_$v.json 2> $O/bench_$v.err
@@ -22,5 +20,7 @@ for rep in 1 2; do
     [ $rc -ne 0 ] && exit $rc
   done
 done
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python3 bench_matrix.py > $O/matrix.json 2> $O/matrix.err
 rc=$?; echo "matrix rc=$rc"; cut -c1-600 $O/matrix.json; exit $rc
