@@ -25,6 +25,7 @@
 #define MTB_PNAN 0x40000000u    // props handle flag of a per-doc set holding NaN (an incr annotate): such a set
                                 // matches no set, itself included (matchProperties: NaN !== NaN)
 #define MTB_NOKEY ((int32_t)0x80000000)
+#define MTB_DELTA_OLD 0x80000000u  // catch-up delta entry tag: a rewrite annotate's property set before the op
 // Window lists are allocated in power-of-two capacities (8 << class) from the document's list slice;
 // released lists go to a per-class free stack whose heads live in the slice's first 16 words.
 #define MTB_LCLASSES 16

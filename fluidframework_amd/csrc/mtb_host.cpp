@@ -1796,7 +1796,10 @@ void replay(mtb_dev* b, mtb_stats* out) {
         cap = s.seg_cap + 4ull * b->docs[i].pending.size() + 1;
       } else if (!s.err) {
         for (const mtb_op& o : b->docs[i].pending) {
-          if (o.flags & MTB_F_DELTA) cap += o.type == MTB_OP_INSERT ? 1 : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1;
+          if (o.flags & MTB_F_DELTA)  // (a rewrite annotate's segments get a second entry: the set before)
+            cap += o.type == MTB_OP_INSERT ? 1
+                   : ((o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1) *
+                         (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_REWRITE) ? 2 : 1);
           if (o.type == MTB_OP_REGEN) cap += (uint64_t)o.pos1 * (s.seg_used + 16);  // one entry per regenerated op
         }
       }
@@ -2548,13 +2551,8 @@ void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
       cm.count = (uint32_t)recs.size();
       if ((int64_t)base.ref_seq != (int64_t)base.seq - 1) {
         cm.resolved = false;
-        for (mtb_op& r : recs) {
-          if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE))
-            raise(MTB_E_UNSUPPORTED, "unsupported: catch-up rewriting of a lagging rewrite annotate");
-          if (r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_INCR))
-            raise(MTB_E_UNSUPPORTED, "unsupported: catch-up rewriting of a lagging incr annotate");
+        for (mtb_op& r : recs)
           if (r.type == MTB_OP_INSERT || r.type == MTB_OP_REMOVE || r.type == MTB_OP_ANNOTATE) r.flags |= MTB_F_DELTA;
-        }
       }
       d.catchup.push_back(std::move(cm));
       if (d.catchup.size() > 20) {  // "Do GC every once in a while"
@@ -2678,7 +2676,7 @@ void resolve_catch_up(mtb_dev* b, uint32_t i) {
   HIPCHK(hipMemcpy(ent.data(), b->dDelta.p + 4 * s.delta_base, ent.size() * 4, hipMemcpyDeviceToHost));
   d.cached = false;
   download_doc(b, i);
-  std::unordered_map<uint32_t, std::vector<uint32_t>> byRec;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> byRec;  // (MTB_DELTA_OLD-tagged: a rewrite's sets before)
   for (uint32_t e = 0; e < s.delta_used; e++) byRec[ent[4 * e]].push_back(e);
   for (auto& m : d.catchup) {
     if (m.resolved) continue;
@@ -2687,9 +2685,17 @@ void resolve_catch_up(mtb_dev* b, uint32_t i) {
       const mtb_op& r = d.applied[k];
       auto it = byRec.find(k);
       if (it == byRec.end()) continue;  // no delta segments: no event
-      struct Ev { int pos1, pos2; std::string props; hj::Value pv; bool hasPos2; std::string json; };
+      struct Ev { int pos1, pos2; std::string props; hj::Value pv; bool hasPos2, nan; std::string json; };
       std::vector<Ev> ev;
-      for (uint32_t e : it->second) {
+      const bool rewrite = r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE);
+      const std::vector<uint32_t>* before = nullptr;  // a rewrite's entries with the sets before it, same order
+      if (rewrite) {
+        auto ot = byRec.find(k | MTB_DELTA_OLD);
+        if (ot == byRec.end() || ot->second.size() != it->second.size()) raise(MTB_E_ASSERT, "catch-up: rewrite delta entries unpaired");
+        before = &ot->second;
+      }
+      for (size_t ei = 0; ei < it->second.size(); ei++) {
+        const uint32_t e = it->second[ei];
         const int position = (int)ent[4 * e + 1];
         const int len = (int)ent[4 * e + 2];
         const uint32_t ph = ent[4 * e + 3];
@@ -2725,29 +2731,49 @@ void resolve_catch_up(mtb_dev* b, uint32_t i) {
             x.pos2 = position + len;
             ev.push_back(std::move(x));
           }
-        } else {  // ANNOTATE: props[key] = segment.properties?.[key] ?? null for the op's keys
+        } else {  // ANNOTATE: props[key] = segment.properties?.[key] ?? null over the propertyDeltas keys
+          // (segmentPropertiesManager.ts:107-154: a rewrite's keys are first the old keys it deleted -- those
+          // its props leave falsy -- in their order, then the op's keys; otherwise the op's keys)
           const uint32_t* opl = b->in.pool.data() + b->in.pidx[2 * r.props];
           const PropView sv = props_of(b, d, ph);
+          std::vector<uint32_t> keys;
+          if (rewrite) {
+            const PropView ov = props_of(b, d, ent[4 * (*before)[ei] + 3]);
+            for (uint32_t z = 0; z < ov.n(); z++) {
+              const uint32_t key = ov.p[1 + 2 * z];
+              bool truthy = false;
+              for (uint32_t q = 0; q < opl[0]; q++)
+                if (opl[1 + 2 * q] == key) truthy = opl[2 + 2 * q] != MTB_NONE && !(b->in.valFalsy[opl[2 + 2 * q]] & 1);
+              if (!truthy) keys.push_back(key);
+            }
+          }
+          for (uint32_t q = 0; q < opl[0]; q++)
+            if (std::find(keys.begin(), keys.end(), opl[1 + 2 * q]) == keys.end()) keys.push_back(opl[1 + 2 * q]);
           std::string pj = "{";
-          for (uint32_t q = 0; q < opl[0]; q++) {
-            const uint32_t key = opl[1 + 2 * q];
+          bool nan = false;  // an incr's NaN (JSON null): matchProperties never equal (NaN !== NaN)
+          for (size_t q = 0; q < keys.size(); q++) {
             if (q) pj += ',';
-            hj::quote(pj, b->in.keys[key]);
+            hj::quote(pj, b->in.keys[keys[q]]);
             pj += ':';
             std::string val = "null";
             for (uint32_t z = 0; z < sv.n(); z++)
-              if (sv.p[1 + 2 * z] == key) val = b->in.valJson[sv.p[2 + 2 * z]];
+              if (sv.p[1 + 2 * z] == keys[q]) {
+                val = b->in.valJson[sv.p[2 + 2 * z]];
+                nan |= sv.p[2 + 2 * z] == b->in.nanVal;
+              }
             pj += val;
           }
           pj += "}";
           hj::Value pv = hj::parse(pj.data(), pj.size());
-          if (!ev.empty() && ev.back().hasPos2 && ev.back().pos2 == position && js_match_props(&ev.back().pv, &pv)) {
+          if (!ev.empty() && ev.back().hasPos2 && ev.back().pos2 == position && !nan && !ev.back().nan &&
+              js_match_props(&ev.back().pv, &pv)) {
             ev.back().pos2 += len;
           } else {
             Ev x{};
             x.pos1 = position;
             x.pos2 = position + len;
             x.hasPos2 = true;
+            x.nan = nan;
             x.props = pj;
             x.pv = std::move(pv);
             ev.push_back(std::move(x));

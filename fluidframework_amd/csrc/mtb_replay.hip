@@ -2366,16 +2366,17 @@ struct Eng {
   // ------------------------------------------------------------------ catch-up deltas
   // SequenceDeltaEvent ranges (sequenceDelta.ts:43-56) for SharedSegmentSequence's rewriting of lagging
   // messages (sequence.ts:697-733): one entry per delta segment, in tree order: [record, segment id ->
-  // local position after the op, cachedLength, property set after the op].
+  // local position after the op, cachedLength, property set after the op]; a rewrite annotate's segments
+  // get a second entry each, tagged MTB_DELTA_OLD, holding the set before the op (its deleted keys).
   __device__ __forceinline__ gptr<uint32_t> dslice() const { return UP(sh->tab.delta) + ds->delta_base * 4; }
-  __device__ __forceinline__ void delta_emit(bool sel, uint32_t sid, uint32_t len, uint32_t props) {
+  __device__ __forceinline__ void delta_emit(bool sel, uint32_t sid, uint32_t len, uint32_t props, uint32_t tag = 0) {
     const unsigned long long m = __ballot(sel);
     if (!m) return;
     const uint32_t n = (uint32_t)__popcll(m);
     if (delta_used + n > U(sh->capv[6])) { fail(DERR_CAP_DELTA); return; }
     if (sel) {
       const auto e = dslice() + 4 * (delta_used + rank_below(m));
-      e[0] = cur_k;
+      e[0] = cur_k | tag;
       e[1] = sid;
       e[2] = len;
       e[3] = props;
@@ -2582,7 +2583,10 @@ struct Eng {
         am &= ~__ballot(mine);
         wsync();
       }
-      if (COLD(delta_on)) delta_emit(visit, id & ~MTB_LEAF, (uint32_t)len, lane < count ? V.f[F_PROPS][lane] : 0u);
+      if (COLD(delta_on)) {
+        delta_emit(visit, id & ~MTB_LEAF, (uint32_t)len, lane < count ? V.f[F_PROPS][lane] : 0u);
+        if (rewrite) delta_emit(visit, id & ~MTB_LEAF, (uint32_t)len, props, MTB_DELTA_OLD);
+      }
     }
     // addToLRUSet for the first visited segment (the block's needsScour then becomes true)
     const int t = first_set(vm);

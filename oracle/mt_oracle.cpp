@@ -985,10 +985,15 @@ static JVal combine_incr(const Comb& c, const JVal* prev) {
   }
   return cur;
 }
-static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq = UniversalSeq, bool collaborating = false) {
+// deltaKeys (when given) receives the keys of the returned propertyDeltas, in their insertion order
+static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq = UniversalSeq, bool collaborating = false,
+                       std::vector<u16str>* deltaKeys = nullptr) {
   s->hasPropManager = true;
   if (!s->props) s->props = JObj();
   if (collaborating && s->pendingRewrite > 0 && seq != UnassignedSeq && seq != UniversalSeq) return;
+  auto addDelta = [&](const u16str& k) {
+    if (deltaKeys && std::find(deltaKeys->begin(), deltaKeys->end(), k) == deltaKeys->end()) deltaKeys->push_back(k);
+  };
   JObj& old = *s->props;
   const bool rewrite = comb.kind == Comb::Rewrite, combining = comb.kind == Comb::Incr;
   auto shouldModify = [&](const u16str& k) {
@@ -1000,7 +1005,10 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
     for (auto& kv : old) keys.push_back(kv.first);
     for (auto& k : keys) {
       const JVal* nv = obj_get(newProps, k);
-      if (js_falsy(nv) && shouldModify(k)) obj_del(old, k);
+      if (js_falsy(nv) && shouldModify(k)) {
+        addDelta(k);
+        obj_del(old, k);
+      }
     }
   }
   for (auto& kv : newProps) {
@@ -1012,6 +1020,7 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
         continue;
       }
     }
+    addDelta(kv.first);
     if (combining) obj_set(old, kv.first, combine_incr(comb, obj_get(old, kv.first)));
     else if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
@@ -1020,7 +1029,6 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
 
 // annotateRange (mergeTree.ts:1895-1958)
 void MergeTree::annotateRange(int start, int end, const JObj& props, const Comb& comb, int refSeq, int clientId, int seq) {
-  const bool rewrite = comb.kind == Comb::Rewrite;
   ensureIntervalBoundary(start, refSeq, clientId);
   ensureIntervalBoundary(end, refSeq, clientId);
   std::vector<Seg*> annotated;
@@ -1036,11 +1044,13 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, const Comb&
     if (ta == JVal::Str) return a->str == b->str;
     return true;
   };
+  std::vector<std::vector<u16str>> deltaKeys;  // each annotated segment's propertyDeltas keys
   auto annotate = [&](Seg* s, int, int, int) -> bool {
     if (opId && s->isMarker && !same_id(opId, s->props ? obj_get(*s->props, u"markerId") : nullptr))
       fail_assert("0x5ad", "Cannot change the markerId of an existing marker");
     annotated.push_back(s);
-    applyProps(s, props, comb, seq, window.collaborating);
+    if (onDelta) deltaKeys.emplace_back();
+    applyProps(s, props, comb, seq, window.collaborating, onDelta ? &deltaKeys.back() : nullptr);
     counters.segsTouched += 1;
     if (window.collaborating) {
       if (seq == UnassignedSeq) group = addToPendingList(s, group, localSeq);
@@ -1051,9 +1061,7 @@ void MergeTree::annotateRange(int start, int end, const JObj& props, const Comb&
   auto post = [&](Block*) {};
   nodeMap(refSeq, clientId, annotate, post, start, end);
   if (onDelta && !annotated.empty()) {
-    if (rewrite) fail_unsupported("catch-up rewriting of a rewrite annotate");
-    if (comb.kind == Comb::Incr) fail_unsupported("catch-up rewriting of an incr annotate");
-    onDelta(2, annotated, &props);
+    onDelta(2, annotated, &deltaKeys);
   }
   if (window.collaborating && seq != UnassignedSeq) zamboniSegments();
 }
@@ -1406,17 +1414,19 @@ void Doc::applyMsg(const JVal& msg) {
       const bool transform = (int)rs->num != seqN - 1;
       std::vector<JVal> ops;
       if (transform)
-        mt.onDelta = [&](int op, const std::vector<Seg*>& segs, const JObj* props) {
+        mt.onDelta = [&](int op, const std::vector<Seg*>& segs, const std::vector<std::vector<u16str>>* keys) {
           std::vector<JVal> evOps;  // per event
           std::vector<std::pair<int, Seg*>> ranges;
           for (Seg* s : segs) ranges.push_back({mt.localPosition(s), s});
-          for (auto& [position, s] : ranges) {
-            if (op == 2) {
+          for (size_t ri = 0; ri < ranges.size(); ri++) {
+            const int position = ranges[ri].first;
+            Seg* s = ranges[ri].second;
+            if (op == 2) {  // props[key] = segment.properties?.[key] ?? null over the segment's delta keys
               JVal pv;
               pv.t = JVal::Obj;
-              for (auto& kv : *props) {
-                const JVal* cur = s->props ? obj_get(*s->props, kv.first) : nullptr;
-                pv.obj.push_back({kv.first, cur && cur->t != JVal::Undef ? *cur : JVal::null()});
+              for (auto& k : (*keys)[ri]) {
+                const JVal* cur = s->props ? obj_get(*s->props, k) : nullptr;
+                pv.obj.push_back({k, cur && cur->t != JVal::Undef ? *cur : JVal::null()});
               }
               JVal* last = evOps.empty() ? nullptr : &evOps.back();
               const JVal* lp2 = last ? obj_get(last->obj, u"pos2") : nullptr;

@@ -202,7 +202,7 @@ class MergeTree {
   void zamboniSegments();
   // mergeTreeDeltaCallback (INSERT 0 / REMOVE 1 / ANNOTATE 2 with the annotate's props), fired after the
   // op is applied and before its zamboni, only for non-empty delta segment lists
-  std::function<void(int, const std::vector<Seg*>&, const JObj*)> onDelta;
+  std::function<void(int, const std::vector<Seg*>&, const std::vector<std::vector<u16str>>*)> onDelta;  // annotates: each segment's propertyDeltas keys
   // MergeTreeMaintenanceType.UNLINK observer (zamboni.ts:139-148)
   std::function<void(Seg*)> onUnlink;
   // getContainingSegment (mergeTree.ts:787-813) and getPosition (:1240) for PermutationVector

@@ -612,12 +612,15 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
     return initial, msgs
 
 
-def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello incr world", p_incr=0.15):
+def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello incr world", p_incr=0.15,
+                  p_rewrite=0.0):
     """A sequenced op log whose annotates are partly combiningOp "incr" annotates (segmentPropertiesManager.ts:
     145-147 -> combine(op, previous, undefined) of properties.ts:24-69): numeric keys "n" / "m" (incr makes
     them NaN, JSON null, never matchProperties-equal), a string key "s" that incr never names, null deletes,
-    some incr ops with a numeric defaultValue / minValue; inserts with props, removes.  Every message is
-    applied to a generator oracle as it is made.  Returns (initial text, messages)."""
+    some incr ops with a numeric defaultValue / minValue; inserts with props, removes.  With `p_rewrite` that
+    fraction of the annotates are combiningOp "rewrite" annotates (falsy values -- 0, "", null -- delete or
+    re-append keys, :107-154).  Every message is applied to a generator oracle as it is made.  Returns
+    (initial text, messages)."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -649,7 +652,11 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
             b = min(n, a + rng.randint(1, 6))
             if x < 0.6:
                 op = {"type": 1, "pos1": a, "pos2": b}
-            elif x < 0.6 + p_incr:
+            elif x < 0.6 + p_rewrite:
+                props = rng.choice([{"n": 1}, {"s": "a", "m": 0}, {"m": None}, {"n": 0, "s": "b"}, {"s": ""},
+                                    {"m": 2, "n": 2}])
+                op = {"type": 2, "pos1": a, "pos2": b, "props": props, "combiningOp": {"name": "rewrite"}}
+            elif x < 0.6 + p_rewrite + p_incr:
                 comb = {"name": "incr"}
                 r = rng.random()
                 if r < 0.2:

@@ -205,3 +205,75 @@ def test_legacy_load_with_catch_up_continues_the_reference_logs(g, chunk):
         assert B.dump_segments(i) == loaded[i].dump_segments(), name
         gb, gs = B.summarize_legacy(i)
         assert [list(x) for x in gb] == loaded[i].summarize_legacy()["blobs"], name
+
+
+def test_catch_up_rewriting_kat_on_the_engine():
+    """The hand-derived catch-up known answer of tests/test_oracle.py::test_catch_up_rewriting_kat on the engine:
+    a lagging rewrite's ops name its deleted keys (old order) then its own (segmentPropertiesManager.ts:107-154,
+    kernel entries tagged MTB_DELTA_OLD carry the sets before it); a lagging incr's NaN values never coalesce."""
+    import json
+    from fluidframework_amd import MergeTreeBatch
+    B = MergeTreeBatch(1, catch_up=True)
+    B[0].insertTextLocal(0, "abcdef", {"s": "x", "m": 0})
+    B[0].startOrUpdateCollaboration("A")
+    msg = dict(type="op", minimumSequenceNumber=0, referenceSequenceNumber=0)
+    B[0].applyMsg(dict(msg, clientId="c1", sequenceNumber=1, contents={"type": 0, "pos1": 0, "seg": "zz"}))
+    B[0].applyMsg(dict(msg, clientId="c2", sequenceNumber=2, contents={
+        "type": 2, "pos1": 2, "pos2": 4, "props": {"n": 1, "m": 0}, "combiningOp": {"name": "rewrite"}}))
+    B[0].applyMsg(dict(msg, clientId="c3", sequenceNumber=3, contents={
+        "type": 2, "pos1": 0, "pos2": 4, "props": {"m": 1}, "combiningOp": {"name": "incr"}}))
+    B.flush()
+    gb, _ = B.summarize_legacy(0)
+    cu = json.loads(dict(gb)["catchupOps"])
+    assert [m["contents"] for m in cu] == [
+        {"type": 0, "pos1": 0, "seg": "zz"},
+        {"pos1": 4, "pos2": 6, "props": {"s": None, "m": 0, "n": 1}, "type": 2},
+        {"ops": [{"pos1": 2, "pos2": 4, "props": {"m": None}, "type": 2},
+                 {"pos1": 4, "pos2": 6, "props": {"m": None}, "type": 2}], "type": 3}]
+    assert list(cu[1]["contents"]["props"]) == ["s", "m", "n"]
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_catch_up_rewriting_of_rewrite_and_incr_annotates(new_mode):
+    """Lagging rewrite and incr annotates in the catch-up blob (createOpsFromDelta, sequence.ts:120-172): the
+    engine's legacy summary with catch-up equals the oracle's mid-log; loadSequence of it on the engine equals
+    the oracle that loaded the same blobs (dump), and both continue to the same text and dump."""
+    from fluidframework_amd import MergeTreeBatch
+    from helpers import make_incr_log
+    from pyoracle import OracleDoc
+    n, cut = 12, 450
+    logs = [make_incr_log(300 + i, 700, lag=24, new_mode=new_mode, p_incr=0.15 if i % 2 else 0.0, p_rewrite=0.2)
+            for i in range(n)]
+    B = MergeTreeBatch(n, new_length_calc=new_mode, catch_up=True)
+    oracles = []
+    for i, (init, msgs) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("A")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("A")
+        o.enable_catch_up()
+        for m in msgs[:cut]:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    L = MergeTreeBatch(n, new_length_calc=new_mode)
+    loaded = []
+    for i, o in enumerate(oracles):
+        gb, gs = B.summarize_legacy(i)
+        osum = o.summarize_legacy()
+        assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy + catch-up blobs differ"
+        r = OracleDoc(new_length_calc=new_mode)
+        r.apply_catch_up(r.load_v1(osum["blobs"], "loader"))
+        assert L[i].loadSequence(osum["blobs"], "loader")
+        loaded.append(r)
+    L.flush()
+    for i, r in enumerate(loaded):
+        assert L.dump_segments(i) == r.dump_segments(), f"doc {i}: dump after catch-up"
+        for m in logs[i][1][cut:]:
+            L[i].applyMsg(m)
+            r.apply_msg(m)
+    L.flush()
+    for i, r in enumerate(loaded):
+        assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"

@@ -311,6 +311,92 @@ def test_catch_up_messages_replay_to_the_final_text(idx):
     assert r.get_text() == d["groups"][-1]["resultText"], name
 
 
+def _catch_up_kat_doc():
+    """"abcdef" {s: "x", m: 0}; seq 1 inserts "zz" at 0; seq 2 (refSeq 0) rewrites [2, 4) of its view with
+    {n: 1, m: 0}; seq 3 (another client, refSeq 0) incrs m over [0, 4) of its view (two segments, "ab" and "cd")."""
+    o = OracleDoc()
+    o.insert_text_local(0, "abcdef")
+    o.annotate_local(0, 6, {"s": "x", "m": 0})
+    o.start_collab("A")
+    o.enable_catch_up()
+    msg = dict(type="op", minimumSequenceNumber=0, referenceSequenceNumber=0)
+    o.apply_msg(dict(msg, clientId="c1", sequenceNumber=1, contents={"type": 0, "pos1": 0, "seg": "zz"}))
+    o.apply_msg(dict(msg, clientId="c2", sequenceNumber=2, contents={
+        "type": 2, "pos1": 2, "pos2": 4, "props": {"n": 1, "m": 0}, "combiningOp": {"name": "rewrite"}}))
+    o.apply_msg(dict(msg, clientId="c3", sequenceNumber=3, contents={
+        "type": 2, "pos1": 0, "pos2": 4, "props": {"m": 1}, "combiningOp": {"name": "incr"}}))
+    return o
+
+
+def test_catch_up_rewriting_kat():
+    """Hand-derived known answer for createOpsFromDelta over propertyDeltas (segmentPropertiesManager.ts:107-154):
+    the lagging rewrite's props are its deleted keys in their old order (s: gone -> null; m: falsy in the
+    rewrite -> deleted, then re-set to 0) followed by its own key n; the lagging incr's NaN values (JSON null)
+    never matchProperties-equal, so its two adjacent segments stay two ops of a GROUP."""
+    import json
+    o = _catch_up_kat_doc()
+    cu = json.loads(dict(o.summarize_legacy()["blobs"])["catchupOps"])
+    assert [m["contents"] for m in cu] == [
+        {"type": 0, "pos1": 0, "seg": "zz"},
+        {"pos1": 4, "pos2": 6, "props": {"s": None, "m": 0, "n": 1}, "type": 2},
+        {"ops": [{"pos1": 2, "pos2": 4, "props": {"m": None}, "type": 2},
+                 {"pos1": 4, "pos2": 6, "props": {"m": None}, "type": 2}], "type": 3}]
+    assert [list(m["contents"].get("props", {})) for m in cu[1:2]] == [["s", "m", "n"]]
+    assert all(m["referenceSequenceNumber"] == m["sequenceNumber"] - 1 for m in cu[1:])
+
+
+def _char_props(o):
+    """Each visible character's property set (map_range segments), NaN/null-valued keys dropped."""
+    out = []
+    for r in o.map_range():
+        seg = r["segment"]
+        props = {k: v for k, v in (seg.get("properties") or {}).items() if v is not None}
+        out += [props] * seg["cachedLength"]
+    return out
+
+
+@pytest.mark.parametrize("seed,p_incr", [(1, 0.0), (2, 0.0), (3, 0.15), (4, 0.15)])
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_catch_up_rewriting_of_rewrite_and_incr_annotates(seed, p_incr, new_mode):
+    """createOpsFromDelta (sequence.ts:120-172) over a lagging rewrite annotate's propertyDeltas -- the keys it
+    deleted, in their old order, then its own (segmentPropertiesManager.ts:107-154) -- and over an incr's NaN
+    values (never matchProperties-equal, JSON null): a legacy summary taken mid-log with its catch-up blob,
+    loaded and caught up, equals the never-stopped document in text and, for rewrite-only logs, in every
+    character's properties; both then continue to the same text (and properties)."""
+    import json
+    from helpers import make_incr_log
+    init, msgs = make_incr_log(seed, 700, lag=24, new_mode=new_mode, p_incr=p_incr, p_rewrite=0.2)
+    cut = 450
+    src = OracleDoc(new_length_calc=new_mode)
+    src.insert_text_local(0, init)
+    src.start_collab("A")
+    src.enable_catch_up()
+    for m in msgs[:cut]:
+        src.apply_msg(m)
+    blobs = src.summarize_legacy()["blobs"]
+    msn = src.min_seq
+    lagging = [m for m in msgs[:cut] if m["sequenceNumber"] > msn and
+               m["referenceSequenceNumber"] != m["sequenceNumber"] - 1 and "combiningOp" in m["contents"]]
+    assert any(m["contents"]["combiningOp"]["name"] == "rewrite" for m in lagging)
+    if p_incr:
+        assert any(m["contents"]["combiningOp"]["name"] == "incr" for m in lagging)
+    cu = json.loads(dict(blobs)["catchupOps"])
+    assert all(m["referenceSequenceNumber"] == m["sequenceNumber"] - 1 for m in cu)
+    assert not any("combiningOp" in json.dumps(m["contents"]) for m in cu
+                   if m["sequenceNumber"] in {x["sequenceNumber"] for x in lagging})
+    r = OracleDoc(new_length_calc=new_mode)
+    r.apply_catch_up(r.load_v1(blobs, "loader"))
+    assert r.get_text() == src.get_text()
+    if not p_incr:
+        assert _char_props(r) == _char_props(src)
+    for m in msgs[cut:]:
+        src.apply_msg(m)
+        r.apply_msg(m)
+    assert r.get_text() == src.get_text()
+    if not p_incr:
+        assert _char_props(r) == _char_props(src)
+
+
 # ---------------------------------------------------------------- SharedMatrix cells (SparseArray2D)
 def _sa2d_fill(a, r0, c0, nr, nc):  # matrix/src/test/utils.ts fill: value = row * rowCount + col
     for r in range(r0, r0 + nr):
