@@ -1,0 +1,30 @@
+"""Build the engine's measurement variants in-tree (MTB_LIB=fluidframework_amd/libmtb_<name>.so selects one):
+
+  prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
+  profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
+  check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
+  rbl/rbd/rbr/rbx                            rebuild() variants for same-box A/B runs
+
+usage: python3 tools/build_variants.py [name ...]   (default: all)
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fluidframework_amd import build as b  # noqa: E402
+
+VARIANTS = {
+    "prof": ["MTB_PROFILE"],
+    "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
+    "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
+    "rbl": ["MTB_RB_LOADS"],
+    "rbd": ["MTB_RB_LOADS", "MTB_RB_LDS"],
+    "rbr": ["MTB_RB_LOADS", "MTB_RB_REGSORT"],
+    "rbx": ["MTB_RB_LOADS", "MTB_RB_LDS", "MTB_RB_REGSORT"],
+}
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    print(b.build())
+    for n in names:
+        print(b.build(out=os.path.join(b.HERE, f"libmtb_{n}.so"), defines=VARIANTS[n]))
