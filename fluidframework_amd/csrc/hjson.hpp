@@ -247,9 +247,14 @@ inline U16 from_utf8(const std::string& s) {
 // JSON.stringify string quoting (well-formed: lone surrogates escaped as \udXXX)
 inline void quote(std::string& o, const char16_t* s, size_t n) {
   static const char kHex[] = "0123456789abcdef";
+  o.reserve(o.size() + n + 2);
   o += '"';
   for (size_t i = 0; i < n; i++) {
     const uint32_t c = s[i];
+    if (c >= 0x20 && c < 0x80 && c != 0x22 && c != 0x5C) {  // (the common case first)
+      o.push_back((char)c);
+      continue;
+    }
     const char* esc = nullptr;
     switch (c) {
       case 0x22: esc = "\\\""; break;
@@ -279,6 +284,74 @@ inline void quote(std::string& o, const char16_t* s, size_t n) {
   o += '"';
 }
 inline void quote(std::string& o, const U16& s) { quote(o, s.data(), s.size()); }
+
+// Length of the well-formed UTF-8 sequence at p (1-4 bytes), or 0 for an invalid one or an encoded surrogate.
+inline size_t utf8_seq(const uint8_t* p, const uint8_t* e) {
+  const uint8_t c = *p;
+  if (c < 0x80) return 1;
+  size_t n;
+  uint32_t cp;
+  if (c >= 0xC2 && c <= 0xDF) { n = 1; cp = c & 0x1F; }
+  else if (c >= 0xE0 && c <= 0xEF) { n = 2; cp = c & 0x0F; }
+  else if (c >= 0xF0 && c <= 0xF4) { n = 3; cp = c & 0x07; }
+  else return 0;
+  if ((size_t)(e - p) <= n) return 0;
+  for (size_t k = 1; k <= n; k++) {
+    if ((p[k] & 0xC0) != 0x80) return 0;
+    cp = (cp << 6) | (p[k] & 0x3F);
+  }
+  if ((n == 2 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) || (n == 3 && (cp < 0x10000 || cp > 0x10FFFF))) return 0;
+  return n + 1;
+}
+// quote(o, from_utf8(u)) without the UTF-16 round trip, for u well-formed UTF-8 without encoded surrogates (what
+// these serializers produce): bytes pass through and only '"', '\\' and control characters are escaped, exactly
+// as quote() escapes the same code points.  Returns false, leaving o as it was, for any other u.
+inline bool quote_utf8(std::string& o, const std::string& u) {
+  static const char kHex[] = "0123456789abcdef";
+  const size_t base = o.size();
+  o.reserve(base + u.size() + u.size() / 8 + 2);
+  o += '"';
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(u.data());
+  const uint8_t* const e = p + u.size();
+  const uint8_t* run = p;
+  while (p < e) {
+    const uint8_t c = *p;
+    if (c >= 0x20 && c != 0x22 && c != 0x5C && c < 0x80) {
+      p++;
+      continue;
+    }
+    o.append(reinterpret_cast<const char*>(run), (size_t)(p - run));
+    if (c >= 0x80) {
+      const size_t n = utf8_seq(p, e);
+      if (!n) {
+        o.resize(base);
+        return false;
+      }
+      o.append(reinterpret_cast<const char*>(p), n);
+      p += n;
+    } else {
+      switch (c) {
+        case 0x22: o += "\\\""; break;
+        case 0x5C: o += "\\\\"; break;
+        case 0x08: o += "\\b"; break;
+        case 0x0C: o += "\\f"; break;
+        case 0x0A: o += "\\n"; break;
+        case 0x0D: o += "\\r"; break;
+        case 0x09: o += "\\t"; break;
+        default: o += "\\u00"; o += kHex[c >> 4]; o += kHex[c & 15]; break;
+      }
+      p++;
+    }
+    run = p;
+  }
+  o.append(reinterpret_cast<const char*>(run), (size_t)(p - run));
+  o += '"';
+  return true;
+}
+// quote(o, from_utf8(u)) by the fast path when it applies
+inline void quote_u8(std::string& o, const std::string& u) {
+  if (!quote_utf8(o, u)) quote(o, from_utf8(u));
+}
 
 // Number::toString(10) (ECMA-262 7.1.12.1) for finite doubles
 inline std::string number(double x) {

@@ -2079,7 +2079,7 @@ std::string dump_doc(mtb_dev* b, uint32_t i) {
     auto cl = [&](int c) {
       if (!d.perm) return std::to_string(c);
       std::string q;
-      hj::quote(q, hj::from_utf8(d.longId(c)));
+      hj::quote_u8(q, d.longId(c));
       return q;
     };
     o += ',' + std::to_string(seq_out(g.seq)) + ',' + cl(g.client) + ',' + std::to_string(seg_removed(g) ? seq_out(g.rseq) : -1) + ",[";
@@ -2108,6 +2108,13 @@ uint64_t fnv(const std::string& s) {
 
 // utf8ByteLength (runtime-utils summaryUtils.ts:56-71) evaluated on the JS string of `utf8`
 uint64_t utf8_byte_length(const std::string& utf8) {
+  {  // well-formed UTF-8 without encoded surrogates (the serializers' output): its own byte count
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(utf8.data());
+    const uint8_t* const e = p + utf8.size();
+    size_t n = 1;
+    while (p < e && (n = *p < 0x80 ? 1 : hj::utf8_seq(p, e)) != 0) p += n;
+    if (p == e) return utf8.size();
+  }
   U16 s = hj::from_utf8(utf8);
   int64_t n = (int64_t)s.size();
   for (int64_t k = (int64_t)s.size() - 1; k >= 0; k--) {
@@ -2231,17 +2238,17 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
     else o += json_of(is_marker(g), is_marker(g) ? (g.text & ~MTB_MARKER) : 0, is_marker(g) ? U16() : textOf(g), g.props);
     if (g.seq > minSeq) {
       o += ",\"seq\":" + std::to_string(g.seq) + ",\"client\":";
-      hj::quote(o, hj::from_utf8(d.longId(g.client)));
+      hj::quote_u8(o, d.longId(g.client));
     }
     if (seg_removed(g)) {
       if (seg_pending(g.rseq)) raise(MTB_E_ASSERT, "0x065 invalid removed seq");
       rc_list(d, g, rc);
       o += ",\"removedSeq\":" + std::to_string(g.rseq) + ",\"removedClient\":";
-      hj::quote(o, hj::from_utf8(d.longId(rc[0])));
+      hj::quote_u8(o, d.longId(rc[0]));
       o += ",\"removedClientIds\":[";
       for (size_t k = 0; k < rc.size(); k++) {
         if (k) o += ',';
-        hj::quote(o, hj::from_utf8(d.longId(rc[k])));
+        hj::quote_u8(o, d.longId(rc[k]));
       }
       o += "]";
     }
@@ -2257,7 +2264,7 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
     // PermutationVector.summarize (permutationvector.ts:310-325): {segments: <SnapshotV1>, handleTable}
     const std::string ht = handle_table_json(d);
     std::string outer = "{\"segments\":{\"type\":1,\"tree\":" + tree + "},\"handleTable\":{\"type\":2,\"content\":";
-    hj::quote(outer, hj::from_utf8(ht));
+    hj::quote_u8(outer, ht);
     outer += "}}";
     totalBytes += utf8_byte_length(ht);
     summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + outer + "},\"stats\":{\"treeNodeCount\":2,\"blobNodeCount\":" +
@@ -2292,8 +2299,12 @@ void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::s
     totalLength += c.length;
   } while (totalCount < (int)segJson.size());
   auto chunkText = [&](const Chunk& c, bool header) {
-    std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) + ",\"length\":" + std::to_string(c.length) +
-                    ",\"segments\":[";
+    size_t bytes = 256 + 24 * chunks.size();
+    for (int k = 0; k < c.count; k++) bytes += segJson[c.start + k].size() + 1;
+    std::string o;
+    o.reserve(bytes);
+    o += "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) + ",\"length\":" + std::to_string(c.length) +
+         ",\"segments\":[";
     for (int k = 0; k < c.count; k++) {
       if (k) o += ',';
       o += segJson[c.start + k];
@@ -2320,7 +2331,7 @@ void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::s
   for (size_t k = 0; k < blobs.size(); k++) {
     if (k) tree += ',';
     tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
-    hj::quote(tree, hj::from_utf8(blobs[k].second));
+    hj::quote_u8(tree, blobs[k].second);
     tree += "}";
     totalBytes += utf8_byte_length(blobs[k].second);
   }
@@ -2379,19 +2390,19 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
     o = "{\"json\":" + js;
     if (seq > minSeq) {
       o += ",\"seq\":" + std::to_string(seq) + ",\"client\":";
-      hj::quote(o, hj::from_utf8(d.longId((int)(int16_t)(cli & 0xFFFF))));
+      hj::quote_u8(o, d.longId((int)(int16_t)(cli & 0xFFFF)));
     }
     if (rseq >= 0) {
       const int rc0 = (int)(int16_t)(cli >> 16);
       o += ",\"removedSeq\":" + std::to_string(rseq) + ",\"removedClient\":";
-      hj::quote(o, hj::from_utf8(d.longId(rc0)));
+      hj::quote_u8(o, d.longId(rc0));
       o += ",\"removedClientIds\":[";
-      hj::quote(o, hj::from_utf8(d.longId(rc0)));
+      hj::quote_u8(o, d.longId(rc0));
       if (it[7] != MTB_NONE) {
         const uint32_t* rc = words + it[7];
         for (uint32_t q = 0; q < rc[0]; q++) {
           o += ',';
-          hj::quote(o, hj::from_utf8(d.longId((int)rc[1 + q])));
+          hj::quote_u8(o, d.longId((int)rc[1 + q]));
         }
       }
       o += "]";
@@ -2942,7 +2953,7 @@ void summarize_legacy(mtb_dev* b, uint32_t i, const std::string& catchUp, std::v
   for (size_t k = 0; k < blobs.size(); k++) {
     if (k) tree += ',';
     tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
-    hj::quote(tree, hj::from_utf8(blobs[k].second));
+    hj::quote_u8(tree, blobs[k].second);
     tree += "}";
     totalBytes += utf8_byte_length(blobs[k].second);
   }
@@ -3880,7 +3891,7 @@ int mtbx_matrix_summarize(mtb_dev* b, uint32_t matrix, mtb_blob_list* out) {
       tree += hj::dump(*member(sj, u"summary"));
     }
     tree += ",\"cells\":{\"type\":2,\"content\":";
-    hj::quote(tree, hj::from_utf8(cells));
+    hj::quote_u8(tree, cells);
     tree += "}}";
     const std::string summary = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":" +
                                 std::to_string(st[0]) + ",\"blobNodeCount\":" + std::to_string(st[1]) +
