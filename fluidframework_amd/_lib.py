@@ -30,11 +30,11 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
 
 class MtbLaunchInfo(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_uint32), ("wave_slots", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
-                ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("passes", ctypes.c_uint32)]
 
 
 KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 2: "mtb_replay_sched_kernel", 3: "mtb_replay_few_kernel",
-                4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel"}
+                4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel", 7: "mtb_replay_pass_kernel"}
 
 
 class MtbOptions(ctypes.Structure):

@@ -46,6 +46,9 @@ hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState*
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
                                    uint32_t nq, uint32_t spins);  // + mtb_replay_finish_kernel
+hipError_t mtb_launch_replay_passes(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                    uint32_t* freel, Tables tables, uint32_t first, uint32_t count, uint32_t nchunks);
 hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp,
                            FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                            Tables tables, int perm);
@@ -1615,8 +1618,9 @@ void launch_main(mtb_dev* b, const Tables& t) {
     bool markers = false;
     for (uint32_t i = 0; i < b->ndocs && !markers; i++)
       markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot;
-    // more documents than wave slots: the ticket-scheduled kernel (MTB_SCHED=0 turns it off, MTB_CHUNKS sets
-    // the tickets per document)
+    // more documents than wave slots: passes of equal chunks (mtb_replay_pass_kernel, the default), or the
+    // ticket-scheduled persistent kernel (MTB_SCHED=tickets; MTB_CHUNKS sets the tickets per document);
+    // MTB_SCHED=0 launches one wave per whole document
     if (!b->live && !markers && !b->waveSlots) {
       hipDeviceProp_t prop;
       HIPCHK(hipGetDeviceProperties(&prop, b->device));
@@ -1628,7 +1632,39 @@ void launch_main(mtb_dev* b, const Tables& t) {
     b->launch = mtb_launch_info{};
     b->launch.wave_slots = b->waveSlots;
     const char* sv = getenv("MTB_SCHED");
-    if (!b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0')) {
+    const bool many = !b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0');
+    if (many && !(sv && !strcmp(sv, "tickets"))) {
+      // Passes: the ndocs * m tasks (chunk c of document x, chunk-major) cut into launches of whole rounds
+      // of the resident slots, at most ndocs tasks each (a document's chunks land in successive launches).
+      // m (chunks per document, MTB_PASS_CHUNKS) leaves the smallest fraction of a round idle at the end.
+      const uint64_t S = b->waveSlots, D = b->ndocs;
+      uint32_t m = 0;
+      if (const char* cv = getenv("MTB_PASS_CHUNKS")) m = (uint32_t)std::max(1, std::min(64, atoi(cv)));
+      if (!m) {
+        double best = 1e30;
+        for (uint32_t k = 4; k <= 10; k++) {
+          const double rounds = (double)(k * D) / (double)S;
+          const double cost = std::ceil(rounds) / rounds + 0.004 * k;  // idle share of the last round + per-chunk setup
+          if (cost < best) {
+            best = cost;
+            m = k;
+          }
+        }
+      }
+      while (m > 1 && (uint64_t)m * D > 0x7FFFFFFFull) m--;
+      const uint64_t T = (uint64_t)m * D;
+      const uint64_t P = std::max<uint64_t>(1, D / S) * S;  // tasks per launch: whole rounds, <= ndocs
+      uint32_t passes = 0;
+      for (uint64_t first = 0; first < T; first += P, passes++)
+        HIPCHK(mtb_launch_replay_passes(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
+                                        b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, (uint32_t)first,
+                                        (uint32_t)std::min<uint64_t>(P, T - first), m));
+      b->launch.kernel = MTB_KERNEL_PASSES;
+      b->launch.chunks = m;
+      b->launch.passes = passes;
+      return;
+    }
+    if (many) {
       // the chunk plan: cumulative fractions (1/4096) of every document's records per ticket; MTB_CHUNKS=n
       // makes n equal chunks, MTB_CHUNK_PLAN="a,b,..." (relative chunk sizes) any other split.  Chunk c's
       // ticket comes ndocs tickets after chunk c-1's, so a chunk at most ~2x the next keeps waits rare.

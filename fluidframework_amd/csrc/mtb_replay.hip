@@ -4046,6 +4046,23 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   __shared__ Scratch sh;
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+// Batches with more documents than wave slots, as a sequence of launches ("passes"): the tasks (chunk c of
+// document x) are ordered chunk-major, task i = c * ndocs + x, and pass p runs tasks [first, first + grid): one
+// workgroup per task, which replays document x up to the fraction (c + 1) / nchunks of its records.  A pass
+// holds at most one chunk per document (grid <= ndocs) and a chunk's predecessor sits ndocs tasks earlier, in
+// an earlier pass, so the launch boundary orders them.  The host sizes passes as multiples of the resident
+// wave slots: every pass is whole rounds of equal tasks.
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_replay_pass_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                           WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
+                           uint32_t first, uint32_t nchunks) {
+  __shared__ Scratch sh;
+  const uint32_t t = first + blockIdx.x;
+  const uint32_t c = t / ndocs;
+  const uint32_t upto = c + 1 >= nchunks ? 0u : (uint32_t)(((c + 1) * 4096u) / nchunks);
+  replay_doc<MODE_REPLAY>(sh, t - c * ndocs, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
+                          upto);
+}
 // Batches with more documents than wave slots: persistent waves (one grid of the resident slots) take
 // tickets (chunk c, document d); ticket c replays document d's records up to the fraction plan[c] / 4096 of
 // them (the host's chunk plan).  Every document then advances at the same pace and the launch ends within
@@ -4229,6 +4246,12 @@ int mtb_sched_waves_per_cu() {
           hipSuccess || n <= 0)
     return 16;
   return n;
+}
+hipError_t mtb_launch_replay_passes(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                    uint32_t* freel, Tables tables, uint32_t first, uint32_t count, uint32_t nchunks) {
+  hipLaunchKernelGGL(mtb_replay_pass_kernel, dim3(count), dim3(64), 0, stream, KARGS, first, nchunks);
+  return hipGetLastError();
 }
 hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,

@@ -159,14 +159,58 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, qu
     per document (MTB_CHUNKS), per-XCD ticket queues and one global queue (MTB_SCHED_QUEUES=1), and with
     the ticket waits bounded so low that the scheduler aborts (MTB_SCHED_SPINS): the finish kernel then
     replays the rest of every document and the results are the same."""
-    import torch
-    from pyloggen import LogBatch, make_cfg
     monkeypatch.delenv("MTB_CHUNK_PLAN", raising=False)
+    monkeypatch.setenv("MTB_SCHED", "tickets")
     for var, val in (("MTB_CHUNKS", chunks), ("MTB_SCHED_QUEUES", queues), ("MTB_SCHED_SPINS", spins)):
         if val is None:
             monkeypatch.delenv(var, raising=False)
         else:
             monkeypatch.setenv(var, val)
+    B, want, slots = _ragged_batch()
+    st = B.replay()
+    assert st["errors"] == 0
+    li = B.launch_info()
+    assert li["kernel"] == "mtb_replay_sched_kernel" and li["wave_slots"] == slots, li
+    if spins == "0":
+        assert li["aborted"], li  # every hand-over wait gives up at once
+    dg = B.digests()
+    n = len(want)
+    bad = [j for j in range(n) if dg[j] != want[j]]
+    assert not bad, f"{len(bad)}/{n} documents' digests differ from the oracle (first: {bad[:5]})"
+
+
+@pytest.mark.parametrize("chunks", [None, "1", "3", "7"])
+def test_pass_replay_more_documents_than_wave_slots(monkeypatch, chunks):
+    """The default for more documents than resident replay waves: passes (mtb_replay_pass_kernel).  The
+    documents' chunks, chunk-major, are cut into launches of whole rounds of the wave slots, at most one chunk
+    per document each, so the launch boundaries order every document's chunks.  The same 4,608 ragged
+    documents as the ticket test: every digest equal to the oracle's, for the chosen chunk count and for 1, 3
+    and 7 chunks per document (MTB_PASS_CHUNKS); the pass count follows the cut."""
+    monkeypatch.delenv("MTB_SCHED", raising=False)
+    if chunks is None:
+        monkeypatch.delenv("MTB_PASS_CHUNKS", raising=False)
+    else:
+        monkeypatch.setenv("MTB_PASS_CHUNKS", chunks)
+    B, want, slots = _ragged_batch()
+    n = len(want)
+    st = B.replay()
+    assert st["errors"] == 0
+    li = B.launch_info()
+    assert li["kernel"] == "mtb_replay_pass_kernel" and li["wave_slots"] == slots, li
+    per = max(1, n // slots) * slots
+    assert li["passes"] == -(-li["chunks"] * n // per), li
+    if chunks is not None:
+        assert li["chunks"] == int(chunks)
+    dg = B.digests()
+    bad = [j for j in range(n) if dg[j] != want[j]]
+    assert not bad, f"{len(bad)}/{n} documents' digests differ from the oracle (first: {bad[:5]})"
+
+
+def _ragged_batch():
+    """slots + slots / 8 documents with ragged record counts -- whole 300-message logs, message-boundary
+    prefixes of them, and documents with no records -- and the oracle's digest each should end with."""
+    import torch
+    from pyloggen import LogBatch, make_cfg
     lb = LogBatch(make_cfg(seed=606, n_ops=300), 0, 48)
     slots = torch.cuda.get_device_properties(0).multi_processor_count * 16
     n = slots + slots // 8  # more documents than resident replay waves
@@ -195,12 +239,4 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, qu
             if (u, m) not in prefix:
                 prefix[(u, m)] = _prefix_digest(lb, u, m)
             want.append(prefix[(u, m)])
-    st = B.replay()
-    assert st["errors"] == 0
-    li = B.launch_info()
-    assert li["kernel"] == "mtb_replay_sched_kernel" and li["wave_slots"] == slots, li
-    if spins == "0":
-        assert li["aborted"], li  # every hand-over wait gives up at once
-    dg = B.digests()
-    bad = [j for j in range(n) if dg[j] != want[j]]
-    assert not bad, f"{len(bad)}/{n} documents' digests differ from the oracle (first: {bad[:5]})"
+    return B, want, slots
