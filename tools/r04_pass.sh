@@ -16,5 +16,14 @@ for m in default 4 6 default; do
   [ $rc -ne 0 ] && exit $rc
 done
 unset MTB_PASS_CHUNKS
+for lib in libmtb_rbl libmtb_rbd libmtb_rbx; do  # rebuild() variants (same-box A/B against pass_default)
+  MTB_LIB=fluidframework_amd/$lib.so timeout -k 10 600 python3 $B > $O/ab_$lib.json 2> $O/ab_$lib.err
+  rc=$?; echo "$lib rc=$rc $(python3 -c "import json;d=json.load(open('$O/ab_$lib.json'));print(d['value'],d['roofline']['kernel_ms'],d['parity']['mismatches'])" 2>/dev/null)"
+  [ $rc -ne 0 ] && exit $rc
+done
+for v in prof profpack; do  # per-phase cycle counters (MTB_PROFILE builds)
+  MTB_LIB=fluidframework_amd/libmtb_$v.so MTB_PROFILE_OUT=1 timeout -k 10 600 python3 bench.py --no-cpu --no-summary --steps 1 --warmup 0 --parity-sample 4 --traffic off > $O/bench_$v.json 2> $O/bench_$v.err
+  rc=$?; echo "$v rc=$rc"; grep "mtb_profile" $O/bench_$v.err; [ $rc -ne 0 ] && exit $rc
+done
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "not scheduled_replay" > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; exit $rc
