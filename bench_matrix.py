@@ -95,6 +95,7 @@ def main():
     lb = MatrixLogBatch(cfg, 0, n_unique)
     t_gen = time.time() - t0
     B = MatrixBatch(args.matrices)
+    lb.intern_values(B)
     opsb = [[lb.ops_bytes(u, v) for v in (0, 1)] for u in range(n_unique)]
     ids = [[lb.client_ids(u, v) for v in (0, 1)] for u in range(n_unique)]
     t0 = time.time()

@@ -34,7 +34,8 @@ class MtbLaunchInfo(ctypes.Structure):
 
 
 KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 2: "mtb_replay_sched_kernel", 3: "mtb_replay_few_kernel",
-                4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel", 7: "mtb_replay_pass_kernel"}
+                4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel", 7: "mtb_replay_pass_kernel",
+                8: "mtb_replay_tick_kernel"}
 
 
 class MtbOptions(ctypes.Structure):

@@ -245,6 +245,7 @@ struct Tables {
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32
 #define MTB_SCHED_ABORT 256
+#define MTB_SCHED_SPINS 260  // mtb_replay_tick_kernel: the wait bound (spins), written by the host
 #define MTB_SCHED_HDR 288
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

@@ -46,6 +46,9 @@ hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState*
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
                                    uint32_t nq, uint32_t spins);  // + mtb_replay_finish_kernel
+hipError_t mtb_launch_replay_ticks(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t nq);
 hipError_t mtb_launch_replay_passes(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                     uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                     uint32_t* freel, Tables tables, uint32_t first, uint32_t count, uint32_t nchunks);
@@ -469,6 +472,7 @@ struct mtb_dev {
   uint32_t nXcc = 0;                // XCDs of the device (the ticket scheduler's queues)
   mtb_launch_info launch{};         // what the last replay launched (mtb_launch_info)
   uint32_t schedAbortHost = 0;
+  uint32_t schedSpins = 0;  // (source of the wait bound's copy to the device)
   std::vector<uint32_t> schedPlan;  // the ticket scheduler's chunk plan (host copy of the uploaded one)
   Chunks pxSave[5], pxRestore[5];
   bool residentLoad = false;        // the resident records start with LOADSEG records
@@ -1600,7 +1604,7 @@ void apply_cell_events(mtb_dev* b, uint32_t matrix);
 // the scheduler's abort flag, copied back with the stream's next synchronization
 void sched_readback(mtb_dev* b) {
   b->schedAbortHost = 0;
-  if (b->launch.kernel == MTB_KERNEL_SCHED)
+  if (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS)
     HIPCHK(hipMemcpyAsync(&b->schedAbortHost, b->dSched.p + MTB_SCHED_ABORT, sizeof(uint32_t), hipMemcpyDeviceToHost,
                           b->stream));
 }
@@ -1618,9 +1622,10 @@ void launch_main(mtb_dev* b, const Tables& t) {
     bool markers = false;
     for (uint32_t i = 0; i < b->ndocs && !markers; i++)
       markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot;
-    // more documents than wave slots: passes of equal chunks (mtb_replay_pass_kernel, the default), or the
-    // ticket-scheduled persistent kernel (MTB_SCHED=tickets; MTB_CHUNKS sets the tickets per document);
-    // MTB_SCHED=0 launches one wave per whole document
+    // more documents than wave slots: tickets, one per workgroup (mtb_replay_tick_kernel, the default;
+    // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document), the persistent ticket kernel
+    // (MTB_SCHED=tickets), or passes of equal chunks (MTB_SCHED=passes); MTB_SCHED=0 launches one wave per
+    // whole document
     if (!b->live && !markers && !b->waveSlots) {
       hipDeviceProp_t prop;
       HIPCHK(hipGetDeviceProperties(&prop, b->device));
@@ -1633,7 +1638,7 @@ void launch_main(mtb_dev* b, const Tables& t) {
     b->launch.wave_slots = b->waveSlots;
     const char* sv = getenv("MTB_SCHED");
     const bool many = !b->live && !markers && b->ndocs > b->waveSlots && !(sv && sv[0] == '0');
-    if (many && !(sv && !strcmp(sv, "tickets"))) {
+    if (many && sv && !strcmp(sv, "passes")) {
       // Passes: the ndocs * m tasks (chunk c of document x, chunk-major) cut into launches of whole rounds
       // of the resident slots, at most ndocs tasks each (a document's chunks land in successive launches).
       // m (chunks per document, MTB_PASS_CHUNKS) leaves the smallest fraction of a round idle at the end.
@@ -1703,13 +1708,21 @@ void launch_main(mtb_dev* b, const Tables& t) {
       const size_t nw = MTB_SCHED_HDR + (size_t)b->ndocs + nchunks;
       b->dSched.ensure(nw);
       HIPCHK(hipMemsetAsync(b->dSched.p, 0, (MTB_SCHED_HDR + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
-      b->schedPlan = plan;  // (kept alive until the stream has consumed the copy)
+      b->schedPlan = plan;  // (kept alive until the stream has consumed the copies)
+      b->schedSpins = spins;
       HIPCHK(hipMemcpyAsync(b->dSched.p + MTB_SCHED_HDR + b->ndocs, b->schedPlan.data(), nchunks * sizeof(uint32_t),
                             hipMemcpyHostToDevice, b->stream));
-      HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
-                                     b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks,
-                                     b->waveSlots, nq, spins));
-      b->launch.kernel = MTB_KERNEL_SCHED;
+      HIPCHK(hipMemcpyAsync(b->dSched.p + MTB_SCHED_SPINS, &b->schedSpins, sizeof(uint32_t), hipMemcpyHostToDevice,
+                            b->stream));
+      const bool persistent = sv && !strcmp(sv, "tickets");
+      if (persistent)
+        HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
+                                       b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks,
+                                       b->waveSlots, nq, spins));
+      else
+        HIPCHK(mtb_launch_replay_ticks(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
+                                       b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks, nq));
+      b->launch.kernel = persistent ? MTB_KERNEL_SCHED : MTB_KERNEL_TICKS;
       b->launch.chunks = nchunks;
       b->launch.queues = nq;
       return;
@@ -1875,7 +1888,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
-  b->launch.aborted = b->launch.kernel == MTB_KERNEL_SCHED ? b->schedAbortHost : 0u;
+  b->launch.aborted = (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS) ? b->schedAbortHost : 0u;
   pc.mark("kernels");
   if (b->matrix)
     for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
@@ -3531,7 +3544,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     HIPCHK(hipStreamSynchronize(b->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    b->launch.aborted = b->launch.kernel == MTB_KERNEL_SCHED ? b->schedAbortHost : 0u;
+    b->launch.aborted = (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS) ? b->schedAbortHost : 0u;
     mtb_stats st{};
     st.kernel_ms = ms;
     uint32_t short_docs = 0;

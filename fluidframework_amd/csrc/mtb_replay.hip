@@ -4146,6 +4146,56 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     }
   }
 }
+// The tickets again, one per workgroup (grid = documents x chunks, not persistent): a workgroup takes the next
+// ticket of its XCD's queue (or of the next queue with tickets left) as it starts, waits for the document's
+// previous chunk, replays its chunk and exits.  A ticket's previous chunk was taken by a workgroup that
+// started earlier and is resident, so every wait drains.  With no loop around it and no call into it, the
+// engine gets the plain replay kernel's register allocation (no scratch): the wait is a called function
+// (inlined, its loop and acquire fence made the engine spill).  An exhausted wait raises the abort flag as
+// in the persistent kernel, and mtb_replay_finish_kernel replays the rest.
+__device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* prog, uint32_t c, uint32_t spins) {
+  uint32_t n = 0;
+  while (U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c) {
+    if (++n > spins) {
+      if (lane_id() == 0) __hip_atomic_store(&sched[MTB_SCHED_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(16);
+    if (COLD((n & 1023) == 0) &&
+        U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+      return false;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
+  return true;
+}
+extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
+    mtb_replay_tick_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+                           WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
+                           uint32_t* sched, uint32_t nchunks, uint32_t nq) {
+  __shared__ Scratch sh;
+  const uint32_t home = xcc_id() % nq;
+  uint32_t d = MTB_NONE, c = 0;
+  for (uint32_t qi = 0; qi < nq && d == MTB_NONE; qi++) {
+    const uint32_t q = (home + qi) % nq;
+    if (q >= ndocs) continue;
+    const uint32_t nqd = (ndocs - q + nq - 1) / nq;  // documents of queue q
+    uint32_t t = 0;
+    if (lane_id() == 0) t = atomicAdd(&sched[MTB_SCHED_TICK * q], 1u);
+    t = U(t);
+    if (t >= nqd * nchunks) continue;
+    c = t / nqd;
+    d = (t - c * nqd) * nq + q;
+  }
+  if (d == MTB_NONE) return;
+  if (U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) return;
+  uint32_t* prog = &sched[MTB_SCHED_HDR + d];
+  if (c > 0 && !tick_wait(sched, prog, c, U(sched[MTB_SCHED_SPINS]))) return;
+  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
+                          U(sched[MTB_SCHED_HDR + ndocs + c]));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X guide: the write-back completes before the flag)
+  if (lane_id() == 0) __hip_atomic_store(prog, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // After an aborted scheduled launch: every document continues from its op_next (one wave per document;
 // documents that finished have nothing left).  Without an abort every wave leaves at once.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
@@ -4246,6 +4296,15 @@ int mtb_sched_waves_per_cu() {
           hipSuccess || n <= 0)
     return 16;
   return n;
+}
+hipError_t mtb_launch_replay_ticks(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
+                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
+                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t nq) {
+  hipLaunchKernelGGL(mtb_replay_tick_kernel, dim3(ndocs * nchunks), dim3(64), 0, stream, KARGS, sched, nchunks, nq);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mtb_replay_finish_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS, (const uint32_t*)sched);
+  return hipGetLastError();
 }
 hipError_t mtb_launch_replay_passes(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                     uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,

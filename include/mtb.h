@@ -128,14 +128,15 @@ enum {
   MTB_KERNEL_LIVE = 4,     /* live clients (local ops, acks, reconnect) */
   MTB_KERNEL_MARKERS = 5,  /* marker ids / relative positions */
   MTB_KERNEL_MATRIX = 6,   /* SharedMatrix vector pairs */
-  MTB_KERNEL_PASSES = 7    /* more documents than resident waves: launches of equal chunks ("passes") */
+  MTB_KERNEL_PASSES = 7,   /* more documents than resident waves: launches of equal chunks ("passes") */
+  MTB_KERNEL_TICKS = 8     /* more documents than resident waves: one ticket (document chunk) per workgroup */
 };
 typedef struct mtb_launch_info {
   uint32_t kernel;      /* MTB_KERNEL_* */
   uint32_t wave_slots;  /* resident replay waves of the device (CUs x 16) */
-  uint32_t chunks;      /* MTB_KERNEL_SCHED: tickets per document; MTB_KERNEL_PASSES: chunks per document */
-  uint32_t queues;      /* MTB_KERNEL_SCHED: ticket queues (one per XCD) */
-  uint32_t aborted;     /* MTB_KERNEL_SCHED: a ticket wait hit its bound and the finish kernel ran the rest */
+  uint32_t chunks;      /* MTB_KERNEL_SCHED / _TICKS: tickets per document; MTB_KERNEL_PASSES: chunks per document */
+  uint32_t queues;      /* MTB_KERNEL_SCHED / _TICKS: ticket queues (one per XCD) */
+  uint32_t aborted;     /* MTB_KERNEL_SCHED / _TICKS: a ticket wait hit its bound and the finish kernel ran the rest */
   uint32_t passes;      /* MTB_KERNEL_PASSES: kernel launches of the replay */
 } mtb_launch_info;
 

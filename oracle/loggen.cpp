@@ -363,6 +363,7 @@ static int gen_matrix_one(const loggen_cfg& cfg, uint32_t index, loggen_matrix* 
         contents = jobj({{u"type", JVal::number(2)}, {u"row", JVal::number(row)}, {u"col", JVal::number(col)},
                          {u"value", JVal::number(m)}});
         rec.type = 6;  // MTB_OP_SETCELL, no updateSeqNumbers
+        rec.props = (uint32_t)m + 1;  // the value's id when the engine interns "0", "1", ... first (matrix_value_ids)
         for (int v = 0; v < 2; v++) {
           Doc::Record x = rec;
           x.client = shortIn(v, w);

@@ -147,6 +147,13 @@ class MatrixLogBatch:
         m = self.mats[i]
         return ctypes.string_at(m.ops[v], m.n_ops[v] * 32)
 
+    def intern_values(self, B):
+        """A setCell record of message m carries value id m + 1, the id a MatrixBatch gives the JSON text "m"
+        when "0", "1", ... are interned first (id 0 = undefined): intern them into B in that order."""
+        for k in range(self.cfg.n_ops):
+            if B.intern_value(str(k)) != k + 1:
+                raise RuntimeError("the batch interned setCell values before the generator's table")
+
     def client_ids(self, i, v):
         m = self.mats[i]
         return ["obs"] + [f"c{m.client_writer[v][s]}" for s in range(1, m.n_short[v])]

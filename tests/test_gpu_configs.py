@@ -149,18 +149,23 @@ def _message_cut(lb, u, frac):
     return m
 
 
+@pytest.mark.parametrize("mode", ["ticks", "tickets"])
 @pytest.mark.parametrize("chunks,queues,spins", [(None, None, None), ("16", None, None), ("3", "1", None),
                                                  (None, None, "0"), ("16", "1", "40")])
-def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, queues, spins):
-    """More documents than the device's resident replay waves runs the ticket-scheduled kernel (persistent
-    waves, documents advanced chunk by chunk in round-robin): 4,608 documents with ragged record counts --
+def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, mode, chunks, queues, spins):
+    """More documents than the device's resident replay waves runs ticket-scheduled replay -- one ticket per
+    workgroup (mtb_replay_tick_kernel, the default) or persistent waves taking tickets (MTB_SCHED=tickets),
+    documents advanced chunk by chunk in round-robin: 4,608 documents with ragged record counts --
     whole 300-message logs, message-boundary prefixes of them, and documents with no records -- every
     state digest equal to the oracle's, for the default shrinking-chunk plan and for 16 and 3 equal chunks
     per document (MTB_CHUNKS), per-XCD ticket queues and one global queue (MTB_SCHED_QUEUES=1), and with
     the ticket waits bounded so low that the scheduler aborts (MTB_SCHED_SPINS): the finish kernel then
     replays the rest of every document and the results are the same."""
     monkeypatch.delenv("MTB_CHUNK_PLAN", raising=False)
-    monkeypatch.setenv("MTB_SCHED", "tickets")
+    if mode == "tickets":
+        monkeypatch.setenv("MTB_SCHED", "tickets")
+    else:
+        monkeypatch.delenv("MTB_SCHED", raising=False)
     for var, val in (("MTB_CHUNKS", chunks), ("MTB_SCHED_QUEUES", queues), ("MTB_SCHED_SPINS", spins)):
         if val is None:
             monkeypatch.delenv(var, raising=False)
@@ -170,7 +175,8 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, qu
     st = B.replay()
     assert st["errors"] == 0
     li = B.launch_info()
-    assert li["kernel"] == "mtb_replay_sched_kernel" and li["wave_slots"] == slots, li
+    kernel = "mtb_replay_sched_kernel" if mode == "tickets" else "mtb_replay_tick_kernel"
+    assert li["kernel"] == kernel and li["wave_slots"] == slots, li
     if spins == "0":
         assert li["aborted"], li  # every hand-over wait gives up at once
     dg = B.digests()
@@ -181,12 +187,12 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, qu
 
 @pytest.mark.parametrize("chunks", [None, "1", "3", "7"])
 def test_pass_replay_more_documents_than_wave_slots(monkeypatch, chunks):
-    """The default for more documents than resident replay waves: passes (mtb_replay_pass_kernel).  The
+    """Passes (MTB_SCHED=passes, mtb_replay_pass_kernel) for more documents than resident replay waves.  The
     documents' chunks, chunk-major, are cut into launches of whole rounds of the wave slots, at most one chunk
     per document each, so the launch boundaries order every document's chunks.  The same 4,608 ragged
     documents as the ticket test: every digest equal to the oracle's, for the chosen chunk count and for 1, 3
     and 7 chunks per document (MTB_PASS_CHUNKS); the pass count follows the cut."""
-    monkeypatch.delenv("MTB_SCHED", raising=False)
+    monkeypatch.setenv("MTB_SCHED", "passes")
     if chunks is None:
         monkeypatch.delenv("MTB_PASS_CHUNKS", raising=False)
     else:

@@ -94,6 +94,7 @@ def test_generated_matrix_records_match_oracle_checksums(new_mode):
     from pyloggen import MatrixLogBatch, make_cfg
     lb = MatrixLogBatch(make_cfg(seed=77 + int(new_mode), n_ops=3000, lag=48, new_length_calc=new_mode), 0, 64)
     B = MatrixBatch(lb.n, new_length_calc=new_mode)
+    lb.intern_values(B)
     for i in range(lb.n):
         B.init_matrix(i, "obs")
         for v in (0, 1):
@@ -226,6 +227,7 @@ def test_matrix_bench_parity_definition():
     cfg = make_cfg(seed=77, n_clients=6, n_ops=1500, lag=32, pct_set=40)
     lb = MatrixLogBatch(cfg, 0, 24)
     B = MatrixBatch(lb.n)
+    lb.intern_values(B)
     for j in range(lb.n):
         B.init_matrix(j, "obs")
         for v in (0, 1):
