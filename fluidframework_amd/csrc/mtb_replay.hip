@@ -3827,9 +3827,10 @@ using namespace mtbk;
 #ifndef MTB_WAVES_PER_SIMD
 #define MTB_WAVES_PER_SIMD 4
 #endif
+__device__ __forceinline__ uint32_t ds_word(uint32_t w0, uint32_t w1, uint32_t i) { return i < 64 ? rlu(w0, i) : rlu(w1, i - 64); }
 template <int MODE, class SCR>
 __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, int wv,
-                                           DocState* __restrict__ docs,
+                                           DocState* docs,  // (no __restrict__: see mtb_replay_tick_kernel)
                                            uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
                                            uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                                            const Tables& tables, uint32_t upto = 0) {
@@ -3839,46 +3840,53 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.xch = xch;
   e.wv = wv;
   e.ds = ds;
+  // The DocState arrives as two vector loads (lane i: dwords i and 64 + i) read out with v_readlane, never
+  // through the scalar cache: within one launch of mtb_replay_tick_kernel another workgroup wrote it (the
+  // previous chunk's), and the hand-over's acquire does not invalidate the scalar cache.
+  const uint32_t dw0 = reinterpret_cast<const uint32_t*>(ds)[lane_id()];
+  const uint32_t dw1 = lane_id() < 32 ? reinterpret_cast<const uint32_t*>(ds)[64 + lane_id()] : 0u;
+#define DSF(f) ds_word(dw0, dw1, offsetof(DocState, f) / 4)
+#define DSF64(f) (((uint64_t)ds_word(dw0, dw1, offsetof(DocState, f) / 4 + 1) << 32) | ds_word(dw0, dw1, offsetof(DocState, f) / 4))
 #ifdef MTB_CHECK
   {
     uint32_t* rep = &ds->pad3[0];
-    e.segp.p = segp + ds->seg_base, e.segp.cap = &sh.capv[0], e.segp.rep = rep, e.segp.pool = 0;
-    e.blk.p = blks + ds->blk_base, e.blk.cap = &sh.capv[1], e.blk.rep = rep, e.blk.pool = 1;
-    e.lst.p = lists + ds->list_base, e.lst.cap = &sh.capv[2], e.lst.rep = rep, e.lst.pool = 2;
-    e.aux.p = aux + ds->aux_base, e.aux.cap = &sh.capv[5], e.aux.rep = rep, e.aux.pool = 3;
+    e.segp.p = segp + DSF64(seg_base), e.segp.cap = &sh.capv[0], e.segp.rep = rep, e.segp.pool = 0;
+    e.blk.p = blks + DSF64(blk_base), e.blk.cap = &sh.capv[1], e.blk.rep = rep, e.blk.pool = 1;
+    e.lst.p = lists + DSF64(list_base), e.lst.cap = &sh.capv[2], e.lst.rep = rep, e.lst.pool = 2;
+    e.aux.p = aux + DSF64(aux_base), e.aux.cap = &sh.capv[5], e.aux.rep = rep, e.aux.pool = 3;
   }
 #else
-  e.segp = segp + ds->seg_base;
-  e.blk = blks + ds->blk_base;
-  e.lst = lists + ds->list_base;
-  e.aux = aux + ds->aux_base;
+  e.segp = segp + DSF64(seg_base);
+  e.blk = blks + DSF64(blk_base);
+  e.lst = lists + DSF64(list_base);
+  e.aux = aux + DSF64(aux_base);
 #endif
-  Lru* const gheap = heap + ds->heap_base;
-  const mtb_op* const dops = ops + ds->op_base;
+  Lru* const gheap = heap + DSF64(heap_base);
+  const mtb_op* const dops = ops + DSF64(op_base);
   sh.tab = tables;  // (every lane stores the same values)
   sh.gheap = gheap;
-  sh.gfree = freel + ds->free_base;
-  sh.gtext = text + ds->text_base;
+  sh.gfree = freel + DSF64(free_base);
+  sh.gtext = text + DSF64(text_base);
   e.sh = &sh;
   e.lane = lane_id();
-  e.minSeq = ds->min_seq;
-  e.curSeq = ds->cur_seq;
-  e.root = ds->root;
-  e.newMode = ds->new_mode != 0;
-  e.hasNL = (ds->flags & DSF_NEWLINE) != 0;
-  e.seg_used = ds->seg_used;
-  e.blk_used = ds->blk_used;
-  e.free_top = ds->free_top;
-  e.list_used = ds->list_used;
-  e.text_used = ds->text_used;
-  e.heap_cnt = ds->heap_cnt;
-  e.aux_used = ds->aux_used;
-  e.err = ds->err;
+  e.minSeq = (int)DSF(min_seq);
+  e.curSeq = (int)DSF(cur_seq);
+  e.root = DSF(root);
+  e.newMode = DSF(new_mode) != 0;
+  e.hasNL = (DSF(flags) & DSF_NEWLINE) != 0;
+  e.seg_used = DSF(seg_used);
+  e.blk_used = DSF(blk_used);
+  e.free_top = DSF(free_top);
+  e.list_used = DSF(list_used);
+  e.text_used = DSF(text_used);
+  e.heap_cnt = DSF(heap_cnt);
+  e.aux_used = DSF(aux_used);
+  e.err = (int)DSF(err);
   e.n_mod = 0;
   e.ops_applied = 0;
   e.text_bytes = 0;
-  uint32_t k = ds->op_next;
-  const uint32_t n = ds->n_ops;
+  uint32_t k = DSF(op_next);
+  const uint32_t n = DSF(n_ops);
   // a scheduler ticket replays up to upto/4096 of the document's records (0: all of them)
   const uint32_t kend = upto ? (uint32_t)(((uint64_t)n * upto + 4095) >> 12) : n;
   uint32_t errk = n;  // MODE_MATRIX: index after the record that failed
@@ -3891,21 +3899,21 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
 #ifdef MTB_NO_MKREMAP  // (test builds: shows the reused-id tests depend on the re-mapping)
   e.mkDup = false;
 #else
-  e.mkDup = (ds->flags & DSF_MKDUP) != 0;
+  e.mkDup = (DSF(flags) & DSF_MKDUP) != 0;
 #endif
   e.ann_mk = 0;
-  e.delta_used = ds->delta_used;
+  e.delta_used = DSF(delta_used);
   e.cur_k = 0;
   e.sp_internal = false;
-  e.local_seq = ds->local_seq;
-  e.pend_dir = ds->pend_dir;
-  e.pend_head = ds->pend_head;
-  e.pend_n = ds->pend_n;
-  e.pend_cap = ds->pend_cap;
+  e.local_seq = (int)DSF(local_seq);
+  e.pend_dir = DSF(pend_dir);
+  e.pend_head = DSF(pend_head);
+  e.pend_n = DSF(pend_n);
+  e.pend_cap = DSF(pend_cap);
   e.grp_open = false;
   e.pk_rw = false;
   if (e.lane < 6) sh.capv[e.lane] = (&ds->seg_cap)[e.lane];
-  if (e.lane == 6) sh.capv[6] = ds->delta_cap;
+  if (e.lane == 6) sh.capv[6] = DSF(delta_cap);
   sh.ins[0] = (int32_t)MTB_NONE;  // (every lane stores the same values)
   sh.ins[1] = sh.ins[2] = sh.ins[3] = -1;
   for (int i = 0; i < NPH; i++) e.prof[i] = 0;
@@ -4100,7 +4108,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
   return x;
 }
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
-    mtb_replay_sched_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+    mtb_replay_sched_kernel(DocState* docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                             WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
                             uint32_t* sched, uint32_t nchunks, uint32_t nq, uint32_t spins) {
   __shared__ Scratch sh;
@@ -4169,7 +4177,7 @@ __device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* p
   return true;
 }
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
-    mtb_replay_tick_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+    mtb_replay_tick_kernel(DocState* docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                            WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
                            uint32_t* sched, uint32_t nchunks, uint32_t nq) {
   __shared__ Scratch sh;
@@ -4199,7 +4207,7 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
 // After an aborted scheduled launch: every document continues from its op_next (one wave per document;
 // documents that finished have nothing left).  Without an abort every wave leaves at once.
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
-    mtb_replay_finish_kernel(DocState* __restrict__ docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
+    mtb_replay_finish_kernel(DocState* docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                              WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
                              const uint32_t* sched) {
   __shared__ Scratch sh;
