@@ -33,7 +33,7 @@ class MtbLaunchInfo(ctypes.Structure):
                 ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("passes", ctypes.c_uint32)]
 
 
-KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 2: "mtb_replay_sched_kernel", 3: "mtb_replay_few_kernel",
+KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 3: "mtb_replay_few_kernel",
                 4: "mtb_live_kernel", 5: "mtb_markers_kernel", 6: "mtb_matrix_kernel", 7: "mtb_replay_pass_kernel",
                 8: "mtb_replay_tick_kernel"}
 

@@ -241,7 +241,7 @@ struct Tables {
 #define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
 #define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
 #define DERR_INCR 24         // an incr annotate over a string / object value (not NaN: unsupported on the device)
-// ticket scheduler words (mtb_replay_sched_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
+// ticket scheduler words (mtb_replay_tick_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32
 #define MTB_SCHED_ABORT 256

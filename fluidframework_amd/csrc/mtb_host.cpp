@@ -42,10 +42,6 @@ hipError_t mtb_launch_replay(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                              Tables tables, int variant);  // 0 replay, 1 live clients, 2 marker ids
 int mtb_sched_waves_per_cu();
-hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
-                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
-                                   uint32_t nq, uint32_t spins);  // + mtb_replay_finish_kernel
 hipError_t mtb_launch_replay_ticks(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t nq);
@@ -467,7 +463,7 @@ struct mtb_dev {
   DevBuf<FBlk> dPBlk;
   DevBuf<uint32_t> dPX;             // loaded documents: initial blocks / segp / lists / aux words
   DevBuf<uint32_t> dDelta;          // catch-up delta entries (4 words each), per-document slices
-  DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_sched_kernel)
+  DevBuf<uint32_t> dSched;          // ticket scheduler words (mtb_replay_tick_kernel)
   uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x the sched kernel's occupancy)
   uint32_t nXcc = 0;                // XCDs of the device (the ticket scheduler's queues)
   mtb_launch_info launch{};         // what the last replay launched (mtb_launch_info)
@@ -1604,7 +1600,7 @@ void apply_cell_events(mtb_dev* b, uint32_t matrix);
 // the scheduler's abort flag, copied back with the stream's next synchronization
 void sched_readback(mtb_dev* b) {
   b->schedAbortHost = 0;
-  if (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS)
+  if (b->launch.kernel == MTB_KERNEL_TICKS)
     HIPCHK(hipMemcpyAsync(&b->schedAbortHost, b->dSched.p + MTB_SCHED_ABORT, sizeof(uint32_t), hipMemcpyDeviceToHost,
                           b->stream));
 }
@@ -1623,9 +1619,8 @@ void launch_main(mtb_dev* b, const Tables& t) {
     for (uint32_t i = 0; i < b->ndocs && !markers; i++)
       markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot;
     // more documents than wave slots: tickets, one per workgroup (mtb_replay_tick_kernel, the default;
-    // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document), the persistent ticket kernel
-    // (MTB_SCHED=tickets), or passes of equal chunks (MTB_SCHED=passes); MTB_SCHED=0 launches one wave per
-    // whole document
+    // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document) or passes of equal chunks (MTB_SCHED=passes);
+    // MTB_SCHED=0 launches one wave per whole document
     if (!b->live && !markers && !b->waveSlots) {
       hipDeviceProp_t prop;
       HIPCHK(hipGetDeviceProperties(&prop, b->device));
@@ -1714,15 +1709,9 @@ void launch_main(mtb_dev* b, const Tables& t) {
                             hipMemcpyHostToDevice, b->stream));
       HIPCHK(hipMemcpyAsync(b->dSched.p + MTB_SCHED_SPINS, &b->schedSpins, sizeof(uint32_t), hipMemcpyHostToDevice,
                             b->stream));
-      const bool persistent = sv && !strcmp(sv, "tickets");
-      if (persistent)
-        HIPCHK(mtb_launch_replay_sched(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
-                                       b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks,
-                                       b->waveSlots, nq, spins));
-      else
-        HIPCHK(mtb_launch_replay_ticks(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
-                                       b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks, nq));
-      b->launch.kernel = persistent ? MTB_KERNEL_SCHED : MTB_KERNEL_TICKS;
+      HIPCHK(mtb_launch_replay_ticks(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p,
+                                     b->dText.p, b->dHeap.p, b->dAux.p, b->dFree.p, t, b->dSched.p, nchunks, nq));
+      b->launch.kernel = MTB_KERNEL_TICKS;
       b->launch.chunks = nchunks;
       b->launch.queues = nq;
       return;
@@ -1888,7 +1877,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
-  b->launch.aborted = (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS) ? b->schedAbortHost : 0u;
+  b->launch.aborted = b->launch.kernel == MTB_KERNEL_TICKS ? b->schedAbortHost : 0u;
   pc.mark("kernels");
   if (b->matrix)
     for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
@@ -3544,7 +3533,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
     HIPCHK(hipStreamSynchronize(b->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    b->launch.aborted = (b->launch.kernel == MTB_KERNEL_SCHED || b->launch.kernel == MTB_KERNEL_TICKS) ? b->schedAbortHost : 0u;
+    b->launch.aborted = b->launch.kernel == MTB_KERNEL_TICKS ? b->schedAbortHost : 0u;
     mtb_stats st{};
     st.kernel_ms = ms;
     uint32_t short_docs = 0;

@@ -858,22 +858,15 @@ struct Eng {
   // each block child k, the entries of k's own list plus entries derived from k's segment children
   // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
   // where P's metadata lives.
-  // zready: the caller already staged P's slots and count in sh->zr (from the LDS view or registers), which
-  // saves the dependent fetch of P's record
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out, bool zready = false) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
-    int count;
-    if (zready) {
-      count = U(Z.count);
-    } else {
-      const uint32_t* src = bw(P);
-      const uint32_t w = src[lane];
-      count = U((int)src[FB_HDR]);
-      (&Z.f[0][0])[lane] = w;
-      wsync();
-    }
+    const uint32_t* src = bw(P);
+    const uint32_t w = src[lane];
+    const int count = U((int)src[FB_HDR]);
+    (&Z.f[0][0])[lane] = w;
+    wsync();
     // lane (k, s): segment child s of block child k
     const int k = lane >> 3, s = lane & 7;
     uint32_t ck = MTB_NONE;
@@ -884,25 +877,6 @@ struct Eng {
     uint32_t scli = 0, srcx = 0;
     if (kblk) {
       const uint32_t* c = bw(ck);
-#ifdef MTB_RB_LOADS
-      // the child's count, slot id and fields in one round trip (the record is always readable)
-      const int ccount = (int)c[FB_HDR];
-      const uint32_t sid = c[F_ID * 8 + s];
-      const int l0 = (int)c[F_LEN * 8 + s], q0 = (int)c[F_SEQ * 8 + s], r0 = (int)c[F_RSEQ * 8 + s];
-      const uint32_t c0 = c[F_CLI * 8 + s], x0 = c[F_RCX * 8 + s];
-      if (s < ccount && (sid & MTB_LEAF)) {
-        slen = l0;
-        sseq = q0;
-        srseq = r0;
-        scli = c0;
-        srcx = x0;
-        if (sseq > minSeq) ne++;
-        if (srseq >= 0 && srseq > minSeq) {
-          ne++;
-          if (srcx) nov = (int)aux[srcx];
-        }
-      }
-#else
       const int ccount = (int)c[FB_HDR];
       if (s < ccount) {
         const uint32_t sid = c[F_ID * 8 + s];
@@ -919,7 +893,6 @@ struct Eng {
           }
         }
       }
-#endif
     }
     // the block children's own lists (metadata in P's slots), concatenated
     uint32_t lc = 0, lo = 0;
@@ -945,66 +918,6 @@ struct Eng {
       for (int o = 32; o > 0; o >>= 1) novt += __shfl_xor(novt, o, 64);
     }
     const uint32_t total = (uint32_t)(nder + novt + ltotal);
-#ifdef MTB_RB_REGSORT
-    // Only derived entries (the children are leaf-level blocks, no overlapping removers): counting-sort them
-    // straight from registers into the final list (no unsorted copy to write, re-read and free).
-    if (ltotal == 0 && novt == 0 && total > MTB_SORT_MIN) {
-      const bool insv = ne >= 1 && sseq > minSeq, remv = srseq >= 0 && srseq > minSeq && ne >= 1;
-      const int bi = sseq - minSeq - 1, br = srseq - minSeq - 1;
-      const bool over = (insv && (bi < 0 || bi >= MTB_SORT_BUCKETS)) || (remv && (br < 0 || br >= MTB_SORT_BUCKETS));
-      if (!__ballot(over)) {
-        list_free(old_loff, old_lcap);
-        uint32_t* hist = &sh->hold[0][0];
-        for (int i = lane; i < MTB_SORT_BUCKETS / 2; i += 64) hist[i] = 0;
-        wsync();
-        if (insv) atomicAdd(&hist[bi >> 1], 1u << ((bi & 1) * 16));
-        if (remv) atomicAdd(&hist[br >> 1], 1u << ((br & 1) * 16));
-        wsync();
-        uint32_t wv[8];
-        uint32_t tot = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          wv[q] = hist[8 * lane + q];
-          tot += (wv[q] & 0xFFFF) + (wv[q] >> 16);
-        }
-        int incl = (int)tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int t = __shfl_up(incl, o, 64);
-          if (lane >= o) incl += t;
-        }
-        uint32_t run = (uint32_t)incl - tot;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const uint32_t c0 = run;
-          run += wv[q] & 0xFFFF;
-          hist[8 * lane + q] = c0 | (run << 16);
-          run += wv[q] >> 16;
-        }
-        wsync();
-        uint32_t cap2;
-        const uint32_t no2 = list_alloc(total + total / 2 + 4, cap2);
-        if (bad()) return;
-        if (insv) {
-          const uint32_t sft = (uint32_t)(bi & 1) * 16;
-          const uint32_t old = atomicAdd(&hist[bi >> 1], 1u << sft);
-          u32x4 e = {(uint32_t)sseq, (uint32_t)WE_KEY(cli_client(scli), WK_MAIN, k), (uint32_t)slen, 0u};
-          lst4()[no2 + ((old >> sft) & 0xFFFF)] = e;
-        }
-        if (remv) {
-          const uint32_t sft = (uint32_t)(br & 1) * 16;
-          const uint32_t old = atomicAdd(&hist[br >> 1], 1u << sft);
-          u32x4 e = {(uint32_t)srseq, (uint32_t)WE_KEY(cli_rc0(scli), WK_MAIN, k), (uint32_t)(-slen), 0u};
-          lst4()[no2 + ((old >> sft) & 0xFFFF)] = e;
-        }
-        wsync();
-        loff_out = no2;
-        lcnt_out = total;
-        lcap_out = cap2;
-        return;
-      }
-    }
-#endif
     uint32_t cap;
     const uint32_t no = list_alloc(total + total / 2 + 4, cap);
     if (bad()) return;
@@ -1312,19 +1225,9 @@ struct Eng {
         X = U(P.b);
         meta_of(L, ooff, ocnt, ocap);
         phase = 4;
-#ifdef MTB_RB_LDS
-        // P's record is the LDS view of depth L (insert_slot kept it in step with HBM)
-        (&sh->zr.f[0][0])[lane] = (&P.f[0][0])[lane];
-        if (lane == 0) sh->zr.count = P.count;
-        wsync();
-#endif
       }
       uint32_t a, c2, e;
-#ifdef MTB_RB_LDS
-      rebuild(X, ooff, ocap, a, c2, e, phase == 4);
-#else
       rebuild(X, ooff, ocap, a, c2, e);
-#endif
       if (err) break;
       if (phase == 2) {
         sp_loffL = a;
@@ -3108,43 +3011,15 @@ struct Eng {
       // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
       // site; rebuild uses the union as scratch)
       uint32_t a = 0, c2 = 0, e = 0;
-#ifdef MTB_RB_LDS
-      uint32_t za = 0, zc = 0, ze = 0;  // lane q: new block q's list metadata (P's slot q)
-#endif
       for (int q = 0; q <= cc; q++) {
         const bool isP = q == cc;
         const uint32_t nb = isP ? parent : rlu(nbs, q);
         a = c2 = e = 0;
-#ifdef MTB_RB_LDS
-        if (isP) {  // P's new slots, staged from registers (no dependent fetch of the record just written)
-          const int fld = lane >> 3, s = lane & 7;
-          // (lane-varying sources: ds_bpermute with every lane active)
-          const uint32_t x0 = (uint32_t)__shfl((int)nbs, s, 64), x1 = (uint32_t)__shfl(lens, s, 64);
-          const uint32_t x2 = (uint32_t)__shfl((int)za, s, 64), x3 = (uint32_t)__shfl((int)zc, s, 64);
-          const uint32_t x4 = (uint32_t)__shfl((int)ze, s, 64);
-          uint32_t v = fld == F_ID ? MTB_NONE : 0u;
-          if (s < cc) v = fld == F_ID ? x0 : fld == F_LEN ? x1 : fld == F_SEQ ? x2 : fld == F_RSEQ ? x3 : fld == F_CLI ? x4 : 0u;
-          (&sh->zr.f[0][0])[lane] = v;
-          if (lane == 0) sh->zr.count = cc;
-          wsync();
-        }
-#endif
         if (isP || rl(kbs, q)) {
-#ifdef MTB_RB_LDS
-          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e, isP);
-#else
           rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e);
-#endif
           if (bad()) return;
         }
         if (isP) break;
-#ifdef MTB_RB_LDS
-        if (lane == q) {
-          za = a;
-          zc = c2;
-          ze = e;
-        }
-#endif
         const int len = rl(lens, q);
         if (lane == 0) {
           FBlk& P = blk[parent];
@@ -4071,96 +3946,34 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   replay_doc<MODE_REPLAY>(sh, t - c * ndocs, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
                           upto);
 }
-// Batches with more documents than wave slots: persistent waves (one grid of the resident slots) take
-// tickets (chunk c, document d); ticket c replays document d's records up to the fraction plan[c] / 4096 of
-// them (the host's chunk plan).  Every document then advances at the same pace and the launch ends within
-// about one ticket of the ideal, instead of a last partial "round" of whole documents (10,000 documents on
-// 4,096 slots = 2.44 rounds).
+// Batches with more documents than wave slots: tickets (chunk c, document d), one per workgroup (grid =
+// documents x chunks).  Ticket c replays document d's records up to the fraction plan[c] / 4096 of them (the
+// host's chunk plan), so every document advances at the same pace and the launch ends within about one ticket
+// of the ideal, instead of a last partial "round" of whole documents (10,000 documents on 4,096 slots = 2.44
+// rounds).  A workgroup takes the next ticket of its XCD's queue (HW_REG_XCC_ID; or of the next queue with
+// tickets left) as it starts, waits for the document's previous chunk, replays its chunk and exits.
 //
 // Queues (L2 affinity, speed only): documents are split into nq queues (d mod nq, nq = the device's XCD
-// count); a wave serves the queue of the XCD it runs on (HW_REG_XCC_ID) first, so a document's chunks
-// normally run on one XCD and the next chunk finds the document's hot records in that XCD's L2; a wave
-// whose queue is exhausted helps the others.  Correctness never depends on where a wave runs: every
-// hand-over is an agent-scope release (after the chunk's stores) and acquire (before the next chunk's
-// loads), as for any two workgroups.  In queue q, ticket t = c * n_q + j names document d = j * nq + q;
-// it waits for ticket t - n_q (the same document's previous chunk), which a running wave took earlier, so
-// the waits always drain.  A wait longer than `spins` polls raises the abort flag and every wave leaves
-// between tickets (each document's state is then consistent at its op_next); mtb_replay_finish_kernel,
-// launched right after, replays the rest of every document when the flag is set.
-// sched: [32 q] next ticket of queue q (one line each), [MTB_SCHED_ABORT] abort flag, [MTB_SCHED_HDR + d]
-// chunks of document d completed (zeroed before launch), [MTB_SCHED_HDR + ndocs + c] the plan: cumulative
-// record fraction of chunk c in 1/4096 (the last one 4096).
-// one ticket: the replay engine as a called function (its register allocation stays the replay kernel's
-// instead of being shaped by the ticket loop around it)
-// (the slices are passed as global-address-space pointers: a called function cannot infer that of plain
-// pointer arguments, and its memory accesses would all be flat instructions)
-__device__ __attribute__((noinline)) void sched_ticket(Scratch& sh, uint32_t d, gptr<DocState> docs, uint32_t ndocs,
-                                                       gptr<const mtb_op> ops, gptr<uint32_t> segp, gptr<FBlk> blks,
-                                                       gptr<WEnt> lists, gptr<uint16_t> text, gptr<Lru> heap,
-                                                       gptr<uint32_t> aux, gptr<uint32_t> freel, const Tables& tables,
-                                                       uint32_t upto) {
-  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, (DocState*)docs, ndocs, (const mtb_op*)ops, (uint32_t*)segp, (FBlk*)blks,
-                          (WEnt*)lists, (uint16_t*)text, (Lru*)heap, (uint32_t*)aux, (uint32_t*)freel, tables, upto);
-}
+// count), so a document's chunks normally run on one XCD.  Correctness never depends on where a workgroup
+// runs: every hand-over is an agent-scope release (after the chunk's stores) and acquire (before the next
+// chunk's loads).  In queue q, ticket t = c * n_q + j names document d = j * nq + q; it waits for ticket
+// t - n_q (the same document's previous chunk), which a workgroup that started earlier took and is running,
+// so the waits always drain.  The DocState is read with vector loads (replay_doc): the scalar cache is not
+// invalidated by the acquire.  A wait longer than `spins` polls raises the abort flag; later workgroups leave
+// at once, and mtb_replay_finish_kernel, launched right after, replays the rest of every document (each
+// document's state is consistent at its op_next).
+// sched: [32 q] next ticket of queue q (one line each), [MTB_SCHED_ABORT] abort flag, [MTB_SCHED_SPINS] the
+// wait bound, [MTB_SCHED_HDR + d] chunks of document d completed (zeroed before launch), [MTB_SCHED_HDR +
+// ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096).
+//
+// (Rounds 2-3 ran the tickets on persistent waves, the engine a called function between them.  In round 4 that
+// kernel faulted in some builds; its replacement keeps the plain replay kernel's register allocation.  The
+// wait is a called function: inlined, its loop and acquire fence made the engine spill.)
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
   return x;
 }
-extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
-    mtb_replay_sched_kernel(DocState* docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
-                            WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
-                            uint32_t* sched, uint32_t nchunks, uint32_t nq, uint32_t spins) {
-  __shared__ Scratch sh;
-  const int lane = lane_id();
-  const uint32_t home = xcc_id() % nq;
-  for (uint32_t qi = 0; qi < nq; qi++) {
-    const uint32_t q = (home + qi) % nq;
-    if (q >= ndocs) continue;
-    const uint32_t nqd = (ndocs - q + nq - 1) / nq;  // documents of queue q
-    const uint32_t total = nqd * nchunks;
-    for (;;) {
-      if (U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) return;
-      uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(&sched[MTB_SCHED_TICK * q], 1u);
-      t = U(t);
-      if (t >= total) break;
-      const uint32_t j = t % nqd, c = t / nqd;
-      const uint32_t d = j * nq + q;
-      uint32_t* prog = &sched[MTB_SCHED_HDR + d];
-      if (c > 0) {
-        uint32_t n = 0;
-        bool ready;
-        while (!(ready = U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= c) && n < spins) {
-          n++;
-          __builtin_amdgcn_s_sleep(16);
-          // another wave gave up: leave now (this ticket's chunk is replayed by the finish kernel)
-          if (COLD((n & 1023) == 0) &&
-              U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
-            return;
-        }
-        if (!ready) {
-          if (lane == 0) __hip_atomic_store(&sched[MTB_SCHED_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
-      }
-      sched_ticket(sh, d, (gptr<DocState>)docs, ndocs, (gptr<const mtb_op>)ops, (gptr<uint32_t>)segp,
-                   (gptr<FBlk>)blks, (gptr<WEnt>)lists, (gptr<uint16_t>)text, (gptr<Lru>)heap, (gptr<uint32_t>)aux,
-                   (gptr<uint32_t>)freel, tables, U(sched[MTB_SCHED_HDR + ndocs + c]));
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X guide: the write-back completes before the flag)
-      if (lane == 0) __hip_atomic_store(prog, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-// The tickets again, one per workgroup (grid = documents x chunks, not persistent): a workgroup takes the next
-// ticket of its XCD's queue (or of the next queue with tickets left) as it starts, waits for the document's
-// previous chunk, replays its chunk and exits.  A ticket's previous chunk was taken by a workgroup that
-// started earlier and is resident, so every wait drains.  With no loop around it and no call into it, the
-// engine gets the plain replay kernel's register allocation (no scratch): the wait is a called function
-// (inlined, its loop and acquire fence made the engine spill).  An exhausted wait raises the abort flag as
-// in the persistent kernel, and mtb_replay_finish_kernel replays the rest.
 __device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* prog, uint32_t c, uint32_t spins) {
   uint32_t n = 0;
   while (U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c) {
@@ -4300,11 +4113,12 @@ hipError_t mtb_launch_observer(KPARAMS) {
 // resident waves of the scheduled kernel per CU (its grid is exactly the device's resident slots)
 int mtb_sched_waves_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(mtb_replay_sched_kernel), 64, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(mtb_replay_tick_kernel), 64, 0) !=
           hipSuccess || n <= 0)
     return 16;
   return n;
 }
+// tickets, then mtb_replay_finish_kernel (it replays the rest of every document after an abort, else exits)
 hipError_t mtb_launch_replay_ticks(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t nq) {
@@ -4318,16 +4132,6 @@ hipError_t mtb_launch_replay_passes(hipStream_t stream, uint32_t ndocs, DocState
                                     uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                     uint32_t* freel, Tables tables, uint32_t first, uint32_t count, uint32_t nchunks) {
   hipLaunchKernelGGL(mtb_replay_pass_kernel, dim3(count), dim3(64), 0, stream, KARGS, first, nchunks);
-  return hipGetLastError();
-}
-hipError_t mtb_launch_replay_sched(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
-                                   uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
-                                   uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t waves,
-                                   uint32_t nq, uint32_t spins) {
-  hipLaunchKernelGGL(mtb_replay_sched_kernel, dim3(waves), dim3(64), 0, stream, KARGS, sched, nchunks, nq, spins);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mtb_replay_finish_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS, (const uint32_t*)sched);
   return hipGetLastError();
 }
 #endif

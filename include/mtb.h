@@ -123,7 +123,7 @@ enum {
 enum {
   MTB_KERNEL_NONE = 0,
   MTB_KERNEL_REPLAY = 1,   /* one wave per document */
-  MTB_KERNEL_SCHED = 2,    /* ticket-scheduled persistent waves (more documents than resident waves) */
+  MTB_KERNEL_SCHED = 2,    /* (retired in round 4: ticket-scheduled persistent waves, see MTB_KERNEL_TICKS) */
   MTB_KERNEL_FEW = 3,      /* one wave per document, large LDS heap (few documents) */
   MTB_KERNEL_LIVE = 4,     /* live clients (local ops, acks, reconnect) */
   MTB_KERNEL_MARKERS = 5,  /* marker ids / relative positions */
@@ -134,9 +134,9 @@ enum {
 typedef struct mtb_launch_info {
   uint32_t kernel;      /* MTB_KERNEL_* */
   uint32_t wave_slots;  /* resident replay waves of the device (CUs x 16) */
-  uint32_t chunks;      /* MTB_KERNEL_SCHED / _TICKS: tickets per document; MTB_KERNEL_PASSES: chunks per document */
-  uint32_t queues;      /* MTB_KERNEL_SCHED / _TICKS: ticket queues (one per XCD) */
-  uint32_t aborted;     /* MTB_KERNEL_SCHED / _TICKS: a ticket wait hit its bound and the finish kernel ran the rest */
+  uint32_t chunks;      /* MTB_KERNEL_TICKS: tickets per document; MTB_KERNEL_PASSES: chunks per document */
+  uint32_t queues;      /* MTB_KERNEL_TICKS: ticket queues (one per XCD) */
+  uint32_t aborted;     /* MTB_KERNEL_TICKS: a ticket wait hit its bound and the finish kernel ran the rest */
   uint32_t passes;      /* MTB_KERNEL_PASSES: kernel launches of the replay */
 } mtb_launch_info;
 

@@ -149,23 +149,18 @@ def _message_cut(lb, u, frac):
     return m
 
 
-@pytest.mark.parametrize("mode", ["ticks", "tickets"])
 @pytest.mark.parametrize("chunks,queues,spins", [(None, None, None), ("16", None, None), ("3", "1", None),
                                                  (None, None, "0"), ("16", "1", "40")])
-def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, mode, chunks, queues, spins):
+def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, chunks, queues, spins):
     """More documents than the device's resident replay waves runs ticket-scheduled replay -- one ticket per
-    workgroup (mtb_replay_tick_kernel, the default) or persistent waves taking tickets (MTB_SCHED=tickets),
-    documents advanced chunk by chunk in round-robin: 4,608 documents with ragged record counts --
+    workgroup (mtb_replay_tick_kernel), documents advanced chunk by chunk in round-robin: 4,608 documents with ragged record counts --
     whole 300-message logs, message-boundary prefixes of them, and documents with no records -- every
     state digest equal to the oracle's, for the default shrinking-chunk plan and for 16 and 3 equal chunks
     per document (MTB_CHUNKS), per-XCD ticket queues and one global queue (MTB_SCHED_QUEUES=1), and with
     the ticket waits bounded so low that the scheduler aborts (MTB_SCHED_SPINS): the finish kernel then
     replays the rest of every document and the results are the same."""
     monkeypatch.delenv("MTB_CHUNK_PLAN", raising=False)
-    if mode == "tickets":
-        monkeypatch.setenv("MTB_SCHED", "tickets")
-    else:
-        monkeypatch.delenv("MTB_SCHED", raising=False)
+    monkeypatch.delenv("MTB_SCHED", raising=False)
     for var, val in (("MTB_CHUNKS", chunks), ("MTB_SCHED_QUEUES", queues), ("MTB_SCHED_SPINS", spins)):
         if val is None:
             monkeypatch.delenv(var, raising=False)
@@ -175,8 +170,7 @@ def test_scheduled_replay_more_documents_than_wave_slots(monkeypatch, mode, chun
     st = B.replay()
     assert st["errors"] == 0
     li = B.launch_info()
-    kernel = "mtb_replay_sched_kernel" if mode == "tickets" else "mtb_replay_tick_kernel"
-    assert li["kernel"] == kernel and li["wave_slots"] == slots, li
+    assert li["kernel"] == "mtb_replay_tick_kernel" and li["wave_slots"] == slots, li
     if spins == "0":
         assert li["aborted"], li  # every hand-over wait gives up at once
     dg = B.digests()

@@ -3,7 +3,6 @@
   prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
-  rbl/rbd/rbr/rbx                            rebuild() variants for same-box A/B runs
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -17,10 +16,6 @@ VARIANTS = {
     "prof": ["MTB_PROFILE"],
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
-    "rbl": ["MTB_RB_LOADS"],
-    "rbd": ["MTB_RB_LOADS", "MTB_RB_LDS"],
-    "rbr": ["MTB_RB_LOADS", "MTB_RB_REGSORT"],
-    "rbx": ["MTB_RB_LOADS", "MTB_RB_LDS", "MTB_RB_REGSORT"],
 }
 
 if __name__ == "__main__":
