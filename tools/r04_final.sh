@@ -20,6 +20,10 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_B
 rc=$?; echo "sq2 rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --output-format csv -d $O/tcc -o tcc -- python3 $B > $O/tcc.log 2>&1
 rc=$?; echo "tcc rc=$rc"; [ $rc -ne 0 ] && exit $rc
+for v in prof profpack; do  # per-phase cycle counters (MTB_PROFILE builds) on cfg2, tick-scheduled
+  MTB_LIB=fluidframework_amd/libmtb_$v.so MTB_PROFILE_OUT=1 timeout -k 10 600 python3 $B > $O/bench_$v.json 2> $O/bench_$v.err
+  rc=$?; echo "$v rc=$rc"; grep "mtb_profile" $O/bench_$v.err; [ $rc -ne 0 ] && exit $rc
+done
 L="bench.py --workload long-doc --steps 1 --warmup 0 --traffic off --no-summary"
 timeout -k 10 600 python3 -u $L > $O/long_doc.json 2> $O/long_doc.err
 rc=$?; echo "long-doc rc=$rc"; cut -c1-400 $O/long_doc.json; [ $rc -ne 0 ] && exit $rc
