@@ -1681,8 +1681,8 @@ void launch_main(mtb_dev* b, const Tables& t) {
       if (sizes.empty()) {
         if (const char* cv = getenv("MTB_CHUNKS"))
           sizes.assign((size_t)std::max(1, std::min(64, atoi(cv))), 1.0);
-        else  // default: shrinking chunks (6/16, 4/16, 2/16, then four of 1/16): few hand-overs, a fine tail
-          sizes = {6, 4, 2, 1, 1, 1, 1};
+        else  // default: 12/16, 3/16 and 1/16 of every document: three tickets, a fine tail (round-4 sweep)
+          sizes = {12, 3, 1};
       }
       if (sizes.size() > 64) sizes.resize(64);
       while (sizes.size() > 1 && (uint64_t)sizes.size() * b->ndocs > 0x7FFFFFFFull) sizes.pop_back();  // tickets fit 31 bits
