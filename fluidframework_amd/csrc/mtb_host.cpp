@@ -1177,7 +1177,7 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
   c.seg = (uint32_t)(2 * n + 64);
   c.blk = (uint32_t)(n / 2 + 256);
   c.list = (uint32_t)(8 * n + 8192);
-  c.text = (uint32_t)(5 * (payload + init) + 4096);
+  c.text = (uint32_t)(8 * (payload + init) + 4096);  // (scour's appends re-copy merged runs: text outgrows payload)
   c.heap = (uint32_t)(n + 256);
   c.aux = (uint32_t)(16 * n + 4096);
   return c;
@@ -1751,7 +1751,9 @@ void replay(mtb_dev* b, mtb_stats* out) {
     for (uint32_t i = 0; i < b->ndocs; i++) {
       HostDoc& d = b->docs[i];
       const DocState& s = b->hst[i];
-      Caps need = doc_caps(d, d.totalOps, d.totalPayload + s.text_used);
+      // (the same requirement device_init laid the slices out for: caps_for's text term already counts the
+      // initial text, so adding text_used here made every fresh batch re-lay out at twice the caps)
+      Caps need = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
       if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap ||
           (d.perm && 2 * (d.totalSetcell + d.initText.size() / 2 + 4) > s.text_cap)) {
         want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
