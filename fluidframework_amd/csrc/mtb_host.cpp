@@ -1177,7 +1177,10 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
   c.seg = (uint32_t)(2 * n + 64);
   c.blk = (uint32_t)(n / 2 + 256);
   c.list = (uint32_t)(8 * n + 8192);
-  c.text = (uint32_t)(8 * (payload + init) + 4096);  // (scour's appends re-copy merged runs: text outgrows payload)
+  // text: scour's appends re-copy merged runs, so the arena outgrows the payload (cfg2 documents use ~5.7x their
+  // payload, the 1M-char cfg4 document ~16x: its long initial segments are split and re-merged); the initial
+  // text counts 15x for that reason (these were the caps every batch ran with through round 3)
+  c.text = (uint32_t)std::min<uint64_t>(10 * payload + 15 * init + 4096, 0xFFFFFFF0u);
   c.heap = (uint32_t)(n + 256);
   c.aux = (uint32_t)(16 * n + 4096);
   return c;
