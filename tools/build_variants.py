@@ -3,6 +3,7 @@
   prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
+  heap      MTB_HEAP_SUBTREE                 LRU heap fixDown five levels per round trip (A/B candidate)
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -16,6 +17,7 @@ VARIANTS = {
     "prof": ["MTB_PROFILE"],
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
+    "heap": ["MTB_HEAP_SUBTREE"],
 }
 
 if __name__ == "__main__":
