@@ -1450,20 +1450,6 @@ struct Eng {
     x.maxSeq = U(x.maxSeq);
     return x;
   }
-  // entry k of this lane (k differs across lanes)
-  __device__ __forceinline__ Lru hget_lane(uint32_t k) const {
-    Lru x;
-    if (heap_lds) {
-      const u32x2 y = *reinterpret_cast<const u32x2*>(&sh->heap[k]);
-      x.seg = y.x;
-      x.maxSeq = (int)y.y;
-    } else {
-      const auto g = UP(sh->gheap) + k;
-      x.seg = g->seg;
-      x.maxSeq = g->maxSeq;
-    }
-    return x;
-  }
   // children j and j + 1 (j even) with one round trip: a 16-byte LDS read, or two global loads in flight
   __device__ __forceinline__ void hget2(uint32_t j, Lru& a, Lru& b) const {
     if (heap_lds) {
@@ -1527,50 +1513,6 @@ struct Eng {
     const uint32_t count = heap_cnt;
     uint32_t k = 1;
     // fixDown with the last element placed at the root (collections/heap.ts:50-64)
-#ifdef MTB_HEAP_SUBTREE
-    // Five levels per round trip: lane L loads node (k << l) + L + 2 - 2^l of the subtree below k (l = the
-    // level of lane L, 1..5; lanes 62/63 idle), then the descent picks children out of the lanes.  The moves
-    // store to the path above the subtree, which the next round's loads (strictly below) never read.
-    const int lvl = 31 - __clz((int)lane + 2);
-    while ((k << 1) <= count) {
-      const uint32_t node = (k << lvl) + (uint32_t)lane + 2u - (1u << lvl);
-      uint32_t vs = 0, vm = 0;
-      if (lane < 62 && node <= count) {
-        const Lru x = hget_lane(node);
-        vs = x.seg;
-        vm = (uint32_t)x.maxSeq;
-      }
-      uint32_t rel = 0;
-      int lev = 0;
-      bool stop = false;
-      for (; lev < 5; lev++) {
-        const uint32_t cur = (k << lev) + rel, j = cur << 1;
-        if (j > count) {
-          stop = true;
-          break;
-        }
-        const int L = (2 << lev) - 2 + 2 * (int)rel;
-        Lru a, bb;
-        a.seg = rlu(vs, L);
-        a.maxSeq = rl((int)vm, L);
-        bb.seg = rlu(vs, L + 1);
-        bb.maxSeq = rl((int)vm, L + 1);
-        uint32_t r2 = rel << 1;
-        if (j < count && a.maxSeq - bb.maxSeq > 0) {
-          r2++;
-          a = bb;
-        }
-        if (last.maxSeq - a.maxSeq <= 0) {
-          stop = true;
-          break;
-        }
-        hset(cur, a);
-        rel = r2;
-      }
-      k = (k << lev) + rel;
-      if (stop) break;
-    }
-#else
     while ((k << 1) <= count) {
       uint32_t j = k << 1;
       Lru a, bb;
@@ -1583,7 +1525,6 @@ struct Eng {
       hset(k, a);
       k = j;
     }
-#endif
     if (count >= 1) hset(k, last);
     return top;
   }

@@ -3,7 +3,6 @@
   prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
-  heap      MTB_HEAP_SUBTREE                 LRU heap fixDown five levels per round trip (A/B candidate)
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -17,7 +16,6 @@ VARIANTS = {
     "prof": ["MTB_PROFILE"],
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
-    "heap": ["MTB_HEAP_SUBTREE"],
 }
 
 if __name__ == "__main__":
