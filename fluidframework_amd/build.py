@@ -42,15 +42,15 @@ def _headers():
         [os.path.join(ROOT, "include", "mtb.h")]
 
 
-def build(force=False, arch="gfx950", out=OUT, defines=()):
+def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
     if not force and out == OUT and not needs_build():
         return OUT
     from concurrent.futures import ThreadPoolExecutor
-    tag = "_".join(d.replace("=", "") for d in defines) or "base"
+    tag = "_".join([d.replace("=", "") for d in defines] + [x.strip("-").replace("-", "") for x in extra]) or "base"
     odir = os.path.join(OBJ_DIR, f"{arch}_{tag}")
     os.makedirs(odir, exist_ok=True)
     base = ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
-        [f"-D{d}" for d in defines]
+        [f"-D{d}" for d in defines] + list(extra)
     jobs = []  # (object, command, sources it depends on)
     hip = SRCS[0]
     for g in KERNEL_GROUPS:
