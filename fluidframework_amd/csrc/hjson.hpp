@@ -244,45 +244,77 @@ inline U16 from_utf8(const std::string& s) {
   return out;
 }
 
-// JSON.stringify string quoting (well-formed: lone surrogates escaped as \udXXX)
-inline void quote(std::string& o, const char16_t* s, size_t n) {
+// JSON.stringify string quoting (well-formed: lone surrogates escaped as \udXXX).  Writes through a pointer into
+// room made up front: before unit i the string holds at least (n - i) + 1 unwritten bytes (one per remaining
+// unit plus the closing quote), and an escape makes room for its own expansion.  Returns whether every unit was
+// below 0x80 (the output is then ASCII).
+inline bool quote16(std::string& o, const char16_t* s, size_t n) {
   static const char kHex[] = "0123456789abcdef";
-  o.reserve(o.size() + n + 2);
-  o += '"';
+  size_t at = o.size();
+  o.resize(at + n + 18);
+  char* w = &o[0];
+  w[at++] = '"';
+  bool ascii = true;
   for (size_t i = 0; i < n; i++) {
     const uint32_t c = s[i];
     if (c >= 0x20 && c < 0x80 && c != 0x22 && c != 0x5C) {  // (the common case first)
-      o.push_back((char)c);
+      w[at++] = (char)c;
       continue;
     }
-    const char* esc = nullptr;
+    if (at + 14 + (n - i) > o.size()) {
+      o.resize((at + 14 + (n - i)) * 5 / 4 + 16);
+      w = &o[0];
+    }
+    char e2 = 0;
     switch (c) {
-      case 0x22: esc = "\\\""; break;
-      case 0x5C: esc = "\\\\"; break;
-      case 0x08: esc = "\\b"; break;
-      case 0x0C: esc = "\\f"; break;
-      case 0x0A: esc = "\\n"; break;
-      case 0x0D: esc = "\\r"; break;
-      case 0x09: esc = "\\t"; break;
+      case 0x22: e2 = '"'; break;
+      case 0x5C: e2 = '\\'; break;
+      case 0x08: e2 = 'b'; break;
+      case 0x0C: e2 = 'f'; break;
+      case 0x0A: e2 = 'n'; break;
+      case 0x0D: e2 = 'r'; break;
+      case 0x09: e2 = 't'; break;
       default: break;
     }
-    if (esc) { o += esc; continue; }
+    if (e2) {
+      w[at++] = '\\';
+      w[at++] = e2;
+      continue;
+    }
+    if (c >= 0x80) ascii = false;
     const bool lead = c >= 0xD800 && c < 0xDC00, trail = c >= 0xDC00 && c < 0xE000;
+    uint32_t cp = c;
     if (lead && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] < 0xE000) {
-      put_utf8(o, 0x10000 + ((c - 0xD800) << 10) + (s[i + 1] - 0xDC00));
+      cp = 0x10000 + ((c - 0xD800) << 10) + (s[i + 1] - 0xDC00);
       i++;
     } else if (c < 0x20 || lead || trail) {
-      o += "\\u";
-      o += kHex[(c >> 12) & 15];
-      o += kHex[(c >> 8) & 15];
-      o += kHex[(c >> 4) & 15];
-      o += kHex[c & 15];
+      w[at++] = '\\';
+      w[at++] = 'u';
+      w[at++] = kHex[(c >> 12) & 15];
+      w[at++] = kHex[(c >> 8) & 15];
+      w[at++] = kHex[(c >> 4) & 15];
+      w[at++] = kHex[c & 15];
+      continue;
+    }
+    if (cp < 0x800) {
+      w[at++] = (char)(0xC0 | (cp >> 6));
+      w[at++] = (char)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      w[at++] = (char)(0xE0 | (cp >> 12));
+      w[at++] = (char)(0x80 | ((cp >> 6) & 0x3F));
+      w[at++] = (char)(0x80 | (cp & 0x3F));
     } else {
-      put_utf8(o, c);
+      w[at++] = (char)(0xF0 | (cp >> 18));
+      w[at++] = (char)(0x80 | ((cp >> 12) & 0x3F));
+      w[at++] = (char)(0x80 | ((cp >> 6) & 0x3F));
+      w[at++] = (char)(0x80 | (cp & 0x3F));
     }
   }
-  o += '"';
+  w[at++] = '"';
+  o.resize(at);
+  return ascii;
 }
+inline void quote(std::string& o, const char16_t* s, size_t n) { quote16(o, s, n); }
 inline void quote(std::string& o, const U16& s) { quote(o, s.data(), s.size()); }
 
 // Length of the well-formed UTF-8 sequence at p (1-4 bytes), or 0 for an invalid one or an encoded surrogate.
@@ -305,47 +337,60 @@ inline size_t utf8_seq(const uint8_t* p, const uint8_t* e) {
 }
 // quote(o, from_utf8(u)) without the UTF-16 round trip, for u well-formed UTF-8 without encoded surrogates (what
 // these serializers produce): bytes pass through and only '"', '\\' and control characters are escaped, exactly
-// as quote() escapes the same code points.  Returns false, leaving o as it was, for any other u.
+// as quote() escapes the same code points.  Returns false, leaving o as it was, for any other u.  Pointer writes
+// with the room rule of quote16 (one byte per remaining input byte, plus the closing quote).
 inline bool quote_utf8(std::string& o, const std::string& u) {
   static const char kHex[] = "0123456789abcdef";
   const size_t base = o.size();
-  o.reserve(base + u.size() + u.size() / 8 + 2);
-  o += '"';
+  o.resize(base + u.size() + u.size() / 4 + 18);
+  char* w = &o[0];
+  size_t at = base;
+  w[at++] = '"';
   const uint8_t* p = reinterpret_cast<const uint8_t*>(u.data());
   const uint8_t* const e = p + u.size();
-  const uint8_t* run = p;
   while (p < e) {
     const uint8_t c = *p;
     if (c >= 0x20 && c != 0x22 && c != 0x5C && c < 0x80) {
+      w[at++] = (char)c;
       p++;
       continue;
     }
-    o.append(reinterpret_cast<const char*>(run), (size_t)(p - run));
+    if (at + 8 + (size_t)(e - p) > o.size()) {
+      o.resize((at + 8 + (size_t)(e - p)) * 5 / 4 + 16);
+      w = &o[0];
+    }
     if (c >= 0x80) {
       const size_t n = utf8_seq(p, e);
       if (!n) {
         o.resize(base);
         return false;
       }
-      o.append(reinterpret_cast<const char*>(p), n);
+      memcpy(w + at, p, n);
+      at += n;
       p += n;
-    } else {
-      switch (c) {
-        case 0x22: o += "\\\""; break;
-        case 0x5C: o += "\\\\"; break;
-        case 0x08: o += "\\b"; break;
-        case 0x0C: o += "\\f"; break;
-        case 0x0A: o += "\\n"; break;
-        case 0x0D: o += "\\r"; break;
-        case 0x09: o += "\\t"; break;
-        default: o += "\\u00"; o += kHex[c >> 4]; o += kHex[c & 15]; break;
-      }
-      p++;
+      continue;
     }
-    run = p;
+    w[at++] = '\\';
+    switch (c) {
+      case 0x22: w[at++] = '"'; break;
+      case 0x5C: w[at++] = '\\'; break;
+      case 0x08: w[at++] = 'b'; break;
+      case 0x0C: w[at++] = 'f'; break;
+      case 0x0A: w[at++] = 'n'; break;
+      case 0x0D: w[at++] = 'r'; break;
+      case 0x09: w[at++] = 't'; break;
+      default:
+        w[at++] = 'u';
+        w[at++] = '0';
+        w[at++] = '0';
+        w[at++] = kHex[c >> 4];
+        w[at++] = kHex[c & 15];
+        break;
+    }
+    p++;
   }
-  o.append(reinterpret_cast<const char*>(run), (size_t)(p - run));
-  o += '"';
+  w[at++] = '"';
+  o.resize(at);
   return true;
 }
 // quote(o, from_utf8(u)) by the fast path when it applies

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <charconv>
 #include <map>
 #include <mutex>
 #include <optional>
@@ -2155,7 +2156,15 @@ uint64_t utf8_byte_length(const std::string& utf8) {
     const uint8_t* p = reinterpret_cast<const uint8_t*>(utf8.data());
     const uint8_t* const e = p + utf8.size();
     size_t n = 1;
-    while (p < e && (n = *p < 0x80 ? 1 : hj::utf8_seq(p, e)) != 0) p += n;
+    while (p < e) {
+      uint64_t w8;
+      if (e - p >= 8 && (memcpy(&w8, p, 8), (w8 & 0x8080808080808080ull) == 0)) {  // eight ASCII bytes
+        p += 8;
+        continue;
+      }
+      if ((n = *p < 0x80 ? 1 : hj::utf8_seq(p, e)) == 0) break;
+      p += n;
+    }
     if (p == e) return utf8.size();
   }
   U16 s = hj::from_utf8(utf8);
@@ -2324,61 +2333,113 @@ void summarize(mtb_dev* b, uint32_t i, std::vector<std::pair<std::string, std::s
 
 // SnapshotV1.emit (snapshotV1.ts:122-178): the serialized segments cut into chunks of about chunkSize
 // UTF-16 units (header + body_i) and the summary tree's blobs (runtime-utils summaryUtils.ts:138-198)
-void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::string>& segJson, const std::vector<int>& segLen,
-                    std::vector<std::pair<std::string, std::string>>& blobs, std::string& tree, uint64_t& totalBytes) {
-  const int chunkSize = b->opts.chunk_size > 0 ? b->opts.chunk_size : 10000;
-  struct Chunk { int start = 0, count = 0, length = 0; };
-  std::vector<Chunk> chunks;
+struct V1Chunk {
+  int start = 0, count = 0, length = 0;
+};
+struct V1Chunks {
+  std::vector<V1Chunk> c;
   int totalCount = 0, totalLength = 0;
+};
+void append_int(std::string& o, int64_t v) {
+  char buf[24];
+  const auto r = std::to_chars(buf, buf + sizeof buf, v);
+  o.append(buf, (size_t)(r.ptr - buf));
+}
+V1Chunks v1_chunks(mtb_dev* b, const std::vector<int>& segLen) {
+  const int chunkSize = b->opts.chunk_size > 0 ? b->opts.chunk_size : 10000;
+  V1Chunks r;
   do {
-    Chunk c;
-    c.start = totalCount;
-    while (c.length < chunkSize && c.start + c.count < (int)segJson.size()) {
+    V1Chunk c;
+    c.start = r.totalCount;
+    while (c.length < chunkSize && c.start + c.count < (int)segLen.size()) {
       c.length += segLen[c.start + c.count];
       c.count++;
     }
-    chunks.push_back(c);
-    totalCount += c.count;
-    totalLength += c.length;
-  } while (totalCount < (int)segJson.size());
-  auto chunkText = [&](const Chunk& c, bool header) {
-    size_t bytes = 256 + 24 * chunks.size();
-    for (int k = 0; k < c.count; k++) bytes += segJson[c.start + k].size() + 1;
-    std::string o;
-    o.reserve(bytes);
-    o += "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) + ",\"length\":" + std::to_string(c.length) +
-         ",\"segments\":[";
-    for (int k = 0; k < c.count; k++) {
-      if (k) o += ',';
-      o += segJson[c.start + k];
-    }
-    o += "],\"startIndex\":" + std::to_string(c.start);
-    if (header) {
-      o += ",\"headerMetadata\":{\"minSequenceNumber\":" + std::to_string(minSeq) + ",\"sequenceNumber\":" + std::to_string(curSeq) +
-           ",\"orderedChunkMetadata\":[";
-      for (size_t k = 0; k < chunks.size(); k++) {
-        if (k) o += ',';
-        o += k == 0 ? std::string("{\"id\":\"header\"}") : "{\"id\":\"body_" + std::to_string(k - 1) + "\"}";
+    r.c.push_back(c);
+    r.totalCount += c.count;
+    r.totalLength += c.length;
+  } while (r.totalCount < (int)segLen.size());
+  return r;
+}
+void v1_chunk_open(std::string& o, const V1Chunk& c) {
+  o += "{\"version\":\"1\",\"segmentCount\":";
+  append_int(o, c.count);
+  o += ",\"length\":";
+  append_int(o, c.length);
+  o += ",\"segments\":[";
+}
+void v1_chunk_close(std::string& o, const V1Chunks& cs, size_t k, int minSeq, int curSeq) {
+  o += "],\"startIndex\":";
+  append_int(o, cs.c[k].start);
+  if (k == 0) {
+    o += ",\"headerMetadata\":{\"minSequenceNumber\":";
+    append_int(o, minSeq);
+    o += ",\"sequenceNumber\":";
+    append_int(o, curSeq);
+    o += ",\"orderedChunkMetadata\":[";
+    for (size_t q = 0; q < cs.c.size(); q++) {
+      if (q) o += ',';
+      if (q == 0) {
+        o += "{\"id\":\"header\"}";
+      } else {
+        o += "{\"id\":\"body_";
+        append_int(o, (int64_t)q - 1);
+        o += "\"}";
       }
-      o += "],\"totalLength\":" + std::to_string(totalLength) + ",\"totalSegmentCount\":" + std::to_string(totalCount) + "}";
     }
+    o += "],\"totalLength\":";
+    append_int(o, cs.totalLength);
+    o += ",\"totalSegmentCount\":";
+    append_int(o, cs.totalCount);
     o += "}";
-    return o;
-  };
-  blobs.clear();
-  blobs.push_back({"header", chunkText(chunks[0], true)});
-  for (size_t k = 1; k < chunks.size(); k++) blobs.push_back({"body_" + std::to_string(k - 1), chunkText(chunks[k], false)});
-  // ISummaryTreeWithStats (runtime-utils summaryUtils.ts:138-198)
-  tree = "{";
+  }
+  o += "}";
+}
+std::string v1_blob_name(size_t k) { return k == 0 ? std::string("header") : "body_" + std::to_string(k - 1); }
+// ISummaryTreeWithStats.summary.tree of the blobs (runtime-utils summaryUtils.ts:138-198), appended to o
+void v1_tree(std::string& o, const std::vector<std::pair<std::string, std::string>>& blobs, uint64_t& totalBytes) {
+  o += '{';
   totalBytes = 0;
   for (size_t k = 0; k < blobs.size(); k++) {
-    if (k) tree += ',';
-    tree += "\"" + blobs[k].first + "\":{\"type\":2,\"content\":";
-    hj::quote_u8(tree, blobs[k].second);
-    tree += "}";
+    if (k) o += ',';
+    o += '"';
+    o += blobs[k].first;
+    o += "\":{\"type\":2,\"content\":";
+    hj::quote_u8(o, blobs[k].second);
+    o += '}';
     totalBytes += utf8_byte_length(blobs[k].second);
   }
-  tree += "}";
+  o += '}';
+}
+void v1_stats(std::string& o, int treeNodeCount, size_t blobNodeCount, uint64_t totalBytes) {
+  o += "},\"stats\":{\"treeNodeCount\":";
+  append_int(o, treeNodeCount);
+  o += ",\"blobNodeCount\":";
+  append_int(o, (int64_t)blobNodeCount);
+  o += ",\"handleNodeCount\":0,\"totalBlobSize\":";
+  append_int(o, (int64_t)totalBytes);
+  o += ",\"unreferencedBlobSize\":0}}";
+}
+void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::string>& segJson, const std::vector<int>& segLen,
+                    std::vector<std::pair<std::string, std::string>>& blobs, std::string& tree, uint64_t& totalBytes) {
+  const V1Chunks cs = v1_chunks(b, segLen);
+  blobs.clear();
+  for (size_t k = 0; k < cs.c.size(); k++) {
+    const V1Chunk& c = cs.c[k];
+    size_t bytes = 256 + 24 * cs.c.size();
+    for (int q = 0; q < c.count; q++) bytes += segJson[c.start + q].size() + 1;
+    std::string o;
+    o.reserve(bytes);
+    v1_chunk_open(o, c);
+    for (int q = 0; q < c.count; q++) {
+      if (q) o += ',';
+      o += segJson[c.start + q];
+    }
+    v1_chunk_close(o, cs, k, minSeq, curSeq);
+    blobs.push_back({v1_blob_name(k), std::move(o)});
+  }
+  tree.clear();
+  v1_tree(tree, blobs, totalBytes);
 }
 
 // SnapshotV1 of a SharedString document from the device extraction (mtb_extract_v1_kernel): the same JSON
@@ -2388,10 +2449,6 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
   const HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
   const int minSeq = s.min_seq, curSeq = s.cur_seq;
-  std::vector<std::string> segJson;
-  std::vector<int> segLen;
-  segJson.reserve(ni);
-  segLen.reserve(ni);
   auto pview = [&](uint32_t h) {
     PropView v;
     if (!h) return v;
@@ -2399,45 +2456,51 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
     else v.p = words + (h & ~EX_INLINE_HOST);
     return v;
   };
-  for (uint32_t k = 0; k < ni; k++) {
-    const uint32_t* it = items + 8 * (size_t)k;
+  // the chunks first (they depend on the segment lengths only), then every segment's JSON written straight
+  // into its chunk's blob: the bytes of summarize()'s segJson + emit_v1_chunks, without the per-segment strings
+  std::vector<int> segLen(ni);
+  for (uint32_t k = 0; k < ni; k++) segLen[k] = (int)items[8 * (size_t)k + 1];
+  const V1Chunks cs = v1_chunks(b, segLen);
+  auto seg_json = [&](std::string& o, const uint32_t* it) {
     const uint32_t fl = it[0], len = it[1], toff = it[2];
     const bool marker = (fl & 2u) != 0;
     const uint32_t refType = fl >> 8;
-    std::string o;
     PropView pv = pview(it[3]);
     const bool hasProps = pv.n() > 0;  // empty props normalized to undefined (snapshotV1.ts:199-206)
-    std::string js;
+    const bool info = (fl & 1u) != 0;  // else a coalesced (or single) segment below the MSN: its JSON alone
+    if (info) o += "{\"json\":";
     if (marker) {
-      js += "{\"marker\":{";
-      if (refType) js += "\"refType\":" + std::to_string(refType - 1);
-      js += "}";
-      if (hasProps) { js += ",\"props\":"; props_json(b, js, pv); }
-      js += "}";
+      o += "{\"marker\":{";
+      if (refType) {
+        o += "\"refType\":";
+        append_int(o, (int64_t)refType - 1);
+      }
+      o += "}";
+      if (hasProps) { o += ",\"props\":"; props_json(b, o, pv); }
+      o += "}";
     } else if (hasProps) {
-      js += "{\"text\":";
-      hj::quote(js, reinterpret_cast<const char16_t*>(txt + toff), len);
-      js += ",\"props\":";
-      props_json(b, js, pv);
-      js += "}";
+      o += "{\"text\":";
+      hj::quote(o, reinterpret_cast<const char16_t*>(txt + toff), len);
+      o += ",\"props\":";
+      props_json(b, o, pv);
+      o += "}";
     } else {
-      hj::quote(js, reinterpret_cast<const char16_t*>(txt + toff), len);
+      hj::quote(o, reinterpret_cast<const char16_t*>(txt + toff), len);
     }
-    if (!(fl & 1u)) {  // a coalesced (or single) segment below the MSN
-      segJson.push_back(std::move(js));
-      segLen.push_back((int)len);
-      continue;
-    }
+    if (!info) return;
     const int seq = (int)it[4], rseq = (int)it[6];
     const uint32_t cli = it[5];
-    o = "{\"json\":" + js;
     if (seq > minSeq) {
-      o += ",\"seq\":" + std::to_string(seq) + ",\"client\":";
+      o += ",\"seq\":";
+      append_int(o, seq);
+      o += ",\"client\":";
       hj::quote_u8(o, d.longId((int)(int16_t)(cli & 0xFFFF)));
     }
     if (rseq >= 0) {
       const int rc0 = (int)(int16_t)(cli >> 16);
-      o += ",\"removedSeq\":" + std::to_string(rseq) + ",\"removedClient\":";
+      o += ",\"removedSeq\":";
+      append_int(o, rseq);
+      o += ",\"removedClient\":";
       hj::quote_u8(o, d.longId(rc0));
       o += ",\"removedClientIds\":[";
       hj::quote_u8(o, d.longId(rc0));
@@ -2451,15 +2514,28 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
       o += "]";
     }
     o += "}";
-    segJson.push_back(std::move(o));
-    segLen.push_back((int)len);
+  };
+  blobs.clear();
+  size_t blobBytes = 0;
+  for (size_t k = 0; k < cs.c.size(); k++) {
+    const V1Chunk& c = cs.c[k];
+    std::string o;
+    o.reserve((size_t)c.length + (size_t)c.length / 8 + 64 * (size_t)c.count + 256 + 24 * cs.c.size());
+    v1_chunk_open(o, c);
+    for (int q = 0; q < c.count; q++) {
+      if (q) o += ',';
+      seg_json(o, items + 8 * (size_t)(c.start + q));
+    }
+    v1_chunk_close(o, cs, k, minSeq, curSeq);
+    blobBytes += o.size();
+    blobs.push_back({v1_blob_name(k), std::move(o)});
   }
-  std::string tree;
+  summaryJson.clear();
+  summaryJson.reserve(blobBytes + blobBytes / 4 + 256);
+  summaryJson += "{\"summary\":{\"type\":1,\"tree\":";
   uint64_t totalBytes = 0;
-  emit_v1_chunks(b, minSeq, curSeq, segJson, segLen, blobs, tree, totalBytes);
-  summaryJson = "{\"summary\":{\"type\":1,\"tree\":" + tree + "},\"stats\":{\"treeNodeCount\":1,\"blobNodeCount\":" +
-                std::to_string(blobs.size()) + ",\"handleNodeCount\":0,\"totalBlobSize\":" + std::to_string(totalBytes) +
-                ",\"unreferencedBlobSize\":0}}";
+  v1_tree(summaryJson, blobs, totalBytes);
+  v1_stats(summaryJson, 1, blobs.size(), totalBytes);
 }
 
 // mtb_extract_v1_kernel over documents `ids` (count pass, offsets, emit pass, one download per output).
