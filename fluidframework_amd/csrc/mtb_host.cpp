@@ -451,6 +451,11 @@ struct mtb_dev {
   DevBuf<uint32_t> dAux, dFree;
   DevBuf<uint32_t> dPool, dPidx, dValClass, dKeyRank;
   DevBuf<uint8_t> dValFalsy;
+  // host staging of the SnapshotV1 extraction (extract_docs), kept and reused by later summaries: a call does
+  // not pay for freeing (or re-faulting) the previous call's hundreds of MB
+  std::unique_ptr<uint32_t[]> exItems, exWords;
+  std::unique_ptr<uint16_t[]> exText;
+  size_t exItemsCap = 0, exWordsCap = 0, exTextCap = 0;
   DevBuf<uint64_t> dKHash, dVHash;  // state digest: FNV-1a of each key's UTF-8 / each value's JSON text
   DevBuf<uint64_t> dDigest;         // per document {digest, segments, observer length} of the last replay
   std::vector<uint64_t> digests;
@@ -2540,13 +2545,23 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
 
 // mtb_extract_v1_kernel over documents `ids` (count pass, offsets, emit pass, one download per output).
 // ok[k]: document ids[k] was extracted (a SharedString document replayed without error).
-struct Extracted {
+struct Extracted {  // (items / text / words point into the batch's staging buffers)
   std::vector<uint8_t> ok;
   std::vector<uint32_t> cnt;
   std::vector<uint64_t> off;
-  std::unique_ptr<uint32_t[]> items, words;
-  std::unique_ptr<uint16_t[]> text;
+  const uint32_t* items = nullptr;
+  const uint32_t* words = nullptr;
+  const uint16_t* text = nullptr;
 };
+template <class T>
+T* staging(std::unique_ptr<T[]>& p, size_t& cap, size_t need) {
+  if (need > cap) {
+    p.reset();
+    p.reset(new T[need]);
+    cap = need;
+  }
+  return p.get();
+}
 void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
   const uint32_t n = (uint32_t)ids.size();
   ex.ok.assign(n, 0);
@@ -2596,12 +2611,15 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
   HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
   HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
                                b->dValClass.p, dc.p, doff.p, dItems.p, dText.p, dWords.p));
-  ex.items.reset(new uint32_t[8 * ti + 8]);
-  ex.text.reset(new uint16_t[tt + 1]);
-  ex.words.reset(new uint32_t[tw + 1]);
-  if (ti) HIPCHK(hipMemcpyAsync(ex.items.get(), dItems.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-  if (tt) HIPCHK(hipMemcpyAsync(ex.text.get(), dText.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
-  if (tw) HIPCHK(hipMemcpyAsync(ex.words.get(), dWords.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  uint32_t* hItems = staging(b->exItems, b->exItemsCap, 8 * ti + 8);
+  uint16_t* hText = staging(b->exText, b->exTextCap, tt + 1);
+  uint32_t* hWords = staging(b->exWords, b->exWordsCap, tw + 1);
+  ex.items = hItems;
+  ex.text = hText;
+  ex.words = hWords;
+  if (ti) HIPCHK(hipMemcpyAsync(hItems, dItems.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  if (tt) HIPCHK(hipMemcpyAsync(hText, dText.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
+  if (tw) HIPCHK(hipMemcpyAsync(hWords, dWords.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
 }
 
@@ -2609,7 +2627,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
 void summarize_any(mtb_dev* b, uint32_t doc, std::vector<std::pair<std::string, std::string>>& blobs, std::string& summary) {
   Extracted ex;
   extract_docs(b, {doc}, ex);
-  if (ex.ok[0]) summarize_items(b, doc, ex.items.get(), ex.cnt[0], ex.text.get(), ex.words.get(), blobs, summary);
+  if (ex.ok[0]) summarize_items(b, doc, ex.items, ex.cnt[0], ex.text, ex.words, blobs, summary);
   else summarize(b, doc, blobs, summary);
 }
 
@@ -3813,8 +3831,8 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
           std::vector<std::pair<std::string, std::string>> blobs;
           std::string summary;
           if (ex.ok[k]) {
-            summarize_items(b, list[k], ex.items.get() + ex.off[3 * k], ex.cnt[3 * k], ex.text.get() + ex.off[3 * k + 1],
-                            ex.words.get() + ex.off[3 * k + 2], blobs, summary);
+            summarize_items(b, list[k], ex.items + ex.off[3 * k], ex.cnt[3 * k], ex.text + ex.off[3 * k + 1],
+                            ex.words + ex.off[3 * k + 2], blobs, summary);
           } else {
             summarize(b, list[k], blobs, summary);
           }
