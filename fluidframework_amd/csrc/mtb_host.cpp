@@ -15,9 +15,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <atomic>
 #include <charconv>
 #include <map>
+#include <condition_variable>
 #include <mutex>
 #include <optional>
 #include <cmath>
@@ -456,6 +458,8 @@ struct mtb_dev {
   std::unique_ptr<uint32_t[]> exItems, exWords;
   std::unique_ptr<uint16_t[]> exText;
   size_t exItemsCap = 0, exWordsCap = 0, exTextCap = 0;
+  DevBuf<uint32_t> dExItems, dExWords;  // ... and its device output (no hipFree, which waits for the device, per call)
+  DevBuf<uint16_t> dExText;
   DevBuf<uint64_t> dKHash, dVHash;  // state digest: FNV-1a of each key's UTF-8 / each value's JSON text
   DevBuf<uint64_t> dDigest;         // per document {digest, segments, observer length} of the last replay
   std::vector<uint64_t> digests;
@@ -2543,7 +2547,6 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
   v1_stats(summaryJson, 1, blobs.size(), totalBytes);
 }
 
-// mtb_extract_v1_kernel over documents `ids` (count pass, offsets, emit pass, one download per output).
 // ok[k]: document ids[k] was extracted (a SharedString document replayed without error).
 struct Extracted {  // (items / text / words point into the batch's staging buffers)
   std::vector<uint8_t> ok;
@@ -2552,6 +2555,34 @@ struct Extracted {  // (items / text / words point into the batch's staging buff
   const uint32_t* items = nullptr;
   const uint32_t* words = nullptr;
   const uint16_t* text = nullptr;
+  // Download in pieces (extract_docs with pieces > 1): piece p holds the outputs of the extracted documents
+  // [first[p], first[p + 1]) in extraction order; copy_piece() downloads one and marks it ready, and a
+  // serializer thread waits (wait_doc) only for the piece of the document it takes.
+  uint32_t npieces = 0;
+  std::vector<uint32_t> pieceOf;               // position in ids -> piece (extracted documents)
+  std::vector<std::array<uint64_t, 3>> first;  // per piece + 1: items word, text unit, words word offsets
+  uint32_t* hItems = nullptr;
+  uint32_t* hWords = nullptr;
+  uint16_t* hText = nullptr;
+  std::unique_ptr<std::atomic<int>[]> ready;   // 1 copied, -1 failed
+  std::mutex mu;
+  std::condition_variable cv;
+  bool wait_doc(uint32_t k) {  // false: the download failed
+    if (!npieces) return true;
+    std::atomic<int>& r = ready[pieceOf[k]];
+    if (r.load(std::memory_order_acquire) == 0) {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return r.load(std::memory_order_acquire) != 0; });
+    }
+    return r.load(std::memory_order_acquire) > 0;
+  }
+  void mark(uint32_t p, int v) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      ready[p].store(v, std::memory_order_release);
+    }
+    cv.notify_all();
+  }
 };
 template <class T>
 T* staging(std::unique_ptr<T[]>& p, size_t& cap, size_t need) {
@@ -2562,11 +2593,25 @@ T* staging(std::unique_ptr<T[]>& p, size_t& cap, size_t need) {
   }
   return p.get();
 }
-void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
+void copy_piece(mtb_dev* b, Extracted& ex, uint32_t p) {
+  const auto& a = ex.first[p];
+  const auto& z = ex.first[p + 1];
+  if (z[0] > a[0])
+    HIPCHK(hipMemcpyAsync(ex.hItems + a[0], b->dExItems.p + a[0], (z[0] - a[0]) * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  if (z[1] > a[1])
+    HIPCHK(hipMemcpyAsync(ex.hText + a[1], b->dExText.p + a[1], (z[1] - a[1]) * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
+  if (z[2] > a[2])
+    HIPCHK(hipMemcpyAsync(ex.hWords + a[2], b->dExWords.p + a[2], (z[2] - a[2]) * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+}
+// mtb_extract_v1_kernel over documents `ids` (count pass, offsets, emit pass).  pieces <= 1: the outputs are
+// downloaded before it returns; else the caller downloads them with copy_piece(0 .. ex.npieces - 1).
+void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, uint32_t pieces = 1) {
   const uint32_t n = (uint32_t)ids.size();
   ex.ok.assign(n, 0);
   ex.cnt.assign(3 * (size_t)n + 3, 0);
   ex.off.assign(3 * (size_t)n + 3, 0);
+  ex.npieces = 0;
   std::vector<uint32_t> dev;  // positions in ids
   for (uint32_t k = 0; k < n; k++) {
     const uint32_t i = ids[k];
@@ -2578,8 +2623,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
   if (!nf) return;
   std::vector<uint32_t> di(nf), cnt(3 * (size_t)nf);
   for (uint32_t f = 0; f < nf; f++) di[f] = ids[dev[f]];
-  DevBuf<uint32_t> dl, dc, dItems, dWords;
-  DevBuf<uint16_t> dText;
+  DevBuf<uint32_t> dl, dc;
   DevBuf<uint64_t> doff;
   dl.ensure(nf);
   dc.ensure(3 * (size_t)nf);
@@ -2604,23 +2648,35 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex) {
     ex.cnt[3 * k] = cnt[3 * f];
     for (int q = 0; q < 3; q++) ex.off[3 * k + q] = off[3 * f + q];
   }
-  dItems.ensure(8 * ti + 8);
-  dText.ensure(tt + 1);
-  dWords.ensure(tw + 1);
+  b->dExItems.ensure(8 * ti + 8);
+  b->dExText.ensure(tt + 1);
+  b->dExWords.ensure(tw + 1);
   doff.ensure(3 * (size_t)nf);
   HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
   HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
-                               b->dValClass.p, dc.p, doff.p, dItems.p, dText.p, dWords.p));
-  uint32_t* hItems = staging(b->exItems, b->exItemsCap, 8 * ti + 8);
-  uint16_t* hText = staging(b->exText, b->exTextCap, tt + 1);
-  uint32_t* hWords = staging(b->exWords, b->exWordsCap, tw + 1);
-  ex.items = hItems;
-  ex.text = hText;
-  ex.words = hWords;
-  if (ti) HIPCHK(hipMemcpyAsync(hItems, dItems.p, 8 * ti * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-  if (tt) HIPCHK(hipMemcpyAsync(hText, dText.p, tt * sizeof(uint16_t), hipMemcpyDeviceToHost, b->stream));
-  if (tw) HIPCHK(hipMemcpyAsync(hWords, dWords.p, tw * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
-  HIPCHK(hipStreamSynchronize(b->stream));
+                               b->dValClass.p, dc.p, doff.p, b->dExItems.p, b->dExText.p, b->dExWords.p));
+  ex.hItems = staging(b->exItems, b->exItemsCap, 8 * ti + 8);
+  ex.hText = staging(b->exText, b->exTextCap, tt + 1);
+  ex.hWords = staging(b->exWords, b->exWordsCap, tw + 1);
+  ex.items = ex.hItems;
+  ex.text = ex.hText;
+  ex.words = ex.hWords;
+  const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(pieces, nf));
+  ex.first.assign(P + 1, {0, 0, 0});
+  ex.pieceOf.assign(n, 0);
+  for (uint32_t p = 0; p < P; p++) {
+    const uint32_t fa = (uint32_t)((uint64_t)p * nf / P), fb = (uint32_t)((uint64_t)(p + 1) * nf / P);
+    for (uint32_t f = fa; f < fb; f++) ex.pieceOf[dev[f]] = p;
+    ex.first[p] = {off[3 * fa], off[3 * fa + 1], off[3 * fa + 2]};
+  }
+  ex.first[P] = {8 * ti, tt, tw};
+  if (pieces <= 1) {
+    copy_piece(b, ex, 0);
+    return;
+  }
+  ex.npieces = P;
+  ex.ready.reset(new std::atomic<int>[P]);
+  for (uint32_t p = 0; p < P; p++) ex.ready[p].store(0);
 }
 
 // SnapshotV1 of one document: the device extraction when it applies, else the host path
@@ -3812,7 +3868,8 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     // PermutationVectors and failed documents take the host path over the downloaded tree
     std::vector<uint32_t> ids(list);
     Extracted ex;
-    extract_docs(b, ids, ex);
+    // the outputs come back in pieces while the serializer threads start on the first ones
+    extract_docs(b, ids, ex, n >= 256 ? 8 : 1);
     pc.mark("extract");
     std::vector<uint32_t> fast, slow;
     for (uint32_t k = 0; k < n; k++) (ex.ok[k] ? fast : slow).push_back(k);
@@ -3831,6 +3888,7 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
           std::vector<std::pair<std::string, std::string>> blobs;
           std::string summary;
           if (ex.ok[k]) {
+            if (!ex.wait_doc(k)) raise(MTB_E_HIP, "SnapshotV1 extraction download failed");
             summarize_items(b, list[k], ex.items + ex.off[3 * k], ex.cnt[3 * k], ex.text + ex.off[3 * k + 1],
                             ex.words + ex.off[3 * k + 2], blobs, summary);
           } else {
@@ -3849,9 +3907,21 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, n));
     std::vector<std::thread> ts;
     for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
+    std::string copyErr;
+    for (uint32_t p = 0; p < ex.npieces; p++) {  // (this thread downloads, then serializes too)
+      try {
+        copy_piece(b, ex, p);
+        ex.mark(p, 1);
+      } catch (const MtbError& e) {
+        copyErr = e.msg;
+        for (uint32_t q = p; q < ex.npieces; q++) ex.mark(q, -1);
+        break;
+      }
+    }
     work();
     for (auto& t : ts) t.join();
     pc.mark("serialize");
+    if (!copyErr.empty()) raise(MTB_E_HIP, copyErr);
     for (uint32_t k = 0; k < n; k++)
       if (!errs[k].empty()) raise(MTB_E_ARG, "document " + std::to_string(list[k]) + ": " + errs[k]);
   });
