@@ -272,7 +272,8 @@ void mtb_blob_list_free(mtb_blob_list* l);
 /* mtb_summarize_v1 for n documents at once (out[k] for docs[k]; free each with mtb_blob_list_free): one
  * replay for the optional updateSeqNumbers(msn, seq), one bulk download of the documents' slices and the
  * summaries serialized on `threads` host threads.  No reference counterpart (the reference summarizes
- * one channel at a time); each blob list equals what mtb_summarize_v1 returns for that document. */
+ * one channel at a time); each blob list equals what mtb_summarize_v1 returns for that document.  The
+ * batch keeps the extraction's staging (host and device, sized by the largest call) until it is destroyed. */
 int mtb_summarize_v1_many(mtb_batch* b, uint32_t n, const uint32_t* docs, int64_t msn, int64_t seq, uint32_t threads,
                           mtb_blob_list* out);
 /* FNV-1a 64 over a blob list (each blob's path, 0, content, 0; then the summary JSON): a compact
