@@ -93,6 +93,7 @@ struct MtbError {
 // ------------------------------------------------------------------ interning
 struct Interner {
   std::vector<U16> keys;
+  std::vector<std::string> keyJson;  // each key quoted as a JSON string (the summary serializers' props)
   std::map<U16, uint32_t> keyId;
   std::vector<uint32_t> keyRank;
   std::vector<uint8_t> keyKinds;  // bit0 primitive seen, bit1 object-like seen
@@ -111,6 +112,8 @@ struct Interner {
     if (it != keyId.end()) return it->second;
     uint32_t id = (uint32_t)keys.size();
     keys.push_back(k);
+    keyJson.emplace_back();
+    hj::quote(keyJson.back(), k);
     keyId[k] = id;
     uint32_t r;
     keyRank.push_back(hj::array_index(k, &r) ? r : MTB_NONE);
@@ -2053,7 +2056,7 @@ void props_json(mtb_dev* b, std::string& o, PropView v) {
   o += '{';
   for (uint32_t i = 0; i < v.n(); i++) {
     if (i) o += ',';
-    hj::quote(o, b->in.keys[v.p[1 + 2 * i]]);
+    o += b->in.keyJson[v.p[1 + 2 * i]];
     o += ':';
     o += b->in.valJson[v.p[2 + 2 * i]];
   }
@@ -3868,8 +3871,13 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     // PermutationVectors and failed documents take the host path over the downloaded tree
     std::vector<uint32_t> ids(list);
     Extracted ex;
-    // the outputs come back in pieces while the serializer threads start on the first ones
-    extract_docs(b, ids, ex, n >= 256 ? 8 : 1);
+    // MTB_SUMMARY_PIECES=P > 1: the outputs come back in P pieces while the serializer threads start on the
+    // first ones.  Off by default: on the 16-CPU share of a GPU box the runtime's pageable staging copies compete
+    // with the serializer threads and the overlap gained nothing (profiles/r04/summary/: 1 / 8 / 32 pieces
+    // 0.216-0.222 / 0.226-0.244 / 0.210-0.216 s for 10,000 summaries)
+    uint32_t pieces = 1;
+    if (const char* e = getenv("MTB_SUMMARY_PIECES")) pieces = (uint32_t)std::max(1, atoi(e));
+    extract_docs(b, ids, ex, pieces);
     pc.mark("extract");
     std::vector<uint32_t> fast, slow;
     for (uint32_t k = 0; k < n; k++) (ex.ok[k] ? fast : slow).push_back(k);
