@@ -2193,7 +2193,7 @@ uint64_t utf8_byte_length(const std::string& utf8) {
 void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::string>& segJson, const std::vector<int>& segLen,
                     std::vector<std::pair<std::string, std::string>>& blobs, std::string& tree, uint64_t& totalBytes);
 #define EX_INLINE_HOST 0x40000000u  // mtb_extract_v1_kernel: a property set copied into the words output
-void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni, const uint16_t* txt, const uint32_t* words,
+void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t nwords, const uint16_t* txt, const uint32_t* words,
                      std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson);
 
 // SnapshotV1.extractSync + emit (snapshotV1.ts:122-312) over the downloaded document.
@@ -2456,7 +2456,7 @@ void emit_v1_chunks(mtb_dev* b, int minSeq, int curSeq, const std::vector<std::s
 
 // SnapshotV1 of a SharedString document from the device extraction (mtb_extract_v1_kernel): the same JSON
 // as summarize() without downloading the tree.
-void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni, const uint16_t* txt, const uint32_t* words,
+void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t nwords, const uint16_t* txt, const uint32_t* words,
                      std::vector<std::pair<std::string, std::string>>& blobs, std::string& summaryJson) {
   const HostDoc& d = b->docs[i];
   const DocState& s = b->hst[i];
@@ -2470,8 +2470,13 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
   };
   // the chunks first (they depend on the segment lengths only), then every segment's JSON written straight
   // into its chunk's blob: the bytes of summarize()'s segJson + emit_v1_chunks, without the per-segment strings
+  // items are 4 words, 8 with merge info (EX_META): their starts first
+  std::vector<uint32_t> at;
+  at.reserve(nwords / 4 + 1);
+  for (uint32_t w = 0; w + 4 <= nwords; w += (items[w] & 1u) ? 8u : 4u) at.push_back(w);
+  const uint32_t ni = (uint32_t)at.size();
   std::vector<int> segLen(ni);
-  for (uint32_t k = 0; k < ni; k++) segLen[k] = (int)items[8 * (size_t)k + 1];
+  for (uint32_t k = 0; k < ni; k++) segLen[k] = (int)items[at[k] + 1];
   const V1Chunks cs = v1_chunks(b, segLen);
   auto seg_json = [&](std::string& o, const uint32_t* it) {
     const uint32_t fl = it[0], len = it[1], toff = it[2];
@@ -2536,7 +2541,7 @@ void summarize_items(mtb_dev* b, uint32_t i, const uint32_t* items, uint32_t ni,
     v1_chunk_open(o, c);
     for (int q = 0; q < c.count; q++) {
       if (q) o += ',';
-      seg_json(o, items + 8 * (size_t)(c.start + q));
+      seg_json(o, items + at[c.start + q]);
     }
     v1_chunk_close(o, cs, k, minSeq, curSeq);
     blobBytes += o.size();
@@ -2640,7 +2645,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, u
   for (uint32_t f = 0; f < nf; f++) {
     const bool good = cnt[3 * f] != MTB_NONE;  // else the device walk did not trust the tree: host path
     if (!good) cnt[3 * f] = cnt[3 * f + 1] = cnt[3 * f + 2] = 0;
-    off[3 * f] = 8 * ti;
+    off[3 * f] = ti;
     off[3 * f + 1] = tt;
     off[3 * f + 2] = tw;
     ti += cnt[3 * f];
@@ -2651,14 +2656,14 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, u
     ex.cnt[3 * k] = cnt[3 * f];
     for (int q = 0; q < 3; q++) ex.off[3 * k + q] = off[3 * f + q];
   }
-  b->dExItems.ensure(8 * ti + 8);
+  b->dExItems.ensure(ti + 8);
   b->dExText.ensure(tt + 1);
   b->dExWords.ensure(tw + 1);
   doff.ensure(3 * (size_t)nf);
   HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
   HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
                                b->dValClass.p, dc.p, doff.p, b->dExItems.p, b->dExText.p, b->dExWords.p));
-  ex.hItems = staging(b->exItems, b->exItemsCap, 8 * ti + 8);
+  ex.hItems = staging(b->exItems, b->exItemsCap, ti + 8);
   ex.hText = staging(b->exText, b->exTextCap, tt + 1);
   ex.hWords = staging(b->exWords, b->exWordsCap, tw + 1);
   ex.items = ex.hItems;
@@ -2672,7 +2677,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, u
     for (uint32_t f = fa; f < fb; f++) ex.pieceOf[dev[f]] = p;
     ex.first[p] = {off[3 * fa], off[3 * fa + 1], off[3 * fa + 2]};
   }
-  ex.first[P] = {8 * ti, tt, tw};
+  ex.first[P] = {ti, tt, tw};
   if (pieces <= 1) {
     copy_piece(b, ex, 0);
     return;

@@ -4345,13 +4345,14 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
 // (below the MSN and not removed: TextSegment.canAppend + matchProperties, or PermutationSegment.canAppend)
 // or kept with their merge info.  The host serializes the result (mtb_host.cpp summarize_items) instead of
 // downloading the whole tree.  Per document the output is
-//   items : 8 words per snapshot segment: [flags (EX_META, EX_MARKER | refType+1 << 8), length, text offset
+//   items : per snapshot segment [flags (EX_META, EX_MARKER | refType+1 << 8), length, text offset
 //           (PermutationSegment: its start), props (0; MTB_GPROPS | pool offset; EX_INLINE | word offset of a
-//           copied [n, (k, v)*n] set), seq, client | removedClientIds[0] << 16, removedSeq, word offset of
-//           [n, c1..cn] further removers (MTB_NONE: none)]
+//           copied [n, (k, v)*n] set)], and when it keeps its merge info (EX_META) 4 more words [seq, client |
+//           removedClientIds[0] << 16, removedSeq, word offset of [n, c1..cn] further removers (MTB_NONE:
+//           none)]: 4 or 8 words, read in order
 //   text  : the UTF-16 of every item (a coalesced run's pieces back to back)
 //   words : inlined per-document property sets and remover lists
-// Pass 1 (off == nullptr) counts (items, text units, words) into cnt[3 k]; pass 2 writes at off[3 k..].
+// Pass 1 (off == nullptr) counts (item words, text units, words) into cnt[3 k]; pass 2 writes at off[3 k..].
 #define EX_META 1u
 #define EX_MARKER 2u
 #define EX_INLINE 0x40000000u
@@ -4398,7 +4399,7 @@ extern "C" __global__ void __launch_bounds__(64)
   uint32_t* I = emit ? items + off[3 * k] : nullptr;
   uint16_t* OT = emit ? otext + off[3 * k + 1] : nullptr;
   uint32_t* OW = emit ? owords + off[3 * k + 2] : nullptr;
-  uint32_t ni = 0, nt = 0, nw = 0;  // counts so far (uniform)
+  uint32_t ni = 0, nt = 0, nw = 0;  // item words, text units, words so far (uniform)
   // the open coalescing candidate (`prev`): its item index, length, last UTF-16 unit, marker, props
   bool open = false;
   uint32_t p_item = 0, p_len = 0, p_props = 0, p_start = 0;
@@ -4421,7 +4422,7 @@ extern "C" __global__ void __launch_bounds__(64)
     nt += len;
   };
   auto close_prev = [&]() {
-    if (open && emit && lane == 0) I[8 * p_item + 1] = p_len;
+    if (open && emit && lane == 0) I[p_item + 1] = p_len;
     open = false;
   };
   int d = 0;
@@ -4495,13 +4496,14 @@ extern "C" __global__ void __launch_bounds__(64)
         close_prev();
         // a new candidate item (its length is written when it closes)
         const uint32_t po = perm ? 0u : props_out(props);
-        if (emit && lane < 8) {
+        if (emit && lane < 4) {
           const uint32_t v = lane == 0 ? (marker ? (EX_MARKER | (((txt & ~MTB_MARKER)) << 8)) : 0u)
                              : lane == 2 ? (perm ? txt : marker ? 0u : nt) : lane == 3 ? po : 0u;
-          I[8 * ni + lane] = v;
+          I[ni + lane] = v;
         }
         open = true;
-        p_item = ni++;
+        p_item = ni;
+        ni += 4;
         p_len = len;
         p_props = props;
         p_start = txt;
@@ -4530,9 +4532,9 @@ extern "C" __global__ void __launch_bounds__(64)
         const uint32_t v = lane == 0 ? (EX_META | (marker ? (EX_MARKER | (((txt & ~MTB_MARKER)) << 8)) : 0u))
                            : lane == 1 ? len : lane == 2 ? (perm ? txt : toff) : lane == 3 ? po
                            : lane == 4 ? (uint32_t)seq : lane == 5 ? cli : lane == 6 ? (uint32_t)rseq : ro;
-        I[8 * ni + lane] = v;
+        I[ni + lane] = v;
       }
-      ni++;
+      ni += 8;
     }
     __syncthreads();
     if (lane == 0) nxt[d] = c;
