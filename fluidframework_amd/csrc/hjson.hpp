@@ -337,60 +337,67 @@ inline size_t utf8_seq(const uint8_t* p, const uint8_t* e) {
 }
 // quote(o, from_utf8(u)) without the UTF-16 round trip, for u well-formed UTF-8 without encoded surrogates (what
 // these serializers produce): bytes pass through and only '"', '\\' and control characters are escaped, exactly
-// as quote() escapes the same code points.  Returns false, leaving o as it was, for any other u.  Pointer writes
-// with the room rule of quote16 (one byte per remaining input byte, plus the closing quote).
+// as quote() escapes the same code points.  Returns false, leaving o as it was, for any other u.  The summary
+// blobs it escapes are a quarter quotes, so an ASCII byte takes no branch: its replacement (1, 2 or 6 bytes)
+// comes from a table as one 8-byte copy into a per-thread scratch with 8 bytes of slack, appended at the end.
+struct JsonEscTab {
+  char s[128][8];
+  uint8_t n[128];
+  JsonEscTab() {
+    static const char kHex[] = "0123456789abcdef";
+    for (int c = 0; c < 128; c++) {
+      memset(s[c], 0, 8);
+      const char* e = nullptr;
+      switch (c) {
+        case 0x22: e = "\\\""; break;
+        case 0x5C: e = "\\\\"; break;
+        case 0x08: e = "\\b"; break;
+        case 0x0C: e = "\\f"; break;
+        case 0x0A: e = "\\n"; break;
+        case 0x0D: e = "\\r"; break;
+        case 0x09: e = "\\t"; break;
+        default: break;
+      }
+      if (e) {
+        memcpy(s[c], e, 2);
+        n[c] = 2;
+      } else if (c < 0x20) {
+        const char u[6] = {'\\', 'u', '0', '0', kHex[c >> 4], kHex[c & 15]};
+        memcpy(s[c], u, 6);
+        n[c] = 6;
+      } else {
+        s[c][0] = (char)c;
+        n[c] = 1;
+      }
+    }
+  }
+};
 inline bool quote_utf8(std::string& o, const std::string& u) {
-  static const char kHex[] = "0123456789abcdef";
-  const size_t base = o.size();
-  o.resize(base + u.size() + u.size() / 4 + 18);
-  char* w = &o[0];
-  size_t at = base;
+  static const JsonEscTab T;
+  thread_local std::vector<char> buf;
+  const size_t need = 6 * u.size() + 16;
+  if (buf.size() < need) buf.resize(need);
+  char* w = buf.data();
+  size_t at = 0;
   w[at++] = '"';
   const uint8_t* p = reinterpret_cast<const uint8_t*>(u.data());
   const uint8_t* const e = p + u.size();
   while (p < e) {
     const uint8_t c = *p;
-    if (c >= 0x20 && c != 0x22 && c != 0x5C && c < 0x80) {
-      w[at++] = (char)c;
+    if (c < 0x80) {
+      memcpy(w + at, T.s[c], 8);
+      at += T.n[c];
       p++;
       continue;
     }
-    if (at + 8 + (size_t)(e - p) > o.size()) {
-      o.resize((at + 8 + (size_t)(e - p)) * 5 / 4 + 16);
-      w = &o[0];
-    }
-    if (c >= 0x80) {
-      const size_t n = utf8_seq(p, e);
-      if (!n) {
-        o.resize(base);
-        return false;
-      }
-      memcpy(w + at, p, n);
-      at += n;
-      p += n;
-      continue;
-    }
-    w[at++] = '\\';
-    switch (c) {
-      case 0x22: w[at++] = '"'; break;
-      case 0x5C: w[at++] = '\\'; break;
-      case 0x08: w[at++] = 'b'; break;
-      case 0x0C: w[at++] = 'f'; break;
-      case 0x0A: w[at++] = 'n'; break;
-      case 0x0D: w[at++] = 'r'; break;
-      case 0x09: w[at++] = 't'; break;
-      default:
-        w[at++] = 'u';
-        w[at++] = '0';
-        w[at++] = '0';
-        w[at++] = kHex[c >> 4];
-        w[at++] = kHex[c & 15];
-        break;
-    }
-    p++;
+    const size_t n = utf8_seq(p, e);
+    if (!n) return false;
+    memcpy(w + at, p, n);
+    at += n;
+    p += n;
   }
   w[at++] = '"';
-  o.resize(at);
+  o.append(w, at);
   return true;
 }
 // quote(o, from_utf8(u)) by the fast path when it applies
