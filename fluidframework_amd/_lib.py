@@ -17,7 +17,7 @@ ERRORS = {0: "MTB_OK", -1: "MTB_E_ARG", -2: "MTB_E_NODEV", -3: "MTB_E_HIP", -4: 
           -5: "MTB_E_INSERT", -6: "MTB_E_UNSUPPORTED", -7: "MTB_E_CAPACITY", -8: "MTB_E_PARSE"}
 
 # every entry point declared in include/mtb.h
-EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free", "mtb_doc_init",
+EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free", "mtb_build_id", "mtb_doc_init",
            "mtb_doc_load_v1", "mtb_docs_load_v1", "mtb_matrix_init", "mtb_matrix_apply_msg_json",
            "mtb_matrix_intern_value", "mtb_matrix_summarize", "mtb_matrix_get_cell", "mtb_matrix_load",
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
@@ -84,6 +84,8 @@ def lib():
     L.mtb_last_error.restype = ctypes.c_char_p
     L.mtb_last_error.argtypes = [vp]
     L.mtb_free.argtypes = [vp]
+    L.mtb_build_id.restype = ctypes.c_char_p
+    L.mtb_build_id.argtypes = []
     L.mtb_doc_init.argtypes = [vp, u32, vp, sz, ctypes.c_char_p, u32, u32]
     L.mtb_doc_load_v1.argtypes = [vp, u32, ctypes.POINTER(MtbBlob), u32, ctypes.c_char_p]
     L.mtb_docs_load_v1.argtypes = [vp, u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.POINTER(MtbBlob)),

@@ -25,32 +25,75 @@ def _stale(out, deps):
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def needs_build():
-    deps = SRCS + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))] + \
-        [os.path.join(ROOT, "include", "mtb.h")]
-    return _stale(OUT, deps)
-
+# The engine is rebuilt by CONTENT, not by mtime: build() hashes every source and header that goes into
+# libmtb.so together with the compile flags, embeds that hash in the library (a generated translation unit
+# holding BUILD_ID_TAG + hex), and rebuilds whenever the hash found in an existing libmtb.so differs -- a
+# prebuilt library that came with a tree (newer by mtime, or not) is never trusted.  Objects under build/obj
+# carry the hash of their own inputs in a sidecar file in the same way.
+BUILD_ID_TAG = b"MTB_SOURCE_SHA256="
 
 # the kernel file is compiled once per kernel group (mtb_replay.hip MTB_TU_*), in parallel with the host
-# sources; objects are kept under build/ and rebuilt when a source or header is newer
+# sources
 KERNEL_GROUPS = (1, 2, 3, 4, 5)
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 
 
 def _headers():
-    return [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith((".h", ".hpp"))] + \
-        [os.path.join(ROOT, "include", "mtb.h")]
+    return sorted([os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
+                   if f.endswith((".h", ".hpp"))]) + [os.path.join(ROOT, "include", f) for f in ("mtb.h", "mtb_testing.h")]
+
+
+def _digest(paths, flags):
+    import hashlib
+    h = hashlib.sha256()
+    for f in flags:
+        h.update(f.encode() + b"\0")
+    for p in paths:
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _base_flags(arch, defines, extra):
+    return ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
+        [f"-D{d}" for d in defines] + list(extra)
+
+
+def source_id(arch="gfx950", defines=(), extra=()):
+    """The hash build() embeds in the library it makes from the current sources and flags."""
+    return _digest(SRCS + _headers(), _base_flags(arch, defines, extra))
+
+
+def embedded_id(path=OUT):
+    """The source hash embedded in a built library, or None (missing, or built without one)."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    i = data.find(BUILD_ID_TAG)
+    if i < 0:
+        return None
+    j = i + len(BUILD_ID_TAG)
+    return data[j:j + 64].decode("ascii", "replace")
+
+
+def needs_build(out=OUT, arch="gfx950", defines=(), extra=()):
+    return embedded_id(out) != source_id(arch, defines, extra)
 
 
 def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
-    if not force and out == OUT and not needs_build():
-        return OUT
+    sid = source_id(arch, defines, extra)
+    if not force and embedded_id(out) == sid:
+        return out
     from concurrent.futures import ThreadPoolExecutor
     tag = "_".join([d.replace("=", "") for d in defines] + [x.strip("-").replace("-", "") for x in extra]) or "base"
     odir = os.path.join(OBJ_DIR, f"{arch}_{tag}")
     os.makedirs(odir, exist_ok=True)
-    base = ["hipcc", "-x", "hip", f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
-        [f"-D{d}" for d in defines] + list(extra)
+    base = _base_flags(arch, defines, extra)
+    hdrs = _headers()
     jobs = []  # (object, command, sources it depends on)
     hip = SRCS[0]
     for g in KERNEL_GROUPS:
@@ -59,18 +102,34 @@ def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
     for src in SRCS[1:]:
         o = os.path.join(odir, os.path.basename(src) + ".o")
         jobs.append((o, base + ["-c", src, "-o", o], [src]))
-    hdrs = _headers()
+    idsrc = os.path.join(odir, "mtb_build_id.c")
+    with open(idsrc, "w") as fh:  # the embedded source hash (found by embedded_id, also mtb_build_id())
+        fh.write('const char mtb_build_id_str[] = "%s%s";\n'
+                 'const char* mtb_build_id(void) { return mtb_build_id_str + %d; }\n'
+                 % (BUILD_ID_TAG.decode(), sid, len(BUILD_ID_TAG)))
+    ido = idsrc[:-2] + ".o"
+    jobs.append((ido, ["gcc", "-O2", "-fPIC", "-c", idsrc, "-o", ido], None))
 
     def run(job):
         o, cmd, deps = job
-        if force or _stale(o, deps + hdrs):
+        if deps is None:
             subprocess.check_call(cmd)
+            return o
+        key = _digest(deps + hdrs, cmd)
+        stamp = o + ".sha256"
+        old = open(stamp).read() if os.path.exists(stamp) and os.path.exists(o) else None
+        if force or old != key:
+            subprocess.check_call(cmd)
+            with open(stamp, "w") as fh:
+                fh.write(key)
         return o
 
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(workers) as ex:
         objs = list(ex.map(run, jobs))
-    subprocess.check_call(["hipcc", f"--offload-arch={arch}", "-shared", "-fPIC", "-o", out] + objs)
+    tmp = out + ".tmp"
+    subprocess.check_call(["hipcc", f"--offload-arch={arch}", "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, out)
     return out
 
 
@@ -88,8 +147,5 @@ def build_napi(force=False):
 
 
 if __name__ == "__main__":
-    if "--variants" in sys.argv:  # occupancy variants for tuning runs (MTB_LIB=...)
-        for w in (4, 5, 6):
-            print(build(force=True, out=os.path.join(HERE, f"libmtb_w{w}.so"), defines=[f"MTB_WAVES_PER_SIMD={w}"]))
     print(build(force="--force" in sys.argv))
     print(build_napi(force="--force" in sys.argv))

@@ -421,17 +421,21 @@ class Client:
         r = self.load(storage, clientId)
         msgs = r["catchupOps"]
         if msgs:
-            cw = r["collabWindow"]  # (from the header: the batch need not replay before the other loads)
-            cur = cw["currentSeq"]
+            # the window follows each applied message as getCollabWindow() does in the reference (computed
+            # here, not read back: the batch need not replay before the other documents' loads):
+            # updateSeqNumbers sets currentSeq, and setMinSeq moves minSeq up to the message's MSN
+            cw = r["collabWindow"]
+            cur, msn = cw["currentSeq"], cw["minSeq"]
             for m in msgs:
-                if (m["minimumSequenceNumber"] < cw["minSeq"] or m["referenceSequenceNumber"] < cw["minSeq"] or
-                        m["sequenceNumber"] <= cw["minSeq"] or m["sequenceNumber"] <= cur):
+                if (m["minimumSequenceNumber"] < msn or m["referenceSequenceNumber"] < msn or
+                        m["sequenceNumber"] <= msn or m["sequenceNumber"] <= cur):
                     raise MergeTreeError(-1, "Invalid catchup operations in snapshot: " + json.dumps(
                         {"op": {"seq": m["sequenceNumber"], "minSeq": m["minimumSequenceNumber"],
                                 "refSeq": m["referenceSequenceNumber"]},
-                         "collabWindow": {"seq": cur, "minSeq": cw["minSeq"]}}))
+                         "collabWindow": {"seq": cur, "minSeq": msn}}))
                 self.applyMsg(m)
                 cur = m["sequenceNumber"]
+                msn = max(msn, m["minimumSequenceNumber"])
         return msgs
 
     def applyMsg(self, msg, local=False):

@@ -37,6 +37,7 @@ int mtbx_matrix_get_cell(mtb_dev* b, uint32_t matrix, uint32_t row, uint32_t col
 int mtbx_replay(mtb_dev* b, mtb_stats* out);
 int mtbx_get_text(mtb_dev* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* len_out);
 int mtbx_get_length(mtb_dev* b, uint32_t doc, uint32_t* len_out);
+int mtbx_test_set_root_child(mtb_dev* b, uint32_t doc, uint32_t value, uint32_t* old_out);
 int mtbx_get_seq(mtb_dev* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq);
 int mtbx_dump_segments(mtb_dev* b, uint32_t doc, char** out, size_t* out_len);
 int mtbx_doc_checksum(mtb_dev* b, uint32_t doc, uint64_t* out);

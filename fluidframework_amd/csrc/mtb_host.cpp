@@ -1855,7 +1855,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
           if (o.flags & MTB_F_DELTA)  // (a rewrite annotate's segments get a second entry: the set before)
             cap += o.type == MTB_OP_INSERT ? 1
                    : ((o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1) *
-                         (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_REWRITE) ? 2 : 1);
+                         (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_REWRITE ? 2 : 1);
           if (o.type == MTB_OP_REGEN) cap += (uint64_t)o.pos1 * (s.seg_used + 16);  // one entry per regenerated op
         }
       }
@@ -2009,10 +2009,12 @@ struct FlatSeg {
 void flatten(const HostDoc& d, uint32_t root, std::vector<FlatSeg>& out, bool withPath) {
   std::vector<int> path;
   struct Fr { uint32_t b; int i; };
+  if (root >= d.blks.size()) raise(MTB_E_INTERNAL, "corrupt tree: root block outside the slice");
   std::vector<Fr> st{{root, 0}};
+  size_t entered = 1;
   while (!st.empty()) {
     Fr& f = st.back();
-    const Blk& B = d.blks.at(f.b);
+    const Blk& B = d.blks[f.b];
     if (f.i >= B.count) {
       st.pop_back();
       if (!path.empty()) path.pop_back();
@@ -2029,6 +2031,8 @@ void flatten(const HostDoc& d, uint32_t root, std::vector<FlatSeg>& out, bool wi
       }
       out.push_back(std::move(fs));
     } else {
+      // a child outside the slice or a cycle (more blocks entered than exist) is an engine fault, not input
+      if (c >= d.blks.size() || ++entered > d.blks.size()) raise(MTB_E_INTERNAL, "corrupt tree: bad block child");
       path.push_back(i);
       st.push_back({c, 0});
     }
@@ -2899,7 +2903,7 @@ void resolve_catch_up(mtb_dev* b, uint32_t i) {
       if (it == byRec.end()) continue;  // no delta segments: no event
       struct Ev { int pos1, pos2; std::string props; hj::Value pv; bool hasPos2, nan; std::string json; };
       std::vector<Ev> ev;
-      const bool rewrite = r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_REWRITE);
+      const bool rewrite = r.type == MTB_OP_ANNOTATE && (r.flags & MTB_F_COMB) == MTB_F_REWRITE;
       const std::vector<uint32_t>* before = nullptr;  // a rewrite's entries with the sets before it, same order
       if (rewrite) {
         auto ot = byRec.find(k | MTB_DELTA_OLD);
@@ -3737,6 +3741,24 @@ int mtbx_get_text(mtb_dev* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* l
   });
 }
 
+// Test hook (include/mtb_testing.h): overwrite the child id in the root block's last slot with `value` and
+// return the old id, so tests can give the device walks a tree they must refuse (an engine fault, never input).
+int mtbx_test_set_root_child(mtb_dev* b, uint32_t doc, uint32_t value, uint32_t* old_out) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!d.onDevice || !b->devInit || doc >= b->hst.size()) raise(MTB_E_ARG, "document has not been replayed");
+    const DocState& s = b->hst[doc];
+    FBlk r;
+    FBlk* dp = b->dBlks.p + s.blk_base + s.root;
+    HIPCHK(hipMemcpy(&r, dp, sizeof r, hipMemcpyDeviceToHost));
+    if (r.count == 0 || r.count > MTB_MAXCH) raise(MTB_E_ARG, "the root block has no child slot to change");
+    if (old_out) *old_out = r.f[F_ID][r.count - 1];
+    r.f[F_ID][r.count - 1] = value == 0xFFFFFFFEu ? s.root : value;
+    HIPCHK(hipMemcpy(dp, &r, sizeof r, hipMemcpyHostToDevice));
+    d.cached = false;
+  });
+}
+
 int mtbx_get_length(mtb_dev* b, uint32_t doc, uint32_t* len_out) {
   return guarded(b, [&] {
     docref(b, doc);
@@ -3919,6 +3941,18 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
     };
     const uint32_t nt = std::max<uint32_t>(1, std::min<uint32_t>(threads ? threads : 1, n));
     std::vector<std::thread> ts;
+    // on any exit (a thread that cannot start included): fail the pieces nobody marked, so no worker waits
+    // for them, and join every worker before the vector is destroyed
+    struct JoinGuard {
+      Extracted& ex;
+      std::vector<std::thread>& ts;
+      ~JoinGuard() {
+        for (uint32_t q = 0; q < ex.npieces; q++)
+          if (ex.ready[q].load(std::memory_order_acquire) == 0) ex.mark(q, -1);
+        for (auto& t : ts)
+          if (t.joinable()) t.join();
+      }
+    } guard{ex, ts};
     for (uint32_t t = 1; t < nt; t++) ts.emplace_back(work);
     std::string copyErr;
     for (uint32_t p = 0; p < ex.npieces; p++) {  // (this thread downloads, then serializes too)
@@ -3927,6 +3961,10 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
         ex.mark(p, 1);
       } catch (const MtbError& e) {
         copyErr = e.msg;
+        for (uint32_t q = p; q < ex.npieces; q++) ex.mark(q, -1);
+        break;
+      } catch (...) {  // (bad_alloc, system_error): no worker may wait for a piece that never comes
+        copyErr = "SnapshotV1 extraction download failed";
         for (uint32_t q = p; q < ex.npieces; q++) ex.mark(q, -1);
         break;
       }

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "mtb_dev.h"
+#include "../../include/mtb_testing.h"
 
 struct mtb_batch {
   uint32_t ndocs = 0;
@@ -362,6 +363,10 @@ int mtb_get_text(mtb_batch* b, uint32_t doc, uint16_t* buf, size_t cap, size_t* 
 }
 
 int mtb_get_length(mtb_batch* b, uint32_t doc, uint32_t* len_out) { DOC_CALL(doc, mtbx_get_length(d_, l_, len_out)); }
+
+int mtb_test_set_root_child(mtb_batch* b, uint32_t doc, uint32_t value, uint32_t* old_out) {
+  DOC_CALL(doc, mtbx_test_set_root_child(d_, l_, value, old_out));
+}
 
 int mtb_get_seq(mtb_batch* b, uint32_t doc, uint32_t* cur_seq, uint32_t* min_seq) {
   DOC_CALL(doc, mtbx_get_seq(d_, l_, cur_seq, min_seq));

@@ -3642,7 +3642,7 @@ struct Eng {
         const uint32_t dfrom = delta_used;
         if (isLive) sh->memo[2] = 0;
         node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props,
-                 o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_REWRITE) ? 1 : (o.flags & MTB_F_INCR) ? 2 : 0);
+                 o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_COMB) >> 2);  // 1 rewrite, 2 incr, 3 consensus
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);
@@ -4389,13 +4389,16 @@ extern "C" __global__ void __launch_bounds__(64)
   const uint32_t k = blockIdx.x;
   const int lane = threadIdx.x;
   if (k >= n) return;
+  const bool emit = off != nullptr;
+  // emit pass: a document the count pass could not trust (MTB_NONE, still in cnt) got no room in the outputs
+  // (its offsets are the next document's); the host serializes it from its slices, so write nothing
+  if (emit && cnt[3 * k] == MTB_NONE) return;
   const DocState& s = docs[list[k]];
   const FBlk* B = blks + s.blk_base;
   const uint16_t* T = text + s.text_base;
   const uint32_t* A = aux + s.aux_base;
   const bool perm = (s.flags & DSF_PERM) != 0;
   const int minSeq = s.min_seq;
-  const bool emit = off != nullptr;
   uint32_t* I = emit ? items + off[3 * k] : nullptr;
   uint16_t* OT = emit ? otext + off[3 * k + 1] : nullptr;
   uint32_t* OW = emit ? owords + off[3 * k + 2] : nullptr;

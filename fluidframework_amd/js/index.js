@@ -318,17 +318,21 @@ class Client {
     const { catchupOpsP } = await this.load(runtime, storage);
     const msgs = await catchupOpsP;
     if (msgs.length) {
-      const cw = this.loadedWindow;  // (from the header: no flush before the batch's other loads)
+      // the window follows each applied message as getCollabWindow() does in the reference (computed, not
+      // read back, so the batch's other loads need no flush): currentSeq = seq, minSeq up to the MSN
+      const cw = this.loadedWindow;
       let cur = cw.currentSeq;
+      let msn = cw.minSeq;
       for (const m of msgs) {
-        if (m.minimumSequenceNumber < cw.minSeq || m.referenceSequenceNumber < cw.minSeq ||
-            m.sequenceNumber <= cw.minSeq || m.sequenceNumber <= cur) {
+        if (m.minimumSequenceNumber < msn || m.referenceSequenceNumber < msn ||
+            m.sequenceNumber <= msn || m.sequenceNumber <= cur) {
           throw new Error(`Invalid catchup operations in snapshot: ${JSON.stringify({
             op: { seq: m.sequenceNumber, minSeq: m.minimumSequenceNumber, refSeq: m.referenceSequenceNumber },
-            collabWindow: { seq: cur, minSeq: cw.minSeq } })}`);
+            collabWindow: { seq: cur, minSeq: msn } })}`);
         }
         this.applyMsg(m);
         cur = m.sequenceNumber;
+        msn = Math.max(msn, m.minimumSequenceNumber);
       }
     }
     return msgs;

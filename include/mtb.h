@@ -46,10 +46,14 @@ enum {
 enum {
   MTB_F_LAST = 0x01,    /* run updateSeqNumbers(msn, seq) after this record (client.ts:874) */
   MTB_F_MARKER = 0x02,  /* insert: Marker segment, pos2 = refType (0xFFFFFFFF = undefined) */
-  MTB_F_REWRITE = 0x04, /* annotate: combiningOp {name:"rewrite"} */
+  /* Bits 0x02-0x40 mean different things per record type (and the engine's internal records reuse 0x10 /
+   * 0x20): test a flag only after testing the record's type. */
+  MTB_F_COMB = 0x0C,    /* annotate: the combiningOp kind, a 2-bit field (compare masked: (flags & MTB_F_COMB)) */
+  MTB_F_REWRITE = 0x04, /*   {name:"rewrite"} (segmentPropertiesManager.ts:107-123) */
+  MTB_F_INCR = 0x08,    /*   {name:"incr"}: every key of props becomes combine(op, previous, undefined)
+                             (properties.ts:24-69), NaN for numeric / boolean / absent previous values */
+  MTB_F_CONSENSUS = 0x0C, /* {name:"consensus"}: combine(op, previous, undefined, seq) (properties.ts:46-62) */
   MTB_F_SEGOBJ = 0x08,  /* insert: seg given as {text, props?} object (props id may be 0) */
-  MTB_F_INCR = 0x08,    /* annotate: combiningOp {name:"incr"} -- every key of props becomes combine(op, previous,
-                           undefined) (properties.ts:24-69), NaN for numeric / boolean / absent previous values */
   MTB_F_PERMSEG = 0x40, /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
   MTB_F_DELTA = 0x80    /* record the op's delta ranges (catch-up rewriting, MTB_BATCH_CATCHUP) */
 };
@@ -151,6 +155,9 @@ int mtb_batch_create(const mtb_options* opts, uint32_t ndocs, uint32_t device_ma
 void mtb_batch_destroy(mtb_batch* b);
 const char* mtb_last_error(mtb_batch* b);
 void mtb_free(void* p);
+/* The SHA-256 of the sources, headers and compile flags this library was built from (build.py embeds it;
+ * a library whose hash differs from the tree's is rebuilt).  Not a reference interface. */
+const char* mtb_build_id(void);
 
 /* Initial detached content (inserted locally before collaboration, like client.replay.spec.ts:27)
  * and startOrUpdateCollaboration(observer_long_id, min_seq, cur_seq) (client.ts:1133). */

@@ -1571,8 +1571,9 @@ void Doc::applyRecordParsed(const Record& r, const uint16_t* text, const std::ve
       const JVal* p = propsOf(r.props);
       static const JObj empty;
       const JObj& o = (p && p->t == JVal::Obj) ? p->obj : empty;
-      Comb comb;  // MTB_F_REWRITE 0x04, MTB_F_INCR 0x08 (annotate records)
-      comb.kind = (r.flags & 0x04) ? Comb::Rewrite : (r.flags & 0x08) ? Comb::Incr : Comb::None;
+      Comb comb;  // MTB_F_COMB 0x0C of annotate records: 0x04 rewrite, 0x08 incr, 0x0C consensus
+      const int ck = (r.flags >> 2) & 3;
+      comb.kind = ck == 1 ? Comb::Rewrite : ck == 2 ? Comb::Incr : ck == 3 ? Comb::Consensus : Comb::None;
       mt.annotateRange((int)r.pos1, (int)r.pos2, o, comb, (int)r.refSeq, r.client, (int)r.seq);
       break;
     }

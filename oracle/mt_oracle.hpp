@@ -38,7 +38,7 @@ constexpr int UNDEF_LEN = -1;              // `undefined` result of nodeLength
 // defaultValue plus undefined -- NaN for numbers, booleans, null and undefined; a string gets "undefined"
 // appended; then minValue when truthy and larger).  "consensus" and other names are not restated.
 struct Comb {
-  enum Kind { None, Rewrite, Incr } kind = None;
+  enum Kind { None, Rewrite, Incr, Consensus } kind = None;
   JVal defaultValue;  // Undef when absent
   JVal minValue;
 };

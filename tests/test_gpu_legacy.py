@@ -277,3 +277,32 @@ def test_catch_up_rewriting_of_rewrite_and_incr_annotates(new_mode):
     L.flush()
     for i, r in enumerate(loaded):
         assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"
+
+
+def test_catch_up_validation_follows_the_moving_window_on_the_engine():
+    """loadSequence reads the collab window again for every catch-up message (sequence.ts:578-585): after a
+    message raised minSeq to its MSN, a later message with a lower MSN is "Invalid catchup operations in
+    snapshot" -- on the Python drop-in as on the oracle (ADVICE r04)."""
+    import json
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from pyoracle import OracleDoc, OracleError
+    from test_oracle import _msn_backwards
+    name, d = replay_fixtures()[3]
+    src = OracleDoc()
+    src.insert_text_local(0, d["initialText"])
+    src.start_collab("A")
+    src.enable_catch_up()
+    for grp in d["groups"][:20]:
+        for m in grp["msgs"]:
+            src.apply_msg(msg_from_compact(m))
+    blobs = src.summarize_legacy()["blobs"]
+    known = {"header", "body"}
+    k = next(i for i, (p, _) in enumerate(blobs) if p not in known)
+    bad = [list(b) for b in blobs]
+    bad[k][1] = json.dumps(_msn_backwards(json.loads(blobs[k][1])))
+    o = OracleDoc()
+    with pytest.raises(OracleError, match="Invalid catchup"):
+        o.apply_catch_up(o.load_v1(bad, "loader"))
+    B = MergeTreeBatch(1, catch_up=True)
+    with pytest.raises(MergeTreeError, match="Invalid catchup operations in snapshot"):
+        B[0].loadSequence(bad, "loader")

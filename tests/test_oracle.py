@@ -282,6 +282,28 @@ def test_catch_up_validation_rejects_stale_messages():
         r.apply_catch_up([dict(msgs[0], sequenceNumber=r.current_seq)])
 
 
+def _msn_backwards(msgs):
+    """The catch-up list with one message's MSN raised to its refSeq, above the next message's MSN: that next
+    message then lies below the window the raised one moved (setMinSeq), which sequence.ts:578-585 rejects."""
+    i = next(i for i in range(len(msgs) - 1)
+             if msgs[i]["referenceSequenceNumber"] > msgs[i + 1]["minimumSequenceNumber"])
+    out = [dict(m) for m in msgs]
+    out[i]["minimumSequenceNumber"] = out[i]["referenceSequenceNumber"]
+    return out
+
+
+def test_catch_up_validation_follows_the_moving_window():
+    """getCollabWindow() is read again for every catch-up message (sequence.ts:578-585): a message whose MSN
+    is below an earlier message's MSN is rejected, not only one below the header's window."""
+    name, d = FIXTURES[3]
+    _, blobs = _legacy_midstream(d, 20)
+    r = OracleDoc()
+    msgs = r.load_v1(blobs, "loader")
+    assert len(msgs) >= 2
+    with pytest.raises(OracleError, match="Invalid catchup"):
+        r.apply_catch_up(_msn_backwards(msgs))
+
+
 @pytest.mark.parametrize("idx", [0, 3, 9, 17, 26])
 def test_catch_up_messages_replay_to_the_final_text(idx):
     """SnapshotLegacy + catch-up (sequence.ts:680-748): the header/body text at the MSN, then the stored

@@ -1,4 +1,5 @@
-"""Build the engine's measurement variants in-tree (MTB_LIB=fluidframework_amd/libmtb_<name>.so selects one):
+"""Build the engine's measurement variants into tools/lib/ (MTB_LIB=tools/lib/libmtb_<name>.so selects one;
+they are profiling builds, not part of the package):
 
   prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
@@ -12,6 +13,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fluidframework_amd import build as b  # noqa: E402
 
+LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 VARIANTS = {
     "prof": ["MTB_PROFILE"],
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
@@ -22,4 +24,5 @@ if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     print(b.build())
     for n in names:
-        print(b.build(out=os.path.join(b.HERE, f"libmtb_{n}.so"), defines=VARIANTS[n]))
+        os.makedirs(LIBDIR, exist_ok=True)
+        print(b.build(out=os.path.join(LIBDIR, f"libmtb_{n}.so"), defines=VARIANTS[n]))
