@@ -251,4 +251,6 @@ struct Tables {
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)
 #define DSF_PERM 2         // a PermutationVector (SharedMatrix rows or cols)
 #define MTB_GRP_REWRITE 0x80000000u  // pending ANNOTATE group / orphan props word: the local op was a rewrite
+#define DSF_OBS_SHIFT 16  // flags >> 16: the reference's short id of the engine's client 0 (a loaded summary's
+                          // observer; mtb_host.cpp HostDoc::obsRef), mapped back by the digest
 #define DSF_MKDUP 4        // a marker id is carried by two markers: blockUpdate re-maps ids (mergeTree.ts:296-306)

@@ -401,6 +401,12 @@ struct HostDoc {
     return s;
   }
   std::string longId(int s) const { return s >= 0 && s < (int)longIds.size() ? longIds[s] : std::string("original"); }
+  // The engine numbers the document's own client (the observer / live client) 0.  A loaded summary names its
+  // clients first (snapshotLoader.ts:94-131), so the reference gives the observer a later short id: obsRef.
+  // Engine ids 0 and obsRef are swapped against the reference's; ref_id maps either way (an involution) where
+  // short ids leave the engine (segment dumps, map_range, getLongClientId, the GPU digest).
+  uint16_t obsRef = 0;
+  int ref_id(int c) const { return c < 0 ? c : c == 0 ? obsRef : c == obsRef ? 0 : c; }
 };
 
 template <class T>
@@ -589,7 +595,7 @@ uint32_t position(const hj::Value& op, const char16_t* k, const char16_t* rel, H
   if (v && v->kind == hj::Value::kNum) return (uint32_t)v->n;
   const hj::Value* rp = member(op, rel);
   if (rp && rp->truthy()) {
-    if (!d) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions here (catch-up or matrix batches)");
+    if (!d) raise(MTB_E_UNSUPPORTED, "unsupported: relative positions in a matrix batch");
     if (rp->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: relative position is not an object");
     auto key = marker_key(member(*rp, u"id"));
     if (!key) raise(MTB_E_UNSUPPORTED, "unsupported: relative position without a marker id (posFromRelativePos -1)");
@@ -626,8 +632,10 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
   const hj::Value* t = member(op, u"type");
   const int type = t && t->kind == hj::Value::kNum ? (int)t->n : -1;
   mtb_op r = base;
-  // relative positions: observer replay in plain SharedString batches
-  HostDoc* rel = (b->matrix || (b->opts.flags & MTB_BATCH_CATCHUP)) ? nullptr : &d;
+  // relative positions: SharedString batches (catch-up tracking included: a message that saw everything before
+  // it is stored verbatim, relative positions and all, and a lagging one is rewritten from its delta entries,
+  // sequence.ts:704-726); not in matrix batches
+  HostDoc* rel = b->matrix ? nullptr : &d;
   if (type == 0) {
     r.pos1 = position(op, u"pos1", u"relativePos1", rel, &r);
     const hj::Value* seg = member(op, u"seg");
@@ -1051,6 +1059,27 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
       if (cs && cs->kind == hj::Value::kArr)
         for (auto& sp : cs->items) body.push_back(load_spec(b, d, sp, d.payload, pc));
     }
+  // the observer becomes engine id 0 (HostDoc::obsRef): swap it with the header's first client everywhere
+  const uint16_t so = d.client(d.observer);
+  if (so != 0) {
+    auto sw = [&](int16_t& c) { c = (int16_t)(c == 0 ? so : c == (int16_t)so ? 0 : c); };
+    auto swap_seg = [&](LoadSeg& g) {
+      sw(g.client);
+      sw(g.rc0);
+      if (g.rcx)
+        for (uint32_t i = 0; i < d.img.aux[g.rcx]; i++) {
+          int16_t c = (int16_t)(int32_t)d.img.aux[g.rcx + 1 + i];
+          sw(c);
+          d.img.aux[g.rcx + 1 + i] = (uint32_t)(int32_t)c;
+        }
+    };
+    for (auto& g : hdr) swap_seg(g);
+    for (auto& g : body) swap_seg(g);
+    std::swap(d.longIds[0], d.longIds[so]);
+    d.shortOf[d.longIds[0]] = 0;
+    d.shortOf[d.longIds[so]] = so;
+    d.obsRef = so;
+  }
   build_load_image(d, hdr);
   // idToSegment after reloadFromSegments: blockUpdate maps the live header markers (mergeTree.ts:296-306)
   if (!d.markerAmbig.empty()) {
@@ -1770,9 +1799,28 @@ void replay(mtb_dev* b, mtb_stats* out) {
       // (the same requirement device_init laid the slices out for: caps_for's text term already counts the
       // initial text, so adding text_used here made every fresh batch re-lay out at twice the caps)
       Caps need = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
+      // ... and what the slices already hold plus the per-record margin for the pending records: a document can
+      // outgrow the record-count formula (a live client holding thousands of unacked inserts keeps an entry per
+      // insert in every ancestor's window list, and list rebuilds allocate before they free)
+      if (s.seg_cap) {
+        // (caps_for's per-record terms without its constants, which the formula above already carries)
+        const uint64_t np = d.pending.size();
+        auto at_least = [](uint32_t& c, uint64_t v) { c = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, v), 0xFFFFFFF0u); };
+        at_least(need.seg, (uint64_t)s.seg_used + 2 * np);
+        at_least(need.blk, (uint64_t)s.blk_used + np / 2);
+        at_least(need.list, (uint64_t)s.list_used + s.list_used / 2 + 8 * np);
+        at_least(need.heap, (uint64_t)s.heap_cnt + np);
+        at_least(need.aux, (uint64_t)s.aux_used + s.aux_used / 4 + 16 * np);
+      }
       if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap ||
           (d.perm && 2 * (d.totalSetcell + d.initText.size() / 2 + 4) > s.text_cap)) {
         want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
+        auto twice = [](uint32_t& c, uint32_t v) { c = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, 2ull * v), 0xFFFFFFF0u); };
+        twice(want[i].seg, need.seg);
+        twice(want[i].blk, need.blk);
+        twice(want[i].list, need.list);
+        twice(want[i].heap, need.heap);
+        twice(want[i].aux, need.aux);
         grow = true;
       } else {
         want[i] = Caps{0, 0, 0, 0, 0, 0};
@@ -1828,6 +1876,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
     mtb_op* out = ops.get() + opOff[i];
     s.mk_cap = (uint32_t)d.markerAmbig.size();
     if (d.markerDup) s.flags |= DSF_MKDUP;
+    s.flags = (s.flags & 0xFFFFu) | ((uint32_t)d.obsRef << DSF_OBS_SHIFT);
     for (mtb_op o : d.pending) {
       // text offsets move with the arena; a PermutationSegment's LOADSEG payload is its handle start
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_LOADSEG) && !(o.flags & MTB_F_MARKER) && !d.perm) o.payload += base;
@@ -1851,11 +1900,16 @@ void replay(mtb_dev* b, mtb_stats* out) {
         // three created per record)
         cap = s.seg_cap + 4ull * b->docs[i].pending.size() + 1;
       } else if (!s.err) {
+        // a marker-relative range is resolved on the device: bound it by the document's length, itself bounded
+        // by the text and segments it holds plus what the records before it insert
+        uint64_t lenBound = (uint64_t)s.text_used + s.seg_used + 1;
         for (const mtb_op& o : b->docs[i].pending) {
+          if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_RELPOS)) lenBound += (o.flags & MTB_F_MARKER) ? 1 : o.pos2;
+          else if (o.type == MTB_OP_INSERT) lenBound += 1 + o.pos2;
+          const uint64_t range = (o.flags & MTB_F_RELPOS) ? lenBound : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0);
           if (o.flags & MTB_F_DELTA)  // (a rewrite annotate's segments get a second entry: the set before)
             cap += o.type == MTB_OP_INSERT ? 1
-                   : ((o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0) + 1) *
-                         (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_REWRITE ? 2 : 1);
+                   : (range + 1) * (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_REWRITE ? 2 : 1);
           if (o.type == MTB_OP_REGEN) cap += (uint64_t)o.pos1 * (s.seg_used + 16);  // one entry per regenerated op
         }
       }
@@ -1981,6 +2035,14 @@ void replay(mtb_dev* b, mtb_stats* out) {
     fprintf(stderr, "mtb_profile max usage: seg %llu blk %llu list %llu text %llu heap %llu aux %llu (records %llu, ops %llu)\n",
             (unsigned long long)mx[0], (unsigned long long)mx[1], (unsigned long long)mx[2], (unsigned long long)mx[3],
             (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mxo);
+  }
+  if (getenv("MTB_SLICE_TRACE")) {  // per-document slice use after each replay (capacity debugging)
+    for (uint32_t i = 0; i < b->ndocs && i < 4; i++) {
+      const DocState& s = b->hst[i];
+      fprintf(stderr, "mtb_slices doc %u ops %llu: seg %u/%u blk %u/%u list %u/%u text %u/%u heap %u/%u aux %u/%u\n", i,
+              (unsigned long long)b->docs[i].totalOps, s.seg_used, s.seg_cap, s.blk_used, s.blk_cap, s.list_used,
+              s.list_cap, s.text_used, s.text_cap, s.heap_cnt, s.heap_cap, s.aux_used, s.aux_cap);
+    }
   }
   if (getenv("MTB_CHECK_OUT")) {  // MTB_CHECK builds: slice-bound violations per document (DocState.pad3)
     static const char* pools[4] = {"segp", "blk", "lst", "aux"};
@@ -2137,7 +2199,7 @@ std::string dump_doc(mtb_dev* b, uint32_t i) {
     }
     // PermutationVectors name clients by long id: their short ids depend on setCell interning order
     auto cl = [&](int c) {
-      if (!d.perm) return std::to_string(c);
+      if (!d.perm) return std::to_string(d.ref_id(c));
       std::string q;
       hj::quote_u8(q, d.longId(c));
       return q;
@@ -4015,7 +4077,7 @@ int mtbx_client_long_id(mtb_dev* b, uint32_t doc, uint32_t short_id, char* buf, 
   return guarded(b, [&] {
     HostDoc& d = docref(b, doc);
     if (short_id >= d.longIds.size()) raise(MTB_E_ARG, "unknown short client id");
-    const std::string& s = d.longIds[short_id];
+    const std::string& s = d.longIds[d.ref_id((int)short_id)];
     if (len_out) *len_out = s.size();
     if (buf) {
       if (cap < s.size() + 1) raise(MTB_E_ARG, "buffer too small");
@@ -4243,11 +4305,11 @@ int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t
           hj::quote(o, reinterpret_cast<const char16_t*>(d.text.data() + g.text), (size_t)g.len);
         }
         o += ",\"cachedLength\":" + std::to_string(g.len) + ",\"seq\":" + std::to_string(seq_out(g.seq)) +
-             ",\"clientId\":" + std::to_string(g.client);
+             ",\"clientId\":" + std::to_string(d.ref_id(g.client));
         if (seg_removed(g)) {
           o += ",\"removedSeq\":" + std::to_string(seq_out(g.rseq)) + ",\"removedClientIds\":[";
           rc_list(d, g, rc);
-          for (size_t q = 0; q < rc.size(); q++) o += (q ? "," : "") + std::to_string(rc[q]);
+          for (size_t q = 0; q < rc.size(); q++) o += (q ? "," : "") + std::to_string(d.ref_id(rc[q]));
           o += "]";
         }
         PropView pv = props_of(b, d, g.props);

@@ -4205,6 +4205,9 @@ extern "C" __global__ void __launch_bounds__(64)
   const uint32_t blk_used = s.blk_used, text_cap = s.text_cap, aux_used = s.aux_used;
   const bool perm = (s.flags & DSF_PERM) != 0;
   const uint32_t root = s.root;
+  // client ids as the reference numbers them: engine id 0 and the observer's reference id swap places
+  const int obs = (int)(s.flags >> DSF_OBS_SHIFT);
+  auto rid = [&](int c) -> uint32_t { return (uint32_t)(c < 0 ? c : c == 0 ? obs : c == obs ? 0 : c); };
   const int sg = lane >> 3, q = lane & 7;  // leaf blocks: lane (segment slot, part)
   uint64_t acc = 0;
   uint64_t nsegs = 0;
@@ -4271,10 +4274,10 @@ extern "C" __global__ void __launch_bounds__(64)
         }
         uint64_t Rc = 0;
         if ((int32_t)rseq >= 0) {
-          Rc = dg_mix(1, (uint32_t)(int32_t)(int16_t)(cli >> 16));
+          Rc = dg_mix(1, rid((int16_t)(cli >> 16)));
           if (rcx) {
             const uint32_t n = rcx < aux_used ? A[rcx] : 0;
-            for (uint32_t i = 0; i < n && rcx + 1 + i < aux_used; i++) Rc += dg_mix(i + 2, A[rcx + 1 + i]);
+            for (uint32_t i = 0; i < n && rcx + 1 + i < aux_used; i++) Rc += dg_mix(i + 2, rid((int32_t)A[rcx + 1 + i]));
           }
         }
         uint64_t Ph = 0;
@@ -4289,7 +4292,7 @@ extern "C" __global__ void __launch_bounds__(64)
         h = dg_mix(h, t);
         h = dg_mix(h, len);
         h = dg_mix(h, (int32_t)seq >= MTB_PEND ? 0xFFFFFFFFu : seq);  // unacked: UnassignedSequenceNumber
-        h = dg_mix(h, (uint32_t)(int32_t)(int16_t)(cli & 0xFFFF));
+        h = dg_mix(h, rid((int16_t)(cli & 0xFFFF)));
         h = dg_mix(h, (int32_t)rseq >= MTB_PEND ? 0xFFFFFFFFu : rseq);
         h = dg_mix(h, Rc);
         h = dg_mix(h, Ph);

@@ -192,7 +192,7 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
  * client.ts:641-662).  A local annotate's keys stay pending on its segments until its ack (remote annotates
  * leave them alone, segmentPropertiesManager.ts:60-157; a local rewrite annotate counts as a pending rewrite).
  * Marker-relative positions resolve in the client's own view.  Matrix and catch-up batches are
- * MTB_E_UNSUPPORTED. */
+ * MTB_E_UNSUPPORTED (a live client's own ops are not tracked as catch-up messages). */
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
 /* A detached edit before collaboration (TestClient.insertTextLocal / removeRangeLocal / annotateRangeLocal
  * while the collab window is not collaborating, client.ts:196-247 with getLocalSequenceNumber() =

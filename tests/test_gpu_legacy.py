@@ -306,3 +306,65 @@ def test_catch_up_validation_follows_the_moving_window_on_the_engine():
     B = MergeTreeBatch(1, catch_up=True)
     with pytest.raises(MergeTreeError, match="Invalid catchup operations in snapshot"):
         B[0].loadSequence(bad, "loader")
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_catch_up_with_marker_relative_positions(new_mode):
+    """SharedString's default configuration (SnapshotLegacy + messagesSinceMSNChange) with annotateMarker and
+    other marker-relative ops (opBuilder.ts:25-43): a message that saw everything before it is stored verbatim,
+    relative positions and all, a lagging one is rewritten from its delta to absolute positions
+    (sequence.ts:704-726, createOpsFromDelta :120-172).  Mid-log legacy summaries with catch-up blobs equal the
+    oracle's byte for byte; loadSequence of them on the engine (relative positions resolved against the loaded
+    markers) equals the oracle that loaded the same blobs, and both continue to the same text and dump."""
+    import json
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from helpers import make_marker_log
+    from pyoracle import OracleDoc, OracleError
+    n, cut = 10, 500
+    logs = [make_marker_log(700 + i, 900, n_clients=3 + i % 3, lag=4 + 3 * i, new_mode=new_mode) for i in range(n)]
+    B = MergeTreeBatch(n, new_length_calc=new_mode, catch_up=True)
+    oracles = []
+    for i, (init, msgs) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("A")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("A")
+        o.enable_catch_up()
+        for m in msgs[:cut]:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    L = MergeTreeBatch(n, new_length_calc=new_mode)
+    loaded, verbatim_rel, refused = {}, 0, 0
+    for i, o in enumerate(oracles):
+        gb, gs = B.summarize_legacy(i)
+        osum = o.summarize_legacy()
+        assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy + catch-up blobs differ"
+        cu = json.loads(dict(osum["blobs"])["catchupOps"])
+        verbatim_rel += sum(1 for m in cu if "relativePos1" in json.dumps(m["contents"]))
+        r = OracleDoc(new_length_calc=new_mode)
+        try:
+            r.apply_catch_up(r.load_v1(osum["blobs"], "loader"))
+        except OracleError as e:
+            # a verbatim message naming a marker removed at or below the MSN: the summary has no such marker
+            # (posFromRelativePos -1); both refuse the document
+            assert "names no marker" in str(e)
+            with pytest.raises(MergeTreeError, match="names no marker"):
+                L[i].loadSequence(osum["blobs"], "loader")
+            refused += 1
+            continue
+        assert L[i].loadSequence(osum["blobs"], "loader")
+        loaded[i] = r
+    assert verbatim_rel > 0, "the catch-up blobs hold no relative-position message"
+    assert len(loaded) >= n // 2, f"{refused} of {n} documents refused"
+    L.flush()
+    for i, r in loaded.items():
+        assert L.dump_segments(i) == r.dump_segments(), f"doc {i}: dump after catch-up"
+        for m in logs[i][1][cut:]:
+            L[i].applyMsg(m)
+            r.apply_msg(m)
+    L.flush()
+    for i, r in loaded.items():
+        assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"
