@@ -153,7 +153,7 @@ struct Lru {
   int32_t maxSeq;
 };
 
-struct DocState {     // 320 bytes
+struct DocState {     // 448 bytes
   // slice bases (elements) and capacities
   uint64_t op_base;
   uint64_t seg_base, blk_base, list_base, text_base, heap_base, aux_base, free_base;
@@ -196,8 +196,12 @@ struct DocState {     // 320 bytes
   uint32_t pend_cap;    // directory entries (a power of two, 0: none yet; doubles when full)
   uint32_t mk_all;      // aux offset of [n, cap, (segment, ordinal)*]: every marker inserted with an id (0: none)
   uint32_t pad3[4];
+  // phantom partial lengths of a loaded summary's removed collaborator-inserted body segments (DSF_PHANTOM):
+  // aux offset of [n, cap, (block, removedSeq, length, removedClientIds[0], removers list, -, -, -) * cap]
+  uint32_t ph;
+  uint32_t pad4[15];
 };
-static_assert(sizeof(DocState) == 384, "DocState is copied as 96 dwords (mtb_rewind_kernel)");
+static_assert(sizeof(DocState) == 448, "DocState is read as 112 dwords (two vector loads, mtb_rewind_kernel)");
 
 // Batch-global interned tables (read-only on the device).
 struct Tables {
@@ -253,4 +257,5 @@ struct Tables {
 #define MTB_GRP_REWRITE 0x80000000u  // pending ANNOTATE group / orphan props word: the local op was a rewrite
 #define DSF_OBS_SHIFT 16  // flags >> 16: the reference's short id of the engine's client 0 (a loaded summary's
                           // observer; mtb_host.cpp HostDoc::obsRef), mapped back by the digest
+#define DSF_PHANTOM 8      // a loaded summary left phantom partial lengths (DocState.ph; mtb_replay.hip)
 #define DSF_MKDUP 4        // a marker id is carried by two markers: blockUpdate re-maps ids (mergeTree.ts:296-306)

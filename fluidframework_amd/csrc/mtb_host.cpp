@@ -257,6 +257,7 @@ struct LoadImage {
   uint32_t root = 0;
   uint32_t mk_map = 0, mk_n = 0;  // idToSegment of the live header markers (in `aux`)
   uint32_t mk_all = 0;            // DocState.mk_all: the live header markers with an id (in `aux`)
+  uint32_t ph = 0;                // DocState.ph: the phantom partial-length table (in `aux`; 0 = none)
 };
 
 // ------------------------------------------------------------------ SharedMatrix cells
@@ -361,6 +362,7 @@ struct HostDoc {
   uint64_t totalPayload = 0;
   // SnapshotV1 load (mtb_doc_load_v1): the reloaded header; the body segments are LOADSEG records
   bool loaded = false;
+  bool phantom = false;  // a loaded summary with removed collaborator-inserted body segments (DSF_PHANTOM)
   // SharedSegmentSequence.messagesSinceMSNChange (MTB_BATCH_CATCHUP, sequence.ts:697-748): stored
   // messages; a lagging one is rewritten from the delta entries of its records (pending[first, +count))
   struct CatchMsg {
@@ -1081,6 +1083,20 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
     d.obsRef = so;
   }
   build_load_image(d, hdr);
+  // removed body segments inserted by collaborating clients: their inserts take blockUpdateLength's incremental
+  // path and leave phantom partial lengths (mtb_replay.hip "phantom partial lengths"); the table starts empty
+  {
+    size_t nph = 0;
+    for (const LoadSeg& g : body) nph += g.rseq >= 0 && g.client != -2;
+    if (nph && !d.perm) {
+      const uint32_t cap = (uint32_t)std::min<size_t>(8 * nph + 16, 1u << 20);
+      d.img.ph = (uint32_t)d.img.aux.size();
+      d.img.aux.push_back(0);
+      d.img.aux.push_back(cap);
+      d.img.aux.resize(d.img.aux.size() + 8ull * cap, 0u);
+      d.phantom = true;
+    }
+  }
   // idToSegment after reloadFromSegments: blockUpdate maps the live header markers (mergeTree.ts:296-306)
   if (!d.markerAmbig.empty()) {
     LoadImage& im = d.img;
@@ -1113,9 +1129,9 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
       while (j < body.size() && body[j].client == -2 && body[j].seq == 0) j++;
     for (size_t k = i; k < j; k++) {
       const LoadSeg& g = body[k];
-      if (g.rseq >= 0 && g.client != -2)
-        raise(MTB_E_UNSUPPORTED, "unsupported: removed body segment inserted by a collaborating client "
-                                 "(blockUpdateLength's incremental path, mergeTree.ts:2419-2431)");
+      if (g.rseq >= 0 && g.client != -2 && d.perm)
+        raise(MTB_E_UNSUPPORTED, "unsupported: removed PermutationVector body segment inserted by a collaborating "
+                                 "client (blockUpdateLength's incremental path, mergeTree.ts:2419-2431)");
       mtb_op r{};
       r.type = MTB_OP_LOADSEG;
       r.flags = (uint8_t)((g.marker ? MTB_F_MARKER : 0) | (k == i ? MTB_F_LDFIRST : 0) | (k + 1 == j ? MTB_F_LDLAST : 0));
@@ -1336,6 +1352,8 @@ void device_init(mtb_dev* b) {
       s.mk_map = im.mk_map;
       s.mk_n = im.mk_n;
       s.mk_all = im.mk_all;
+      s.ph = im.ph;
+      if (d.phantom) s.flags |= DSF_PHANTOM;
       s.heap_cnt = 0;
       s.text_used = (uint32_t)d.initText.size();
       segc.add(recs.size(), s.seg_base, im.segp.size());
@@ -1661,8 +1679,8 @@ void launch_main(mtb_dev* b, const Tables& t) {
     // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
     // batches where some document met a marker id
     bool markers = false;
-    for (uint32_t i = 0; i < b->ndocs && !markers; i++)
-      markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot;
+    for (uint32_t i = 0; i < b->ndocs && !markers; i++)  // (the marker variant carries the phantom tables too)
+      markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot || b->docs[i].phantom;
     // more documents than wave slots: tickets, one per workgroup (mtb_replay_tick_kernel, the default;
     // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document) or passes of equal chunks (MTB_SCHED=passes);
     // MTB_SCHED=0 launches one wave per whole document

@@ -304,6 +304,12 @@ struct Eng {
   bool pk_rw;                   // MODE_LIVE: pending_keys found a pending local rewrite on the segment
   int32_t* xch;                 // MODE_MATRIX: the workgroup's setCell exchange slots [2 parities][2 waves]
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
+  // phantom partial lengths of loaded documents (see "phantom partial lengths" below)
+  static constexpr bool hasPh = MODE == MODE_LOAD || MODE == MODE_MARKERS || MODE == MODE_LIVE;
+  uint32_t ph_off;              // DocState.ph: aux offset of the table (0: none)
+  bool phDoc;                   // DSF_PHANTOM (hasPh modes)
+  int ph_split_top;             // the topmost depth the last fix_overflow split (MTB_VDEPTH: none)
+  bool ph_ow;                   // markRangeRemoved's _overwrite, set during the current op's nodeMap
   uint64_t prof[NPH];
   uint32_t evc[NCN];
 
@@ -549,9 +555,18 @@ struct Eng {
     }
     PROF_CNT(CN_ENTRIES, done < lcnt ? done : lcnt);
     wsync();
+    int phs = 0;  // the phantom surplus of a block child (loaded documents only)
+    if constexpr (hasPh) {
+      if (COLD(phDoc) && !(isLive && C == 0)) {
+        const int c0 = lane < MTB_MAXCH ? sh->corr[lane] : 0;  // (ph_view reuses corr[])
+        phs = ph_view(w, count, Rl, C);
+        if (lane < MTB_MAXCH) sh->corr[lane] = c0;
+        wsync();
+      }
+    }
     if (lane < count) {
       k.id = w;
-      k.rl = (w & MTB_LEAF) ? leaf_len((int)flen, (int)k.seq, (int)k.rseq, k.cli, frcx, R, C) : (int)flen - sh->corr[lane];
+      k.rl = (w & MTB_LEAF) ? leaf_len((int)flen, (int)k.seq, (int)k.rseq, k.cli, frcx, R, C) : (int)flen - sh->corr[lane] + phs;
       V.rl[lane] = k.rl;
     }
     if (lane == 0) {
@@ -1167,6 +1182,14 @@ struct Eng {
         b = U(sh->v[level].b);
         nb = split_block(level);
         if (err) break;
+        if constexpr (hasPh) {
+          if (COLD(phDoc)) {  // split (mergeTree.ts:1858-1871): both halves nodeUpdateLengthNewStructure
+            ph_combine(b);
+            ph_combine(nb);
+            ph_split_top = level;
+            if (err) break;
+          }
+        }
         phase = sp_internal ? 1 : 3;
         continue;
       }
@@ -1254,6 +1277,9 @@ struct Eng {
           blk[X].lcap = e;
         }
         wsync();
+        if constexpr (hasPh) {
+          if (COLD(phDoc)) ph_combine(X);  // updateRoot (mergeTree.ts:1268-1277)
+        }
         break;
       }
     }
@@ -1275,6 +1301,123 @@ struct Eng {
       const uint32_t n = rcx ? U(aux[rcx]) : 0u;
       for (uint32_t i = 0; i < n && !err; i++) append_levels(0, d, rseq, (int)U(aux[rcx + 1 + i]), WK_OVERLAP, len);
     }
+  }
+
+  // ------------------------------------------------------------------ phantom partial lengths
+  // A SnapshotV1 load appends a removed body segment P inserted by a collaborating client alone, through
+  // blockUpdateLength's incremental path (snapshotLoader.ts:242-254 -> mergeTree.ts:2436-2453): every block
+  // that update() reaches adds P's cachedLength at P's seq (removedSeq !== seq, partialLengths.ts:636-686) and
+  // nothing ever records P's removal there.  The window lists stay exact; the surplus is a per-document table
+  // in the aux arena (DocState.ph): [n, cap, (block, rseq, len, rc0, rcx, -, -, -) * cap].  A block child's
+  // length in a remote view then adds len(P) for each of its entries whose exact-list removal would count:
+  // rseq <= max(refSeq, minSeq), or the viewer is one of P's removers.  Entries follow the reference's
+  // recombinations (PartialSequenceLengths.combine, :256-338): a recombined block of segments has none, a
+  // recombined block of blocks the union of its children's; update() leaves them.
+  __device__ __forceinline__ void ph_add(uint32_t node, uint32_t rseq, uint32_t len, uint32_t rc0, uint32_t rcx) {
+    const uint32_t n = U(aux[ph_off]), cap = U(aux[ph_off + 1]);
+    if (n >= cap) {
+      const uint32_t ncap = 2 * cap + 8;
+      const uint32_t h = alloc_aux(2 + 8 * ncap);
+      if (bad()) return;
+      for (uint32_t i = lane; i < 8 * n; i += 64) aux[h + 2 + i] = aux[ph_off + 2 + i];
+      if (lane == 0) {
+        aux[h] = n;
+        aux[h + 1] = ncap;
+      }
+      wsync();
+      ph_off = h;
+    }
+    if (lane < 8) {
+      const uint32_t v = lane == 0 ? node : lane == 1 ? rseq : lane == 2 ? len : lane == 3 ? rc0 : lane == 4 ? rcx : 0u;
+      aux[ph_off + 2 + 8 * n + lane] = v;
+    }
+    if (lane == 0) aux[ph_off] = n + 1;
+    wsync();
+  }
+  __device__ __forceinline__ void ph_clear(uint32_t node) {
+    const uint32_t n = U(aux[ph_off]);
+    uint32_t w = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      const bool v = i < n;
+      uint32_t e[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) e[q] = v ? aux[ph_off + 2 + 8 * i + q] : 0u;
+      const bool keep = v && e[0] != node;
+      const unsigned long long m = __ballot(keep);
+      wsync();  // (the chunk is read before its entries move down: w <= base)
+      if (keep) {
+        const uint32_t o = w + rank_below(m);
+#pragma unroll
+        for (int q = 0; q < 5; q++) aux[ph_off + 2 + 8 * o + q] = e[q];
+      }
+      w += (uint32_t)__popcll(m);
+      wsync();
+    }
+    if (lane == 0) aux[ph_off] = w;
+    wsync();
+  }
+  // nodeUpdateLengthNewStructure(X) / PartialSequenceLengths.combine(X) for the table
+  __device__ __forceinline__ void ph_combine(uint32_t X) {
+    ph_clear(X);
+    if (bad()) return;
+    const uint32_t cnt = U(blk[X].count);
+    const uint32_t c0 = cnt ? U(blk[X].f[F_ID][0]) : (uint32_t)MTB_LEAF;
+    if (c0 & MTB_LEAF) return;  // a block of segments: fromLeaves, exact
+    const uint32_t kid = (uint32_t)lane < cnt ? blk[X].f[F_ID][lane] : MTB_NONE;
+    const uint32_t n = U(aux[ph_off]);
+    for (uint32_t base = 0; base < n && !err; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      const uint32_t node = i < n ? aux[ph_off + 2 + 8 * i] : MTB_NONE;
+      bool match = false;
+      for (uint32_t q = 0; q < cnt; q++) match |= node == rlu(kid, (int)q);
+      unsigned long long m = __ballot(match);
+      while (m && !err) {
+        const uint32_t t = base + (uint32_t)first_set(m);
+        m &= m - 1;
+        const uint32_t o = ph_off + 2 + 8 * t;
+        ph_add(X, U(aux[o + 1]), U(aux[o + 2]), U(aux[o + 3]), U(aux[o + 4]));
+      }
+    }
+  }
+  // blockUpdatePathLengths(b, .., newStructure = true): b and every ancestor, bottom-up
+  __device__ __forceinline__ void ph_up(uint32_t b) {
+    for (int guard = 0; b != MTB_NONE && !err; guard++) {
+      if (guard >= MTB_VDEPTH || b >= blk_used) { fail(DERR_SHAPE); return; }
+      ph_combine(b);
+      b = U(blk[b].parent);
+    }
+  }
+  // the surplus of each block child of the record on lanes 0..7 (ids `w`) in the (Rl, C) view, into corr[]
+  __device__ __forceinline__ int ph_view(uint32_t w, int count, int Rl, int C) {
+    if (lane < MTB_MAXCH) sh->corr[lane] = 0;
+    wsync();
+    const uint32_t n = U(aux[ph_off]);
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      uint32_t node = MTB_NONE, rseq = 0, len = 0, rc0 = 0, rcx = 0;
+      if (i < n) {
+        const uint32_t o = ph_off + 2 + 8 * i;
+        node = aux[o];
+        rseq = aux[o + 1];
+        len = aux[o + 2];
+        rc0 = aux[o + 3];
+        rcx = aux[o + 4];
+      }
+      int j = -1;
+      for (int q = 0; q < count; q++)
+        if (node == rlu(w, q) && !(node & MTB_LEAF)) j = q;
+      if (j >= 0) {
+        bool vis = (int)rseq <= Rl || (int)(int16_t)rc0 == C;
+        if (!vis && rcx) {
+          const uint32_t nr = aux[rcx];
+          for (uint32_t r = 0; r < nr && !vis; r++) vis = (int)aux[rcx + 1 + r] == C;
+        }
+        if (vis) atomicAdd(&sh->corr[j], (int)len);
+      }
+    }
+    wsync();
+    return lane < MTB_MAXCH ? sh->corr[lane] : 0;
   }
 
   // blockInsert's continuePredicate (mergeTree.ts:1611-1615, forwardExcursion mergeTreeNodeWalk.ts:121-138):
@@ -1713,6 +1856,7 @@ struct Eng {
   // set when a remote remove overtook it), join the LRU in group order, and their paths' lists are rebuilt.
   __device__ __forceinline__ void ack_group(int S, int opType) {
     if (pend_n == 0) return;
+    bool ack_ow = false;
     const auto e = grp_ent(0);
     const uint32_t off = U(e[1]), cnt = U(e[2]);
     if (off + cnt > aux_used) { fail(DERR_SHAPE); return; }
@@ -1743,6 +1887,7 @@ struct Eng {
       } else {
         if (rs < 0) { fail(DERR_ACK_REMOVE); return; }
         if (rs >= MTB_PEND && lane == 0) blk[b].f[F_RSEQ][j] = (uint32_t)S;
+        if (rs < MTB_PEND) ack_ow = true;  // a remote remove overtook it: overwrite (mergeTree.ts:1300-1312)
       }
       n_mod += 1;
       wsync();
@@ -1766,6 +1911,18 @@ struct Eng {
       const uint32_t b = U(segp[U(aux[off + i])]);  // (ids checked above)
       if (b != prev) rebuild_up(b);
       prev = b;
+    }
+    if constexpr (hasPh) {
+      // blockUpdatePathLengths(node, seq, clientId, overwrite): recombined only with overwrite
+      if (COLD(phDoc && ack_ow)) {
+        prev = MTB_NONE;
+        for (uint32_t i = 0; i < cnt && !err; i++) {
+          const uint32_t b = U(segp[U(aux[off + i])]);
+          bool seen = false;
+          for (uint32_t q = 0; q < i; q++) seen |= U(segp[U(aux[off + q])]) == b;
+          if (!seen) ph_up(b);
+        }
+      }
     }
     view_clear();
   }
@@ -1975,6 +2132,16 @@ struct Eng {
       const uint32_t b = E(i, 1);
       if (b != prev) rebuild_up(b);
       prev = b;
+    }
+    if constexpr (hasPh) {
+      if (COLD(phDoc)) {  // (mergeTree.ts:2320-2331: every ancestor of the moved segments recombined)
+        prev = MTB_NONE;
+        for (uint32_t i = 0; i < n && !err; i++) {
+          const uint32_t b = E(i, 1);
+          if (b != prev) ph_up(b);
+          prev = b;
+        }
+      }
     }
   }
   // normalizeSegmentsOnRebase (mergeTree.ts:2357-2390): runs of removed / unacked segments holding both an
@@ -2410,6 +2577,9 @@ struct Eng {
       // overlapping removes (already removed): append C to removedClientIds (copy-on-write list) and an
       // OVERLAP entry on every ancestor list (no observer-length change)
       unsigned long long om = __ballot(visit && rseq >= 0 && !(isLive && rseq >= MTB_PEND));
+      if constexpr (hasPh) {
+        if (__ballot(visit && rseq >= 0)) ph_ow = true;  // _overwrite (mergeTree.ts:1978-1995)
+      }
       if (COLD(om))
       while (om) {
         const int t = first_set(om);
@@ -2514,6 +2684,7 @@ struct Eng {
   // the next child descended into is the first slot at or after the cursor that overlaps the range.
   __device__ __forceinline__ void node_map(int start, int end, int R, int C, int S, bool remove, uint32_t opId, int comb) {
     if (end == start) return;
+    ph_ow = false;
     int d = 0;
     bool exiting = false;  // a leaf block reached `end`: every open block is only flushed from here on
     walk_depth = -1;       // (pp[] holds the node_map block starts below)
@@ -2584,6 +2755,14 @@ struct Eng {
           blk[sh->path[d]].len = v;
         }
         wsync();
+      }
+      if constexpr (hasPh) {
+        // afterMarkRemoved (mergeTree.ts:2019-2026): once the op overwrote a removal, each block it finishes
+        // is recombined (nodeUpdateLengthNewStructure), the earlier ones were updated
+        if (COLD(phDoc && ph_ow)) {
+          ph_combine(U(sh->path[d]));
+          if (bad()) return;
+        }
       }
       if (d == 0) break;
       d--;
@@ -2965,7 +3144,12 @@ struct Eng {
       // the new blocks reuse the siblings' records (block identity is not observable): no free-stack
       // round trip; siblings beyond the new count go back to the free stack
       for (int i = 0; i < pc; i++) {
-        if (i >= cc) free_blk(rlu(kids, i));
+        if (i >= cc) {
+          free_blk(rlu(kids, i));
+          if constexpr (hasPh) {
+            if (COLD(phDoc)) ph_clear(rlu(kids, i));
+          }
+        }
         list_free(rlu(kloff, i), rlu(kcap, i));
       }
       if (nh > 0) {
@@ -2982,6 +3166,12 @@ struct Eng {
           const uint32_t nb = q < pc ? rlu(kids, q) : alloc_blk();
           if (bad()) return;
           const int len = place_children(nb, taken, n);
+          if constexpr (hasPh) {
+            if (COLD(phDoc)) {  // the packed block's nodeUpdateLengthNewStructure (zamboni.ts:103)
+              ph_combine(nb);
+              if (bad()) return;
+            }
+          }
           bool kblk = false;
           if (lane < n) kblk = !(sh->hold[F_ID][taken + lane] & MTB_LEAF);
           const int kb = __ballot(kblk) != 0;
@@ -3038,6 +3228,9 @@ struct Eng {
       if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {
         parent = pparent;
         continue;
+      }
+      if constexpr (hasPh) {
+        if (COLD(phDoc)) ph_up(parent);  // blockUpdatePathLengths(parent, .., true) (zamboni.ts:116-118)
       }
       break;
     }
@@ -3229,8 +3422,14 @@ struct Eng {
         place_children(b, 0, nh);
         PROF_ZADD(PH_PLACE, tz);
         tz = PROF_T();
-        if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) pack_parent(parent);
-        else mk_remap_hold(0, nh);  // blockUpdatePathLengths(block, .., true) (zamboni.ts:55)
+        if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) {
+          pack_parent(parent);
+        } else {
+          mk_remap_hold(0, nh);  // blockUpdatePathLengths(block, .., true) (zamboni.ts:55)
+          if constexpr (hasPh) {
+            if (COLD(phDoc)) ph_up(b);
+          }
+        }
         PROF_ADD(PH_PACK, tz);
       } else {
         PROF_ZADD(PH_PLACE, tz);
@@ -3495,7 +3694,24 @@ struct Eng {
         fail(DERR_INSERT);
         return;
       }
+      const int dins = U(ins_depth);
+      ph_split_top = MTB_VDEPTH;
       settle();
+      if (bad()) return;
+      if constexpr (hasPh) {
+        if (COLD(phDoc)) {
+          if (C == -2) {
+            // NonCollabClient: blockUpdateLength recombines every block of the path (mergeTree.ts:2447-2452)
+            ph_up(U(ins_blk));
+          } else if (rseq >= 0) {
+            // a removed segment of a collaborating client: update() adds it to every path block that did
+            // not split (the split halves were recombined; the new root too)
+            const int top = ph_split_top < dins + 1 ? ph_split_top : dins + 1;
+            for (int i = 0; i < top && !err; i++) ph_add(U(sh->path[i]), (uint32_t)rseq, (uint32_t)len, o.msn, o.pos1);
+          }
+          if (bad()) return;
+        }
+      }
       if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);
       ld_pos += len;
     }
@@ -3719,7 +3935,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   // through the scalar cache: within one launch of mtb_replay_tick_kernel another workgroup wrote it (the
   // previous chunk's), and the hand-over's acquire does not invalidate the scalar cache.
   const uint32_t dw0 = reinterpret_cast<const uint32_t*>(ds)[lane_id()];
-  const uint32_t dw1 = lane_id() < 32 ? reinterpret_cast<const uint32_t*>(ds)[64 + lane_id()] : 0u;
+  const uint32_t dw1 = lane_id() < (int)(sizeof(DocState) / 4 - 64) ? reinterpret_cast<const uint32_t*>(ds)[64 + lane_id()] : 0u;
 #define DSF(f) ds_word(dw0, dw1, offsetof(DocState, f) / 4)
 #define DSF64(f) (((uint64_t)ds_word(dw0, dw1, offsetof(DocState, f) / 4 + 1) << 32) | ds_word(dw0, dw1, offsetof(DocState, f) / 4))
 #ifdef MTB_CHECK
@@ -3778,6 +3994,10 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
 #endif
   e.ann_mk = 0;
   e.delta_used = DSF(delta_used);
+  e.ph_off = DSF(ph);
+  e.phDoc = Eng<MODE, SCR>::hasPh && (DSF(flags) & DSF_PHANTOM) != 0 && e.ph_off != 0;
+  e.ph_split_top = MTB_VDEPTH;
+  e.ph_ow = false;
   e.cur_k = 0;
   e.sp_internal = false;
   e.local_seq = (int)DSF(local_seq);
@@ -3893,6 +4113,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
     ds->heap_cnt = e.heap_cnt;
     ds->aux_used = e.aux_used;
     ds->delta_used = e.delta_used;
+    ds->ph = e.ph_off;
     if (MODE == MODE_LIVE) {
       ds->local_seq = e.local_seq;
       ds->pend_dir = e.pend_dir;
@@ -4567,14 +4788,14 @@ hipError_t mtb_launch_extract_v1(hipStream_t stream, const DocState* docs, const
 // DocState header, the root block and the initial segment's parent; ops and payload stay resident.
 extern "C" __global__ void mtb_rewind_kernel(DocState* docs, const DocState* pristine, uint32_t ndocs, uint32_t* segp,
                                              const uint32_t* psegp, FBlk* blks, const FBlk* pblk) {
-  // one 64-lane wave per document: lanes copy the 384-byte header and the 320-byte root block
+  // one 64-lane wave per document: lanes copy the DocState header and the 320-byte root block
   const uint32_t i = blockIdx.x;
   const int l = threadIdx.x;
   if (i >= ndocs) return;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(pristine + i);
   uint32_t* dst = reinterpret_cast<uint32_t*>(docs + i);
   dst[l] = src[l];
-  if (l < 32) dst[64 + l] = src[64 + l];
+  if (l < (int)(sizeof(DocState) / 4 - 64)) dst[64 + l] = src[64 + l];
   const uint64_t bb = pristine[i].blk_base, sb = pristine[i].seg_base;
   const uint32_t* ps = reinterpret_cast<const uint32_t*>(pblk + i);
   uint32_t* bd = reinterpret_cast<uint32_t*>(blks + bb);

@@ -675,3 +675,50 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
         msgs.append(m)
     gen.close()
     return initial, msgs
+
+
+def make_tail_log(seed, n_msgs, n_clients=4, lag=48, initial_len=12000, lo=10200, new_mode=False, inserters=None):
+    """A multi-client log that edits only positions >= `lo` of a long initial text (remote views, lagging
+    refSeqs, inserts / removes / annotates; MSN = the lowest refSeq); only the clients in `inserters` (indices,
+    default all) insert.  With lo = initial_len and one inserter, a SnapshotV1 summary taken mid-log loads in
+    the reference too (every body segment is visible in the (refSeq 0, inserter) view the loader appends it in,
+    snapshotLoader.ts:201-254), and its body holds that client's segments removed above the MSN by any client:
+    phantom partial lengths.  Returns (text, msgs)."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed)
+    text = "".join(rng.choice("abcdefghij ") for _ in range(initial_len))
+    ids = [f"client-{k}" for k in range(n_clients)]
+    gen = OracleDoc(new_length_calc=new_mode)
+    gen.insert_text_local(0, text)
+    gen.start_collab("gen-observer")
+    short = {}
+    for cid in ids:
+        gen.add_client(cid)
+        short[cid] = len(short) + 1
+    ref = [0] * n_clients
+    msgs = []
+    ins = list(range(n_clients)) if inserters is None else list(inserters)
+    for seq in range(1, n_msgs + 1):
+        k = rng.randrange(n_clients)
+        ref[k] = max(ref[k], seq - 1 - rng.randint(0, lag))
+        R, cid = ref[k], ids[k]
+        n = gen.remote_length(R, short[cid])
+        r = rng.random()
+        if k not in ins and n <= lo + 2:
+            k = ins[0]
+            R, cid = ref[k], ids[k]
+            n = gen.remote_length(R, short[cid])
+        if k in ins and (r < 0.5 or n <= lo + 2):
+            op = {"type": 0, "pos1": rng.randint(lo, n), "seg": "".join(rng.choice("XYZ\n") for _ in range(rng.randint(1, 5)))}
+        else:
+            a = rng.randint(lo, n - 1)
+            b = min(n, a + rng.randint(1, 6))
+            op = {"type": 1, "pos1": a, "pos2": b} if r < 0.8 else \
+                {"type": 2, "pos1": a, "pos2": b, "props": {"k": rng.randint(0, 2)}}
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": min(ref),
+             "type": "op", "contents": op}
+        gen.apply_msg(m)
+        msgs.append(m)
+    gen.close()
+    return text, msgs

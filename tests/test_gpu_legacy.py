@@ -363,8 +363,14 @@ def test_catch_up_with_marker_relative_positions(new_mode):
     for i, r in loaded.items():
         assert L.dump_segments(i) == r.dump_segments(), f"doc {i}: dump after catch-up"
         for m in logs[i][1][cut:]:
+            try:
+                r.apply_msg(m)
+            except OracleError as e:  # (as above: a marker the loaded summary does not hold)
+                assert "names no marker" in str(e)
+                with pytest.raises(MergeTreeError, match="names no marker"):
+                    L[i].applyMsg(m)
+                break
             L[i].applyMsg(m)
-            r.apply_msg(m)
     L.flush()
     for i, r in loaded.items():
         assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"

@@ -141,12 +141,13 @@ def test_host_rejects_unresolvable_relative_positions_at_pack_time():
     L[0].applyMsg(_msg("B", 2, 1, 0, mk))
     L[0].insertSegmentLocal(0, "x")
     L[0].applyMsg(_msg("B", 3, 2, 0, rm))
-    # a live client's local ops and catch-up batches take absolute positions only
+    # catch-up batches take relative positions too (round 5: tests/test_gpu_legacy.py)
     C = MergeTreeBatch(1, catch_up=True)
     C[0].startOrUpdateCollaboration("A")
     C[0].applyMsg(_msg("B", 1, 0, 0, mk))
-    with pytest.raises(MergeTreeError, match="relative positions here"):
-        C[0].applyMsg(_msg("B", 2, 1, 0, {"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
+    C[0].applyMsg(_msg("B", 2, 1, 0, {"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
+    with pytest.raises(MergeTreeError, match="names no marker"):
+        C[0].applyMsg(_msg("B", 3, 2, 0, {"type": 0, "relativePos1": {"id": "zz"}, "seg": "x"}))
 
 
 def test_annotate_may_not_change_a_marker_id():
