@@ -215,7 +215,15 @@ struct Tables {
   uint32_t class_trivial;    // every matchProperties class holds one value id: classes compare as value ids
   uint32_t mk_key;           // key id of "markerId" (MTB_NONE: no property set names it)
   uint32_t nan_val;          // value id of NaN (incr annotates; MTB_NONE: none packed); val_falsy bit 1 marks
-                             // the values that incr turns into NaN (numbers, booleans, NaN)
+                             // the values that incr turns into NaN (numbers, booleans, NaN); bit 2 objects whose
+                             // seq is -1 (a consensus annotate completes them in place)
+  // matchProperties of keys whose values are no equivalence (mtb_host.cpp Interner): key_irr[k] = 1 + offset
+  // of [n, n x n bits] in irr (0: regular key, compare val_class); bit (i * n + j) = matchProperties(v_i, v_j)
+  // for the key's values of local index i (first argument) and j (val_local)
+  const uint32_t* key_irr;
+  const uint32_t* val_local;
+  const uint32_t* irr;
+  uint32_t irr_any;          // irregular keys exist: matchProperties is neither symmetric nor reflexive there
 };
 
 // device error codes (DocState.err)
@@ -244,7 +252,11 @@ struct Tables {
 #define DERR_REGEN 21      // regeneratePendingOp without the pending group(s) it names (0x033 / 0x035)
 #define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
 #define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
+#define DERR_STALE 25        // a summary body insert whose incremental partial-length update leaves stale cumulative
+                             // lengths (partialLengths.ts:543-577 addSeq below newer entries): unsupported
 #define DERR_INCR 24         // an incr annotate over a string / object value (not NaN: unsupported on the device)
+#define DERR_CONSENSUS 26    // a consensus annotate over an object value whose seq is -1 (completed in place, shared
+                             // with split clones) or, with a null defaultValue, over a segment lacking the key
 // ticket scheduler words (mtb_replay_tick_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32

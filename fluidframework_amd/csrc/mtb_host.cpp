@@ -59,7 +59,7 @@ hipError_t mtb_launch_matrix(hipStream_t stream, uint32_t ndocs, DocState* docs,
                              Tables tables);
 hipError_t mtb_launch_extract_v1(hipStream_t stream, const DocState* docs, const uint32_t* list, uint32_t n,
                                  const FBlk* blks, const uint16_t* text, const uint32_t* aux, const uint32_t* pool,
-                                 const uint32_t* vcl, uint32_t* cnt, const uint64_t* off, uint32_t* items,
+                                 const Tables& tab, uint32_t* cnt, const uint64_t* off, uint32_t* items,
                                  uint16_t* otext, uint32_t* owords);
 hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState* docs, const FBlk* blks,
                              const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint64_t* khash,
@@ -90,15 +90,70 @@ struct MtbError {
     if (e_ != hipSuccess) raise(MTB_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
+// matchProperties (properties.ts:71-96) restated on parsed JSON values (JS semantics for the keys of
+// primitives: strings expose their indices, other primitives none)
+std::vector<U16> js_keys_of(const hj::Value* v) {
+  std::vector<U16> k;
+  if (!v) return k;
+  if (v->kind == hj::Value::kObj) for (auto& m : v->members) k.push_back(m.first);
+  else if (v->kind == hj::Value::kArr) for (size_t i = 0; i < v->items.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
+  else if (v->kind == hj::Value::kStr) for (size_t i = 0; i < v->s.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
+  return k;
+}
+bool js_get_of(const hj::Value* v, const U16& key, hj::Value& tmp, const hj::Value*& out) {
+  out = nullptr;
+  if (!v) return false;
+  if (v->kind == hj::Value::kObj) { out = v->find(key.c_str()); return out != nullptr; }
+  uint32_t idx;
+  if (!hj::array_index(key, &idx)) return false;
+  if (v->kind == hj::Value::kArr && idx < v->items.size()) { out = &v->items[idx]; return true; }
+  if (v->kind == hj::Value::kStr && idx < v->s.size()) { tmp.kind = hj::Value::kStr; tmp.s = U16(1, v->s[idx]); out = &tmp; return true; }
+  return false;
+}
+bool js_strict_eq(const hj::Value* a, const hj::Value* b) {
+  if (!a || !b) return a == b;
+  if (a->kind != b->kind) return false;
+  switch (a->kind) {
+    case hj::Value::kNull: case hj::Value::kUndef: return true;
+    case hj::Value::kBool: return a->b == b->b;
+    case hj::Value::kNum: return a->n == b->n;
+    case hj::Value::kStr: return a->s == b->s;
+    default: return a == b;  // object identity
+  }
+}
+bool js_match_props(const hj::Value* a, const hj::Value* b) {
+  if ((!a || !a->truthy()) && (!b || !b->truthy())) return true;
+  const auto ka = js_keys_of(a), kb = js_keys_of(b);
+  if (ka.size() != kb.size()) return false;
+  for (auto& k : ka) {
+    hj::Value ta, tb;
+    const hj::Value *av = nullptr, *bv = nullptr;
+    if (!js_get_of(b, k, tb, bv) || !bv || bv->kind == hj::Value::kUndef) return false;
+    js_get_of(a, k, ta, av);
+    if (bv->kind == hj::Value::kObj || bv->kind == hj::Value::kArr || bv->kind == hj::Value::kNull) {
+      if (!js_match_props(av, bv)) return false;
+    } else if (!js_strict_eq(bv, av)) {
+      return false;
+    }
+  }
+  return true;
+}
+// one key's step of matchProperties (properties.ts:84-92): b's value an object, array or null recurses,
+// anything else compares strictly
+bool js_match_value(const hj::Value* a, const hj::Value* b) {
+  if (!b || b->kind == hj::Value::kUndef) return false;
+  if (b->kind == hj::Value::kObj || b->kind == hj::Value::kArr || b->kind == hj::Value::kNull) return js_match_props(a, b);
+  return js_strict_eq(b, a);
+}
+
 // ------------------------------------------------------------------ interning
 struct Interner {
   std::vector<U16> keys;
   std::vector<std::string> keyJson;  // each key quoted as a JSON string (the summary serializers' props)
   std::map<U16, uint32_t> keyId;
   std::vector<uint32_t> keyRank;
-  std::vector<uint8_t> keyKinds;  // bit0 primitive seen, bit1 object-like seen
   std::vector<std::string> valJson;
-  std::unordered_map<std::string, uint32_t> valId;
+  std::unordered_map<std::string, uint32_t> valId;  // "<key id>:" + JSON -> value id (values are per key)
   std::vector<uint32_t> valClass;
   std::vector<uint8_t> valFalsy;
   std::unordered_map<std::string, uint32_t> classId;
@@ -106,6 +161,20 @@ struct Interner {
   std::vector<uint32_t> pidx{0, 0};  // props id 0 = none
   std::unordered_map<std::string, uint32_t> propsByJson;
   bool dirty = true;
+  // matchProperties (properties.ts:71-96) exactly.  A value id belongs to one key.  A key is regular when, at
+  // each path inside its values, one kind occurs (primitive, object-like, null) and no member is undefined:
+  // matchProperties between its values is then the equality of their canonical forms (valClass, symmetric and
+  // reflexive).  Any other key is irregular -- a primitive against an object ({k:5} vs {k:{}} matches, the
+  // reverse does not), a nested null, a consensus value's undefined member -- and matchProperties(a, b) of each
+  // ordered pair of its values is tabulated (irrRows; a = the run head's, zamboni.ts:155, snapshotV1.ts:240).
+  static constexpr uint32_t kIrrMax = 4096;  // values of one irregular key (the table is n^2 bits)
+  std::vector<std::unordered_map<std::string, uint8_t>> keyPaths;  // path -> kinds (1 prim, 2 object, 4 null, 8 undef)
+  std::vector<uint8_t> keyIrr;
+  std::vector<std::vector<uint32_t>> keyVals;              // the key's value ids, in interning order
+  std::vector<std::vector<std::vector<uint8_t>>> irrRows;  // irregular key: [i][j] = matchProperties(v_i, v_j)
+  std::vector<uint32_t> valLocal;                          // value -> index in its key's list
+  std::vector<hj::Value> valStore;
+  uint32_t nIrr = 0;
 
   uint32_t key(const U16& k) {
     auto it = keyId.find(k);
@@ -117,19 +186,21 @@ struct Interner {
     keyId[k] = id;
     uint32_t r;
     keyRank.push_back(hj::array_index(k, &r) ? r : MTB_NONE);
-    keyKinds.push_back(0);
+    keyPaths.emplace_back();
+    keyIrr.push_back(0);
+    keyVals.emplace_back();
+    irrRows.emplace_back();
     dirty = true;
     return id;
   }
-  // matchProperties equivalence class (properties.ts:71): arrays compare like objects with index keys
+  // canonical form: arrays compare like objects with index keys
   static void canon(std::string& o, const hj::Value& v) {
     switch (v.kind) {
       case hj::Value::kBool: o += v.b ? "b1" : "b0"; return;
       case hj::Value::kNum: o += "n" + hj::number(v.n); return;
       case hj::Value::kStr: o += "s"; hj::quote(o, v.s); return;
-      case hj::Value::kNull:
-      case hj::Value::kUndef:
-        raise(MTB_E_UNSUPPORTED, "unsupported: null nested inside a property value (matchProperties is not an equivalence there)");
+      case hj::Value::kNull: o += "z"; return;
+      case hj::Value::kUndef: o += "u"; return;
       case hj::Value::kArr:
       case hj::Value::kObj: {
         std::vector<std::pair<U16, const hj::Value*>> m;
@@ -146,10 +217,6 @@ struct Interner {
         for (auto& e : m) {
           hj::quote(o, e.first);
           o += ":";
-          if (e.second->kind != hj::Value::kObj && e.second->kind != hj::Value::kArr &&
-              e.second->kind != hj::Value::kBool && e.second->kind != hj::Value::kNum &&
-              e.second->kind != hj::Value::kStr)
-            raise(MTB_E_UNSUPPORTED, "unsupported: null nested inside a property value");
           canon(o, *e.second);
           o += ",";
         }
@@ -158,15 +225,35 @@ struct Interner {
       }
     }
   }
-  uint32_t value(uint32_t k, const hj::Value& v) {
+  void note_paths(uint32_t k, const hj::Value& v, std::string& path) {
     const bool objLike = v.kind == hj::Value::kObj || v.kind == hj::Value::kArr;
-    keyKinds[k] |= objLike ? 2 : 1;
-    if (keyKinds[k] == 3)
-      raise(MTB_E_UNSUPPORTED, "unsupported: property key holds both primitive and object values");
-    std::string js = hj::dump(v);
-    auto it = valId.find(js);
-    if (it != valId.end()) return it->second;
-    std::string c;
+    const uint8_t kind = v.kind == hj::Value::kNull ? 4 : v.kind == hj::Value::kUndef ? 8 : objLike ? 2 : 1;
+    uint8_t& m = keyPaths[k][path];
+    m |= kind;
+    if ((m & (m - 1)) || (m & 8)) keyIrr[k] = 1;
+    if (!objLike) return;
+    const size_t n0 = path.size();
+    auto step = [&](const U16& key, const hj::Value& x) {
+      path += std::to_string(key.size());
+      path += ':';
+      for (char16_t c : key) { path += (char)(c & 0xFF); path += (char)(c >> 8); }
+      note_paths(k, x, path);
+      path.resize(n0);
+    };
+    if (v.kind == hj::Value::kArr) {
+      for (size_t i = 0; i < v.items.size(); i++) {
+        std::string t = std::to_string(i);
+        step(U16(t.begin(), t.end()), v.items[i]);
+      }
+    } else {
+      for (auto& e : v.members) step(e.first, e.second);
+    }
+  }
+  // `js`: the JSON the summaries write for the value (JSON.stringify drops undefined members)
+  uint32_t add_value(uint32_t k, const std::string& idKey, const std::string& js, const hj::Value& v) {
+    std::string path;
+    note_paths(k, v, path);
+    std::string c = std::to_string(k) + ":";
     canon(c, v);
     auto ci = classId.find(c);
     uint32_t cls;
@@ -178,12 +265,113 @@ struct Interner {
     }
     uint32_t id = (uint32_t)valJson.size();
     valJson.push_back(js);
-    valId[js] = id;
+    valId[idKey] = id;
     valClass.push_back(cls);
-    // bit 0: JS falsy; bit 1: incr makes it NaN (number / boolean + undefined, properties.ts:38-45)
-    valFalsy.push_back((v.truthy() ? 0 : 1) | (v.kind == hj::Value::kNum || v.kind == hj::Value::kBool ? 2 : 0));
+    // bit 0: JS falsy; bit 1: incr makes it NaN (number / boolean + undefined, properties.ts:38-45); bit 2: an
+    // object whose seq is -1 (consensus completes it in place, properties.ts:56-60)
+    const hj::Value* sq = v.kind == hj::Value::kObj ? v.find(u"seq") : nullptr;
+    valFalsy.push_back((v.truthy() ? 0 : 1) | (v.kind == hj::Value::kNum || v.kind == hj::Value::kBool ? 2 : 0) |
+                       (sq && sq->kind == hj::Value::kNum && sq->n == -1 ? 4 : 0));
+    valLocal.push_back((uint32_t)keyVals[k].size());
+    keyVals[k].push_back(id);
+    valStore.push_back(v);
+    if (keyIrr[k] && keyVals[k].size() > kIrrMax)
+      raise(MTB_E_UNSUPPORTED, "unsupported: more than 4096 distinct values under one property key whose values "
+                               "matchProperties does not compare as an equivalence");
     dirty = true;
     return id;
+  }
+  uint32_t value(uint32_t k, const hj::Value& v) {
+    std::string js = hj::dump(v);
+    std::string idKey = std::to_string(k) + ":" + js;
+    auto it = valId.find(idKey);
+    if (it != valId.end()) return it->second;
+    return add_value(k, idKey, js, v);
+  }
+  // combine(consensus, undefined, undefined, seq) (properties.ts:46-55): a fresh {value: undefined, seq} --
+  // {"seq":seq} in JSON, and never matched as the second argument of matchProperties (its undefined member)
+  uint32_t consensus_value(uint32_t k, int seq) {
+    std::string idKey = "\x02" + std::to_string(k) + ":" + std::to_string(seq);
+    auto it = valId.find(idKey);
+    if (it != valId.end()) return it->second;
+    hj::Value v;
+    v.kind = hj::Value::kObj;
+    v.members.push_back({u"value", hj::Value()});
+    hj::Value sv;
+    sv.kind = hj::Value::kNum;
+    sv.n = seq;
+    v.members.push_back({u"seq", sv});
+    return add_value(k, idKey, "{\"seq\":" + std::to_string(seq) + "}", v);
+  }
+  // matchProperties(value a, value b) of two values of key k (properties.ts:84-92)
+  bool value_match(uint32_t k, uint32_t a, uint32_t b) {
+    if (!keyIrr[k]) return valClass[a] == valClass[b];
+    irr_rows(k);
+    return irrRows[k][valLocal[a]][valLocal[b]] != 0;
+  }
+  void irr_rows(uint32_t k) {
+    auto& M = irrRows[k];
+    const auto& vs = keyVals[k];
+    const size_t n0 = M.size(), n = vs.size();
+    if (n0 == n) return;
+    for (auto& row : M) row.resize(n);
+    M.resize(n);
+    for (size_t i = 0; i < n; i++) {
+      M[i].resize(n);
+      for (size_t j = i < n0 ? n0 : 0; j < n; j++) M[i][j] = js_match_value(&valStore[vs[i]], &valStore[vs[j]]) ? 1 : 0;
+    }
+  }
+  // device tables: keyOff[k] = 1 + offset of [n, bits of n x n (row a, column b)] in bits, 0 for a regular key
+  void irr_tables(std::vector<uint32_t>& keyOff, std::vector<uint32_t>& localOf, std::vector<uint32_t>& bits) {
+    keyOff.assign(keys.size(), 0);
+    localOf.assign(valJson.size(), MTB_NONE);
+    bits.assign(1, 0);
+    nIrr = 0;
+    for (uint32_t k = 0; k < keys.size(); k++) {
+      if (!keyIrr[k]) continue;
+      nIrr++;
+      irr_rows(k);
+      const auto& vs = keyVals[k];
+      const size_t n = vs.size();
+      keyOff[k] = (uint32_t)bits.size() + 1;
+      bits.push_back((uint32_t)n);
+      const size_t o = bits.size();
+      bits.resize(o + (n * n + 31) / 32, 0);
+      for (size_t i = 0; i < n; i++) {
+        localOf[vs[i]] = (uint32_t)i;
+        for (size_t j = 0; j < n; j++)
+          if (irrRows[k][i][j]) bits[o + (i * n + j) / 32] |= 1u << ((i * n + j) % 32);
+      }
+    }
+  }
+  // an annotate's consensus op-props (properties.ts:46-62, a sequenced op at `seq`; the op's values are never
+  // read): each key of props id `pid` holds what a segment lacking the key gets -- {value: undefined, seq} with
+  // no defaultValue, else the defaultValue (its seq completed when -1: the op's own object, shared by the op's
+  // segments alone), or MTB_NONE for a null defaultValue (the reference throws reading its seq).  A segment that
+  // has the key keeps its value (the device; one whose value is an object with seq -1 fails, DERR_CONSENSUS).
+  uint32_t consensus_props(uint32_t pid, const hj::Value* dv, int seq) {
+    const std::string memo = "\x03" + std::to_string(pid) + ":" + std::to_string(seq) + ":" + (dv ? hj::dump(*dv) : "-");
+    auto it = propsByJson.find(memo);
+    if (it != propsByJson.end()) return it->second;
+    const uint32_t off = pidx[2 * pid], n = pool[off];
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t k = pool[off + 1 + 2 * i];
+      uint32_t v;
+      if (!dv || dv->kind == hj::Value::kUndef) {
+        v = consensus_value(k, seq);
+      } else if (dv->kind == hj::Value::kNull) {
+        v = MTB_NONE;
+      } else {
+        hj::Value d = *dv;
+        if (d.kind == hj::Value::kObj)
+          for (auto& m : d.members)
+            if (m.first == u"seq" && m.second.kind == hj::Value::kNum && m.second.n == -1) m.second.n = seq;
+        v = value(k, d);
+      }
+      kv.push_back({k, v});
+    }
+    return props_kv(memo, kv);
   }
   // NaN, the value an incr annotate gives a numeric key: JSON null (JSON.stringify), its own matchProperties
   // class; a set holding it is flagged MTB_PNAN by the device and matches nothing (NaN !== NaN)
@@ -196,6 +384,8 @@ struct Interner {
     classId["\x01NaN"] = cls;
     valClass.push_back(cls);
     valFalsy.push_back(1 | 2);
+    valLocal.push_back(MTB_NONE);
+    valStore.push_back(hj::Value());
     dirty = true;
     return nanVal;
   }
@@ -214,6 +404,12 @@ struct Interner {
       const uint32_t v = m.second.kind == hj::Value::kNull ? MTB_NONE : value(k, m.second);
       kv.push_back({k, v});
     }
+    return props_kv(js, kv);
+  }
+  // a props id from (key, value id) pairs (MTB_NONE: null); `memo` names it for reuse
+  uint32_t props_kv(const std::string& memo, const std::vector<std::pair<uint32_t, uint32_t>>& kv) {
+    auto it = propsByJson.find(memo);
+    if (it != propsByJson.end()) return it->second;
     const uint32_t opOff = (uint32_t)pool.size();
     pool.push_back((uint32_t)kv.size());
     for (auto& e : kv) { pool.push_back(e.first); pool.push_back(e.second); }
@@ -226,7 +422,7 @@ struct Interner {
     const uint32_t id = (uint32_t)(pidx.size() / 2);
     pidx.push_back(opOff);
     pidx.push_back(setOff);
-    propsByJson[js] = id;
+    propsByJson[memo] = id;
     dirty = true;
     return id;
   }
@@ -462,7 +658,7 @@ struct mtb_dev {
   DevBuf<uint16_t> dText;
   DevBuf<Lru> dHeap;
   DevBuf<uint32_t> dAux, dFree;
-  DevBuf<uint32_t> dPool, dPidx, dValClass, dKeyRank;
+  DevBuf<uint32_t> dPool, dPidx, dValClass, dKeyRank, dKeyIrr, dValLocal, dIrr;
   DevBuf<uint8_t> dValFalsy;
   // host staging of the SnapshotV1 extraction (extract_docs), kept and reused by later summaries: a call does
   // not pay for freeing (or re-faulting) the previous call's hundreds of MB
@@ -504,6 +700,7 @@ struct mtb_dev {
   ~mtb_dev() {
     dDocs.release(); dOps.release(); dSegs.release(); dBlks.release(); dLists.release(); dText.release();
     dHeap.release(); dAux.release(); dFree.release(); dPool.release(); dPidx.release(); dValClass.release();
+    dKeyIrr.release(); dValLocal.release(); dIrr.release();
     dKeyRank.release(); dValFalsy.release(); dPristine.release(); dPSeg.release(); dPBlk.release(); dPX.release(); dDelta.release(); dSched.release(); dKHash.release(); dVHash.release(); dDigest.release();
     dMvSrc.release(); dMvDst.release(); dMvLen.release(); dStageW.release(); dStageH.release();
     if (ev0) (void)hipEventDestroy(ev0);
@@ -715,8 +912,14 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
             raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with a non-numeric defaultValue (string concatenation)");
           r.flags |= MTB_F_INCR;
           b->in.nan();
+        } else if (name && name->kind == hj::Value::kStr && name->s == u"consensus") {
+          // a local consensus value is {value: undefined, seq: -1}, completed in place at the ack (client.ts:1050-1058)
+          if ((r.flags & MTB_F_LOCAL) || r.client == (uint16_t)MTB_LOCAL_CLIENT)
+            raise(MTB_E_UNSUPPORTED, "unsupported: local consensus annotate (its value object is completed in place at the ack)");
+          r.flags |= MTB_F_CONSENSUS;
+          r.props = b->in.consensus_props(r.props, member(*comb, u"defaultValue"), (int)r.seq);
         } else {
-          raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite / incr (consensus mutates shared value objects)");
+          raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite / incr / consensus");
         }
       }
     }
@@ -1436,6 +1639,13 @@ void upload_tables(mtb_dev* b) {
   up(b->dValClass, in.valClass);
   up(b->dValFalsy, in.valFalsy);
   up(b->dKeyRank, in.keyRank);
+  {  // matchProperties of irregular keys' value pairs (Interner::irr_tables)
+    std::vector<uint32_t> keyOff, localOf, bits;
+    in.irr_tables(keyOff, localOf, bits);
+    up(b->dKeyIrr, keyOff);
+    up(b->dValLocal, localOf);
+    up(b->dIrr, bits);
+  }
   // state digest hashes of every interned key and value (DESIGN.md "State digest")
   std::vector<uint64_t> kh(in.keys.size()), vh(in.valJson.size());
   for (size_t k = 0; k < kh.size(); k++) kh[k] = fnv_bytes(hj::to_utf8(in.keys[k].data(), in.keys[k].size()));
@@ -1443,6 +1653,24 @@ void upload_tables(mtb_dev* b) {
   up(b->dKHash, kh);
   up(b->dVHash, vh);
   in.dirty = false;
+}
+
+Tables make_tables(mtb_dev* b) {
+  Tables t;
+  t.pool = b->dPool.p;
+  t.pidx = b->dPidx.p;
+  t.val_class = b->dValClass.p;
+  t.val_falsy = b->dValFalsy.p;
+  t.nan_val = b->in.nanVal;
+  t.key_rank = b->dKeyRank.p;
+  t.key_irr = b->dKeyIrr.p;
+  t.val_local = b->dValLocal.p;
+  t.irr = b->dIrr.p;
+  t.irr_any = b->in.nIrr;
+  t.delta = b->dDelta.p;
+  t.class_trivial = b->in.classId.size() == b->in.valJson.size() && !b->in.nIrr ? 1u : 0u;
+  t.mk_key = marker_key_id(b->in);
+  return t;
 }
 
 // State digest v1 of every document (mtb_digest_kernel) after a replay: fills the stats' segments_final,
@@ -1583,6 +1811,11 @@ std::string derr_text(int e) {
     case DERR_ASSERT_MKID: return "0x5ad Cannot change the markerId of an existing marker";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     case DERR_INCR: return "unsupported: incr combiningOp over a string or object property value (string concatenation)";
+    case DERR_CONSENSUS: return "unsupported: consensus annotate over an object value whose seq is -1 (the reference completes "
+                                "it in place, shared with split clones), or with a null defaultValue over a segment lacking the key "
+                                "(the reference throws reading its seq)";
+    case DERR_STALE: return "unsupported: summary body segment older than entries already in its blocks' partial lengths "
+                            "(the reference's addSeq leaves their cumulative lengths stale, partialLengths.ts:543-577)";
     default: return "device error " + std::to_string(e);
   }
 }
@@ -1944,16 +2177,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   pc.mark("upload");
   if (!b->haveRewind) capture_pristine(b);
   pc.mark("pristine");
-  Tables t;
-  t.pool = b->dPool.p;
-  t.pidx = b->dPidx.p;
-  t.val_class = b->dValClass.p;
-  t.val_falsy = b->dValFalsy.p;
-  t.nan_val = b->in.nanVal;
-  t.key_rank = b->dKeyRank.p;
-  t.delta = b->dDelta.p;
-  t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
-  t.mk_key = marker_key_id(b->in);
+  const Tables t = make_tables(b);
   b->residentLoad = anyLoad;
   HIPCHK(hipEventRecord(b->ev0, b->stream));
   if (anyLoad)  // summary bodies first (LOADSEG records head their documents' records)
@@ -2146,6 +2370,7 @@ void props_json(mtb_dev* b, std::string& o, PropView v) {
   }
   o += '}';
 }
+// matchProperties(a, c) (properties.ts:71-96): a is the run head's set
 bool props_match(mtb_dev* b, PropView a, PropView c) {
   if (a.n() != c.n()) return false;
   if (b->in.nanVal != MTB_NONE)  // NaN !== NaN: a set holding NaN matches nothing
@@ -2156,7 +2381,7 @@ bool props_match(mtb_dev* b, PropView a, PropView c) {
     for (uint32_t q = 0; q < c.n(); q++) {
       if (c.p[1 + 2 * q] == a.p[1 + 2 * i]) {
         found = true;
-        if (b->in.valClass[c.p[2 + 2 * q]] != b->in.valClass[a.p[2 + 2 * i]]) return false;
+        if (!b->in.value_match(a.p[1 + 2 * i], a.p[2 + 2 * i], c.p[2 + 2 * q])) return false;
       }
     }
     if (!found) return false;
@@ -2721,7 +2946,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, u
   dc.ensure(3 * (size_t)nf);
   HIPCHK(hipMemcpyAsync(dl.p, di.data(), nf * sizeof(uint32_t), hipMemcpyHostToDevice, b->stream));
   HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
-                               b->dValClass.p, dc.p, nullptr, nullptr, nullptr, nullptr));
+                               make_tables(b), dc.p, nullptr, nullptr, nullptr, nullptr));
   HIPCHK(hipMemcpyAsync(cnt.data(), dc.p, 3 * (size_t)nf * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
   std::vector<uint64_t> off(3 * (size_t)nf);
@@ -2746,7 +2971,7 @@ void extract_docs(mtb_dev* b, const std::vector<uint32_t>& ids, Extracted& ex, u
   doff.ensure(3 * (size_t)nf);
   HIPCHK(hipMemcpyAsync(doff.p, off.data(), 3 * (size_t)nf * sizeof(uint64_t), hipMemcpyHostToDevice, b->stream));
   HIPCHK(mtb_launch_extract_v1(b->stream, b->dDocs.p, dl.p, nf, b->dBlks.p, b->dText.p, b->dAux.p, b->dPool.p,
-                               b->dValClass.p, dc.p, doff.p, b->dExItems.p, b->dExText.p, b->dExWords.p));
+                               make_tables(b), dc.p, doff.p, b->dExItems.p, b->dExText.p, b->dExWords.p));
   ex.hItems = staging(b->exItems, b->exItemsCap, ti + 8);
   ex.hText = staging(b->exText, b->exTextCap, tt + 1);
   ex.hWords = staging(b->exWords, b->exWordsCap, tw + 1);
@@ -2863,54 +3088,6 @@ void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
   }
 }
 
-// matchProperties (properties.ts:71-96) restated on parsed JSON values (JS semantics for the keys of
-// primitives: strings expose their indices, other primitives none)
-std::vector<U16> js_keys_of(const hj::Value* v) {
-  std::vector<U16> k;
-  if (!v) return k;
-  if (v->kind == hj::Value::kObj) for (auto& m : v->members) k.push_back(m.first);
-  else if (v->kind == hj::Value::kArr) for (size_t i = 0; i < v->items.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
-  else if (v->kind == hj::Value::kStr) for (size_t i = 0; i < v->s.size(); i++) { std::string t = std::to_string(i); k.push_back(U16(t.begin(), t.end())); }
-  return k;
-}
-bool js_get_of(const hj::Value* v, const U16& key, hj::Value& tmp, const hj::Value*& out) {
-  out = nullptr;
-  if (!v) return false;
-  if (v->kind == hj::Value::kObj) { out = v->find(key.c_str()); return out != nullptr; }
-  uint32_t idx;
-  if (!hj::array_index(key, &idx)) return false;
-  if (v->kind == hj::Value::kArr && idx < v->items.size()) { out = &v->items[idx]; return true; }
-  if (v->kind == hj::Value::kStr && idx < v->s.size()) { tmp.kind = hj::Value::kStr; tmp.s = U16(1, v->s[idx]); out = &tmp; return true; }
-  return false;
-}
-bool js_strict_eq(const hj::Value* a, const hj::Value* b) {
-  if (!a || !b) return a == b;
-  if (a->kind != b->kind) return false;
-  switch (a->kind) {
-    case hj::Value::kNull: case hj::Value::kUndef: return true;
-    case hj::Value::kBool: return a->b == b->b;
-    case hj::Value::kNum: return a->n == b->n;
-    case hj::Value::kStr: return a->s == b->s;
-    default: return a == b;  // object identity
-  }
-}
-bool js_match_props(const hj::Value* a, const hj::Value* b) {
-  if ((!a || !a->truthy()) && (!b || !b->truthy())) return true;
-  const auto ka = js_keys_of(a), kb = js_keys_of(b);
-  if (ka.size() != kb.size()) return false;
-  for (auto& k : ka) {
-    hj::Value ta, tb;
-    const hj::Value *av = nullptr, *bv = nullptr;
-    if (!js_get_of(b, k, tb, bv) || !bv || bv->kind == hj::Value::kUndef) return false;
-    js_get_of(a, k, ta, av);
-    if (bv->kind == hj::Value::kObj || bv->kind == hj::Value::kArr || bv->kind == hj::Value::kNull) {
-      if (!js_match_props(av, bv)) return false;
-    } else if (!js_strict_eq(bv, av)) {
-      return false;
-    }
-  }
-  return true;
-}
 
 // Replay one matrix's cell events of this replay into its CellStore.  Both vectors' record streams hold
 // every setCell; a clear logged at record k of either stream happened after the setCells before k and
@@ -3047,20 +3224,26 @@ void resolve_catch_up(mtb_dev* b, uint32_t i) {
             if (std::find(keys.begin(), keys.end(), opl[1 + 2 * q]) == keys.end()) keys.push_back(opl[1 + 2 * q]);
           std::string pj = "{";
           bool nan = false;  // an incr's NaN (JSON null): matchProperties never equal (NaN !== NaN)
+          hj::Value pv;      // the values themselves (a consensus value's undefined member included)
+          pv.kind = hj::Value::kObj;
           for (size_t q = 0; q < keys.size(); q++) {
             if (q) pj += ',';
             hj::quote(pj, b->in.keys[keys[q]]);
             pj += ':';
             std::string val = "null";
+            hj::Value x;
+            x.kind = hj::Value::kNull;
             for (uint32_t z = 0; z < sv.n(); z++)
               if (sv.p[1 + 2 * z] == keys[q]) {
-                val = b->in.valJson[sv.p[2 + 2 * z]];
-                nan |= sv.p[2 + 2 * z] == b->in.nanVal;
+                const uint32_t v = sv.p[2 + 2 * z];
+                val = b->in.valJson[v];
+                nan |= v == b->in.nanVal;
+                if (v != b->in.nanVal) x = b->in.valStore[v];
               }
             pj += val;
+            pv.members.push_back({b->in.keys[keys[q]], std::move(x)});
           }
           pj += "}";
-          hj::Value pv = hj::parse(pj.data(), pj.size());
           if (!ev.empty() && ev.back().hasPos2 && ev.back().pos2 == position && !nan && !ev.back().nan &&
               js_match_props(&ev.back().pv, &pv)) {
             ev.back().pos2 += len;
@@ -3700,6 +3883,8 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
       }
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_ANNOTATE) && o.props >= b->in.pidx.size() / 2)
         raise(MTB_E_ARG, "record props id out of range");
+      if (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_CONSENSUS)  // (no defaultValue in records)
+        o.props = b->in.consensus_props(o.props, nullptr, (int)o.seq);
       if (o.type == MTB_OP_INSERT && (o.flags & MTB_F_MARKER)) o.payload = 0;  // set below (marker id ordinal)
       if (o.client >= d.longIds.size() && o.type != MTB_OP_NOOP)
         raise(MTB_E_ARG, "record client id not registered (mtb_add_client)");
@@ -3759,16 +3944,7 @@ int mtbx_get_launch_info(mtb_dev* b, mtb_launch_info* out) {
 int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
   return guarded(b, [&] {
     if (!b->haveRewind) raise(MTB_E_ARG, "no resident records");
-    Tables t;
-    t.pool = b->dPool.p;
-    t.pidx = b->dPidx.p;
-    t.val_class = b->dValClass.p;
-    t.val_falsy = b->dValFalsy.p;
-  t.nan_val = b->in.nanVal;
-    t.key_rank = b->dKeyRank.p;
-    t.delta = b->dDelta.p;
-    t.class_trivial = b->in.classId.size() == b->in.valJson.size() ? 1u : 0u;
-    t.mk_key = marker_key_id(b->in);
+    const Tables t = make_tables(b);
     HIPCHK(hipEventRecord(b->ev0, b->stream));
     if (b->residentLoad)
       HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
@@ -4271,6 +4447,26 @@ int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int 
 // and getPropertiesAtPosition (client.ts:1101) are views of it.  Output: a JSON array of
 // {"pos", "start", "end", "segment"} per visited leaf (start / end relative to the segment, as the
 // reference's handler receives them), at most `limit` entries (0 = all).
+namespace {
+// The phantom surplus of each block of a loaded document (mtb_replay.hip "phantom partial lengths") in the
+// (R, C) view; empty for the local view and for documents without a table.
+std::unordered_map<uint32_t, int64_t> phantom_surplus(const HostDoc& d, const DocState& s, int R, int C) {
+  std::unordered_map<uint32_t, int64_t> sur;
+  if (!s.ph || !(s.flags & DSF_PHANTOM) || C == 0 || (size_t)s.ph + 2 > d.aux.size()) return sur;
+  const uint32_t n = d.aux[s.ph];
+  if ((size_t)s.ph + 2 + 8ull * n > d.aux.size()) raise(MTB_E_INTERNAL, "corrupt phantom table");
+  const int Rl = std::max(R, (int)s.min_seq);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t* e = d.aux.data() + s.ph + 2 + 8ull * i;
+    bool vis = (int)e[1] <= Rl || (int)(int16_t)e[3] == C;
+    if (!vis && e[4] && e[4] < d.aux.size())
+      for (uint32_t r = 0; r < d.aux[e[4]] && e[4] + 1 + r < d.aux.size() && !vis; r++) vis = (int)d.aux[e[4] + 1 + r] == C;
+    if (vis) sur[e[0]] += e[2];
+  }
+  return sur;
+}
+}  // namespace
+
 int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq, const char* long_client_id,
                   uint32_t limit, char** out, size_t* out_len) {
   return guarded(b, [&] {
@@ -4296,19 +4492,109 @@ int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t
       lens[k] = leaf_length(d, d.segs[fl[k].id], R, C, newMode, (int)s.min_seq, rc);
       if (lens[k] > 0) total += lens[k];
     }
-    const int64_t endPos = end < 0 ? total : end;
-    std::string o = "[";
-    uint32_t n = 0;
-    int64_t pos = 0;
-    if (endPos != start)
-      for (size_t k = 0; k < fl.size() && pos < endPos; k++) {
-        const int len = lens[k];
-        if (len <= 0) continue;  // undefined or zero: Skip
-        const int64_t next = pos + len;
-        if (start >= next) {
-          pos = next;
+    // nodeMap (mergeTree.ts:2531-2582) visits leaves in order; a block is skipped whole when `start` lies past
+    // its length.  Block lengths are the sums of their leaves' except for a loaded document's phantom surplus,
+    // which moves the position past a skipped block (and the default end, the root's length): those documents
+    // take the walk over the blocks (visit[k] = leaf k's position, -1 = skipped or past the end)
+    std::unordered_map<uint32_t, int64_t> sur = phantom_surplus(d, s, R, C);
+    std::vector<int64_t> at;
+    int64_t endPos = end < 0 ? total : end;
+    if (!sur.empty()) {
+      std::unordered_map<uint32_t, int64_t> blen;  // leaf sums + surplus, post-order
+      {
+        struct Fr { uint32_t b; int i; int64_t acc; };
+        std::vector<Fr> st{{s.root, 0, 0}};
+        size_t k = 0;
+        while (!st.empty()) {
+          Fr& f = st.back();
+          const Blk& B = d.blks.at(f.b);
+          if (f.i >= B.count) {
+            const uint32_t fb = f.b;
+            const int64_t acc = f.acc;
+            auto it = sur.find(fb);
+            blen[fb] = acc + (it == sur.end() ? 0 : it->second);
+            st.pop_back();
+            if (!st.empty()) st.back().acc += acc;  // (the parent's exact part: its leaves only)
+            continue;
+          }
+          const uint32_t c = B.child[f.i++];
+          if (c & MTB_LEAF) {
+            f.acc += lens[k] > 0 ? lens[k] : 0;
+            k++;
+          } else {
+            st.push_back({c, 0, 0});
+          }
+        }
+      }
+      if (end < 0) endPos = blen[s.root];
+      at.assign(fl.size(), -1);
+      int64_t pos = 0;
+      bool exit = false;
+      struct Fr { uint32_t b; int i; };
+      std::vector<Fr> st{{s.root, 0}};
+      size_t k = 0;
+      // (leaf indices follow flatten's order: a skipped block's leaves are counted past)
+      auto count_leaves = [&](uint32_t b0) {
+        std::vector<uint32_t> q{b0};
+        size_t c = 0;
+        while (!q.empty()) {
+          const Blk& B = d.blks.at(q.back());
+          q.pop_back();
+          for (int i = B.count - 1; i >= 0; i--) {
+            if (B.child[i] & MTB_LEAF) c++;
+            else q.push_back(B.child[i]);
+          }
+        }
+        return c;
+      };
+      while (!st.empty() && !exit) {
+        Fr& f = st.back();
+        const Blk& B = d.blks.at(f.b);
+        if (f.i >= B.count) {
+          st.pop_back();
           continue;
         }
+        const uint32_t c = B.child[f.i++];
+        if (endPos <= pos) { exit = true; break; }
+        if (c & MTB_LEAF) {
+          const int len = lens[k];
+          if (len > 0) {
+            if (start >= pos + len) {
+              pos += len;
+            } else {
+              at[k] = pos;
+              pos += len;
+            }
+          }
+          k++;
+        } else {
+          const int64_t len = blen[c];
+          if (len == 0) { k += count_leaves(c); continue; }
+          if (start >= pos + len) {
+            pos += len;
+            k += count_leaves(c);
+            continue;
+          }
+          st.push_back({c, 0});
+        }
+      }
+    }
+    std::string o = "[";
+    uint32_t n = 0;
+    int64_t base = 0;
+    if (endPos != start)
+      for (size_t k = 0; k < fl.size(); k++) {
+        const int len = lens[k];
+        int64_t pos = base;
+        if (!sur.empty()) {
+          if (at[k] < 0) continue;
+          pos = at[k];
+        }
+        if (pos >= endPos) break;
+        if (len <= 0) continue;  // undefined or zero: Skip
+        const int64_t next = pos + len;
+        base += len;
+        if (start >= next) continue;
         const Seg& g = d.segs[fl[k].id];
         if (n) o += ',';
         o += "{\"pos\":" + std::to_string(pos) + ",\"start\":" + std::to_string(start - pos) + ",\"end\":" +
@@ -4336,7 +4622,6 @@ int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t
           props_json(b, o, pv);
         }
         o += "}}";
-        pos = next;
         if (++n == limit) break;
       }
     o += "]";

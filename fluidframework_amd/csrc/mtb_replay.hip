@@ -47,6 +47,15 @@
 #define MTB_TU_MISC 5     // digest, rewind, moves, launch dispatch
 
 namespace mtbk {
+// matchProperties(va, vb) (properties.ts:84-92) of two values of key k, with irregular keys in the batch
+// (Tables::key_irr; a regular key's values compare by class)
+__device__ __forceinline__ bool irr_value_match(const Tables& t, uint32_t k, uint32_t va, uint32_t vb) {
+  const uint32_t o = t.key_irr[k];
+  if (!o) return va == vb || t.val_class[va] == t.val_class[vb];
+  const uint32_t n = t.irr[o - 1];
+  const uint32_t bit = t.val_local[va] * n + t.val_local[vb];
+  return ((t.irr[o + bit / 32] >> (bit % 32)) & 1u) != 0;
+}
 
 // MTB_PROFILE builds accumulate s_memtime cycles per replay phase and event counts into DocState
 // (diagnostic only; `MTB_PROFILE_OUT=1` prints them per op).
@@ -310,6 +319,7 @@ struct Eng {
   bool phDoc;                   // DSF_PHANTOM (hasPh modes)
   int ph_split_top;             // the topmost depth the last fix_overflow split (MTB_VDEPTH: none)
   bool ph_ow;                   // markRangeRemoved's _overwrite, set during the current op's nodeMap
+  uint32_t ld_stale;            // MODE_LOAD: bit d = the walk's depth-d block holds entries newer than the segment
   uint64_t prof[NPH];
   uint32_t evc[NCN];
 
@@ -1183,10 +1193,10 @@ struct Eng {
         nb = split_block(level);
         if (err) break;
         if constexpr (hasPh) {
+          ph_split_top = level;  // (split halves are recombined: no stale update there, see apply_loadseg)
           if (COLD(phDoc)) {  // split (mergeTree.ts:1858-1871): both halves nodeUpdateLengthNewStructure
             ph_combine(b);
             ph_combine(nb);
-            ph_split_top = level;
             if (err) break;
           }
         }
@@ -1313,7 +1323,8 @@ struct Eng {
   // rseq <= max(refSeq, minSeq), or the viewer is one of P's removers.  Entries follow the reference's
   // recombinations (PartialSequenceLengths.combine, :256-338): a recombined block of segments has none, a
   // recombined block of blocks the union of its children's; update() leaves them.
-  __device__ __forceinline__ void ph_add(uint32_t node, uint32_t rseq, uint32_t len, uint32_t rc0, uint32_t rcx) {
+  __device__ __forceinline__ void ph_add(uint32_t node, uint32_t rseq, uint32_t len, uint32_t rc0, uint32_t rcx,
+                                         uint32_t seq = 0) {
     const uint32_t n = U(aux[ph_off]), cap = U(aux[ph_off + 1]);
     if (n >= cap) {
       const uint32_t ncap = 2 * cap + 8;
@@ -1328,7 +1339,8 @@ struct Eng {
       ph_off = h;
     }
     if (lane < 8) {
-      const uint32_t v = lane == 0 ? node : lane == 1 ? rseq : lane == 2 ? len : lane == 3 ? rc0 : lane == 4 ? rcx : 0u;
+      const uint32_t v = lane == 0 ? node : lane == 1 ? rseq : lane == 2 ? len : lane == 3 ? rc0 : lane == 4 ? rcx
+                         : lane == 5 ? seq : 0u;
       aux[ph_off + 2 + 8 * n + lane] = v;
     }
     if (lane == 0) aux[ph_off] = n + 1;
@@ -1340,16 +1352,16 @@ struct Eng {
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       const bool v = i < n;
-      uint32_t e[5];
+      uint32_t e[6];
 #pragma unroll
-      for (int q = 0; q < 5; q++) e[q] = v ? aux[ph_off + 2 + 8 * i + q] : 0u;
+      for (int q = 0; q < 6; q++) e[q] = v ? aux[ph_off + 2 + 8 * i + q] : 0u;
       const bool keep = v && e[0] != node;
       const unsigned long long m = __ballot(keep);
       wsync();  // (the chunk is read before its entries move down: w <= base)
       if (keep) {
         const uint32_t o = w + rank_below(m);
 #pragma unroll
-        for (int q = 0; q < 5; q++) aux[ph_off + 2 + 8 * o + q] = e[q];
+        for (int q = 0; q < 6; q++) aux[ph_off + 2 + 8 * o + q] = e[q];
       }
       w += (uint32_t)__popcll(m);
       wsync();
@@ -1376,7 +1388,7 @@ struct Eng {
         const uint32_t t = base + (uint32_t)first_set(m);
         m &= m - 1;
         const uint32_t o = ph_off + 2 + 8 * t;
-        ph_add(X, U(aux[o + 1]), U(aux[o + 2]), U(aux[o + 3]), U(aux[o + 4]));
+        ph_add(X, U(aux[o + 1]), U(aux[o + 2]), U(aux[o + 3]), U(aux[o + 4]), U(aux[o + 5]));
       }
     }
   }
@@ -1418,6 +1430,70 @@ struct Eng {
     }
     wsync();
     return lane < MTB_MAXCH ? sh->corr[lane] : 0;
+  }
+
+  // Would PartialSequenceLengths.update(N, S) (partialLengths.ts:636-686) meet an entry newer than S in N's
+  // partials?  addSeq (:543-577) then inserts S below it without raising the later entries' cumulative `len`:
+  // their lengths stay short by S's seglen from then on.  Only a summary body's inserts can be older than what
+  // a block already holds.  N = the block at depth d of the walk (d >= 1); its entries are the list entries of
+  // its parent (depth d - 1) tagged with N's slot, plus the phantom inserts of N's table.  Checked as the walk
+  // places the segment, before its own entries are appended.
+  // A phantom's removal entries (seq = its rseq) are in the exact list but not in the reference's partials: a
+  // removal entry newer than S counts only when the removals of that op under N outweigh N's phantoms of it.
+  __device__ __forceinline__ bool stale_at(int d, int S) {
+    uint32_t loff, lcnt, lcap;
+    meta_of(d - 1, loff, lcnt, lcap);
+    const uint32_t slot = U(sh->slot[d - 1]), N = U(sh->path[d]);
+    bool st = false, rem = false;
+    for (uint32_t base = 0; base < lcnt; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      if (i < lcnt) {
+        const WEnt e = lst[loff + i];
+        if (e.seq > S && e.seq > minSeq && ((uint32_t)e.ck >> 20) == slot) {
+          if (((uint32_t)e.ck >> 16 & 0xF) == WK_OVERLAP || e.delta < 0) rem = true;  // (a removal's entries)
+          else st = true;
+        }
+      }
+    }
+    if constexpr (hasPh) {
+      if (phDoc) {
+        const uint32_t n = U(aux[ph_off]);
+        for (uint32_t base = 0; base < n; base += 64) {
+          const uint32_t i = base + (uint32_t)lane;
+          if (i < n) st |= aux[ph_off + 2 + 8 * i] == N && (int)aux[ph_off + 2 + 8 * i + 5] > S;
+        }
+        if (__ballot(st) == 0 && __ballot(rem) != 0) st = COLD(ph_rem_stale(loff, lcnt, slot, N, S));
+        return __ballot(st) != 0;
+      }
+    }
+    return __ballot(st || rem) != 0;
+  }
+  // some op newer than S removed under N more than N's phantoms of that op (lane-uniform result)
+  __device__ __noinline__ bool ph_rem_stale(uint32_t loff, uint32_t lcnt, uint32_t slot, uint32_t N, int S) {
+    const uint32_t n = U(aux[ph_off]);
+    for (uint32_t j = 0; j < lcnt; j++) {
+      const WEnt c = lst[loff + j];
+      if (!(c.seq > S && c.seq > minSeq && ((uint32_t)c.ck >> 20) == slot && ((uint32_t)c.ck >> 16 & 0xF) == WK_MAIN &&
+            c.delta < 0))
+        continue;
+      int acc = 0;  // removed under N at c.seq minus N's phantom lengths removed at c.seq
+      for (uint32_t base = 0; base < lcnt; base += 64) {
+        const uint32_t i = base + (uint32_t)lane;
+        if (i < lcnt) {
+          const WEnt e = lst[loff + i];
+          if (e.seq == c.seq && ((uint32_t)e.ck >> 20) == slot && ((uint32_t)e.ck >> 16 & 0xF) == WK_MAIN && e.delta < 0)
+            acc -= e.delta;
+        }
+      }
+      for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t i = base + (uint32_t)lane;
+        if (i < n && aux[ph_off + 2 + 8 * i] == N && (int)aux[ph_off + 2 + 8 * i + 1] == c.seq)
+          acc -= (int)aux[ph_off + 2 + 8 * i + 2];
+      }
+      for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+      if (acc > 0) return true;
+    }
+    return false;
   }
 
   // blockInsert's continuePredicate (mergeTree.ts:1611-1615, forwardExcursion mergeTreeNodeWalk.ts:121-138):
@@ -1546,8 +1622,15 @@ struct Eng {
       insert_slot(d, at);
       mk_remap_view(d);
       add_len_levels(0, d, d, candLen);
-      if constexpr (isLoad) load_entries(d, S, C);
-      else append_levels(0, d, S, C, WK_MAIN, candLen);
+      if constexpr (isLoad) {
+        ld_stale = 0;
+        if (C != -2)  // (a collaborating client's segment: update() on the path, see stale_at)
+          for (int i = 1; i <= d; i++)
+            if (stale_at(i, S)) ld_stale |= 1u << i;
+        load_entries(d, S, C);
+      } else {
+        append_levels(0, d, S, C, WK_MAIN, candLen);
+      }
       pending_fix = d;
       return true;
     }
@@ -2284,10 +2367,12 @@ struct Eng {
     return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS))
                             : GP((const uint32_t*)RAW(aux) + (h & ~MTB_PNAN));
   }
-  // matchProperties (properties.ts:71-96) on interned property sets
+  // matchProperties (properties.ts:71-96) on interned property sets; a = the run head's set.  With irregular
+  // keys in the batch (tab.irr_any) it is neither reflexive nor symmetric there: no shortcut on equal handles.
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
     if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
-    if (a == b) return true;
+    const bool irr = U(sh->tab.irr_any) != 0;
+    if (a == b && !irr) return true;
     const gptr<const uint32_t> pa = a ? props_ptr(a) : nullptr;
     const gptr<const uint32_t> pb = b ? props_ptr(b) : nullptr;
     const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
@@ -2299,7 +2384,9 @@ struct Eng {
         if (pb[1 + 2 * q] == k) {
           found = true;
           const uint32_t va = pa[2 + 2 * i], vb = pb[2 + 2 * q];
-          if (va != vb) {
+          if (irr) {
+            if (!mtbk::irr_value_match(sh->tab, k, va, vb)) return false;
+          } else if (va != vb) {
             if (U(sh->tab.class_trivial)) return false;
             const auto vcl = UP(sh->tab.val_class);
             if (vcl[va] != vcl[vb]) return false;
@@ -2313,7 +2400,7 @@ struct Eng {
   }
   // PropertiesManager.addProperties for a sequenced remote op (segmentPropertiesManager.ts:60-157).
   // The key/value list is staged in LDS; all lanes run the (short) edit loop uniformly.
-  // comb: 0 none, 1 rewrite, 2 incr (the annotate's combiningOp)
+  // comb: 0 none, 1 rewrite, 2 incr, 3 consensus (the annotate's combiningOp)
   __device__ __forceinline__ uint32_t props_apply(uint32_t old, uint32_t opId, int comb) {
     const uint32_t mo = U(memo_old), mn = U(memo_new);
     if (HOT(old == mo && mn)) return mn;
@@ -2375,6 +2462,15 @@ struct Eng {
         // defaultValue) + undefined is NaN for numbers / booleans / NaN; strings and objects are not restated
         if (at >= 0 && !(sh->tab.val_falsy[sh->pv[at]] & 2)) { fail(DERR_INCR); return 0; }
         v = U(sh->tab.nan_val);
+      } else if (COLD(comb == 3)) {
+        // consensus (properties.ts:46-62): a present value stays -- unless it is an object whose seq is -1,
+        // completed in place by the reference (shared with split clones): refused; an absent one takes the
+        // host-made value (Interner::consensus_props; MTB_NONE: a null defaultValue, the reference throws)
+        if (at >= 0) {
+          if (sh->tab.val_falsy[sh->pv[at]] & 4) { fail(DERR_CONSENSUS); return 0; }
+          continue;
+        }
+        if (v == MTB_NONE) { fail(DERR_CONSENSUS); return 0; }
       }
       if (v == MTB_NONE) {
         if (at >= 0) {
@@ -2630,7 +2726,7 @@ struct Eng {
             continue;
           }
 #endif
-          if (!nk || comb == 2) continue;  // (a combiningOp modifies pending keys too, shouldModifyKey :95-106)
+          if (!nk || comb >= 2) continue;  // (a combiningOp modifies pending keys too, shouldModifyKey :95-106)
           const uint32_t np = props_apply_slow(rlu(props, t), opId, comb, nk);
           if (bad()) return 0;
           memo_old = MTB_NONE;  // (an edit with exclusions is never reused)
@@ -2944,6 +3040,32 @@ struct Eng {
             const bool ok = props_match(rlu(f[F_PROPS], t - 1), rlu(f[F_PROPS], t));
             if (lane == t) eq = ok;
           }
+        }
+        if (COLD(U(sh->tab.irr_any) != 0)) {
+          // irregular keys: matchProperties is no equivalence, so each segment is compared with its run's head
+          // (scourNode's prevSegment, zamboni.ts:151-177), block by block, the length rule included
+          const unsigned long long bm = __ballot(base), cm = __ballot(cand);
+          unsigned long long okm = 0;
+          int head = -1, runLen = 0;
+          for (int t = 0; t < 64; t++) {
+            if ((t & 7) == 0) head = -1;
+            if (!((cm >> t) & 1)) {
+              head = -1;
+              continue;
+            }
+            const int lt = rl(klen0, t);
+            bool ok = false;
+            if (head >= 0 && ((bm >> t) & 1) && (runLen <= 256 || lt <= 256))
+              ok = props_match(rlu(f[F_PROPS], head), rlu(f[F_PROPS], t));
+            if (ok) {
+              runLen += lt;
+              okm |= 1ull << t;
+            } else {
+              head = t;
+              runLen = lt;
+            }
+          }
+          eq = ((okm >> lane) & 1) != 0;
         }
         compat = base && eq;
         // length rule: the run length before this segment (segmented scan restarting at run heads)
@@ -3698,16 +3820,20 @@ struct Eng {
       ph_split_top = MTB_VDEPTH;
       settle();
       if (bad()) return;
+      // a collaborating client's segment takes update() on every path block that did not split (the split halves
+      // and a new root were recombined): refuse when that leaves stale cumulative lengths below the root (the
+      // root's own partial lengths are never walked)
+      const int top = ph_split_top < dins + 1 ? ph_split_top : dins + 1;
+      if (C != -2 && (ld_stale & ((1u << top) - 1u))) { fail(DERR_STALE); return; }
       if constexpr (hasPh) {
         if (COLD(phDoc)) {
           if (C == -2) {
             // NonCollabClient: blockUpdateLength recombines every block of the path (mergeTree.ts:2447-2452)
             ph_up(U(ins_blk));
           } else if (rseq >= 0) {
-            // a removed segment of a collaborating client: update() adds it to every path block that did
-            // not split (the split halves were recombined; the new root too)
-            const int top = ph_split_top < dins + 1 ? ph_split_top : dins + 1;
-            for (int i = 0; i < top && !err; i++) ph_add(U(sh->path[i]), (uint32_t)rseq, (uint32_t)len, o.msn, o.pos1);
+            // a removed segment of a collaborating client: update() records its insert, never its removal
+            for (int i = 0; i < top && !err; i++)
+              ph_add(U(sh->path[i]), (uint32_t)rseq, (uint32_t)len, o.msn, o.pos1, (uint32_t)S);
           }
           if (bad()) return;
         }
@@ -3998,6 +4124,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
   e.phDoc = Eng<MODE, SCR>::hasPh && (DSF(flags) & DSF_PHANTOM) != 0 && e.ph_off != 0;
   e.ph_split_top = MTB_VDEPTH;
   e.ph_ow = false;
+  e.ld_stale = 0;
   e.cur_k = 0;
   e.sp_internal = false;
   e.local_seq = (int)DSF(local_seq);
@@ -4582,9 +4709,9 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
 #define EX_INLINE 0x40000000u
 namespace mtbk {
 __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uint32_t* pool, const uint32_t* A,
-                                               const uint32_t* vcl) {
+                                               const Tables& tab) {
   if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
-  if (a == b) return true;
+  if (a == b && !tab.irr_any) return true;
   const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + a) : nullptr;
   const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + b) : nullptr;
   const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
@@ -4594,7 +4721,9 @@ __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uin
     bool found = false;
     for (uint32_t q = 0; q < nb; q++)
       if (pb[1 + 2 * q] == k) {
-        if (vcl[pa[2 + 2 * i]] != vcl[pb[2 + 2 * q]]) return false;
+        if (tab.irr_any ? !irr_value_match(tab, k, pa[2 + 2 * i], pb[2 + 2 * q])
+                        : tab.val_class[pa[2 + 2 * i]] != tab.val_class[pb[2 + 2 * q]])
+          return false;
         found = true;
         break;
       }
@@ -4605,7 +4734,7 @@ __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uin
 }  // namespace mtbk
 extern "C" __global__ void __launch_bounds__(64)
     mtb_extract_v1_kernel(const DocState* __restrict__ docs, const uint32_t* list, uint32_t n, const FBlk* blks,
-                          const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const uint32_t* vcl,
+                          const uint16_t* text, const uint32_t* aux, const uint32_t* pool, const Tables tab,
                           uint32_t* cnt, const uint64_t* off, uint32_t* items, uint16_t* otext, uint32_t* owords) {
   __shared__ uint32_t ids[MTB_DG_DEPTH][MTB_MAXCH];
   __shared__ int32_t bc[MTB_DG_DEPTH], nxt[MTB_DG_DEPTH];
@@ -4709,7 +4838,7 @@ extern "C" __global__ void __launch_bounds__(64)
             append = p_start == MTB_HANDLE_UNALLOC ? txt == MTB_HANDLE_UNALLOC : txt == p_start + p_len;
           } else {
             append = !p_marker && !marker && !(p_len > 0 && p_last == u'\n') && (p_len <= 256 || len <= 256) &&
-                     ex_props_match(p_props, props, pool, A, vcl);
+                     ex_props_match(p_props, props, pool, A, tab);
           }
         }
         if (append) {
@@ -4776,10 +4905,10 @@ extern "C" __global__ void __launch_bounds__(64)
 }
 hipError_t mtb_launch_extract_v1(hipStream_t stream, const DocState* docs, const uint32_t* list, uint32_t n,
                                  const FBlk* blks, const uint16_t* text, const uint32_t* aux, const uint32_t* pool,
-                                 const uint32_t* vcl, uint32_t* cnt, const uint64_t* off, uint32_t* items,
+                                 const Tables& tab, uint32_t* cnt, const uint64_t* off, uint32_t* items,
                                  uint16_t* otext, uint32_t* owords) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(mtb_extract_v1_kernel, dim3(n), dim3(64), 0, stream, docs, list, n, blks, text, aux, pool, vcl, cnt,
+  hipLaunchKernelGGL(mtb_extract_v1_kernel, dim3(n), dim3(64), 0, stream, docs, list, n, blks, text, aux, pool, tab, cnt,
                      off, items, otext, owords);
   return hipGetLastError();
 }

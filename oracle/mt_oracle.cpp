@@ -823,6 +823,7 @@ std::unique_ptr<PartialLengths> MergeTree::combine(Block* b, bool recur) {  // p
 }
 
 void MergeTree::plUpdate(PartialLengths& pl, Block* node, int seq, int clientId) {  // partialLengths.ts:636-686
+  if (node != root && !pl.partialLengths.items.empty() && pl.partialLengths.items.back().seq > seq) counters.staleUpdates++;
   int seqSeglen = 0;
   int segCount = 0;
   for (int i = 0; i < node->childCount; i++) {
@@ -960,10 +961,36 @@ Comb parse_comb(const JVal* comb) {
     c.kind = Comb::Incr;
     if (const JVal* d = obj_get(comb->obj, u"defaultValue")) c.defaultValue = *d;
     if (const JVal* m = obj_get(comb->obj, u"minValue")) c.minValue = *m;
+  } else if (name && name->t == JVal::Str && name->str == u"consensus") {
+    c.kind = Comb::Consensus;
+    if (const JVal* d = obj_get(comb->obj, u"defaultValue")) c.defaultValue = *d;
   } else {
-    fail_unsupported("combiningOp other than rewrite / incr");
+    fail_unsupported("combiningOp other than rewrite / incr / consensus");
   }
   return c;
+}
+// combine(combiningOp, previousValue, undefined, seq) for "consensus" (properties.ts:46-62), sequenced ops:
+// no previous value and no defaultValue gives a fresh {value: undefined, seq} (JSON {"seq":seq}); an object
+// whose seq is -1 gets seq (in place: the op's defaultValue object is shared by the op's segments alone, so a
+// copy equals it; a previous value may be shared with other segments by split clones -- not restated); any
+// other value stays.  A null defaultValue makes the reference throw reading its seq.
+static JVal combine_consensus(const Comb& c, const JVal* prev, int seq) {
+  const bool fromPrev = prev && prev->t != JVal::Undef;
+  JVal cur = fromPrev ? *prev : c.defaultValue;
+  if (cur.t == JVal::Undef) {
+    JVal cv;
+    cv.t = JVal::Obj;
+    obj_set(cv.obj, u"value", JVal::undef());
+    obj_set(cv.obj, u"seq", JVal::number(seq));
+    return cv;
+  }
+  if (cur.t == JVal::Null) fail_unsupported("consensus with a null defaultValue (the reference throws reading its seq)");
+  const JVal* cs = cur.t == JVal::Obj ? obj_get(cur.obj, u"seq") : nullptr;
+  if (cs && cs->t == JVal::Num && cs->num == -1) {
+    if (fromPrev) fail_unsupported("consensus over a property value object whose seq is -1 (mutates a shared object)");
+    obj_set(cur.obj, u"seq", JVal::number(seq));
+  }
+  return cur;
 }
 // combine(combiningOp, previousValue, undefined, seq) for "incr" (properties.ts:24-69)
 static JVal combine_incr(const Comb& c, const JVal* prev) {
@@ -995,7 +1022,7 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
     if (deltaKeys && std::find(deltaKeys->begin(), deltaKeys->end(), k) == deltaKeys->end()) deltaKeys->push_back(k);
   };
   JObj& old = *s->props;
-  const bool rewrite = comb.kind == Comb::Rewrite, combining = comb.kind == Comb::Incr;
+  const bool rewrite = comb.kind == Comb::Rewrite, combining = comb.kind == Comb::Incr || comb.kind == Comb::Consensus;
   auto shouldModify = [&](const u16str& k) {
     return seq == UnassignedSeq || seq == UniversalSeq || s->pendingKeys.find(k) == s->pendingKeys.end() || combining;
   };
@@ -1021,7 +1048,8 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
       }
     }
     addDelta(kv.first);
-    if (combining) obj_set(old, kv.first, combine_incr(comb, obj_get(old, kv.first)));
+    if (comb.kind == Comb::Consensus) obj_set(old, kv.first, combine_consensus(comb, obj_get(old, kv.first), seq));
+    else if (combining) obj_set(old, kv.first, combine_incr(comb, obj_get(old, kv.first)));
     else if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
   }
@@ -1618,6 +1646,8 @@ std::string Doc::removeLocalOp(int start, int end) {
 std::string Doc::annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp) {
   if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
   const Comb comb = parse_comb(combiningOp);  // annotateRangeLocal(start, end, props, combiningOp)
+  // (a local consensus value is {value: undefined, seq: -1}, completed in place at the ack: not restated)
+  if (comb.kind == Comb::Consensus) fail_unsupported("local consensus annotate");
   validLocalRange(start, end, mt.length(), false);
   mt.annotateRange(start, end, props, comb, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   JVal pv;

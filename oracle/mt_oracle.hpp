@@ -36,7 +36,8 @@ constexpr int UNDEF_LEN = -1;              // `undefined` result of nodeLength
 // ICombiningOp of an annotate (ops.ts): none, "rewrite" (segmentPropertiesManager.ts:109-123) or "incr"
 // (properties.ts:24-69: each key becomes combine(op, previousValue, undefined, seq), the previous value or
 // defaultValue plus undefined -- NaN for numbers, booleans, null and undefined; a string gets "undefined"
-// appended; then minValue when truthy and larger).  "consensus" and other names are not restated.
+// appended; then minValue when truthy and larger) or "consensus" for sequenced ops (properties.ts:46-62,
+// combine_consensus).  Other names are not restated.
 struct Comb {
   enum Kind { None, Rewrite, Incr, Consensus } kind = None;
   JVal defaultValue;  // Undef when absent
@@ -156,6 +157,9 @@ struct OracleError : std::runtime_error {
 
 struct Counters {
   uint64_t ops = 0, segsTouched = 0, maxHeap = 0, maxDepth = 0;
+  // PartialSequenceLengths.update below the root met an entry newer than its seq (a summary body's insert):
+  // addSeq leaves the later entries' cumulative lengths stale (the engine refuses such loads)
+  uint64_t staleUpdates = 0;
 };
 
 class MergeTree {

@@ -289,6 +289,7 @@ int orc_num_clients(orc_doc* d) { return (int)d->doc.longIds.size(); }
 const char* orc_client_long_id(orc_doc* d, int i) { return d->doc.longIds.at(i).c_str(); }
 uint64_t orc_ops_applied(orc_doc* d) { return d->doc.mt.counters.ops; }
 uint64_t orc_segs_touched(orc_doc* d) { return d->doc.mt.counters.segsTouched; }
+uint64_t orc_stale_updates(orc_doc* d) { return d->doc.mt.counters.staleUpdates; }
 
 // Summary: returns a JSON object {"blobs":[[path, content],...], "summary": <ISummaryTreeWithStats>}
 int orc_summarize_v1(orc_doc* d, int msn, int seq, char** out, size_t* len) {

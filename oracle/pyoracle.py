@@ -47,6 +47,8 @@ def lib():
         L.orc_ops_applied.argtypes = [vp]
         L.orc_segs_touched.restype = ctypes.c_uint64
         L.orc_segs_touched.argtypes = [vp]
+        L.orc_stale_updates.restype = ctypes.c_uint64
+        L.orc_stale_updates.argtypes = [vp]
         L.orc_summarize_v1.argtypes = [vp, i, i, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_dump_segments.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_checksum.restype = ctypes.c_uint64
@@ -272,6 +274,10 @@ class OracleDoc:
 
     def segs_touched(self):
         return self._L.orc_segs_touched(self._h)
+
+    def stale_updates(self):
+        """Partial-length updates below the root that met newer entries (stale cumulative lengths)."""
+        return self._L.orc_stale_updates(self._h)
 
     def summarize_v1(self, msn=-1, seq=-1):
         p = ctypes.c_void_p()

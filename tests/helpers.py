@@ -75,7 +75,7 @@ def records_to_msgs(ops_bytes, n, text_bytes, props_json, long_ids):
 
 
 def make_v1_summary(seed, n_segments, chunk_len, msn, seq, n_clients=4, p_removed=0.25, p_client=0.0,
-                    client_body=False, client_removed=False):
+                    client_body=False, client_removed=False, inserters=None):
     """A constructed SnapshotV1 summary (snapshotV1.ts layout) for load tests: text / marker / props
     segments; NonCollab segments removed above the MSN by 1-3 clients; optionally segments inserted above
     the MSN by clients (header only unless `client_body`).  Returns [(path, content), ...]."""
@@ -102,7 +102,8 @@ def make_v1_summary(seed, n_segments, chunk_len, msn, seq, n_clients=4, p_remove
             out.append(({"json": spec, "removedSeq": rs, "removedClientIds": rcs}, ln))
         elif u < p_removed + p_client:
             s = rng.randint(msn + 1, seq)
-            m = {"json": spec, "client": rng.choice(clients), "seq": s}
+            m = {"json": spec, "client": rng.choice(clients if inserters is None else [clients[k] for k in inserters]),
+                 "seq": s}
             if client_removed and rng.random() < 0.3 and s < seq:
                 m["removedSeq"] = rng.randint(s + 1, seq)
                 m["removedClientIds"] = [rng.choice(clients)]
@@ -722,3 +723,75 @@ def make_tail_log(seed, n_msgs, n_clients=4, lag=48, initial_len=12000, lo=10200
         msgs.append(m)
     gen.close()
     return text, msgs
+
+
+PROP_PALETTE = [5, {}, "ab", {"0": "a", "1": "b"}, {"x": None}, {"x": 0}, [], 0, "", {"0": "a"}, "a", [1],
+                {"x": {"y": None}}, {"x": {}}, 7, True]
+
+
+def make_props_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello props world", p_cons=0.15):
+    """A sequenced op log whose property values are outside any equivalence of matchProperties
+    (properties.ts:71-96): key "k" mixes primitives, objects, arrays, strings and index objects, nested nulls
+    (PROP_PALETTE); key "j" holds small integers; null deletes.  A fraction `p_cons` of the annotates are remote
+    combiningOp "consensus" annotates (properties.ts:46-62) without a defaultValue, with a primitive one, or with
+    an object one whose seq is -1.  Inserts with props, removes; every message is applied to a generator oracle
+    as it is made.  Returns (initial text, messages)."""
+    import random
+    from pyoracle import OracleDoc
+    rng = random.Random(seed)
+    ids = [f"client-{k}" for k in range(n_clients)]
+    gen = OracleDoc(new_length_calc=new_mode)
+    if initial:
+        gen.insert_text_local(0, initial)
+    gen.start_collab("gen-observer")
+    short = {}
+    for cid in ids:
+        gen.add_client(cid)
+        short[cid] = len(short) + 1
+    ref = [0] * n_clients
+    msgs = []
+    words = ["ab", "c", "xyz", "\n", "more text "]
+
+    def props():
+        r = rng.random()
+        if r < 0.45:
+            return {"k": rng.choice(PROP_PALETTE)}
+        if r < 0.65:
+            return {"k": rng.choice(PROP_PALETTE), "j": rng.randint(0, 2)}
+        if r < 0.8:
+            return {"j": rng.randint(0, 2)}
+        if r < 0.9:
+            return {"k": None}
+        return {"o": rng.choice([{"x": None}, {"x": 0}, 0, {}])}
+
+    for seq in range(1, n_msgs + 1):
+        k = rng.randrange(n_clients)
+        ref[k] = max(ref[k], seq - 1 - rng.randint(0, lag))
+        R, C, cid = ref[k], short[ids[k]], ids[k]
+        n = gen.remote_length(R, C)
+        x = rng.random()
+        if x < 0.4 or n == 0:
+            seg = rng.choice(words)
+            if rng.random() < 0.5:
+                seg = {"text": seg, "props": {kk: v for kk, v in props().items() if v is not None}}
+            op = {"type": 0, "pos1": rng.randint(0, n), "seg": seg}
+        else:
+            a = rng.randrange(n)
+            b = min(n, a + rng.randint(1, 8))
+            if x < 0.55:
+                op = {"type": 1, "pos1": a, "pos2": b}
+            elif x < 0.55 + p_cons:
+                comb = {"name": "consensus"}
+                r = rng.random()
+                if r < 0.25:
+                    comb["defaultValue"] = rng.choice([3, "d", True])
+                elif r < 0.4:
+                    comb["defaultValue"] = {"seq": -1, "v": rng.randint(0, 1)}
+                op = {"type": 2, "pos1": a, "pos2": b, "props": {rng.choice(["k", "c"]): 1}, "combiningOp": comb}
+            else:
+                op = {"type": 2, "pos1": a, "pos2": b, "props": props()}
+        m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": min(ref),
+             "type": "op", "contents": op}
+        gen.apply_msg(m)
+        msgs.append(m)
+    return initial, msgs

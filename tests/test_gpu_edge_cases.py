@@ -122,11 +122,11 @@ def test_ragged_batch_edge_cases_match_oracle(new_mode):
                          "minimumSequenceNumber": 0, "type": "op", "contents": {"type": 0, "pos1": 0, "seg": "no"}})
     B[bad].applyMsg({"clientId": "w", "sequenceNumber": 6, "referenceSequenceNumber": 5, "minimumSequenceNumber": 0,
                      "type": "op", "contents": {"type": 0, "pos1": 50, "seg": "past the end"}})
-    # a null nested inside a property value is outside the engine's subset: rejected loudly at apply
+    # an unknown combiningOp is outside the engine's subset: rejected loudly at apply
     with pytest.raises(MergeTreeError, match="unsupported"):
         B[1].applyMsg({"clientId": "c0", "sequenceNumber": 10 ** 6, "referenceSequenceNumber": 0,
                        "minimumSequenceNumber": 0, "type": "op",
-                       "contents": {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": [{"z": None}]}}})
+                       "contents": {"type": 2, "pos1": 0, "pos2": 1, "props": {"k": 1}, "combiningOp": {"name": "max"}}})
     # first third, then the rest: both flushes replay the whole ragged batch.  The failure is reported
     # once, by the flush whose replay hit it; the other documents' records were replayed by it.
     with pytest.raises(MergeTreeError, match=r"document 7 op \d+: MergeTree insert failed"):

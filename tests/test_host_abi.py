@@ -52,7 +52,9 @@ def test_unsupported_inputs_are_rejected_at_pack_time():
         B[0].applyMsg(dict(base, contents={"type": 0, "relativePos1": {"id": "m1"}, "seg": "x"}))
     with pytest.raises(MergeTreeError, match="combiningOp"):
         B[0].applyMsg(dict(base, contents={"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1},
-                                           "combiningOp": {"name": "consensus"}}))
+                                           "combiningOp": {"name": "max"}}))
+    with pytest.raises(MergeTreeError, match="local consensus"):
+        B[0].applyLocalOp({"type": 2, "pos1": 0, "pos2": 1, "props": {"a": 1}, "combiningOp": {"name": "consensus"}})
     with pytest.raises(MergeTreeError, match="0x038"):
         B[0].applyMsg(dict(base, sequenceNumber=5, contents={"type": 0, "pos1": 0, "seg": "x"}))
         B[0].applyMsg(dict(base, sequenceNumber=4, contents={"type": 0, "pos1": 0, "seg": "y"}))

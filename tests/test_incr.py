@@ -91,10 +91,11 @@ def test_host_incr_packing():
     with pytest.raises(MergeTreeError, match="non-numeric defaultValue"):
         B[0].applyMsg(msg("a", 4, 3, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
                                       "combiningOp": {"name": "incr", "defaultValue": "x"}}))
-    with pytest.raises(MergeTreeError, match="consensus"):
-        B[0].applyMsg(msg("a", 4, 3, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
-                                      "combiningOp": {"name": "consensus"}}))
+    B[0].applyMsg(msg("a", 4, 3, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
+                                  "combiningOp": {"name": "consensus"}}))
     import struct
     ob, n, _ = B.export_pending(0)
     t, fl = struct.unpack_from("<BB", ob, 32)
-    assert t == 2 and fl & 0x08  # MTB_F_INCR
+    assert t == 2 and fl & 0x0C == 0x08  # MTB_F_INCR
+    t, fl = struct.unpack_from("<BB", ob, 32 * 3)
+    assert t == 2 and fl & 0x0C == 0x0C  # MTB_F_CONSENSUS

@@ -1,0 +1,49 @@
+"""matchProperties where it is no equivalence, and remote "consensus" annotates: the hand-derived known answers
+of tests/props_cases.py on the oracle (CPU), and the engine's pack-time handling (the engine's replay parity
+is tests/test_gpu_props_exact.py)."""
+import json
+
+import pytest
+
+import props_cases as pc
+
+
+def _run(init, msgs):
+    from pyoracle import OracleDoc
+    o = OracleDoc(verify=True)
+    if init:
+        o.insert_text_local(0, init)
+    o.start_collab("obs")
+    for m in msgs:
+        o.apply_msg(m)
+    return o
+
+
+@pytest.mark.parametrize("case", pc.CASES, ids=[c[0] for c in pc.CASES])
+def test_known_answers_on_the_oracle(case):
+    name, init, msgs, expected = case
+    o = _run(init, msgs)
+    assert pc.rows(o.dump_segments()) == expected
+    # SnapshotV1 coalesces below the MSN with the same head-first comparison (snapshotV1.ts:238-251): here every
+    # segment is below the MSN, so the header holds the live rows
+    segs = json.loads(o.summarize_v1()["blobs"][0][1])["segments"]
+    assert [[s, None] if isinstance(s, str) else [s["text"], s.get("props")] for s in segs] == expected
+
+
+@pytest.mark.parametrize("case", pc.REFUSED, ids=[c[0] for c in pc.REFUSED])
+def test_refused_cases_on_the_oracle(case):
+    name, init, msgs, err = case
+    with pytest.raises(Exception, match="unsupported"):
+        _run(init, msgs)
+
+
+def test_consensus_values_coalesce_after_a_summary_round_trip():
+    """Live, two {value: undefined, seq} values never match (b.value is undefined); loaded from a summary they
+    are {"seq": S} objects, which do: the loaded document's own summary coalesces them."""
+    from pyoracle import OracleDoc
+    o = _run(*pc.CASES[9][1:3])
+    blobs = o.summarize_v1()["blobs"]
+    p = OracleDoc(verify=True)
+    p.load_v1(blobs, "obs2")
+    segs = json.loads(p.summarize_v1()["blobs"][0][1])["segments"]
+    assert {"text": "cd", "props": {"k": {"seq": 2}}} in segs
