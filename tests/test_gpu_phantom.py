@@ -174,8 +174,8 @@ def test_long_documents_summarized_mid_collaboration(new_mode, chunk):
     from helpers import make_tail_log
     from pyoracle import OracleDoc
     out = []
-    # (seeds 40, 47, 59: clean loads in the old length mode, where the first 16 all go stale or fail)
-    for i in list(range(16)) + [40, 47, 59]:
+    # (seeds 40, 47, 48, 59: clean loads in the old length mode, where the first 16 all go stale or fail)
+    for i in list(range(16)) + [40, 47, 48, 59]:
         text, msgs = make_tail_log(900 + i + 50 * int(new_mode), 1600, lag=24 + 8 * (i % 8), initial_len=9990, lo=9990,
                                    new_mode=new_mode, inserters=[0])
         cut = len(msgs) // 2 + 37 * (i % 8)
