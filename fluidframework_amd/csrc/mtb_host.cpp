@@ -1911,8 +1911,9 @@ void launch_main(mtb_dev* b, const Tables& t) {
   {
     // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
     // batches where some document met a marker id
-    bool markers = false;
-    for (uint32_t i = 0; i < b->ndocs && !markers; i++)  // (the marker variant carries the phantom tables too)
+    // (the marker variant carries the phantom tables and the irregular-key matchProperties too)
+    bool markers = b->in.nIrr != 0;
+    for (uint32_t i = 0; i < b->ndocs && !markers; i++)
       markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot || b->docs[i].phantom;
     // more documents than wave slots: tickets, one per workgroup (mtb_replay_tick_kernel, the default;
     // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document) or passes of equal chunks (MTB_SCHED=passes);

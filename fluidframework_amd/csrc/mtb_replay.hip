@@ -315,6 +315,9 @@ struct Eng {
   int wv;                       // MODE_MATRIX: 0 = rows vector, 1 = cols vector              // depth of a block that reached MaxNodesInBlock children (-1: none)
   // phantom partial lengths of loaded documents (see "phantom partial lengths" below)
   static constexpr bool hasPh = MODE == MODE_LOAD || MODE == MODE_MARKERS || MODE == MODE_LIVE;
+  // property keys whose values matchProperties does not compare as an equivalence (Tables::irr_any): the host
+  // runs such batches on the marker variant, so the observer kernel carries none of that code
+  static constexpr bool hasIrr = MODE == MODE_LOAD || MODE == MODE_MARKERS || MODE == MODE_LIVE;
   uint32_t ph_off;              // DocState.ph: aux offset of the table (0: none)
   bool phDoc;                   // DSF_PHANTOM (hasPh modes)
   int ph_split_top;             // the topmost depth the last fix_overflow split (MTB_VDEPTH: none)
@@ -2367,11 +2370,20 @@ struct Eng {
     return (h & MTB_GPROPS) ? (gptr<const uint32_t>)(UP(sh->tab.pool) + (h & ~MTB_GPROPS))
                             : GP((const uint32_t*)RAW(aux) + (h & ~MTB_PNAN));
   }
+  // Interner pair tables (mtbk::irr_value_match) with uniform operands, the table pointers in SGPRs
+  __device__ __forceinline__ bool irr_match(uint32_t k, uint32_t va, uint32_t vb) const {
+    const uint32_t o = U(UP(sh->tab.key_irr)[k]);
+    if (!o) return va == vb || U(UP(sh->tab.val_class)[va]) == U(UP(sh->tab.val_class)[vb]);
+    const auto T = UP(sh->tab.irr);
+    const auto L = UP(sh->tab.val_local);
+    const uint32_t bit = U(L[va]) * U(T[o - 1]) + U(L[vb]);
+    return ((U(T[o + bit / 32]) >> (bit % 32)) & 1u) != 0;
+  }
   // matchProperties (properties.ts:71-96) on interned property sets; a = the run head's set.  With irregular
   // keys in the batch (tab.irr_any) it is neither reflexive nor symmetric there: no shortcut on equal handles.
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
     if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
-    const bool irr = U(sh->tab.irr_any) != 0;
+    const bool irr = hasIrr && U(sh->tab.irr_any) != 0;
     if (a == b && !irr) return true;
     const gptr<const uint32_t> pa = a ? props_ptr(a) : nullptr;
     const gptr<const uint32_t> pb = b ? props_ptr(b) : nullptr;
@@ -2384,8 +2396,8 @@ struct Eng {
         if (pb[1 + 2 * q] == k) {
           found = true;
           const uint32_t va = pa[2 + 2 * i], vb = pb[2 + 2 * q];
-          if (irr) {
-            if (!mtbk::irr_value_match(sh->tab, k, va, vb)) return false;
+          if (COLD(irr)) {
+            if (!irr_match(U(k), U(va), U(vb))) return false;
           } else if (va != vb) {
             if (U(sh->tab.class_trivial)) return false;
             const auto vcl = UP(sh->tab.val_class);
@@ -3031,41 +3043,40 @@ struct Eng {
         const bool c1c0 = g.c1 == (uint32_t)dpp_shr_t<0x111>((int)g.c0);
         bool eq = !nanPair && (sameH || (sameN && (g.n == 0 || (g.n == 1 && k0k0 && c0c0) ||
                                                    (g.n == 2 && ((k0k0 && c0c0 && k1k1 && c1c1) || (k0k1 && c0c1 && k1k0 && c1c0))))));
-        // more than two keys: a full matchProperties, one neighbour pair at a time (rare)
-        unsigned long long nf = __ballot(base && !sameH && !nanPair && sameN && g.n > 2);
-        if (COLD(nf)) {
-          while (nf) {
-            const int t = first_set(nf);
-            nf &= nf - 1;
-            const bool ok = props_match(rlu(f[F_PROPS], t - 1), rlu(f[F_PROPS], t));
-            if (lane == t) eq = ok;
-          }
-        }
-        if (COLD(U(sh->tab.irr_any) != 0)) {
-          // irregular keys: matchProperties is no equivalence, so each segment is compared with its run's head
-          // (scourNode's prevSegment, zamboni.ts:151-177), block by block, the length rule included
-          const unsigned long long bm = __ballot(base), cm = __ballot(cand);
-          unsigned long long okm = 0;
-          int head = -1, runLen = 0;
-          for (int t = 0; t < 64; t++) {
-            if ((t & 7) == 0) head = -1;
-            if (!((cm >> t) & 1)) {
-              head = -1;
-              continue;
+        // more than two keys: a full matchProperties, one neighbour pair at a time (rare).  With irregular keys in
+        // the batch matchProperties is no equivalence: every candidate is compared with its run's head instead
+        // (scourNode's prevSegment, zamboni.ts:151-177), block by block, the 256-unit length rule included.
+        // (One loop, one inlined matchProperties: a second copy spills the hot scour.)
+        const bool irrB = hasIrr && U(sh->tab.irr_any) != 0;
+        const unsigned long long nf = __ballot(base && !sameH && !nanPair && sameN && g.n > 2);
+        const unsigned long long cm = __ballot(cand), bm = __ballot(base);
+        if (COLD(nf || irrB)) {
+          unsigned long long todo = irrB ? cm : nf, okm = 0;
+          int head = -1, runLen = 0, prev = -2;
+          while (todo) {
+            const int t = first_set(todo);
+            todo &= todo - 1;
+            int a = t - 1, lt = 0;
+            bool need = true;
+            if (irrB) {
+              lt = rl(klen0, t);
+              if (t != prev + 1 || (t & 7) == 0) head = -1;  // (a lane between, or a new block: no prevSegment)
+              prev = t;
+              need = head >= 0 && ((bm >> t) & 1) && (runLen <= 256 || lt <= 256);
+              a = head;
             }
-            const int lt = rl(klen0, t);
-            bool ok = false;
-            if (head >= 0 && ((bm >> t) & 1) && (runLen <= 256 || lt <= 256))
-              ok = props_match(rlu(f[F_PROPS], head), rlu(f[F_PROPS], t));
-            if (ok) {
-              runLen += lt;
-              okm |= 1ull << t;
-            } else {
-              head = t;
-              runLen = lt;
+            const bool ok = need && props_match(rlu(f[F_PROPS], a), rlu(f[F_PROPS], t));
+            if (ok) okm |= 1ull << t;
+            if (irrB) {
+              if (ok) {
+                runLen += lt;
+              } else {
+                head = t;
+                runLen = lt;
+              }
             }
           }
-          eq = ((okm >> lane) & 1) != 0;
+          if (irrB || ((nf >> lane) & 1)) eq = ((okm >> lane) & 1) != 0;
         }
         compat = base && eq;
         // length rule: the run length before this segment (segmented scan restarting at run heads)
