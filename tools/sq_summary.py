@@ -14,7 +14,7 @@ def main():
     for path in sys.argv[3:]:
         with open(path) as f:
             for r in csv.DictReader(f):
-                if r["Kernel_Name"] not in ("mtb_replay_kernel", "mtb_replay_tick_kernel", "mtb_replay_pass_kernel"):
+                if r["Kernel_Name"] not in ("mtb_replay_kernel", "mtb_replay_tick_kernel", "mtb_replay_pass_kernel", "mtb_replay_few_kernel"):
                     continue
                 disp.add((path, r["Dispatch_Id"]))
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
