@@ -400,6 +400,7 @@ struct Eng {
     }
     return len;
   }
+#ifdef MTB_VIS_V1
   // nodeLength for a leaf in a remote perspective (mergeTree.ts:935-1001)
   __device__ __forceinline__ int seg_vis(int len, int seq, int rseq, uint32_t cli, uint32_t rcx, int R, int C) const {
     const bool removed = rseq >= 0;
@@ -419,6 +420,33 @@ struct Eng {
     if (removed && !(isLive && rseq >= MTB_PEND)) return MTB_UNDEF;  // (removedSeq !== Unassigned)
     return 0;
   }
+#else
+  // the further removers [n, c1..cn] of a segment hold C (its removedClientIds[0] is checked by the caller)
+  __device__ __forceinline__ bool rcx_has(uint32_t rcx, int C) const {
+    const uint32_t n = aux[rcx];
+    for (uint32_t i = 0; i < n; i++)
+      if ((int)aux[rcx + 1 + i] == C) return true;
+    return false;
+  }
+  // nodeLength for a leaf in a remote perspective (mergeTree.ts:935-1001).  Per lane and divergent: the
+  // conditions are combined as masks, and only lanes that must read the further removers' list branch.
+  __device__ __forceinline__ int seg_vis(int len, int seq, int rseq, uint32_t cli, uint32_t rcx, int R, int C) const {
+    const bool removed = rseq >= 0;
+    const bool seen = (seq <= R) | (cli_client(cli) == C);
+    const bool rc0 = cli_rc0(cli) == C;
+    if (newMode) {
+      const bool und = removed & (rseq <= minSeq);
+      bool gone = removed & ((rseq <= R) | rc0);
+      if (COLD(removed & !und & !gone & (rcx != 0))) gone = rcx_has(rcx, C);
+      return und ? MTB_UNDEF : (gone | !seen) ? 0 : len;
+    }
+    const bool remR = removed & (rseq <= R);
+    bool rch = rc0;
+    if (COLD(removed & !remR & seen & !rc0 & (rcx != 0))) rch = rcx_has(rcx, C);
+    const bool und = remR | (!seen & removed & !(isLive && rseq >= MTB_PEND));  // (removedSeq !== Unassigned)
+    return und ? MTB_UNDEF : (!seen | (removed & rch)) ? 0 : len;
+  }
+#endif
   // nodeLength of a leaf in the op's perspective: the local client's own view (mergeTree.ts:917-921) or a
   // remote one
   __device__ __forceinline__ int leaf_len(int len, int seq, int rseq, uint32_t cli, uint32_t rcx, int R, int C) const {
@@ -535,12 +563,22 @@ struct Eng {
     const uint32_t hpar = rlu(h, 1);
     const int hsc = rl((int)h, 3), hlen = rl((int)h, 4);
     wsync();
+#ifdef MTB_VIS_V1
     auto correct = [&](const WEnt& e, bool v) {
       if (v && e.seq > Rl) {
         const int c = e.ck & 0xFFFF, kind = (e.ck >> 16) & 0xF;
         if ((kind == WK_MAIN && c != Cm) || (kind == WK_OVERLAP && c == Cm)) atomicAdd(&sh->corr[(e.ck >> 20) & 7], e.delta);
       }
     };
+#else
+    // (the entry's test as one mask: no nested exec-mask branches per entry chunk)
+    auto correct = [&](const WEnt& e, bool v) {
+      const uint32_t ck = (uint32_t)e.ck, kind = (ck >> 16) & 0xF;
+      const bool same = (int)(ck & 0xFFFF) == Cm;
+      const bool hit = v & (e.seq > Rl) & (((kind == WK_MAIN) & !same) | ((kind == WK_OVERLAP) & same));
+      if (hit) atomicAdd(&sh->corr[(ck >> 20) & 7], e.delta);
+    };
+#endif
     correct(e0, v0);
     correct(e1, v1);
     uint32_t done = two ? 128u : 64u;  // entries fetched (from the end when sorted, from the front if not)
