@@ -374,3 +374,50 @@ def test_catch_up_with_marker_relative_positions(new_mode):
     L.flush()
     for i, r in loaded.items():
         assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_catch_up_rewriting_with_irregular_values_and_consensus(new_mode):
+    """Lagging annotates whose values matchProperties does not compare as an equivalence (helpers.make_props_log:
+    primitives against objects, nested nulls, remote consensus values) in the catch-up blob: createOpsFromDelta
+    (sequence.ts:120-172) merges neighbouring ranges with matchProperties(lastAnnotate.props, props) over the
+    segments' own values (a consensus value, its `value` member undefined, never matches).  Blobs equal to the
+    oracle's; loadSequence continues to the same text and dump."""
+    from fluidframework_amd import MergeTreeBatch
+    from helpers import make_props_log
+    from pyoracle import OracleDoc
+    n, cut = 10, 450
+    logs = [make_props_log(600 + i + 20 * int(new_mode), 700, lag=24, new_mode=new_mode) for i in range(n)]
+    B = MergeTreeBatch(n, new_length_calc=new_mode, catch_up=True)
+    oracles = []
+    for i, (init, msgs) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("A")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("A")
+        o.enable_catch_up()
+        for m in msgs[:cut]:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        oracles.append(o)
+    B.flush()
+    L = MergeTreeBatch(n, new_length_calc=new_mode)
+    loaded = []
+    for i, o in enumerate(oracles):
+        gb, gs = B.summarize_legacy(i)
+        osum = o.summarize_legacy()
+        assert [list(x) for x in gb] == osum["blobs"], f"doc {i}: legacy + catch-up blobs differ"
+        r = OracleDoc(new_length_calc=new_mode)
+        r.apply_catch_up(r.load_v1(osum["blobs"], "loader"))
+        assert L[i].loadSequence(osum["blobs"], "loader")
+        loaded.append(r)
+    L.flush()
+    for i, r in enumerate(loaded):
+        assert L.dump_segments(i) == r.dump_segments(), f"doc {i}: dump after catch-up"
+        for m in logs[i][1][cut:]:
+            L[i].applyMsg(m)
+            r.apply_msg(m)
+    L.flush()
+    for i, r in enumerate(loaded):
+        assert L.text(i) == r.get_text() and L.dump_segments(i) == r.dump_segments(), f"doc {i}"
