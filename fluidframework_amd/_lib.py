@@ -22,7 +22,7 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_matrix_intern_value", "mtb_matrix_summarize", "mtb_matrix_get_cell", "mtb_matrix_load",
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
-           "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident",
+           "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident", "mtb_replay_resident_ex", "mtb_refresh_digests",
            "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
            "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op",
            "mtb_get_launch_info", "mtb_detached_op_json", "mtb_maintenance"]
@@ -124,6 +124,8 @@ def lib():
     L.mtb_map_range.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, u32,
                                 ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.mtb_replay_resident.argtypes = [vp, ctypes.POINTER(MtbStats)]
+    L.mtb_replay_resident_ex.argtypes = [vp, ctypes.POINTER(MtbStats), u32]
+    L.mtb_refresh_digests.argtypes = [vp, ctypes.POINTER(MtbStats)]
     L.mtb_export_pending.argtypes = [vp, u32, vp, u32, ctypes.POINTER(u32), vp, sz, ctypes.POINTER(sz)]
     L.mtb_props_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.mtb_client_long_id.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]

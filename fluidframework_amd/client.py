@@ -195,12 +195,20 @@ class MergeTreeBatch:
         """Restore every document to its state before its first replay (records stay in HBM)."""
         self._chk(self._L.mtb_rewind(self._h))
 
-    def replay_resident(self):
-        """Replay the HBM-resident records again (after rewind); returns the stats dict."""
+    def replay_resident(self, digests=True):
+        """Replay the HBM-resident records again (after rewind); returns the stats dict.  digests=False skips the
+        state-digest pass (checksum / segments_final / text_units_final stay 0 until refresh_digests)."""
         st = _lib.MtbStats()
-        self._chk(self._L.mtb_replay_resident(self._h, ctypes.byref(st)))
+        self._chk(self._L.mtb_replay_resident_ex(self._h, ctypes.byref(st), 0 if digests else 1))
         self.last_stats = {f: getattr(st, f) for f, _ in _lib.MtbStats._fields_}
         return self.last_stats
+
+    def refresh_digests(self):
+        """The state digest of every document on its current state (mtb_refresh_digests): the stats dict's
+        checksum, segments_final, text_units_final and the write-back term of bytes_alg."""
+        st = _lib.MtbStats()
+        self._chk(self._L.mtb_refresh_digests(self._h, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in _lib.MtbStats._fields_}
 
     def _ensure_flushed(self):
         if self._dirty:

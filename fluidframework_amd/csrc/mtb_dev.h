@@ -52,7 +52,8 @@ int mtbx_summarize_v1_many(mtb_dev* b, uint32_t n, const uint32_t* docs, int64_t
 int mtbx_summarize_legacy(mtb_dev* b, uint32_t doc, int64_t msn, int64_t seq, const char* catchup_json,
                          size_t catchup_len, mtb_blob_list* out);
 int mtbx_rewind(mtb_dev* b);
-int mtbx_replay_resident(mtb_dev* b, mtb_stats* out);
+int mtbx_replay_resident(mtb_dev* b, mtb_stats* out, uint32_t flags = 0);
+int mtbx_refresh_digests(mtb_dev* b, mtb_stats* out);
 int mtbx_export_pending(mtb_dev* b, uint32_t doc, mtb_op* ops, uint32_t cap, uint32_t* n_out,
                        uint16_t* payload, size_t pcap, size_t* plen_out);
 int mtbx_props_json(mtb_dev* b, uint32_t id, char* buf, size_t cap, size_t* len_out);

@@ -3942,7 +3942,7 @@ int mtbx_get_launch_info(mtb_dev* b, mtb_launch_info* out) {
   });
 }
 
-int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
+int mtbx_replay_resident(mtb_dev* b, mtb_stats* out, uint32_t flags) {
   return guarded(b, [&] {
     if (!b->haveRewind) raise(MTB_E_ARG, "no resident records");
     const Tables t = make_tables(b);
@@ -3973,7 +3973,10 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out) {
       st.bytes_alg += 32ull * s.ops_applied + s.text_bytes + 24ull * s.n_mod;
       if (s.err) st.errors++;
     }
-    run_digest(b, st);
+    if (flags & MTB_REPLAY_NO_DIGEST)
+      b->digests.clear();  // (mtb_refresh_digests)
+    else
+      run_digest(b, st);
     if (out) *out = st;
     if (short_docs)
       raise(MTB_E_INTERNAL, std::to_string(short_docs) + " document(s) did not run all of their records");
@@ -4046,11 +4049,20 @@ int mtbx_dump_segments(mtb_dev* b, uint32_t doc, char** out, size_t* out_len) {
   });
 }
 
+int mtbx_refresh_digests(mtb_dev* b, mtb_stats* out) {
+  return guarded(b, [&] {
+    if (!b->devInit) raise(MTB_E_ARG, "no replay yet");
+    mtb_stats st{};
+    run_digest(b, st);
+    if (out) *out = st;
+  });
+}
+
 int mtbx_doc_digests(mtb_dev* b, uint32_t first, uint32_t n, uint64_t* out) {
   return guarded(b, [&] {
     if (!out && n) raise(MTB_E_ARG, "null output");
     if ((uint64_t)first + n > b->ndocs) raise(MTB_E_ARG, "document range out of bounds");
-    if (b->digests.size() != 3ull * b->ndocs) raise(MTB_E_ARG, "no replay yet");
+    if (b->digests.size() != 3ull * b->ndocs) raise(MTB_E_ARG, "no digests: no replay yet, or one without them (mtb_refresh_digests)");
     for (uint32_t k = 0; k < n; k++) out[k] = b->digests[3ull * (first + k)];
   });
 }

@@ -347,10 +347,23 @@ int mtb_rewind(mtb_batch* b) {
   return all_shards(b, [&](uint32_t s) { return mtbx_rewind(b->shards[s]); });
 }
 
-int mtb_replay_resident(mtb_batch* b, mtb_stats* out) {
+int mtb_replay_resident(mtb_batch* b, mtb_stats* out) { return mtb_replay_resident_ex(b, out, 0); }
+
+int mtb_replay_resident_ex(mtb_batch* b, mtb_stats* out, uint32_t flags) {
   if (!b) return MTB_E_ARG;
   std::vector<mtb_stats> st(b->shards.size());
-  const int rc = all_shards(b, [&](uint32_t s) { return mtbx_replay_resident(b->shards[s], &st[s]); });
+  const int rc = all_shards(b, [&](uint32_t s) { return mtbx_replay_resident(b->shards[s], &st[s], flags); });
+  if (out) {
+    *out = mtb_stats{};
+    for (auto& x : st) merge_stats(*out, x);
+  }
+  return rc;
+}
+
+int mtb_refresh_digests(mtb_batch* b, mtb_stats* out) {
+  if (!b) return MTB_E_ARG;
+  std::vector<mtb_stats> st(b->shards.size());
+  const int rc = all_shards(b, [&](uint32_t s) { return mtbx_refresh_digests(b->shards[s], &st[s]); });
   if (out) {
     *out = mtb_stats{};
     for (auto& x : st) merge_stats(*out, x);

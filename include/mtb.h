@@ -298,6 +298,16 @@ int mtb_summarize_legacy(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, c
  * records resident in HBM; mtb_replay_resident then replays them again without host traffic. */
 int mtb_rewind(mtb_batch* b);
 int mtb_replay_resident(mtb_batch* b, mtb_stats* out);
+/* mtb_replay_resident without the state-digest pass (flags MTB_REPLAY_NO_DIGEST): the statistics' checksum,
+ * segments_final and text_units_final stay 0 and the write-back term of bytes_alg is left out, until
+ * mtb_refresh_digests computes them (and the per-document digests) on the replayed state.  For timing the
+ * replay alone; the digests are verification, not part of Client.applyMsg. */
+#define MTB_REPLAY_NO_DIGEST 1u
+int mtb_replay_resident_ex(mtb_batch* b, mtb_stats* out, uint32_t flags);
+/* The state digest of every document on the current state (mtb_digest_kernel): fills out->checksum,
+ * segments_final, text_units_final and bytes_alg (its write-back term only: 24 B per final segment record +
+ * 2 B per final text unit); mtb_doc_digests reads the per-document values afterwards. */
+int mtb_refresh_digests(mtb_batch* b, mtb_stats* out);
 
 /* ---- host-side inspection (tests): the records/payload packed for `doc` and not yet replayed, the
  * JSON of an interned props id, and the long id of a short client id (Client.getLongClientId,

@@ -124,6 +124,15 @@ def test_multi_shard_batch_on_one_device(monkeypatch):
     st2 = B.replay_resident()
     assert st2["checksum"] == st["checksum"] and st2["ops_applied"] == st["ops_applied"]
     assert B.digests() == [lb.docs[j].digest for j in range(lb.n)]
+    # the bench's timed form: no digest pass in the replay, one afterwards (mtb_refresh_digests)
+    B.rewind()
+    st3 = B.replay_resident(digests=False)
+    assert st3["checksum"] == 0 and st3["ops_applied"] == st["ops_applied"]
+    with pytest.raises(Exception, match="no digests"):
+        B.digests()
+    fin = B.refresh_digests()
+    assert fin["checksum"] == st["checksum"] and st3["bytes_alg"] + fin["bytes_alg"] == st2["bytes_alg"]
+    assert B.digests() == [lb.docs[j].digest for j in range(lb.n)]
 
 
 def _prefix_digest(lb, u, m):
