@@ -22,6 +22,8 @@
 #define MTB_UNDEF (-1)
 #define MTB_MARKER 0x80000000u  // Seg.text flag: marker, low bits = refType + 1 (0 = undefined)
 #define MTB_GPROPS 0x80000000u  // props handle flag: batch-global table (else per-doc aux arena)
+#define MTB_INCR_TAB 0x80000000u  // an incr annotate's op-props value: pool offset of its result table
+                                  // [absent result, n, (string value, result) * n] (Interner::incr_props)
 #define MTB_PNAN 0x40000000u    // props handle flag of a per-doc set holding NaN (an incr annotate): such a set
                                 // matches no set, itself included (matchProperties: NaN !== NaN)
 #define MTB_NOKEY ((int32_t)0x80000000)

@@ -373,6 +373,52 @@ struct Interner {
     }
     return props_kv(memo, kv);
   }
+  // an incr annotate's op-props (properties.ts:24-45 through combine(op, previous, undefined), the op's values
+  // never read): each key's value slot names a pool table [absent result, n, (string value, result) * n]
+  // (MTB_INCR_TAB).  On the device a number / boolean / NaN previous value becomes NaN, an object fails the
+  // document (DERR_INCR), a string s becomes s + "undefined" -- and minValue when that is a string and the
+  // result sorts below it (JS string order; a number or boolean minValue compares with NaN: never) -- looked up
+  // here for every string value the key holds in the batch so far (a document's values were all interned
+  // before its op is packed); an absent key gets defaultValue + undefined (NaN, or a string).
+  static constexpr uint32_t kIncrStrMax = 4096;
+  uint32_t incr_props(uint32_t pid, const hj::Value* dv, const hj::Value* mv) {
+    const uint32_t off = pidx[2 * pid], n = pool[off];
+    std::string memo = "\x04" + std::to_string(pid) + ":" + (dv ? hj::dump(*dv) : "-") + ":" + (mv ? hj::dump(*mv) : "-");
+    for (uint32_t i = 0; i < n; i++) memo += ":" + std::to_string(keyVals[pool[off + 1 + 2 * i]].size());
+    auto it = propsByJson.find(memo);
+    if (it != propsByJson.end()) return it->second;
+    const bool minStr = mv && mv->kind == hj::Value::kStr && !mv->s.empty();
+    auto result = [&](uint32_t k, const U16& s) {
+      hj::Value r;
+      r.kind = hj::Value::kStr;
+      r.s = s + U16(u"undefined");
+      if (minStr && r.s < mv->s) r.s = mv->s;
+      return value(k, r);
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t k = pool[off + 1 + 2 * i];
+      uint32_t absent = nan();
+      if (dv && dv->kind == hj::Value::kStr) absent = result(k, dv->s);
+      std::vector<uint32_t> strs;
+      for (uint32_t v : keyVals[k])
+        if (valStore[v].kind == hj::Value::kStr) strs.push_back(v);
+      if (strs.size() > kIncrStrMax)
+        raise(MTB_E_UNSUPPORTED, "unsupported: incr over a key holding more than 4096 distinct string values");
+      std::vector<uint32_t> tab{absent, (uint32_t)strs.size()};
+      for (uint32_t v : strs) {
+        const U16 sv = valStore[v].s;  // (value() may grow valStore)
+        const uint32_t r = result(k, sv);
+        tab.push_back(v);
+        tab.push_back(r);
+      }
+      const uint32_t t = (uint32_t)pool.size();
+      pool.insert(pool.end(), tab.begin(), tab.end());
+      kv.push_back({k, MTB_INCR_TAB | t});
+    }
+    dirty = true;
+    return props_kv(memo, kv);
+  }
   // NaN, the value an incr annotate gives a numeric key: JSON null (JSON.stringify), its own matchProperties
   // class; a set holding it is flagged MTB_PNAN by the device and matches nothing (NaN !== NaN)
   uint32_t nanVal = MTB_NONE;
@@ -414,11 +460,11 @@ struct Interner {
     pool.push_back((uint32_t)kv.size());
     for (auto& e : kv) { pool.push_back(e.first); pool.push_back(e.second); }
     const uint32_t setOff = (uint32_t)pool.size();
-    uint32_t n = 0;
-    for (auto& e : kv) n += e.second != MTB_NONE;
+    uint32_t n = 0;  // (the set holds values: no nulls, no incr result tables)
+    for (auto& e : kv) n += !(e.second & MTB_INCR_TAB);
     pool.push_back(n);
     for (auto& e : kv)
-      if (e.second != MTB_NONE) { pool.push_back(e.first); pool.push_back(e.second); }
+      if (!(e.second & MTB_INCR_TAB)) { pool.push_back(e.first); pool.push_back(e.second); }
     const uint32_t id = (uint32_t)(pidx.size() / 2);
     pidx.push_back(opOff);
     pidx.push_back(setOff);
@@ -781,6 +827,7 @@ const std::string* props_marker_json(const Interner& in, uint32_t props, bool op
     if (in.pool[off + 1 + 2 * i] == k->second) {
       static const std::string null = "null";
       const uint32_t v = in.pool[off + 2 + 2 * i];
+      if (v != MTB_NONE && v >= in.valJson.size()) return nullptr;  // (an incr's result table, not a value)
       return v == MTB_NONE ? &null : &in.valJson[v];
     }
   return nullptr;
@@ -904,14 +951,17 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
           r.flags |= MTB_F_REWRITE;
         } else if (name && name->kind == hj::Value::kStr && name->s == u"incr") {
           // combine(op, previous, undefined) (segmentPropertiesManager.ts:145-147, properties.ts:24-69): NaN for a
-          // number / boolean / absent previous value when defaultValue is absent or numeric; a string previous
-          // value (string concatenation) fails the document at replay (DERR_INCR)
+          // number / boolean / absent previous value (defaultValue absent or numeric), string concatenation for a
+          // string one (Interner::incr_props); an object or array previous value fails the document (DERR_INCR)
           const hj::Value* dv = member(*comb, u"defaultValue");
-          if (dv && dv->kind != hj::Value::kUndef && dv->kind != hj::Value::kNull && dv->kind != hj::Value::kNum &&
-              dv->kind != hj::Value::kBool)
-            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with a non-numeric defaultValue (string concatenation)");
+          const hj::Value* mv = member(*comb, u"minValue");
+          if (dv && (dv->kind == hj::Value::kObj || dv->kind == hj::Value::kArr))
+            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with an object defaultValue");
+          if (mv && mv->truthy() && (mv->kind == hj::Value::kObj || mv->kind == hj::Value::kArr))
+            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with an object minValue");
           r.flags |= MTB_F_INCR;
           b->in.nan();
+          r.props = b->in.incr_props(r.props, dv, mv);
         } else if (name && name->kind == hj::Value::kStr && name->s == u"consensus") {
           // a local consensus value is {value: undefined, seq: -1}, completed in place at the ack (client.ts:1050-1058)
           if ((r.flags & MTB_F_LOCAL) || r.client == (uint16_t)MTB_LOCAL_CLIENT)
@@ -1810,7 +1860,7 @@ std::string derr_text(int e) {
     case DERR_SCHED: return "internal: the document's records did not all run (replay scheduler invariant)";
     case DERR_ASSERT_MKID: return "0x5ad Cannot change the markerId of an existing marker";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
-    case DERR_INCR: return "unsupported: incr combiningOp over a string or object property value (string concatenation)";
+    case DERR_INCR: return "unsupported: incr combiningOp over an object or array property value";
     case DERR_CONSENSUS: return "unsupported: consensus annotate over an object value whose seq is -1 (the reference completes "
                                 "it in place, shared with split clones), or with a null defaultValue over a segment lacking the key "
                                 "(the reference throws reading its seq)";
@@ -3884,8 +3934,6 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
       }
       if ((o.type == MTB_OP_INSERT || o.type == MTB_OP_ANNOTATE) && o.props >= b->in.pidx.size() / 2)
         raise(MTB_E_ARG, "record props id out of range");
-      if (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_CONSENSUS)  // (no defaultValue in records)
-        o.props = b->in.consensus_props(o.props, nullptr, (int)o.seq);
       if (o.type == MTB_OP_INSERT && (o.flags & MTB_F_MARKER)) o.payload = 0;  // set below (marker id ordinal)
       if (o.client >= d.longIds.size() && o.type != MTB_OP_NOOP)
         raise(MTB_E_ARG, "record client id not registered (mtb_add_client)");
@@ -3901,10 +3949,16 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
         }
       } else if (o.type == MTB_OP_ANNOTATE) {
         o.payload = 0;
-        if (const std::string* js = props_marker_json(b->in, o.props, true)) {
+        if (const std::string* js = props_marker_json(b->in, o.props, true)) {  // (the op's own values)
           const hj::Value v = hj::parse(js->data(), js->size());
           d.markerIdAnnot = true;
           o.payload = annot_marker_test(&v);
+        }
+        // combiningOps: the op-props values the device applies (records carry no defaultValue / minValue)
+        if ((o.flags & MTB_F_COMB) == MTB_F_CONSENSUS) o.props = b->in.consensus_props(o.props, nullptr, (int)o.seq);
+        if ((o.flags & MTB_F_COMB) == MTB_F_INCR) {
+          b->in.nan();
+          o.props = b->in.incr_props(o.props, nullptr, nullptr);
         }
       }
     }

@@ -2508,10 +2508,27 @@ struct Eng {
       for (uint32_t i = 0; i < n; i++)
         if (sh->pk[i] == k) at = (int)i;
       if (COLD(comb == 2)) {
-        // incr: combine(op, previous, undefined) (properties.ts:24-69) -- previous (or the host-checked numeric
-        // defaultValue) + undefined is NaN for numbers / booleans / NaN; strings and objects are not restated
-        if (at >= 0 && !(sh->tab.val_falsy[sh->pv[at]] & 2)) { fail(DERR_INCR); return 0; }
-        v = U(sh->tab.nan_val);
+        // incr: combine(op, previous, undefined) (properties.ts:24-69) -- previous + undefined is NaN for numbers /
+        // booleans / NaN; a string's result (s + "undefined", minValue) and the absent key's come from the op's
+        // table (Interner::incr_props); an object or array is not restated
+        const uint32_t nanv = U(sh->tab.nan_val);
+        const auto T = UP(sh->tab.pool) + (v & ~MTB_INCR_TAB);
+        const bool tab = (v & MTB_INCR_TAB) != 0 && v != MTB_NONE;
+        if (at < 0) {
+          v = tab ? U(T[0]) : nanv;
+        } else if (sh->tab.val_falsy[sh->pv[at]] & 2) {
+          v = nanv;
+        } else {
+          const uint32_t pv0 = sh->pv[at], n = tab ? U(T[1]) : 0u;
+          uint32_t r = MTB_NONE;
+          for (uint32_t base = 0; base < n && r == MTB_NONE; base += 64) {
+            const uint32_t i = base + (uint32_t)lane;
+            const unsigned long long m = __ballot(i < n && T[2 + 2 * i] == pv0);
+            if (m) r = U(T[3 + 2 * (base + (uint32_t)first_set(m))]);
+          }
+          if (r == MTB_NONE) { fail(DERR_INCR); return 0; }
+          v = r;
+        }
       } else if (COLD(comb == 3)) {
         // consensus (properties.ts:46-62): a present value stays -- unless it is an object whose seq is -1,
         // completed in place by the reference (shared with split clones): refused; an absent one takes the

@@ -614,14 +614,15 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
 
 
 def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello incr world", p_incr=0.15,
-                  p_rewrite=0.0):
+                  p_rewrite=0.0, string_incr=False):
     """A sequenced op log whose annotates are partly combiningOp "incr" annotates (segmentPropertiesManager.ts:
     145-147 -> combine(op, previous, undefined) of properties.ts:24-69): numeric keys "n" / "m" (incr makes
     them NaN, JSON null, never matchProperties-equal), a string key "s" that incr never names, null deletes,
     some incr ops with a numeric defaultValue / minValue; inserts with props, removes.  With `p_rewrite` that
     fraction of the annotates are combiningOp "rewrite" annotates (falsy values -- 0, "", null -- delete or
     re-append keys, :107-154).  Every message is applied to a generator oracle as it is made.  Returns
-    (initial text, messages)."""
+    (initial text, messages).  With `string_incr` incr annotates also name the string key "s" (string
+    concatenation: s + "undefined", then a string minValue when larger) and take string defaultValues."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -664,7 +665,12 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
                     comb["defaultValue"] = rng.randint(0, 3)
                 elif r < 0.3:
                     comb["minValue"] = 1
-                op = {"type": 2, "pos1": a, "pos2": b, "props": {rng.choice(["n", "m"]): rng.randint(1, 3)},
+                elif string_incr and r < 0.45:
+                    comb["defaultValue"] = rng.choice(["d", "zz", ""])
+                elif string_incr and r < 0.6:
+                    comb["minValue"] = rng.choice(["b", "bundefined", "zz"])
+                keys = ["n", "m", "s"] if string_incr else ["n", "m"]
+                op = {"type": 2, "pos1": a, "pos2": b, "props": {rng.choice(keys): rng.randint(1, 3)},
                       "combiningOp": comb}
             else:
                 props = rng.choice([{"n": rng.randint(0, 2)}, {"m": rng.randint(0, 2), "s": "w"}, {"n": None},

@@ -88,14 +88,16 @@ def test_host_incr_packing():
     B[0].applyMsg(msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1}, "combiningOp": {"name": "incr"}}))
     B[0].applyMsg(msg("a", 3, 2, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
                                   "combiningOp": {"name": "incr", "defaultValue": 4, "minValue": 2}}))
-    with pytest.raises(MergeTreeError, match="non-numeric defaultValue"):
-        B[0].applyMsg(msg("a", 4, 3, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
-                                      "combiningOp": {"name": "incr", "defaultValue": "x"}}))
     B[0].applyMsg(msg("a", 4, 3, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
+                                  "combiningOp": {"name": "incr", "defaultValue": "x"}}))  # (a string result)
+    with pytest.raises(MergeTreeError, match="object defaultValue"):
+        B[0].applyMsg(msg("a", 5, 4, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
+                                      "combiningOp": {"name": "incr", "defaultValue": {"a": 1}}}))
+    B[0].applyMsg(msg("a", 5, 4, {"type": 2, "pos1": 0, "pos2": 2, "props": {"n": 1},
                                   "combiningOp": {"name": "consensus"}}))
     import struct
     ob, n, _ = B.export_pending(0)
     t, fl = struct.unpack_from("<BB", ob, 32)
     assert t == 2 and fl & 0x0C == 0x08  # MTB_F_INCR
-    t, fl = struct.unpack_from("<BB", ob, 32 * 3)
+    t, fl = struct.unpack_from("<BB", ob, 32 * 4)
     assert t == 2 and fl & 0x0C == 0x0C  # MTB_F_CONSENSUS
