@@ -51,8 +51,11 @@ enum {
   MTB_F_COMB = 0x0C,    /* annotate: the combiningOp kind, a 2-bit field (compare masked: (flags & MTB_F_COMB)) */
   MTB_F_REWRITE = 0x04, /*   {name:"rewrite"} (segmentPropertiesManager.ts:107-123) */
   MTB_F_INCR = 0x08,    /*   {name:"incr"}: every key of props becomes combine(op, previous, undefined)
-                             (properties.ts:24-69), NaN for numeric / boolean / absent previous values */
-  MTB_F_CONSENSUS = 0x0C, /* {name:"consensus"}: combine(op, previous, undefined, seq) (properties.ts:46-62) */
+                             (properties.ts:24-69): NaN for numeric / boolean / absent previous values, a string
+                             gets "undefined" appended (records carry no defaultValue / minValue: the JSON
+                             path, mtb_apply_msg_json, takes them from the op) */
+  MTB_F_CONSENSUS = 0x0C, /* {name:"consensus"}: combine(op, previous, undefined, seq) (properties.ts:46-62) for
+                             a sequenced op: an absent key gets {value: undefined, seq}, a present one stays */
   MTB_F_SEGOBJ = 0x08,  /* insert: seg given as {text, props?} object (props id may be 0) */
   MTB_F_PERMSEG = 0x40, /* insert (matrix batches): PermutationSegment [length, start], pos2 = length */
   MTB_F_DELTA = 0x80    /* record the op's delta ranges (catch-up rewriting, MTB_BATCH_CATCHUP) */
