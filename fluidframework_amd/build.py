@@ -34,7 +34,10 @@ BUILD_ID_TAG = b"MTB_SOURCE_SHA256="
 
 # the kernel file is compiled once per kernel group (mtb_replay.hip MTB_TU_*), in parallel with the host
 # sources
-KERNEL_GROUPS = (1, 2, 3, 4, 5)
+KERNEL_GROUPS = (1, 2, 3, 4, 5, 6)
+# per-group code-generation flags: the few-document kernel (group 6: one wave per document, nothing to hide
+# its latency) schedules for ILP (cfg4 +2.8 % in a same-box A/B; the batch kernels lose 0.3 % with it)
+GROUP_FLAGS = {6: ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]}
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 
 
@@ -63,7 +66,8 @@ def _base_flags(arch, defines, extra):
 
 def source_id(arch="gfx950", defines=(), extra=()):
     """The hash build() embeds in the library it makes from the current sources and flags."""
-    return _digest(SRCS + _headers(), _base_flags(arch, defines, extra))
+    flags = _base_flags(arch, defines, extra) + [f"{g}:{' '.join(f)}" for g, f in sorted(GROUP_FLAGS.items())]
+    return _digest(SRCS + _headers(), flags)
 
 
 def embedded_id(path=OUT):
@@ -98,7 +102,7 @@ def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
     hip = SRCS[0]
     for g in KERNEL_GROUPS:
         o = os.path.join(odir, f"mtb_replay_tu{g}.o")
-        jobs.append((o, base + [f"-DMTB_TU={g}", "-c", hip, "-o", o], [hip]))
+        jobs.append((o, base + GROUP_FLAGS.get(g, []) + [f"-DMTB_TU={g}", "-c", hip, "-o", o], [hip]))
     for src in SRCS[1:]:
         o = os.path.join(odir, os.path.basename(src) + ".o")
         jobs.append((o, base + ["-c", src, "-o", o], [src]))

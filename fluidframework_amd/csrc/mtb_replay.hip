@@ -45,6 +45,7 @@
 #define MTB_TU_MARKERS 3  // marker ids / relative positions
 #define MTB_TU_LOADMAT 4  // SnapshotV1 body load, SharedMatrix
 #define MTB_TU_MISC 5     // digest, rewind, moves, launch dispatch
+#define MTB_TU_FEW 6      // the few-document kernel (its own code-generation flags, build.py GROUP_FLAGS)
 
 namespace mtbk {
 // matchProperties(va, vb) (properties.ts:84-92) of two values of key k, with irregular keys in the batch
@@ -4441,6 +4442,8 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
   if (U(sched[MTB_SCHED_ABORT]) == 0) return;
   replay_doc<MODE_REPLAY>(sh, blockIdx.x, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables);
 }
+#endif
+#if MTB_TU_HAS(MTB_TU_FEW)
 // The same engine for batches of few documents (at most a few per CU, e.g. BASELINE configs[3]'s single
 // long document): LDS is not what limits occupancy there, so the zamboni LRU heap keeps up to 2,047
 // entries in LDS instead of spilling to HBM past 127.
@@ -4514,12 +4517,19 @@ hipError_t mtb_launch_load(hipStream_t stream, uint32_t ndocs, DocState* docs, c
 #endif
 #define KPARAMS hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops, uint32_t* segp, FBlk* blks, \
                 WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables
+#if MTB_TU_HAS(MTB_TU_FEW)
+hipError_t mtb_launch_few(KPARAMS) {
+  hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+  return hipGetLastError();
+}
+#endif
 #if MTB_TU_HAS(MTB_TU_OBS)
 // Up to MTB_FEW_DOCS documents (at most ~4 per CU) replay on the large-LDS-heap variant.
 #define MTB_FEW_DOCS 1024
+hipError_t mtb_launch_few(KPARAMS);
 hipError_t mtb_launch_observer(KPARAMS) {
   if (ndocs <= MTB_FEW_DOCS)
-    hipLaunchKernelGGL(mtb_replay_few_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
+    return mtb_launch_few(stream, ndocs, docs, ops, segp, blks, lists, text, heap, aux, freel, tables);
   else
     hipLaunchKernelGGL(mtb_replay_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS);
   return hipGetLastError();
