@@ -64,9 +64,10 @@ def _base_flags(arch, defines, extra):
         [f"-D{d}" for d in defines] + list(extra)
 
 
-def source_id(arch="gfx950", defines=(), extra=()):
+def source_id(arch="gfx950", defines=(), extra=(), group_flags=None):
     """The hash build() embeds in the library it makes from the current sources and flags."""
-    flags = _base_flags(arch, defines, extra) + [f"{g}:{' '.join(f)}" for g, f in sorted(GROUP_FLAGS.items())]
+    gf = GROUP_FLAGS if group_flags is None else group_flags
+    flags = _base_flags(arch, defines, extra) + [f"{g}:{' '.join(f)}" for g, f in sorted(gf.items())]
     return _digest(SRCS + _headers(), flags)
 
 
@@ -88,12 +89,16 @@ def needs_build(out=OUT, arch="gfx950", defines=(), extra=()):
     return embedded_id(out) != source_id(arch, defines, extra)
 
 
-def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
-    sid = source_id(arch, defines, extra)
+def build(force=False, arch="gfx950", out=OUT, defines=(), extra=(), group_flags=None):
+    """group_flags: per-kernel-group flags instead of GROUP_FLAGS (measurement variants)."""
+    gf = GROUP_FLAGS if group_flags is None else group_flags
+    sid = source_id(arch, defines, extra, gf)
     if not force and embedded_id(out) == sid:
         return out
     from concurrent.futures import ThreadPoolExecutor
     tag = "_".join([d.replace("=", "") for d in defines] + [x.strip("-").replace("-", "") for x in extra]) or "base"
+    if group_flags is not None:
+        tag += "_g" + "_".join(f"{g}" + "".join(c for c in " ".join(f) if c.isalnum()) for g, f in sorted(gf.items()))
     odir = os.path.join(OBJ_DIR, f"{arch}_{tag}")
     os.makedirs(odir, exist_ok=True)
     base = _base_flags(arch, defines, extra)
@@ -102,7 +107,7 @@ def build(force=False, arch="gfx950", out=OUT, defines=(), extra=()):
     hip = SRCS[0]
     for g in KERNEL_GROUPS:
         o = os.path.join(odir, f"mtb_replay_tu{g}.o")
-        jobs.append((o, base + GROUP_FLAGS.get(g, []) + [f"-DMTB_TU={g}", "-c", hip, "-o", o], [hip]))
+        jobs.append((o, base + gf.get(g, []) + [f"-DMTB_TU={g}", "-c", hip, "-o", o], [hip]))
     for src in SRCS[1:]:
         o = os.path.join(odir, os.path.basename(src) + ".o")
         jobs.append((o, base + ["-c", src, "-o", o], [src]))
