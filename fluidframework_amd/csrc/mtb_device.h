@@ -218,7 +218,8 @@ struct Tables {
   uint32_t mk_key;           // key id of "markerId" (MTB_NONE: no property set names it)
   uint32_t nan_val;          // value id of NaN (incr annotates; MTB_NONE: none packed); val_falsy bit 1 marks
                              // the values that incr turns into NaN (numbers, booleans, NaN); bit 2 objects whose
-                             // seq is -1 (a consensus annotate completes them in place)
+                             // seq is -1 (a consensus annotate completes them in place); bit 3 values a set holding
+                             // one of which matches no set (NaN, consensus values: MTB_PNAN handles)
   // matchProperties of keys whose values are no equivalence (mtb_host.cpp Interner): key_irr[k] = 1 + offset
   // of [n, n x n bits] in irr (0: regular key, compare val_class); bit (i * n + j) = matchProperties(v_i, v_j)
   // for the key's values of local index i (first argument) and j (val_local)

@@ -175,6 +175,10 @@ struct Interner {
   std::vector<uint32_t> valLocal;                          // value -> index in its key's list
   std::vector<hj::Value> valStore;
   uint32_t nIrr = 0;
+  // consensus values ({value: undefined, seq}) are matched by nothing as the second argument, and as the first
+  // only by a two-key object {value: null | {} | [], seq: <that seq>} ("cv-like"): such values are refused on a
+  // key that holds consensus values, so a set holding one matches no set (valFalsy bit 3, like NaN)
+  std::vector<uint8_t> keyCv, keyCvLike;
 
   uint32_t key(const U16& k) {
     auto it = keyId.find(k);
@@ -188,6 +192,8 @@ struct Interner {
     keyRank.push_back(hj::array_index(k, &r) ? r : MTB_NONE);
     keyPaths.emplace_back();
     keyIrr.push_back(0);
+    keyCv.push_back(0);
+    keyCvLike.push_back(0);
     keyVals.emplace_back();
     irrRows.emplace_back();
     dirty = true;
@@ -249,10 +255,28 @@ struct Interner {
       for (auto& e : v.members) step(e.first, e.second);
     }
   }
-  // `js`: the JSON the summaries write for the value (JSON.stringify drops undefined members)
-  uint32_t add_value(uint32_t k, const std::string& idKey, const std::string& js, const hj::Value& v) {
+  static bool cv_like(const hj::Value& v) {
+    if (v.kind != hj::Value::kObj || v.members.size() != 2) return false;
+    const hj::Value* val = v.find(u"value");
+    const hj::Value* sq = v.find(u"seq");
+    if (!val || !sq || sq->kind != hj::Value::kNum) return false;
+    return val->kind == hj::Value::kNull || (val->kind == hj::Value::kObj && val->members.empty()) ||
+           (val->kind == hj::Value::kArr && val->items.empty());
+  }
+  // `js`: the JSON the summaries write for the value (JSON.stringify drops undefined members); `cv`: a consensus
+  // value (no paths noted: it never makes its key irregular)
+  uint32_t add_value(uint32_t k, const std::string& idKey, const std::string& js, const hj::Value& v, bool cv = false) {
     std::string path;
-    note_paths(k, v, path);
+    if (cv) {
+      if (keyCvLike[k]) raise(MTB_E_UNSUPPORTED, "unsupported: consensus on a key holding a {value, seq} object value");
+      keyCv[k] = 1;
+    } else {
+      if (cv_like(v)) {
+        if (keyCv[k]) raise(MTB_E_UNSUPPORTED, "unsupported: a {value, seq} object value on a key holding consensus values");
+        keyCvLike[k] = 1;
+      }
+      note_paths(k, v, path);
+    }
     std::string c = std::to_string(k) + ":";
     canon(c, v);
     auto ci = classId.find(c);
@@ -271,7 +295,7 @@ struct Interner {
     // object whose seq is -1 (consensus completes it in place, properties.ts:56-60)
     const hj::Value* sq = v.kind == hj::Value::kObj ? v.find(u"seq") : nullptr;
     valFalsy.push_back((v.truthy() ? 0 : 1) | (v.kind == hj::Value::kNum || v.kind == hj::Value::kBool ? 2 : 0) |
-                       (sq && sq->kind == hj::Value::kNum && sq->n == -1 ? 4 : 0));
+                       (sq && sq->kind == hj::Value::kNum && sq->n == -1 ? 4 : 0) | (cv ? 8 : 0));
     valLocal.push_back((uint32_t)keyVals[k].size());
     keyVals[k].push_back(id);
     valStore.push_back(v);
@@ -301,7 +325,8 @@ struct Interner {
     sv.kind = hj::Value::kNum;
     sv.n = seq;
     v.members.push_back({u"seq", sv});
-    return add_value(k, idKey, "{\"seq\":" + std::to_string(seq) + "}", v);
+    nan();  // (the device's no-match check on new sets runs once a NaN value exists)
+    return add_value(k, idKey, "{\"seq\":" + std::to_string(seq) + "}", v, true);
   }
   // matchProperties(value a, value b) of two values of key k (properties.ts:84-92)
   bool value_match(uint32_t k, uint32_t a, uint32_t b) {
@@ -429,7 +454,7 @@ struct Interner {
     const uint32_t cls = (uint32_t)classId.size();
     classId["\x01NaN"] = cls;
     valClass.push_back(cls);
-    valFalsy.push_back(1 | 2);
+    valFalsy.push_back(1 | 2 | 8);
     valLocal.push_back(MTB_NONE);
     valStore.push_back(hj::Value());
     dirty = true;
@@ -2424,9 +2449,9 @@ void props_json(mtb_dev* b, std::string& o, PropView v) {
 // matchProperties(a, c) (properties.ts:71-96): a is the run head's set
 bool props_match(mtb_dev* b, PropView a, PropView c) {
   if (a.n() != c.n()) return false;
-  if (b->in.nanVal != MTB_NONE)  // NaN !== NaN: a set holding NaN matches nothing
+  if (b->in.nanVal != MTB_NONE)  // NaN !== NaN, consensus values: a set holding one matches nothing
     for (uint32_t i = 0; i < a.n(); i++)
-      if (a.p[2 + 2 * i] == b->in.nanVal || c.p[2 + 2 * i] == b->in.nanVal) return false;
+      if ((b->in.valFalsy[a.p[2 + 2 * i]] & 8) || (b->in.valFalsy[c.p[2 + 2 * i]] & 8)) return false;
   for (uint32_t i = 0; i < a.n(); i++) {
     bool found = false;
     for (uint32_t q = 0; q < c.n(); q++) {

@@ -2586,9 +2586,9 @@ struct Eng {
       aux[h + 2 + 2 * i] = sh->pv[i];
     }
     const uint32_t nanv = U(sh->tab.nan_val);
-    if (COLD(nanv != MTB_NONE)) {  // a set holding NaN matches nothing: its handle says so
+    if (COLD(nanv != MTB_NONE)) {  // a set holding NaN or a consensus value matches nothing: its handle says so
       bool hasNan = false;
-      for (uint32_t i = lane; i < n; i += 64) hasNan |= sh->pv[i] == nanv;
+      for (uint32_t i = lane; i < n; i += 64) hasNan |= (sh->tab.val_falsy[sh->pv[i]] & 8) != 0;
       if (__ballot(hasNan)) h |= MTB_PNAN;
     }
     wsync();

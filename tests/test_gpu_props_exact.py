@@ -124,3 +124,42 @@ def test_property_logs_through_a_summary(new_mode):
     assert st["errors"] == 0, st
     for i, o in enumerate(orc):
         _same(B, i, o, f"log {i}")
+
+
+def test_many_consensus_values_in_one_batch():
+    """Every remote consensus annotate makes a new value per key ({value: undefined, seq}); a batch of many
+    documents holds thousands under one key.  They never make the key irregular (their sets match nothing,
+    MTB_PNAN), so no pair table grows with them."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    from test_reference_kats import msg
+    import random
+    n = 24
+    B = MergeTreeBatch(n)
+    orc = []
+    for i in range(n):
+        rng = random.Random(900 + i)
+        o = OracleDoc()
+        B[i].insertTextLocal(0, "consensus " * 8)
+        o.insert_text_local(0, "consensus " * 8)
+        B[i].startOrUpdateCollaboration("obs")
+        o.start_collab("obs")
+        length = 80
+        for s in range(1, 301):
+            a = rng.randrange(length - 1)
+            if rng.random() < 0.7:
+                op = {"type": 2, "pos1": a, "pos2": min(length, a + rng.randint(1, 6)), "props": {"c": 1},
+                      "combiningOp": {"name": "consensus"}}
+            elif rng.random() < 0.5:
+                op = {"type": 0, "pos1": a, "seg": rng.choice(["ab", "c"])}
+                length += len(op["seg"])
+            else:
+                op = {"type": 2, "pos1": a, "pos2": a + 1, "props": {"c": rng.choice([1, None, "z"])}}
+            m = msg(f"client-{s % 3}", s, s - 1 - rng.randint(0, 3) if s > 4 else s - 1, op, msn=max(0, s - 6))
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        orc.append(o)
+    st = B.flush()
+    assert st["errors"] == 0, st
+    for i, o in enumerate(orc):
+        _same(B, i, o, f"doc {i}")

@@ -47,3 +47,20 @@ def test_consensus_values_coalesce_after_a_summary_round_trip():
     p.load_v1(blobs, "obs2")
     segs = json.loads(p.summarize_v1()["blobs"][0][1])["segments"]
     assert {"text": "cd", "props": {"k": {"seq": 2}}} in segs
+
+
+def test_consensus_beside_cv_like_values_is_refused_at_apply():
+    """A set holding a consensus value matches nothing (like NaN) -- exact as long as its key never holds a
+    two-key {value: null | {} | [], seq} object, the one shape matchProperties(cv, y) can accept: that pairing
+    is refused, in either order."""
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    from test_reference_kats import msg
+    cons = {"type": 2, "pos1": 0, "pos2": 1, "props": {"c": 1}, "combiningOp": {"name": "consensus"}}
+    like = {"type": 0, "pos1": 0, "seg": {"text": "x", "props": {"c": {"value": None, "seq": 4}}}}
+    for first, second in ((like, cons), (cons, like)):
+        B = MergeTreeBatch(1)
+        B[0].insertTextLocal(0, "abc")
+        B[0].startOrUpdateCollaboration("obs")
+        B[0].applyMsg(msg("a", 1, 0, first))
+        with pytest.raises(MergeTreeError, match=r"\{value, seq\}"):
+            B[0].applyMsg(msg("a", 2, 1, second))
