@@ -22,6 +22,7 @@
 #define MTB_UNDEF (-1)
 #define MTB_MARKER 0x80000000u  // Seg.text flag: marker, low bits = refType + 1 (0 = undefined)
 #define MTB_GPROPS 0x80000000u  // props handle flag: batch-global table (else per-doc aux arena)
+#define MTB_NAN_CV 0x80000000u  // Tables::nan_val flag: consensus values (no-match values besides NaN) exist
 #define MTB_INCR_TAB 0x80000000u  // an incr annotate's op-props value: pool offset of its result table
                                   // [absent result, n, (string value, result) * n] (Interner::incr_props)
 #define MTB_PNAN 0x40000000u    // props handle flag of a per-doc set holding NaN (an incr annotate): such a set
@@ -216,7 +217,8 @@ struct Tables {
   uint32_t* delta;           // catch-up delta pool (per-document slices at DocState.delta_base, 4 words/entry)
   uint32_t class_trivial;    // every matchProperties class holds one value id: classes compare as value ids
   uint32_t mk_key;           // key id of "markerId" (MTB_NONE: no property set names it)
-  uint32_t nan_val;          // value id of NaN (incr annotates; MTB_NONE: none packed); val_falsy bit 1 marks
+  uint32_t nan_val;          // value id of NaN (incr annotates; MTB_NONE: none packed), | MTB_NAN_CV when consensus
+                             // values exist; val_falsy bit 1 marks
                              // the values that incr turns into NaN (numbers, booleans, NaN); bit 2 objects whose
                              // seq is -1 (a consensus annotate completes them in place); bit 3 values a set holding
                              // one of which matches no set (NaN, consensus values: MTB_PNAN handles)

@@ -326,6 +326,7 @@ struct Interner {
     sv.n = seq;
     v.members.push_back({u"seq", sv});
     nan();  // (the device's no-match check on new sets runs once a NaN value exists)
+    anyCv = true;
     return add_value(k, idKey, "{\"seq\":" + std::to_string(seq) + "}", v, true);
   }
   // matchProperties(value a, value b) of two values of key k (properties.ts:84-92)
@@ -447,6 +448,7 @@ struct Interner {
   // NaN, the value an incr annotate gives a numeric key: JSON null (JSON.stringify), its own matchProperties
   // class; a set holding it is flagged MTB_PNAN by the device and matches nothing (NaN !== NaN)
   uint32_t nanVal = MTB_NONE;
+  bool anyCv = false;  // consensus values interned (Tables::nan_val | MTB_NAN_CV)
   uint32_t nan() {
     if (nanVal != MTB_NONE) return nanVal;
     nanVal = (uint32_t)valJson.size();
@@ -1736,7 +1738,7 @@ Tables make_tables(mtb_dev* b) {
   t.pidx = b->dPidx.p;
   t.val_class = b->dValClass.p;
   t.val_falsy = b->dValFalsy.p;
-  t.nan_val = b->in.nanVal;
+  t.nan_val = b->in.nanVal == MTB_NONE ? MTB_NONE : b->in.nanVal | (b->in.anyCv ? MTB_NAN_CV : 0u);
   t.key_rank = b->dKeyRank.p;
   t.key_irr = b->dKeyIrr.p;
   t.val_local = b->dValLocal.p;

@@ -2512,7 +2512,7 @@ struct Eng {
         // incr: combine(op, previous, undefined) (properties.ts:24-69) -- previous + undefined is NaN for numbers /
         // booleans / NaN; a string's result (s + "undefined", minValue) and the absent key's come from the op's
         // table (Interner::incr_props); an object or array is not restated
-        const uint32_t nanv = U(sh->tab.nan_val);
+        const uint32_t nanv = U(sh->tab.nan_val) & ~MTB_NAN_CV;
         const auto T = UP(sh->tab.pool) + (v & ~MTB_INCR_TAB);
         const bool tab = (v & MTB_INCR_TAB) != 0 && v != MTB_NONE;
         if (at < 0) {
@@ -2585,10 +2585,12 @@ struct Eng {
       aux[h + 1 + 2 * i] = sh->pk[i];
       aux[h + 2 + 2 * i] = sh->pv[i];
     }
-    const uint32_t nanv = U(sh->tab.nan_val);
-    if (COLD(nanv != MTB_NONE)) {  // a set holding NaN or a consensus value matches nothing: its handle says so
+    const uint32_t nanw = U(sh->tab.nan_val);
+    if (COLD(nanw != MTB_NONE)) {  // a set holding NaN or a consensus value matches nothing: its handle says so
       bool hasNan = false;
-      for (uint32_t i = lane; i < n; i += 64) hasNan |= (sh->tab.val_falsy[sh->pv[i]] & 8) != 0;
+      for (uint32_t i = lane; i < n; i += 64) hasNan |= sh->pv[i] == (nanw & ~MTB_NAN_CV);
+      if (COLD(nanw & MTB_NAN_CV))  // consensus values exist: every no-match value (val_falsy bit 3)
+        for (uint32_t i = lane; i < n; i += 64) hasNan |= (sh->tab.val_falsy[sh->pv[i]] & 8) != 0;
       if (__ballot(hasNan)) h |= MTB_PNAN;
     }
     wsync();
