@@ -30,7 +30,8 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
 
 class MtbLaunchInfo(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_uint32), ("wave_slots", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
-                ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("passes", ctypes.c_uint32)]
+                ("queues", ctypes.c_uint32), ("aborted", ctypes.c_uint32), ("passes", ctypes.c_uint32),
+                ("handover_bad", ctypes.c_uint32), ("cap_retries", ctypes.c_uint32)]
 
 
 KERNEL_NAMES = {0: None, 1: "mtb_replay_kernel", 3: "mtb_replay_few_kernel",

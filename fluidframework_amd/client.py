@@ -283,11 +283,13 @@ class MergeTreeBatch:
         return list(arr[:n])
 
     def launch_info(self):
-        """What the last replay launched: {"kernel": name, "wave_slots", "chunks", "queues", "aborted", "passes"}."""
+        """What the last replay launched: {"kernel": name, "wave_slots", "chunks", "queues", "aborted", "passes",
+        "handover_bad", "cap_retries"}."""
         li = _lib.MtbLaunchInfo()
         self._chk(self._L.mtb_get_launch_info(self._h, ctypes.byref(li)))
         return {"kernel": _lib.KERNEL_NAMES.get(li.kernel), "wave_slots": li.wave_slots, "chunks": li.chunks,
-                "queues": li.queues, "aborted": bool(li.aborted), "passes": li.passes}
+                "queues": li.queues, "aborted": bool(li.aborted), "passes": li.passes,
+                "handover_bad": li.handover_bad, "cap_retries": li.cap_retries}
 
     def map_range(self, doc, start=0, end=-1, ref_seq=-1, long_client_id=None, limit=0):
         """mapRange / nodeMap (mergeTree.ts:2456, 2531) over [start, end) in the (ref_seq, client) view

@@ -11,7 +11,7 @@
 //   heap   : Lru  (8 B)   zamboni LRU heap         (reference: Heap<LRUSegment>, collections/heap.ts)
 //   aux    : u32          property sets and overlapping-remove client lists
 //   freel  : u32          free-block stack
-// A DocState header (384 B) holds each document's slice bases, bump pointers and collab window.
+// A DocState header (448 B) holds each document's slice bases, bump pointers and collab window.
 #pragma once
 #include <stdint.h>
 
@@ -267,6 +267,8 @@ struct Tables {
 #define MTB_SCHED_TICK 32
 #define MTB_SCHED_ABORT 256
 #define MTB_SCHED_SPINS 260  // mtb_replay_tick_kernel: the wait bound (spins), written by the host
+#define MTB_SCHED_BAD 264    // hand-over invariant violations (tick_check): count, then the first's document, chunk,
+                             // expected op_next, seen op_next
 #define MTB_SCHED_HDR 288
 
 #define DSF_NEWLINE 1      // the document's text arena may contain a newline (TextSegment.canAppend, textSegment.ts:71)

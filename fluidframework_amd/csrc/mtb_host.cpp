@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -747,6 +748,7 @@ struct mtb_dev {
   double lastKernelMs = 0;
   // rewind support: state right after the first upload of every document's records
   bool haveRewind = false;
+  bool tightCaps = false;  // slices sized by caps_for's tight formula (large batches; capacity retry in replay())
   std::vector<DocState> hPristine;
   DevBuf<DocState> dPristine;
   DevBuf<uint32_t> dPSeg;
@@ -757,10 +759,11 @@ struct mtb_dev {
   uint32_t waveSlots = 0;           // resident replay waves of the device (CUs x the sched kernel's occupancy)
   uint32_t nXcc = 0;                // XCDs of the device (the ticket scheduler's queues)
   mtb_launch_info launch{};         // what the last replay launched (mtb_launch_info)
-  uint32_t schedAbortHost = 0;
+  uint32_t schedWords[MTB_SCHED_BAD + 5 - MTB_SCHED_ABORT] = {};  // sched[MTB_SCHED_ABORT ..] after the launch
   uint32_t schedSpins = 0;  // (source of the wait bound's copy to the device)
   std::vector<uint32_t> schedPlan;  // the ticket scheduler's chunk plan (host copy of the uploaded one)
   Chunks pxSave[5], pxRestore[5];
+  std::vector<std::array<uint64_t, 10>> pxDoc;  // per document: dPX offset and words of each pool's saved image
   bool residentLoad = false;        // the resident records start with LOADSEG records
   bool live = false;                // a document of the batch has made local ops (mtb_local_op_json)
   bool matrix = false;              // MTB_BATCH_MATRIX: documents 2m / 2m+1 are matrix m's rows / cols
@@ -1507,12 +1510,30 @@ void parallel_docs(uint32_t n, F&& f) {
 struct Caps {
   uint32_t seg, blk, list, text, heap, aux;
 };
-Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
-  // Measured maxima: bench documents (10k records) 15.7k segments, 738 blocks, 3.8k list entries,
-  // 10.2k aux words; reference replay logs (2k records) 11.8k list entries, 21k aux words.  Segments can
-  // never exceed 2 per record (+ the initial one); the other slices keep several-fold headroom.
+// Two sizings.  Generous (batches whose slices take little HBM in total): several-fold headroom over the measured
+// maxima -- bench documents (10k records) 15.7k segments, 743 blocks, 4.4k list entries, 10.5k aux words; the
+// reference replay logs (2k records, long collab windows) 11.8k list entries, 21k aux words.  Tight (large batches,
+// mtb_dev::tightCaps): about twice the maxima measured per record on the bench workload (MTB_USAGE_OUT: blocks
+// 0.075, list entries 0.43, aux words 1.03, heap entries 0.014 per record), so 10,000 cfg2 documents take ~14 GiB
+// instead of 44; a document that outgrows them in its first replay is laid out again with larger slices and
+// replayed from its pristine state (replay(), "capacity retry"), so tight caps never change a result.  Segments
+// never exceed 2 per record (+ the initial one) in either sizing.
+double caps_scale() {  // MTB_CAPS_SCALE: scales the tight caps (tests force the capacity retry with small values)
+  const char* v = getenv("MTB_CAPS_SCALE");
+  return v ? std::max(0.0, atof(v)) : 1.0;
+}
+Caps caps_for(uint64_t n, uint64_t payload, uint64_t init, bool tight = false) {
   Caps c;
   c.seg = (uint32_t)(2 * n + 64);
+  if (tight) {
+    const double f = caps_scale();
+    c.blk = (uint32_t)std::max<double>(8, f * (double)(n / 8 + 128));
+    c.list = (uint32_t)std::max<double>(MTB_LIST_RESERVED + 16, f * (double)(n + 4096));
+    c.text = (uint32_t)std::min<uint64_t>(10 * payload + 15 * init + 4096, 0xFFFFFFF0u);
+    c.heap = (uint32_t)std::max<double>(4, f * (double)(n / 16 + 256));
+    c.aux = (uint32_t)std::max<double>(64, f * (double)(2 * n + 2048));
+    return c;
+  }
   c.blk = (uint32_t)(n / 2 + 256);
   c.list = (uint32_t)(8 * n + 8192);
   // text: scour's appends re-copy merged runs, so the arena outgrows the payload (cfg2 documents use ~5.7x their
@@ -1524,8 +1545,8 @@ Caps caps_for(uint64_t n, uint64_t payload, uint64_t init) {
   return c;
 }
 // caps_for plus what a loaded summary already occupies (header segments, blocks, lists, aux words)
-Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload) {
-  Caps c = caps_for(n, payload, d.initText.size());
+Caps doc_caps(const HostDoc& d, uint64_t n, uint64_t payload, bool tight = false) {
+  Caps c = caps_for(n, payload, d.initText.size(), tight);
   if (d.perm) c.text = (uint32_t)(2 * (d.totalSetcell + d.initText.size() / 2 + 4) + 64);  // the handle table (u32 words)
   if (d.loaded) {
     c.seg += (uint32_t)d.img.segp.size();
@@ -1606,9 +1627,19 @@ void device_init(mtb_dev* b) {
   ensure_stream(b);
   b->hst.assign(b->ndocs, DocState{});
   std::vector<Caps> want(b->ndocs);
+  // tight caps when the generous ones would take more than 8 GiB (MTB_CAPS=tight / generous forces either)
+  double gen = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
-    want[i] = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
+    const Caps c = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
+    gen += 4.0 * c.seg + (double)sizeof(FBlk) * c.blk + (double)sizeof(WEnt) * c.list + 2.0 * c.text +
+           (double)sizeof(Lru) * c.heap + 4.0 * c.aux + 4.0 * c.blk;
+  }
+  const char* cm = getenv("MTB_CAPS");
+  b->tightCaps = cm ? !strcmp(cm, "tight") : gen > 8.0 * (1ull << 30);
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    want[i] = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()), b->tightCaps);
   }
   layout(b, want);
   // initial state: root block (+ the detached initial text segment), collaboration started
@@ -1879,6 +1910,7 @@ std::string derr_text(int e) {
     case DERR_CAP_TEXT: return "capacity: text arena exhausted";
     case DERR_CAP_HEAP: return "capacity: LRU heap exhausted";
     case DERR_CAP_AUX: return "capacity: aux arena exhausted";
+    case DERR_CAP_DELTA: return "capacity: catch-up delta / cell-event slice exhausted";
     case DERR_ASSERT_SEQ: return "0x038 Incoming op sequence# < local collabWindow's currentSequence#";
     case DERR_ASSERT_MSN: return "0x04e/0x04f/0x039 minimum sequence number out of order";
     case DERR_DEPTH: return "tree depth limit exceeded";
@@ -1898,10 +1930,33 @@ std::string derr_text(int e) {
 }
 int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
-  if (e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) return MTB_E_CAPACITY;
+  if ((e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) || e == DERR_CAP_DELTA || e == DERR_CAP_PEND) return MTB_E_CAPACITY;
   if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN || e == DERR_ASSERT_MKID) return MTB_E_ASSERT;
   if (e == DERR_SCHED) return MTB_E_INTERNAL;
   return MTB_E_UNSUPPORTED;
+}
+
+// word offset of a document's slice in pool k of the pristine images (blks, segs, lists, aux, text as u32 words)
+uint64_t px_base(const DocState& s, int k) {
+  switch (k) {
+    case 0: return s.blk_base * (sizeof(FBlk) / 4);
+    case 1: return s.seg_base;
+    case 2: return s.list_base * (sizeof(WEnt) / 4);
+    case 3: return s.aux_base;
+    default: return s.text_base / 2;
+  }
+}
+// the pristine images' way back into the (current) slices
+void px_restore_chunks(mtb_dev* b, const std::vector<uint32_t>* only = nullptr) {
+  for (auto& c : b->pxRestore) c = Chunks{};
+  auto add = [&](uint32_t i) {
+    if (i >= b->pxDoc.size()) return;
+    for (int k = 0; k < 5; k++) b->pxRestore[k].add(b->pxDoc[i][k], px_base(b->hPristine[i], k), b->pxDoc[i][5 + k]);
+  };
+  if (only)
+    for (uint32_t i : *only) add(i);
+  else
+    for (uint32_t i = 0; i < b->ndocs; i++) add(i);
 }
 
 // Snapshot the freshly initialised documents (before their first replay) for mtb_rewind.
@@ -1922,23 +1977,24 @@ void capture_pristine(mtb_dev* b) {
   // documents loaded from a summary: their whole initial tree, window lists and overlap lists
   for (auto& c : b->pxSave) c = Chunks{};
   for (auto& c : b->pxRestore) c = Chunks{};
+  b->pxDoc.assign(b->ndocs, std::array<uint64_t, 10>{});
   uint64_t px = 0;
   for (uint32_t i = 0; i < b->ndocs; i++) {
     if (!b->docs[i].loaded && !b->docs[i].perm) continue;
     const DocState& s = b->hst[i];
     const bool ld = b->docs[i].loaded;
     // loaded documents: their whole initial tree; PermutationVectors: their handle table (text words)
-    const uint64_t base[5] = {s.blk_base * (sizeof(FBlk) / 4), s.seg_base, s.list_base * (sizeof(WEnt) / 4), s.aux_base,
-                              s.text_base / 2};
     const uint64_t len[5] = {ld ? (uint64_t)s.blk_used * (sizeof(FBlk) / 4) : 0, ld ? s.seg_used : 0,
                              ld ? (uint64_t)s.list_used * (sizeof(WEnt) / 4) : 0, ld ? s.aux_used : 0,
                              b->docs[i].perm ? s.text_used / 2 : 0};
     for (int k = 0; k < 5; k++) {
-      b->pxSave[k].add(base[k], px, len[k]);
-      b->pxRestore[k].add(px, base[k], len[k]);
+      b->pxSave[k].add(px_base(s, k), px, len[k]);
+      b->pxDoc[i][k] = px;
+      b->pxDoc[i][5 + k] = len[k];
       px += len[k];
     }
   }
+  px_restore_chunks(b);
   if (px) {
     b->dPX.ensure(px);
     void* pools[5] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p, b->dText.p};
@@ -1971,14 +2027,37 @@ void apply_cell_events(mtb_dev* b, uint32_t matrix);
 // the batch's replay kernel: matrix pairs, live clients (local ops anywhere in the batch so far), or the
 // observer replay engine
 // the scheduler's abort flag, copied back with the stream's next synchronization
+// (and the hand-over invariant's words: tick_check, mtb_replay.hip)
 void sched_readback(mtb_dev* b) {
-  b->schedAbortHost = 0;
+  std::fill(std::begin(b->schedWords), std::end(b->schedWords), 0u);
   if (b->launch.kernel == MTB_KERNEL_TICKS)
-    HIPCHK(hipMemcpyAsync(&b->schedAbortHost, b->dSched.p + MTB_SCHED_ABORT, sizeof(uint32_t), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(b->schedWords, b->dSched.p + MTB_SCHED_ABORT, sizeof b->schedWords, hipMemcpyDeviceToHost,
                           b->stream));
+}
+// after the stream synchronized: the abort flag and hand-over violations into the launch info
+void sched_result(mtb_dev* b) {
+  if (b->launch.kernel != MTB_KERNEL_TICKS) return;
+  const uint32_t* w = b->schedWords - MTB_SCHED_ABORT;
+  b->launch.aborted = w[MTB_SCHED_ABORT];
+  b->launch.handover_bad = w[MTB_SCHED_BAD];
+  if (w[MTB_SCHED_BAD])
+    fprintf(stderr,
+            "mtb: %u ticket hand-over(s) found a stale document state (first: document %u chunk %u, op_next %u expected "
+            "%u); those documents were finished by mtb_replay_finish_kernel\n",
+            w[MTB_SCHED_BAD], w[MTB_SCHED_BAD + 1], w[MTB_SCHED_BAD + 2], w[MTB_SCHED_BAD + 4], w[MTB_SCHED_BAD + 3]);
 }
 
 void launch_main(mtb_dev* b, const Tables& t) {
+  if (getenv("MTB_DEBUG_POOLS")) {  // (fault triage: the pools' address ranges, to place a faulting address)
+    const struct { const char* name; const void* p; size_t bytes; } pools[] = {
+        {"docs", b->dDocs.p, b->dDocs.n * sizeof(DocState)}, {"ops", b->dOps.p, b->dOps.n * sizeof(mtb_op)},
+        {"segs", b->dSegs.p, b->dSegs.n * 4}, {"blks", b->dBlks.p, b->dBlks.n * sizeof(FBlk)},
+        {"lists", b->dLists.p, b->dLists.n * sizeof(WEnt)}, {"text", b->dText.p, b->dText.n * 2},
+        {"heap", b->dHeap.p, b->dHeap.n * sizeof(Lru)}, {"aux", b->dAux.p, b->dAux.n * 4},
+        {"free", b->dFree.p, b->dFree.n * 4}, {"pool", t.pool, b->dPool.n * 4}, {"sched", b->dSched.p, b->dSched.n * 4}};
+    for (const auto& q : pools)
+      fprintf(stderr, "mtb_pool %-6s %p .. %p (%zu bytes)\n", q.name, q.p, (const void*)((const char*)q.p + q.bytes), q.bytes);
+  }
   if (b->matrix) {
     HIPCHK(mtb_launch_matrix(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
                              b->dHeap.p, b->dAux.p, b->dFree.p, t));
@@ -2074,7 +2153,7 @@ void launch_main(mtb_dev* b, const Tables& t) {
       // a wait bound far above any chunk (about a minute); MTB_SCHED_SPINS lowers it (tests force the abort)
       uint32_t spins = 1u << 27;
       if (const char* sp = getenv("MTB_SCHED_SPINS")) spins = (uint32_t)std::max(0L, std::min(1L << 30, atol(sp)));
-      const size_t nw = MTB_SCHED_HDR + (size_t)b->ndocs + nchunks;
+      const size_t nw = MTB_SCHED_HDR + 2 * (size_t)b->ndocs + nchunks;  // progress, plan, hand-over op_next
       b->dSched.ensure(nw);
       HIPCHK(hipMemsetAsync(b->dSched.p, 0, (MTB_SCHED_HDR + (size_t)b->ndocs) * sizeof(uint32_t), b->stream));
       b->schedPlan = plan;  // (kept alive until the stream has consumed the copies)
@@ -2095,6 +2174,91 @@ void launch_main(mtb_dev* b, const Tables& t) {
     b->launch.kernel = b->live ? MTB_KERNEL_LIVE : markers ? MTB_KERNEL_MARKERS
                        : b->ndocs <= 1024 ? MTB_KERNEL_FEW : MTB_KERNEL_REPLAY;
   }
+}
+
+// Capacity retry.  A document whose first replay overflowed one of its slices (DERR_CAP_*, never a result the
+// reference produces) is laid out again with that slice four times larger and replayed from its pristine state, up
+// to MTB_CAP_RETRIES (default 12) times; the other documents keep their state (layout() moves it) and have nothing left
+// to run.  Only documents whose pristine snapshot is their state before this replay qualify (`fresh`); any other
+// overflow stays a sticky MTB_E_CAPACITY.  Returns the number of relaunches.
+int capacity_retry(mtb_dev* b, bool anyLoad, const std::vector<uint8_t>& fresh) {
+  const char* rv = getenv("MTB_CAP_RETRIES");
+  const int maxTries = rv ? std::max(0, atoi(rv)) : 12;
+  int tries = 0;
+  for (; tries < maxTries; tries++) {
+    std::vector<uint32_t> redo;
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      const int e = b->hst[i].err;
+      if (fresh[i] && e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) redo.push_back(i);
+    }
+    if (redo.empty()) break;
+    if (getenv("MTB_TIMING"))
+      fprintf(stderr, "mtb_capacity_retry %d: %zu document(s), first %u (error %d, caps seg %u blk %u list %u text %u heap %u aux %u)\n",
+              tries, redo.size(), redo[0], b->hst[redo[0]].err, b->hst[redo[0]].seg_cap, b->hst[redo[0]].blk_cap,
+              b->hst[redo[0]].list_cap, b->hst[redo[0]].text_cap, b->hst[redo[0]].heap_cap, b->hst[redo[0]].aux_cap);
+    std::vector<Caps> want(b->ndocs, Caps{0, 0, 0, 0, 0, 0});
+    for (uint32_t i : redo) {
+      DocState& s = b->hst[i];
+      Caps c{s.seg_cap, s.blk_cap, s.list_cap, s.text_cap, s.heap_cap, s.aux_cap};
+      auto dbl = [](uint32_t& v) { v = (uint32_t)std::min<uint64_t>(4ull * v + 16, 0xFFFFFFF0u); };
+      switch (s.err) {
+        case DERR_CAP_SEG: dbl(c.seg); break;
+        case DERR_CAP_BLK: dbl(c.blk); dbl(c.heap); break;
+        case DERR_CAP_LIST: dbl(c.list); break;
+        case DERR_CAP_TEXT: dbl(c.text); break;
+        case DERR_CAP_HEAP: dbl(c.heap); break;
+        default: dbl(c.aux); break;
+      }
+      want[i] = c;
+      // layout() moves only the pristine prefix of a document that starts over
+      const DocState& p = b->hPristine[i];
+      s.seg_used = p.seg_used, s.blk_used = p.blk_used, s.list_used = p.list_used, s.text_used = p.text_used;
+      s.heap_cnt = p.heap_cnt, s.aux_used = p.aux_used, s.free_top = p.free_top;
+    }
+    layout(b, want);
+    // the pristine snapshot follows the new slices (rewind restores into them)
+    for (uint32_t i = 0; i < b->ndocs; i++) {
+      DocState& p = b->hPristine[i];
+      const DocState& s = b->hst[i];
+      p.seg_base = s.seg_base, p.blk_base = s.blk_base, p.list_base = s.list_base, p.text_base = s.text_base;
+      p.heap_base = s.heap_base, p.aux_base = s.aux_base, p.free_base = s.free_base;
+      p.seg_cap = s.seg_cap, p.blk_cap = s.blk_cap, p.list_cap = s.list_cap, p.text_cap = s.text_cap;
+      p.heap_cap = s.heap_cap, p.aux_cap = s.aux_cap;
+    }
+    HIPCHK(hipMemcpyAsync(b->dPristine.p, b->hPristine.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+    px_restore_chunks(b);
+    b->haveRewind = true;
+    // the documents that start over: pristine header, root block, initial segment and (loaded) initial tree
+    Chunks bc, sc;
+    for (uint32_t i : redo) {
+      const DocState& p = b->hPristine[i];
+      b->hst[i] = p;
+      b->docs[i].cached = false;
+      bc.add((uint64_t)i * (sizeof(FBlk) / 4), (p.blk_base + p.root) * (sizeof(FBlk) / 4), sizeof(FBlk) / 4);
+      sc.add(i, p.seg_base, 1);
+    }
+    HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
+    move_words(b, b->dPBlk.p, b->dBlks.p, bc);
+    move_words(b, b->dPSeg.p, b->dSegs.p, sc);
+    Chunks all[5];
+    for (int k = 0; k < 5; k++) all[k] = b->pxRestore[k];
+    px_restore_chunks(b, &redo);
+    void* pools[5] = {b->dBlks.p, b->dSegs.p, b->dLists.p, b->dAux.p, b->dText.p};
+    for (int k = 0; k < 5; k++) move_words(b, b->dPX.p, pools[k], b->pxRestore[k]);
+    for (int k = 0; k < 5; k++) b->pxRestore[k] = all[k];
+    const Tables t = make_tables(b);
+    if (anyLoad)
+      HIPCHK(mtb_launch_load(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                             b->dHeap.p, b->dAux.p, b->dFree.p, t, b->matrix ? 1 : 0));
+    launch_main(b, t);
+    sched_readback(b);
+    HIPCHK(hipMemcpyAsync(b->hst.data(), b->dDocs.p, b->ndocs * sizeof(DocState), hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    sched_result(b);
+    for (uint32_t i = 0; i < b->ndocs; i++)
+      if (!b->hst[i].err && b->hst[i].op_next != b->hst[i].n_ops) b->hst[i].err = DERR_SCHED;
+  }
+  return tries;
 }
 
 void replay(mtb_dev* b, mtb_stats* out) {
@@ -2127,11 +2291,11 @@ void replay(mtb_dev* b, mtb_stats* out) {
       const DocState& s = b->hst[i];
       // (the same requirement device_init laid the slices out for: caps_for's text term already counts the
       // initial text, so adding text_used here made every fresh batch re-lay out at twice the caps)
-      Caps need = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()));
+      Caps need = doc_caps(d, d.totalOps, std::max<uint64_t>(d.totalPayload, d.payload.size()), b->tightCaps);
       // ... and what the slices already hold plus the per-record margin for the pending records: a document can
       // outgrow the record-count formula (a live client holding thousands of unacked inserts keeps an entry per
       // insert in every ancestor's window list, and list rebuilds allocate before they free)
-      if (s.seg_cap) {
+      if (s.seg_cap && d.totalOps != d.pending.size()) {  // (a fresh document's slices are the formula's)
         // (caps_for's per-record terms without its constants, which the formula above already carries)
         const uint64_t np = d.pending.size();
         auto at_least = [](uint32_t& c, uint64_t v) { c = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, v), 0xFFFFFFF0u); };
@@ -2143,7 +2307,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
       }
       if (!fits(s, need) || s.text_used + d.payload.size() > s.text_cap ||
           (d.perm && 2 * (d.totalSetcell + d.initText.size() / 2 + 4) > s.text_cap)) {
-        want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used));
+        want[i] = doc_caps(d, 2 * d.totalOps, 2 * (d.totalPayload + s.text_used), b->tightCaps);
         auto twice = [](uint32_t& c, uint32_t v) { c = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, 2ull * v), 0xFFFFFFF0u); };
         twice(want[i].seg, need.seg);
         twice(want[i].blk, need.blk);
@@ -2231,16 +2395,26 @@ void replay(mtb_dev* b, mtb_stats* out) {
       } else if (!s.err) {
         // a marker-relative range is resolved on the device: bound it by the document's length, itself bounded
         // by the text and segments it holds plus what the records before it insert
-        uint64_t lenBound = (uint64_t)s.text_used + s.seg_used + 1;
+        // (a marker's pos2 is its refType, 0xFFFFFFFF when undefined: it adds 1).  A delta holds one entry per
+        // segment the record touches, so a range is also bounded by the segments the document can hold by then:
+        // those it holds plus two per record before it (the record's own boundary splits).
+        uint64_t lenBound = (uint64_t)s.text_used + s.seg_used + 1, segBound = (uint64_t)s.seg_used + 1;
         for (const mtb_op& o : b->docs[i].pending) {
-          if (o.type == MTB_OP_INSERT && !(o.flags & MTB_F_RELPOS)) lenBound += (o.flags & MTB_F_MARKER) ? 1 : o.pos2;
-          else if (o.type == MTB_OP_INSERT) lenBound += 1 + o.pos2;
-          const uint64_t range = (o.flags & MTB_F_RELPOS) ? lenBound : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0);
+          if (o.type == MTB_OP_INSERT) lenBound += (o.flags & MTB_F_MARKER) ? 1 : o.pos2;
+          segBound += 2;
+          const uint64_t range =
+              std::min((o.flags & MTB_F_RELPOS) ? lenBound : (o.pos2 > o.pos1 ? o.pos2 - o.pos1 : 0), segBound);
           if (o.flags & MTB_F_DELTA)  // (a rewrite annotate's segments get a second entry: the set before)
             cap += o.type == MTB_OP_INSERT ? 1
                    : (range + 1) * (o.type == MTB_OP_ANNOTATE && (o.flags & MTB_F_COMB) == MTB_F_REWRITE ? 2 : 1);
           if (o.type == MTB_OP_REGEN) cap += (uint64_t)o.pos1 * (s.seg_used + 16);  // one entry per regenerated op
         }
+      }
+      if (cap > 0xFFFFFFF0ull) {  // the device's cap is 32-bit: such a batch of lagging ops fails its document
+        s.err = DERR_CAP_DELTA;
+        s.err_op = 0;
+        s.n_ops = 0;
+        cap = 0;
       }
       s.delta_cap = (uint32_t)cap;
       tot += cap;
@@ -2253,7 +2427,14 @@ void replay(mtb_dev* b, mtb_stats* out) {
   if (nOps) HIPCHK(hipMemcpyAsync(b->dOps.p, ops.get(), nOps * sizeof(mtb_op), hipMemcpyHostToDevice, b->stream));
   HIPCHK(hipMemcpyAsync(b->dDocs.p, b->hst.data(), b->ndocs * sizeof(DocState), hipMemcpyHostToDevice, b->stream));
   pc.mark("upload");
-  if (!b->haveRewind) capture_pristine(b);
+  // documents whose pristine snapshot (taken now) is their state before this replay: the capacity retry's
+  std::vector<uint8_t> fresh(b->ndocs, 0);
+  if (!b->haveRewind) {
+    capture_pristine(b);
+    if (!b->matrix)
+      for (uint32_t i = 0; i < b->ndocs; i++)
+        fresh[i] = !failedBefore[i] && b->docs[i].totalOps == b->docs[i].pending.size() && b->hst[i].op_next == 0;
+  }
   pc.mark("pristine");
   const Tables t = make_tables(b);
   b->residentLoad = anyLoad;
@@ -2269,7 +2450,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->lastKernelMs = ms;
-  b->launch.aborted = b->launch.kernel == MTB_KERNEL_TICKS ? b->schedAbortHost : 0u;
+  sched_result(b);
   pc.mark("kernels");
   if (b->matrix)
     for (uint32_t i = 0; i + 1 < b->ndocs; i += 2) {
@@ -2280,6 +2461,14 @@ void replay(mtb_dev* b, mtb_stats* out) {
   // the rest): an engine invariant, checked
   for (uint32_t i = 0; i < b->ndocs; i++)
     if (!b->hst[i].err && b->hst[i].op_next != b->hst[i].n_ops) b->hst[i].err = DERR_SCHED;
+  if (getenv("MTB_TIMING")) {
+    uint32_t nf = 0, ne = 0;
+    for (uint32_t i = 0; i < b->ndocs; i++) nf += fresh[i], ne += b->hst[i].err != 0;
+    fprintf(stderr, "mtb_capacity: %u fresh documents, %u with errors, tight caps %d\n", nf, ne, (int)b->tightCaps);
+  }
+  const uint32_t retries = (uint32_t)capacity_retry(b, anyLoad, fresh);
+  b->launch.cap_retries = retries;
+  pc.mark("capacity retry");
   // the records are consumed now: whatever the host post-processing below does, they never run again
   for (uint32_t i = 0; i < b->ndocs; i++) {
     HostDoc& d = b->docs[i];
@@ -2331,6 +2520,30 @@ void replay(mtb_dev* b, mtb_stats* out) {
     }
   }
   run_digest(b, st);
+  if (getenv("MTB_USAGE_OUT")) {  // slice use against capacity per pool (max, 99th percentile, mean), for sizing caps
+    struct P { const char* name; uint32_t DocState::*used; uint32_t DocState::*cap; size_t bytes; };
+    const P pools[] = {{"segs", &DocState::seg_used, &DocState::seg_cap, 4}, {"blks", &DocState::blk_used, &DocState::blk_cap, sizeof(FBlk)},
+                       {"lists", &DocState::list_used, &DocState::list_cap, sizeof(WEnt)}, {"text", &DocState::text_used, &DocState::text_cap, 2},
+                       {"heap", &DocState::heap_cnt, &DocState::heap_cap, sizeof(Lru)}, {"aux", &DocState::aux_used, &DocState::aux_cap, 4}};
+    for (const P& q : pools) {
+      std::vector<double> u, f;
+      double capb = 0;
+      for (uint32_t i = 0; i < b->ndocs; i++) {
+        const DocState& s = b->hst[i];
+        const double ops = std::max<double>(1, (double)b->docs[i].totalOps);
+        u.push_back((double)(s.*q.used) / ops);
+        f.push_back((double)(s.*q.used) / std::max<double>(1, (double)(s.*q.cap)));
+        capb += (double)(s.*q.cap) * (double)q.bytes;
+      }
+      std::sort(u.begin(), u.end());
+      std::sort(f.begin(), f.end());
+      const size_t n = u.size();
+      if (!n) continue;
+      fprintf(stderr, "mtb_usage %-5s per record: max %.3f p99 %.3f mean %.3f | of cap: max %.3f p99 %.3f | cap %.1f MiB/doc\n",
+              q.name, u[n - 1], u[n * 99 / 100], std::accumulate(u.begin(), u.end(), 0.0) / n, f[n - 1], f[n * 99 / 100],
+              capb / n / 1048576.0);
+    }
+  }
   if (getenv("MTB_PROFILE_OUT")) {  // MTB_PROFILE builds: per-phase device cycles and events per op, summed over documents
     double p[11] = {0}, c[9] = {0};
     for (uint32_t i = 0; i < b->ndocs; i++) {
@@ -4038,7 +4251,7 @@ int mtbx_replay_resident(mtb_dev* b, mtb_stats* out, uint32_t flags) {
     HIPCHK(hipStreamSynchronize(b->stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    b->launch.aborted = b->launch.kernel == MTB_KERNEL_TICKS ? b->schedAbortHost : 0u;
+    sched_result(b);
     mtb_stats st{};
     st.kernel_ms = ms;
     uint32_t short_docs = 0;

@@ -400,6 +400,8 @@ int mtb_get_launch_info(mtb_batch* b, mtb_launch_info* out) {
     if (rc) return rc;
     if (s == 0) acc = x;
     acc.aborted |= x.aborted;
+    acc.handover_bad += x.handover_bad;
+    acc.cap_retries = std::max(acc.cap_retries, x.cap_retries);
   }
   *out = acc;
   return 0;

@@ -29,6 +29,9 @@
 //  * The zamboni LRU heap (collections/heap.ts) lives in LDS while it fits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <algorithm>
 
 #include "../../include/mtb.h"
 #include "mtb_device.h"
@@ -95,6 +98,16 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // (no instruction; it only stops the compiler from moving memory operations across it) is enough
 // to make one lane's store visible to another lane's later load of the same document state.
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// MTB_CRUMBS builds (fault triage only): every scheduled ticket leaves breadcrumbs in host-pinned memory, which the
+// host can still read after a device fault has killed the context: crumbs[d] = stage | chunk << 8 (1 ticket taken,
+// 2 replaying, 3 replayed, 4 progress published), crumbs[ndocs + d] = the record the document's wave is applying.
+#ifdef MTB_CRUMBS
+__device__ uint32_t* mtb_crumbs;
+#define CRUMB(i, v) \
+  do { if (lane_id() == 0) __hip_atomic_store(mtb_crumbs + (i), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+#else
+#define CRUMB(i, v) ((void)0)
+#endif
 
 // Cross-lane primitives.  Every scan / sum in this kernel runs over the <=8 children of one block,
 // i.e. lanes 0..7 of DPP row 0, so it is three DPP row_shr steps (plain VALU, no LDS round trip);
@@ -4114,13 +4127,14 @@ using namespace mtbk;
 #define MTB_WAVES_PER_SIMD 4
 #endif
 __device__ __forceinline__ uint32_t ds_word(uint32_t w0, uint32_t w1, uint32_t i) { return i < 64 ? rlu(w0, i) : rlu(w1, i - 64); }
+// Replays document `doc` from its op_next; returns the op_next it leaves (the record after the last one applied).
 template <int MODE, class SCR>
-__device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, int wv,
+__device__ __forceinline__ uint32_t replay_doc(SCR& sh, uint32_t doc, int32_t* xch, int wv,
                                            DocState* docs,  // (no __restrict__: see mtb_replay_tick_kernel)
                                            uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks, WEnt* lists,
                                            uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel,
                                            const Tables& tables, uint32_t upto = 0) {
-  if (doc >= ndocs) return;
+  if (doc >= ndocs) return 0;
   DocState* ds = &docs[doc];
   Eng<MODE, SCR> e;
   e.xch = xch;
@@ -4256,6 +4270,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
         if (cur.type != MTB_OP_LOADSEG) break;  // the summary body precedes every op
       }
       e.cur_k = k;
+      CRUMB(ndocs + doc, k);
       if constexpr (MODE == MODE_MATRIX) {
         if (cur.type == MTB_OP_SETCELL) {
           e.setcell(cur, par);
@@ -4336,6 +4351,7 @@ __device__ __forceinline__ void replay_doc(SCR& sh, uint32_t doc, int32_t* xch, 
     }
     ds->op_next = k;
   }
+  return k;
 }
 
 #define KARGS docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables
@@ -4381,7 +4397,8 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
 // document's state is consistent at its op_next).
 // sched: [32 q] next ticket of queue q (one line each), [MTB_SCHED_ABORT] abort flag, [MTB_SCHED_SPINS] the
 // wait bound, [MTB_SCHED_HDR + d] chunks of document d completed (zeroed before launch), [MTB_SCHED_HDR +
-// ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096).
+// ndocs + c] the plan: cumulative record fraction of chunk c in 1/4096 (the last one 4096), [MTB_SCHED_HDR + ndocs +
+// nchunks + d] the op_next document d's last completed chunk left (tick_check).
 //
 // (Rounds 2-3 ran the tickets on persistent waves, the engine a called function between them.  In round 4 that
 // kernel faulted in some builds; its replacement keeps the plain replay kernel's register allocation.  The
@@ -4406,6 +4423,27 @@ __device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* p
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one acquire per hand-over (the spin reads relaxed)
   return true;
 }
+// The hand-over invariant, checked at every chunk's entry after the acquire: the document's DocState is the one
+// the previous chunk left (its op_next equals the record index that chunk returned, published beside the progress
+// word).  A mismatch means this workgroup would resume from a stale state (round 4's scalar-cache fault had that
+// shape): the chunk is not run, the first mismatch is recorded ([MTB_SCHED_BAD] count, then document, chunk,
+// expected, seen) and the abort flag hands the rest to mtb_replay_finish_kernel, a new launch that reads every
+// DocState afresh.  Both words are read with agent-scope atomic loads (vector memory, never the scalar cache).
+__device__ __attribute__((noinline)) bool tick_check(uint32_t* sched, uint32_t* hand, uint32_t* opn, uint32_t d, uint32_t c) {
+  const uint32_t want = U(__hip_atomic_load(hand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t have = U(__hip_atomic_load(opn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (want == have) return true;
+  if (lane_id() == 0) {
+    if (atomicAdd(&sched[MTB_SCHED_BAD], 1u) == 0) {
+      __hip_atomic_store(&sched[MTB_SCHED_BAD + 1], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sched[MTB_SCHED_BAD + 2], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sched[MTB_SCHED_BAD + 3], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sched[MTB_SCHED_BAD + 4], have, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(&sched[MTB_SCHED_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return false;
+}
 extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     mtb_replay_tick_kernel(DocState* docs, uint32_t ndocs, const mtb_op* ops, uint32_t* segp, FBlk* blks,
                            WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux, uint32_t* freel, Tables tables,
@@ -4425,14 +4463,23 @@ extern "C" __global__ void __launch_bounds__(64, MTB_WAVES_PER_SIMD)
     d = (t - c * nqd) * nq + q;
   }
   if (d == MTB_NONE) return;
+  CRUMB(d, 1 | c << 8);
   if (U(__hip_atomic_load(&sched[MTB_SCHED_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0) return;
   uint32_t* prog = &sched[MTB_SCHED_HDR + d];
-  if (c > 0 && !tick_wait(sched, prog, c, U(sched[MTB_SCHED_SPINS]))) return;
-  replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel, tables,
-                          U(sched[MTB_SCHED_HDR + ndocs + c]));
+  uint32_t* hand = &sched[MTB_SCHED_HDR + ndocs + nchunks + d];  // op_next the previous chunk left
+  if (c > 0) {
+    if (!tick_wait(sched, prog, c, U(sched[MTB_SCHED_SPINS]))) return;
+    if (!tick_check(sched, hand, &docs[d].op_next, d, c)) return;
+  }
+  CRUMB(d, 2 | c << 8);
+  const uint32_t k = replay_doc<MODE_REPLAY>(sh, d, nullptr, 0, docs, ndocs, ops, segp, blks, lists, text, heap, aux, freel,
+                                             tables, U(sched[MTB_SCHED_HDR + ndocs + c]));
+  CRUMB(d, 3 | c << 8);
+  if (c + 1 < nchunks && lane_id() == 0) *hand = k;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X guide: the write-back completes before the flag)
   if (lane_id() == 0) __hip_atomic_store(prog, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  CRUMB(d, 4 | c << 8);
 }
 // After an aborted scheduled launch: every document continues from its op_next (one wave per document;
 // documents that finished have nothing left).  Without an abort every wave leaves at once.
@@ -4548,8 +4595,36 @@ int mtb_sched_waves_per_cu() {
 hipError_t mtb_launch_replay_ticks(hipStream_t stream, uint32_t ndocs, DocState* docs, const mtb_op* ops,
                                    uint32_t* segp, FBlk* blks, WEnt* lists, uint16_t* text, Lru* heap, uint32_t* aux,
                                    uint32_t* freel, Tables tables, uint32_t* sched, uint32_t nchunks, uint32_t nq) {
+#ifdef MTB_CRUMBS
+  static uint32_t* hc = nullptr;
+  static size_t hn = 0;
+  if (hn < 2 * (size_t)ndocs) {
+    if (hc) (void)hipHostFree(hc);
+    if (hipHostMalloc((void**)&hc, 2 * (size_t)ndocs * 4, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return hipErrorOutOfMemory;
+    hn = 2 * (size_t)ndocs;
+  }
+  memset(hc, 0, 2 * (size_t)ndocs * 4);
+  uint32_t* dc = nullptr;
+  (void)hipHostGetDevicePointer((void**)&dc, hc, 0);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(mtb_crumbs), &dc, sizeof dc);
+#endif
   hipLaunchKernelGGL(mtb_replay_tick_kernel, dim3(ndocs * nchunks), dim3(64), 0, stream, KARGS, sched, nchunks, nq);
   hipError_t e = hipGetLastError();
+#ifdef MTB_CRUMBS
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  {
+    uint32_t cnt[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < ndocs; i++) cnt[std::min<uint32_t>(hc[i] & 0xFF, 4)]++;
+    fprintf(stderr, "mtb_crumbs after the tick kernel (%s): stage 0 %u, 1 %u, 2 %u, 3 %u, 4 %u\n", hipGetErrorString(e), cnt[0],
+            cnt[1], cnt[2], cnt[3], cnt[4]);
+    uint32_t shown = 0;
+    for (uint32_t i = 0; i < ndocs; i++) {
+      const uint32_t st = hc[i] & 0xFF;
+      if ((st == 1 || st == 3 || (e != hipSuccess && st == 2)) && shown++ < 40)
+        fprintf(stderr, "mtb_crumbs doc %u stage %u chunk %u record %u\n", i, st, hc[i] >> 8, hc[ndocs + i]);
+    }
+  }
+#endif
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(mtb_replay_finish_kernel, dim3(ndocs), dim3(64), 0, stream, KARGS, (const uint32_t*)sched);
   return hipGetLastError();

@@ -145,6 +145,10 @@ typedef struct mtb_launch_info {
   uint32_t queues;      /* MTB_KERNEL_TICKS: ticket queues (one per XCD) */
   uint32_t aborted;     /* MTB_KERNEL_TICKS: a ticket wait hit its bound and the finish kernel ran the rest */
   uint32_t passes;      /* MTB_KERNEL_PASSES: kernel launches of the replay */
+  uint32_t handover_bad; /* MTB_KERNEL_TICKS: tickets that found their document's state not the one the previous
+                            chunk left (never expected; such documents are finished by a fresh launch) */
+  uint32_t cap_retries;  /* relaunches of the last mtb_replay's capacity retry (documents whose first replay outgrew
+                            their slices, laid out again larger and replayed from their pristine state) */
 } mtb_launch_info;
 
 /* device_mask: the HIP devices the batch spreads over (bit k = device k; 0 = device 0).  With several,

@@ -4,6 +4,7 @@ they are profiling builds, not part of the package):
   prof      MTB_PROFILE                      per-phase cycle counters (mtb_profile lines on stderr)
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
+  ppcrumbs  profpack + MTB_CRUMBS            ticket breadcrumbs in host memory (fault triage, mtb_crumbs lines)
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -18,6 +19,7 @@ VARIANTS = {
     "prof": ["MTB_PROFILE"],
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
+    "ppcrumbs": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CRUMBS"],
 }
 
 if __name__ == "__main__":
