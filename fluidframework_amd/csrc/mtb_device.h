@@ -259,7 +259,7 @@ struct Tables {
 #define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
 #define DERR_STALE 25        // a summary body insert whose incremental partial-length update leaves stale cumulative
                              // lengths (partialLengths.ts:543-577 addSeq below newer entries): unsupported
-#define DERR_INCR 24         // an incr annotate over a string / object value (not NaN: unsupported on the device)
+#define DERR_INCR 24         // an incr annotate over a value its op's result table lacks (engine invariant)
 #define DERR_CONSENSUS 26    // a consensus annotate over an object value whose seq is -1 (completed in place, shared
                              // with split clones) or, with a null defaultValue, over a segment lacking the key
 // ticket scheduler words (mtb_replay_tick_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one

@@ -28,6 +28,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mtb.h"
@@ -148,6 +149,19 @@ bool js_match_value(const hj::Value* a, const hj::Value* b) {
 }
 
 // ------------------------------------------------------------------ interning
+// The property values one document can hold, per key (value ids): those of the props ids it met (its ops, a loaded
+// summary's segments, host-made consensus values; noted lazily) and the results of its incr tables.  An incr
+// annotate's result table covers these only, so its size and the refusal limit are per document, not per batch.
+struct DocVals {
+  std::vector<uint32_t> propsSeen;  // props ids, appended as met (load threads included), noted by Interner::note
+  size_t noted = 0;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> keyVals;
+  std::unordered_set<uint32_t> seen;
+  void add(uint32_t k, uint32_t v) {
+    if (seen.insert(v).second) keyVals[k].push_back(v);
+  }
+};
+
 struct Interner {
   std::vector<U16> keys;
   std::vector<std::string> keyJson;  // each key quoted as a JSON string (the summary serializers' props)
@@ -180,6 +194,10 @@ struct Interner {
   // only by a two-key object {value: null | {} | [], seq: <that seq>} ("cv-like"): such values are refused on a
   // key that holds consensus values, so a set holding one matches no set (valFalsy bit 3, like NaN)
   std::vector<uint8_t> keyCv, keyCvLike;
+  // keys an incr annotate names (they can hold NaN).  matchProperties(NaN, v) is true for an object or array v
+  // without own keys and false otherwise, matchProperties(v, NaN) always false: such a key that also holds object
+  // or array values is irregular (its pairs with NaN are decided on the device from val_falsy bits 3 and 4)
+  std::vector<uint8_t> keyNaN;
 
   uint32_t key(const U16& k) {
     auto it = keyId.find(k);
@@ -195,6 +213,7 @@ struct Interner {
     keyIrr.push_back(0);
     keyCv.push_back(0);
     keyCvLike.push_back(0);
+    keyNaN.push_back(0);
     keyVals.emplace_back();
     irrRows.emplace_back();
     dirty = true;
@@ -277,7 +296,11 @@ struct Interner {
         keyCvLike[k] = 1;
       }
       note_paths(k, v, path);
+      if (keyNaN[k] && (v.kind == hj::Value::kObj || v.kind == hj::Value::kArr)) keyIrr[k] = 1;
     }
+    if (keyIrr[k] && keyVals[k].size() + 1 > kIrrMax)  // (before the value is interned: only this message fails)
+      raise(MTB_E_UNSUPPORTED, "unsupported: more than 4096 distinct values under one property key whose values "
+                               "matchProperties does not compare as an equivalence");
     std::string c = std::to_string(k) + ":";
     canon(c, v);
     auto ci = classId.find(c);
@@ -295,14 +318,13 @@ struct Interner {
     // bit 0: JS falsy; bit 1: incr makes it NaN (number / boolean + undefined, properties.ts:38-45); bit 2: an
     // object whose seq is -1 (consensus completes it in place, properties.ts:56-60)
     const hj::Value* sq = v.kind == hj::Value::kObj ? v.find(u"seq") : nullptr;
+    // bit 4: an object or array without own keys (Object.keys is empty: matchProperties(NaN, it) is true)
+    const bool noKeys = (v.kind == hj::Value::kObj && v.members.empty()) || (v.kind == hj::Value::kArr && v.items.empty());
     valFalsy.push_back((v.truthy() ? 0 : 1) | (v.kind == hj::Value::kNum || v.kind == hj::Value::kBool ? 2 : 0) |
-                       (sq && sq->kind == hj::Value::kNum && sq->n == -1 ? 4 : 0) | (cv ? 8 : 0));
+                       (sq && sq->kind == hj::Value::kNum && sq->n == -1 ? 4 : 0) | (cv ? 8 : 0) | (noKeys ? 16 : 0));
     valLocal.push_back((uint32_t)keyVals[k].size());
     keyVals[k].push_back(id);
     valStore.push_back(v);
-    if (keyIrr[k] && keyVals[k].size() > kIrrMax)
-      raise(MTB_E_UNSUPPORTED, "unsupported: more than 4096 distinct values under one property key whose values "
-                               "matchProperties does not compare as an equivalence");
     dirty = true;
     return id;
   }
@@ -401,47 +423,112 @@ struct Interner {
     return props_kv(memo, kv);
   }
   // an incr annotate's op-props (properties.ts:24-45 through combine(op, previous, undefined), the op's values
-  // never read): each key's value slot names a pool table [absent result, n, (string value, result) * n]
-  // (MTB_INCR_TAB).  On the device a number / boolean / NaN previous value becomes NaN, an object fails the
-  // document (DERR_INCR), a string s becomes s + "undefined" -- and minValue when that is a string and the
-  // result sorts below it (JS string order; a number or boolean minValue compares with NaN: never) -- looked up
-  // here for every string value the key holds in the batch so far (a document's values were all interned
-  // before its op is packed); an absent key gets defaultValue + undefined (NaN, or a string).
+  // never read): each key's value slot names a pool table [absent result, n, (value, result) * n]
+  // (MTB_INCR_TAB).  On the device a number / boolean / NaN previous value becomes NaN; a string, object or array
+  // v becomes String(v) + "undefined" -- and minValue when that is a string, object or array and the result sorts
+  // below its string form (JS string order; a number or boolean minValue compares with NaN: never) -- looked up
+  // here for every such value the key holds in the batch so far (a document's values were all interned before
+  // its op is packed); an absent key gets defaultValue + undefined (NaN, or a string).
+  // String(v) (ECMA-262 ToString): objects "[object Object]", arrays join(",") with undefined / null elements as ""
+  static U16 js_string(const hj::Value& v) {
+    switch (v.kind) {
+      case hj::Value::kBool: return v.b ? U16(u"true") : U16(u"false");
+      case hj::Value::kNum: {
+        if (std::isnan(v.n)) return U16(u"NaN");
+        if (std::isinf(v.n)) return v.n < 0 ? U16(u"-Infinity") : U16(u"Infinity");
+        const std::string t = hj::number(v.n);
+        return U16(t.begin(), t.end());
+      }
+      case hj::Value::kStr: return v.s;
+      case hj::Value::kNull: return U16(u"null");
+      case hj::Value::kUndef: return U16(u"undefined");
+      case hj::Value::kObj: return U16(u"[object Object]");
+      case hj::Value::kArr: {
+        U16 o;
+        for (size_t i = 0; i < v.items.size(); i++) {
+          if (i) o += u",";
+          if (v.items[i].kind != hj::Value::kUndef && v.items[i].kind != hj::Value::kNull) o += js_string(v.items[i]);
+        }
+        return o;
+      }
+    }
+    return U16();
+  }
+  // the values of the props ids `dv` met since the last call (both the op list and the property set of each)
+  void note(DocVals& dv) {
+    for (; dv.noted < dv.propsSeen.size(); dv.noted++) {
+      const uint32_t pid = dv.propsSeen[dv.noted];
+      if (!pid || 2 * pid + 1 >= pidx.size()) continue;
+      for (int w = 0; w < 2; w++) {
+        const uint32_t off = pidx[2 * pid + w];
+        if (!off) continue;
+        const uint32_t n = pool[off];
+        for (uint32_t i = 0; i < n; i++) {
+          const uint32_t v = pool[off + 2 + 2 * i];
+          if (v != MTB_NONE && !(v & MTB_INCR_TAB) && v < valJson.size()) dv.add(pool[off + 1 + 2 * i], v);
+        }
+      }
+    }
+  }
   static constexpr uint32_t kIncrStrMax = 4096;
-  uint32_t incr_props(uint32_t pid, const hj::Value* dv, const hj::Value* mv) {
+  // (doc: the document's values; null: every value of the batch, e.g. records appended without a document context)
+  uint32_t incr_props(uint32_t pid, const hj::Value* dv, const hj::Value* mv, DocVals* doc = nullptr) {
     const uint32_t off = pidx[2 * pid], n = pool[off];
+    if (doc) note(*doc);
     std::string memo = "\x04" + std::to_string(pid) + ":" + (dv ? hj::dump(*dv) : "-") + ":" + (mv ? hj::dump(*mv) : "-");
     for (uint32_t i = 0; i < n; i++) memo += ":" + std::to_string(keyVals[pool[off + 1 + 2 * i]].size());
-    auto it = propsByJson.find(memo);
+    auto it = doc ? propsByJson.end() : propsByJson.find(memo);  // (per-document tables are not shared)
     if (it != propsByJson.end()) return it->second;
-    const bool minStr = mv && mv->kind == hj::Value::kStr && !mv->s.empty();
+    // minValue (when truthy) compares with a string result as its string form (ToPrimitive; a number or boolean
+    // compares NaN: never), and replaces it, itself (an object stays an object), when the result sorts below it
+    const bool minStr = mv && mv->truthy() &&
+                        (mv->kind == hj::Value::kStr || mv->kind == hj::Value::kObj || mv->kind == hj::Value::kArr);
+    const U16 minS = minStr ? js_string(*mv) : U16();
+    // previous values that concatenate: strings, objects and arrays (numbers, booleans and NaN give NaN)
+    auto concat = [](const hj::Value& v) {
+      return v.kind == hj::Value::kStr || v.kind == hj::Value::kObj || v.kind == hj::Value::kArr;
+    };
     auto result = [&](uint32_t k, const U16& s) {
       hj::Value r;
       r.kind = hj::Value::kStr;
       r.s = s + U16(u"undefined");
-      if (minStr && r.s < mv->s) r.s = mv->s;
+      if (minStr && r.s < minS) return value(k, *mv);
       return value(k, r);
     };
     std::vector<std::pair<uint32_t, uint32_t>> kv;
     for (uint32_t i = 0; i < n; i++) {
       const uint32_t k = pool[off + 1 + 2 * i];
-      uint32_t absent = nan();
-      if (dv && dv->kind == hj::Value::kStr) absent = result(k, dv->s);
+      if (!keyNaN[k]) {  // the key can hold NaN from now on
+        keyNaN[k] = 1;
+        auto root = keyPaths[k].find(std::string());
+        if (root != keyPaths[k].end() && (root->second & 2) && !keyIrr[k]) {
+          keyIrr[k] = 1;
+          dirty = true;
+        }
+      }
       std::vector<uint32_t> strs;
-      for (uint32_t v : keyVals[k])
-        if (valStore[v].kind == hj::Value::kStr) strs.push_back(v);
-      if (strs.size() > kIncrStrMax)
-        raise(MTB_E_UNSUPPORTED, "unsupported: incr over a key holding more than 4096 distinct string values");
+      for (uint32_t v : doc ? doc->keyVals[k] : keyVals[k])
+        if (concat(valStore[v])) strs.push_back(v);
+      if (strs.size() > kIncrStrMax)  // (checked before anything is interned: the refusal changes no state)
+        raise(MTB_E_UNSUPPORTED, "unsupported: incr over a key holding more than 4096 distinct string / object values "
+                                 "in one document");
+      uint32_t absent = nan();
+      if (dv && concat(*dv)) absent = result(k, js_string(*dv));
       std::vector<uint32_t> tab{absent, (uint32_t)strs.size()};
       for (uint32_t v : strs) {
-        const U16 sv = valStore[v].s;  // (value() may grow valStore)
+        const U16 sv = js_string(valStore[v]);  // (value() may grow valStore)
         const uint32_t r = result(k, sv);
         tab.push_back(v);
         tab.push_back(r);
       }
+      if (doc) {  // the document can hold the results from now on
+        if (absent != nanVal) doc->add(k, absent);
+        for (size_t j = 3; j < tab.size(); j += 2) doc->add(k, tab[j]);
+      }
       const uint32_t t = (uint32_t)pool.size();
       pool.insert(pool.end(), tab.begin(), tab.end());
       kv.push_back({k, MTB_INCR_TAB | t});
+      if (doc) memo += "@" + std::to_string(t);  // (a per-document table is its own props id)
     }
     dirty = true;
     return props_kv(memo, kv);
@@ -612,6 +699,7 @@ struct CellStore {
 
 // ------------------------------------------------------------------ host mirror of a document
 struct HostDoc {
+  DocVals vals;  // property values the document can hold (incr result tables)
   std::vector<std::string> longIds;
   std::unordered_map<std::string, uint16_t> shortOf;
   std::string observer;
@@ -958,6 +1046,7 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
     if (props && props->truthy()) {
       if (props->kind != hj::Value::kObj) raise(MTB_E_UNSUPPORTED, "unsupported: non-object segment props");
       r.props = b->in.props(*props);
+      d.vals.propsSeen.push_back(r.props);
     }
     out.push_back(r);
   } else if (type == 1 || type == 2) {
@@ -974,6 +1063,7 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
       hj::Value empty;
       empty.kind = hj::Value::kObj;
       r.props = b->in.props(props && props->kind == hj::Value::kObj ? *props : empty);
+      d.vals.propsSeen.push_back(r.props);
       const hj::Value* comb = member(op, u"combiningOp");
       if (comb && comb->kind == hj::Value::kObj) {
         const hj::Value* name = member(*comb, u"name");
@@ -982,22 +1072,19 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
         } else if (name && name->kind == hj::Value::kStr && name->s == u"incr") {
           // combine(op, previous, undefined) (segmentPropertiesManager.ts:145-147, properties.ts:24-69): NaN for a
           // number / boolean / absent previous value (defaultValue absent or numeric), string concatenation for a
-          // string one (Interner::incr_props); an object or array previous value fails the document (DERR_INCR)
+          // string, object or array one (its String() form; Interner::incr_props)
           const hj::Value* dv = member(*comb, u"defaultValue");
           const hj::Value* mv = member(*comb, u"minValue");
-          if (dv && (dv->kind == hj::Value::kObj || dv->kind == hj::Value::kArr))
-            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with an object defaultValue");
-          if (mv && mv->truthy() && (mv->kind == hj::Value::kObj || mv->kind == hj::Value::kArr))
-            raise(MTB_E_UNSUPPORTED, "unsupported: incr combiningOp with an object minValue");
           r.flags |= MTB_F_INCR;
           b->in.nan();
-          r.props = b->in.incr_props(r.props, dv, mv);
+          r.props = b->in.incr_props(r.props, dv, mv, &d.vals);
         } else if (name && name->kind == hj::Value::kStr && name->s == u"consensus") {
           // a local consensus value is {value: undefined, seq: -1}, completed in place at the ack (client.ts:1050-1058)
           if ((r.flags & MTB_F_LOCAL) || r.client == (uint16_t)MTB_LOCAL_CLIENT)
             raise(MTB_E_UNSUPPORTED, "unsupported: local consensus annotate (its value object is completed in place at the ack)");
           r.flags |= MTB_F_CONSENSUS;
           r.props = b->in.consensus_props(r.props, member(*comb, u"defaultValue"), (int)r.seq);
+          d.vals.propsSeen.push_back(r.props);
         } else {
           raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite / incr / consensus");
         }
@@ -1075,6 +1162,7 @@ LoadSeg load_spec(mtb_dev* b, HostDoc& d, const hj::Value& spec, std::vector<uin
     } else {
       g.props = b->in.props(*props);
     }
+    d.vals.propsSeen.push_back(g.props);
   }
   if (!mergeInfo) return g;  // seq = UniversalSequenceNumber, client = NonCollabClient
   auto cid = [&](const hj::Value& v) -> int16_t {
@@ -1919,7 +2007,7 @@ std::string derr_text(int e) {
     case DERR_SCHED: return "internal: the document's records did not all run (replay scheduler invariant)";
     case DERR_ASSERT_MKID: return "0x5ad Cannot change the markerId of an existing marker";
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
-    case DERR_INCR: return "unsupported: incr combiningOp over an object or array property value";
+    case DERR_INCR: return "internal: incr annotate over a value missing from its result table (Interner::incr_props)";
     case DERR_CONSENSUS: return "unsupported: consensus annotate over an object value whose seq is -1 (the reference completes "
                                 "it in place, shared with split clones), or with a null defaultValue over a segment lacking the key "
                                 "(the reference throws reading its seq)";
@@ -2662,17 +2750,23 @@ void props_json(mtb_dev* b, std::string& o, PropView v) {
   o += '}';
 }
 // matchProperties(a, c) (properties.ts:71-96): a is the run head's set
+// NaN and consensus values (valFalsy bit 3) never match as c's; as a's, NaN (no own keys) matches an object or array
+// without own keys (bit 4) and a consensus value nothing (its cv-like partners are refused)
 bool props_match(mtb_dev* b, PropView a, PropView c) {
   if (a.n() != c.n()) return false;
-  if (b->in.nanVal != MTB_NONE)  // NaN !== NaN, consensus values: a set holding one matches nothing
-    for (uint32_t i = 0; i < a.n(); i++)
-      if ((b->in.valFalsy[a.p[2 + 2 * i]] & 8) || (b->in.valFalsy[c.p[2 + 2 * i]] & 8)) return false;
+  const auto& F = b->in.valFalsy;
   for (uint32_t i = 0; i < a.n(); i++) {
     bool found = false;
     for (uint32_t q = 0; q < c.n(); q++) {
       if (c.p[1 + 2 * q] == a.p[1 + 2 * i]) {
         found = true;
-        if (!b->in.value_match(a.p[1 + 2 * i], a.p[2 + 2 * i], c.p[2 + 2 * q])) return false;
+        const uint32_t va = a.p[2 + 2 * i], vc = c.p[2 + 2 * q];
+        if (F[vc] & 8) return false;
+        if (F[va] & 8) {
+          if (!(va == b->in.nanVal && (F[vc] & 16))) return false;
+        } else if (!b->in.value_match(a.p[1 + 2 * i], va, vc)) {
+          return false;
+        }
       }
     }
     if (!found) return false;
@@ -4198,9 +4292,10 @@ int mtbx_append_ops(mtb_dev* b, uint32_t doc, const mtb_op* ops, uint32_t n, con
         if ((o.flags & MTB_F_COMB) == MTB_F_CONSENSUS) o.props = b->in.consensus_props(o.props, nullptr, (int)o.seq);
         if ((o.flags & MTB_F_COMB) == MTB_F_INCR) {
           b->in.nan();
-          o.props = b->in.incr_props(o.props, nullptr, nullptr);
+          o.props = b->in.incr_props(o.props, nullptr, nullptr, &d.vals);
         }
       }
+      if (o.type == MTB_OP_INSERT || o.type == MTB_OP_ANNOTATE) d.vals.propsSeen.push_back(o.props);
     }
     d.payload.insert(d.payload.end(), payload, payload + payload_len);
     d.totalPayload += payload_len;

@@ -54,6 +54,10 @@ namespace mtbk {
 // matchProperties(va, vb) (properties.ts:84-92) of two values of key k, with irregular keys in the batch
 // (Tables::key_irr; a regular key's values compare by class)
 __device__ __forceinline__ bool irr_value_match(const Tables& t, uint32_t k, uint32_t va, uint32_t vb) {
+  // NaN and consensus values (val_falsy bit 3) never match as the second argument; as the first, NaN (falsy: no own
+  // keys) matches an object or array without own keys (bit 4), a consensus value nothing (cv-like values refused)
+  if (t.val_falsy[vb] & 8) return false;
+  if (t.val_falsy[va] & 8) return va == (t.nan_val & ~MTB_NAN_CV) && (t.val_falsy[vb] & 16) != 0;
   const uint32_t o = t.key_irr[k];
   if (!o) return va == vb || t.val_class[va] == t.val_class[vb];
   const uint32_t n = t.irr[o - 1];
@@ -2424,6 +2428,9 @@ struct Eng {
   }
   // Interner pair tables (mtbk::irr_value_match) with uniform operands, the table pointers in SGPRs
   __device__ __forceinline__ bool irr_match(uint32_t k, uint32_t va, uint32_t vb) const {
+    const auto F = UP(sh->tab.val_falsy);  // (NaN / consensus values: irr_value_match)
+    if (U((uint32_t)F[vb]) & 8) return false;
+    if (U((uint32_t)F[va]) & 8) return va == (U(sh->tab.nan_val) & ~MTB_NAN_CV) && (U((uint32_t)F[vb]) & 16) != 0;
     const uint32_t o = U(UP(sh->tab.key_irr)[k]);
     if (!o) return va == vb || U(UP(sh->tab.val_class)[va]) == U(UP(sh->tab.val_class)[vb]);
     const auto T = UP(sh->tab.irr);
@@ -2434,8 +2441,10 @@ struct Eng {
   // matchProperties (properties.ts:71-96) on interned property sets; a = the run head's set.  With irregular
   // keys in the batch (tab.irr_any) it is neither reflexive nor symmetric there: no shortcut on equal handles.
   __device__ __forceinline__ bool props_match(uint32_t a, uint32_t b) const {
-    if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
+    // NaN !== NaN: a set holding NaN or a consensus value matches nothing -- except, with irregular keys, a first
+    // argument holding NaN under a key whose other value is an object or array without own keys (irr_match)
     const bool irr = hasIrr && U(sh->tab.irr_any) != 0;
+    if ((irr ? b : (a | b)) & MTB_PNAN) return false;
     if (a == b && !irr) return true;
     const gptr<const uint32_t> pa = a ? props_ptr(a) : nullptr;
     const gptr<const uint32_t> pb = b ? props_ptr(b) : nullptr;
@@ -2523,8 +2532,8 @@ struct Eng {
         if (sh->pk[i] == k) at = (int)i;
       if (COLD(comb == 2)) {
         // incr: combine(op, previous, undefined) (properties.ts:24-69) -- previous + undefined is NaN for numbers /
-        // booleans / NaN; a string's result (s + "undefined", minValue) and the absent key's come from the op's
-        // table (Interner::incr_props); an object or array is not restated
+        // booleans / NaN; a string's, object's or array's result (String(v) + "undefined", minValue) and the absent
+        // key's come from the op's table (Interner::incr_props; a value missing from it is an engine invariant)
         const uint32_t nanv = U(sh->tab.nan_val) & ~MTB_NAN_CV;
         const auto T = UP(sh->tab.pool) + (v & ~MTB_INCR_TAB);
         const bool tab = (v & MTB_INCR_TAB) != 0 && v != MTB_NONE;
@@ -4408,7 +4417,13 @@ __device__ __forceinline__ uint32_t xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
   return x;
 }
-__device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* prog, uint32_t c, uint32_t spins) {
+// (MTB_TICK_INLINE: the hand-over helpers inlined, so the kernel makes no calls -- fault-triage builds)
+#ifdef MTB_TICK_INLINE
+#define TICK_FN __device__ __forceinline__
+#else
+#define TICK_FN __device__ __attribute__((noinline))
+#endif
+TICK_FN bool tick_wait(uint32_t* sched, uint32_t* prog, uint32_t c, uint32_t spins) {
   uint32_t n = 0;
   while (U(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < c) {
     if (++n > spins) {
@@ -4429,7 +4444,7 @@ __device__ __attribute__((noinline)) bool tick_wait(uint32_t* sched, uint32_t* p
 // shape): the chunk is not run, the first mismatch is recorded ([MTB_SCHED_BAD] count, then document, chunk,
 // expected, seen) and the abort flag hands the rest to mtb_replay_finish_kernel, a new launch that reads every
 // DocState afresh.  Both words are read with agent-scope atomic loads (vector memory, never the scalar cache).
-__device__ __attribute__((noinline)) bool tick_check(uint32_t* sched, uint32_t* hand, uint32_t* opn, uint32_t d, uint32_t c) {
+TICK_FN bool tick_check(uint32_t* sched, uint32_t* hand, uint32_t* opn, uint32_t d, uint32_t c) {
   const uint32_t want = U(__hip_atomic_load(hand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const uint32_t have = U(__hip_atomic_load(opn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (want == have) return true;
@@ -4863,7 +4878,7 @@ hipError_t mtb_launch_digest(hipStream_t stream, uint32_t ndocs, const DocState*
 namespace mtbk {
 __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uint32_t* pool, const uint32_t* A,
                                                const Tables& tab) {
-  if ((a | b) & MTB_PNAN) return false;  // NaN !== NaN
+  if ((tab.irr_any ? b : (a | b)) & MTB_PNAN) return false;  // NaN !== NaN (a's NaN: irr_value_match)
   if (a == b && !tab.irr_any) return true;
   const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + a) : nullptr;
   const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + b) : nullptr;

@@ -121,7 +121,9 @@ void PartialLengths::addClientSeqNumberFromPartial(const PSL& p) {
       if (p.clientId != kv.first) addClientSeqNumber(kv.first, p.seq, kv.second);
 }
 
-static void addSeq(PSLSet& set, int seq, int seqSeglen, int clientId) {  // partialLengths.ts:543-577
+// Returns the amount by which the entries after `seq` are left short: an existing entry at `seq` gets its seglen
+// replaced (not added to) while the later entries' cumulative len keep the old one (0 when nothing follows).
+static int addSeq(PSLSet& set, int seq, int seqSeglen, int clientId) {  // partialLengths.ts:543-577
   PSL* seqPartial = nullptr;
   PSL* penult = nullptr;
   PSL* p = set.latestLeq(seq);
@@ -142,10 +144,12 @@ static void addSeq(PSLSet& set, int seq, int seqSeglen, int clientId) {  // part
     n.seglen = seqSeglen;
     n.seq = seq;
     set.addOrUpdate(n);
-  } else {
-    seqPartial->seglen = seqSeglen;
-    seqPartial->len = len;
+    return 0;
   }
+  const int deficit = set.items.back().seq > seq ? seqSeglen - seqPartial->seglen : 0;
+  seqPartial->seglen = seqSeglen;
+  seqPartial->len = len;
+  return deficit;
 }
 
 // =====================================================================================
@@ -844,8 +848,9 @@ void MergeTree::plUpdate(PartialLengths& pl, Block* node, int seq, int clientId)
     }
   }
   pl.segmentCount = segCount;
-  addSeq(pl.partialLengths, seq, seqSeglen, clientId);
-  addSeq(pl.cli(clientId), seq, seqSeglen, 0);
+  const int d1 = addSeq(pl.partialLengths, seq, seqSeglen, clientId);
+  const int d2 = addSeq(pl.cli(clientId), seq, seqSeglen, 0);
+  if (node != root && (d1 || d2)) counters.staleDeficits++;
   pl.zamboni(window);
 }
 
@@ -992,6 +997,33 @@ static JVal combine_consensus(const Comb& c, const JVal* prev, int seq) {
   }
   return cur;
 }
+// String(v) of a JSON value (ECMA-262 ToString; objects through Object.prototype.toString, arrays through
+// Array.prototype.join(","), whose undefined / null elements become "")
+static u16str js_to_string(const JVal& v) {
+  switch (v.t) {
+    case JVal::Undef: return u"undefined";
+    case JVal::Null: return u"null";
+    case JVal::False: return u"false";
+    case JVal::True: return u"true";
+    case JVal::Num: {
+      if (std::isnan(v.num)) return u"NaN";
+      if (std::isinf(v.num)) return v.num < 0 ? u"-Infinity" : u"Infinity";
+      const std::string n = js_number_to_string(v.num);
+      return u16str(n.begin(), n.end());
+    }
+    case JVal::Str: return v.str;
+    case JVal::Obj: return u"[object Object]";
+    case JVal::Arr: {
+      u16str o;
+      for (size_t i = 0; i < v.arr.size(); i++) {
+        if (i) o += u",";
+        if (v.arr[i].t != JVal::Undef && v.arr[i].t != JVal::Null) o += js_to_string(v.arr[i]);
+      }
+      return o;
+    }
+  }
+  return u"";
+}
 // combine(combiningOp, previousValue, undefined, seq) for "incr" (properties.ts:24-69)
 static JVal combine_incr(const Comb& c, const JVal* prev) {
   JVal cur = prev ? *prev : JVal::undef();
@@ -1003,12 +1035,18 @@ static JVal combine_incr(const Comb& c, const JVal* prev) {
     case JVal::False:
     case JVal::True:
     case JVal::Num: cur = JVal::number(std::nan("")); break;
-    default: fail_unsupported("incr of an object or array property value");
+    default: {  // an object or array: ToPrimitive is its string form, then string concatenation
+      JVal r;
+      r.t = JVal::Str;
+      r.str = js_to_string(cur) + u"undefined";
+      cur = std::move(r);
+    }
   }
   if (!js_falsy(&c.minValue)) {  // if (_currentValue < minValue) _currentValue = minValue
-    if (c.minValue.t == JVal::Obj || c.minValue.t == JVal::Arr) fail_unsupported("incr with an object minValue");
-    // NaN < x is false; "...undefined" < a number compares NaN; two strings compare by UTF-16 code units
-    if (cur.t == JVal::Str && c.minValue.t == JVal::Str && cur.str < c.minValue.str) cur = c.minValue;
+    // NaN < x is false; "...undefined" < a number or boolean compares NaN; against a string, object or array
+    // minValue (ToPrimitive: its string form) two strings compare by UTF-16 code units
+    const bool strMin = c.minValue.t == JVal::Str || c.minValue.t == JVal::Obj || c.minValue.t == JVal::Arr;
+    if (cur.t == JVal::Str && strMin && cur.str < js_to_string(c.minValue)) cur = c.minValue;
   }
   return cur;
 }

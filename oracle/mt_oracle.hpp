@@ -160,6 +160,7 @@ struct Counters {
   // PartialSequenceLengths.update below the root met an entry newer than its seq (a summary body's insert):
   // addSeq leaves the later entries' cumulative lengths stale (the engine refuses such loads)
   uint64_t staleUpdates = 0;
+  uint64_t staleDeficits = 0;  // updates that left entries after their seq short (addSeq over an existing entry)
 };
 
 class MergeTree {

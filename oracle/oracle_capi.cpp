@@ -290,6 +290,7 @@ const char* orc_client_long_id(orc_doc* d, int i) { return d->doc.longIds.at(i).
 uint64_t orc_ops_applied(orc_doc* d) { return d->doc.mt.counters.ops; }
 uint64_t orc_segs_touched(orc_doc* d) { return d->doc.mt.counters.segsTouched; }
 uint64_t orc_stale_updates(orc_doc* d) { return d->doc.mt.counters.staleUpdates; }
+uint64_t orc_stale_deficits(orc_doc* d) { return d->doc.mt.counters.staleDeficits; }
 
 // Summary: returns a JSON object {"blobs":[[path, content],...], "summary": <ISummaryTreeWithStats>}
 int orc_summarize_v1(orc_doc* d, int msn, int seq, char** out, size_t* len) {

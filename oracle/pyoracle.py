@@ -49,6 +49,8 @@ def lib():
         L.orc_segs_touched.argtypes = [vp]
         L.orc_stale_updates.restype = ctypes.c_uint64
         L.orc_stale_updates.argtypes = [vp]
+        L.orc_stale_deficits.restype = ctypes.c_uint64
+        L.orc_stale_deficits.argtypes = [vp]
         L.orc_summarize_v1.argtypes = [vp, i, i, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_dump_segments.argtypes = [vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(sz)]
         L.orc_checksum.restype = ctypes.c_uint64
@@ -278,6 +280,12 @@ class OracleDoc:
     def stale_updates(self):
         """Partial-length updates below the root that met newer entries (stale cumulative lengths)."""
         return self._L.orc_stale_updates(self._h)
+
+    def stale_deficits(self):
+        """Of those, the updates that actually left later entries short: an existing entry at the update's seq got
+        its seglen replaced while entries after it kept cumulative lengths built on the old one (addSeq,
+        partialLengths.ts:543-577)."""
+        return self._L.orc_stale_deficits(self._h)
 
     def summarize_v1(self, msn=-1, seq=-1):
         p = ctypes.c_void_p()

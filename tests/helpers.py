@@ -614,7 +614,7 @@ def make_marker_log(seed, n_msgs, n_clients=4, lag=24, new_mode=False, initial="
 
 
 def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="hello incr world", p_incr=0.15,
-                  p_rewrite=0.0, string_incr=False):
+                  p_rewrite=0.0, string_incr=False, object_incr=False, objs=None, incr_objects=True):
     """A sequenced op log whose annotates are partly combiningOp "incr" annotates (segmentPropertiesManager.ts:
     145-147 -> combine(op, previous, undefined) of properties.ts:24-69): numeric keys "n" / "m" (incr makes
     them NaN, JSON null, never matchProperties-equal), a string key "s" that incr never names, null deletes,
@@ -622,7 +622,9 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
     fraction of the annotates are combiningOp "rewrite" annotates (falsy values -- 0, "", null -- delete or
     re-append keys, :107-154).  Every message is applied to a generator oracle as it is made.  Returns
     (initial text, messages).  With `string_incr` incr annotates also name the string key "s" (string
-    concatenation: s + "undefined", then a string minValue when larger) and take string defaultValues."""
+    concatenation: s + "undefined", then a string minValue when larger) and take string defaultValues.  With
+    `object_incr` a key "o" holds object / array values (inserted and annotated) that incr annotates name too
+    (String(value) + "undefined"), with object / array defaultValues and minValues."""
     import random
     from pyoracle import OracleDoc
     rng = random.Random(seed)
@@ -638,6 +640,8 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
     ref = [0] * n_clients
     msgs = []
     words = ["ab", "c", "xyz", "\n", "more text "]
+    if objs is None:
+        objs = [{"x": 1}, [1, 2], [], [None, "q", [3, [4]]], {"y": [1]}, ["[object Object]"]]
     for seq in range(1, n_msgs + 1):
         k = rng.randrange(n_clients)
         ref[k] = max(ref[k], seq - 1 - rng.randint(0, lag))
@@ -648,6 +652,8 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
             seg = rng.choice(words)
             if rng.random() < 0.3:
                 seg = {"text": seg, "props": {"n": rng.randint(0, 2)} if rng.random() < 0.7 else {"s": "v"}}
+                if object_incr and rng.random() < 0.5:
+                    seg["props"]["o"] = rng.choice(objs)
             op = {"type": 0, "pos1": rng.randint(0, n), "seg": seg}
         else:
             a = rng.randrange(n)
@@ -669,12 +675,18 @@ def make_incr_log(seed, n_msgs, n_clients=4, lag=16, new_mode=False, initial="he
                     comb["defaultValue"] = rng.choice(["d", "zz", ""])
                 elif string_incr and r < 0.6:
                     comb["minValue"] = rng.choice(["b", "bundefined", "zz"])
+                elif object_incr and r < 0.75:
+                    comb["defaultValue" if rng.random() < 0.5 else "minValue"] = rng.choice(objs)
                 keys = ["n", "m", "s"] if string_incr else ["n", "m"]
+                if object_incr and incr_objects:
+                    keys = keys + ["o", "o"]
                 op = {"type": 2, "pos1": a, "pos2": b, "props": {rng.choice(keys): rng.randint(1, 3)},
                       "combiningOp": comb}
             else:
                 props = rng.choice([{"n": rng.randint(0, 2)}, {"m": rng.randint(0, 2), "s": "w"}, {"n": None},
                                     {"s": rng.choice(["a", "b"])}, {"m": None, "n": 1}])
+                if object_incr and rng.random() < 0.4:
+                    props = {"o": rng.choice(objs + [None])}
                 op = {"type": 2, "pos1": a, "pos2": b, "props": props}
         m = {"clientId": cid, "sequenceNumber": seq, "referenceSequenceNumber": R, "minimumSequenceNumber": min(ref),
              "type": "op", "contents": op}

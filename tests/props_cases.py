@@ -77,6 +77,20 @@ CASES = [
      [msg("a", 1, 0, {"type": 2, "pos1": 1, "pos2": 3, "props": {"k": 1},
                       "combiningOp": {"name": "consensus", "defaultValue": "d"}})] + _tick(2),
      [[".a", None], ["bc", {"k": "d"}], ["d", None]]),  # (the tick's "." joins the unannotated "a")
+    # incr makes NaN (JSON null): matchProperties(NaN, {}) recurses into (NaN, {}) whose key lists are both empty,
+    # so a NaN head takes an empty-object (or empty-array) neighbour; the reverse compares {} !== NaN
+    ("NaN head, empty object next: coalesce", "",
+     [_ins("a", 1, 0, 0, "ab", {"k": 5}), _ins("a", 2, 1, 2, "cd", {"k": {}}),
+      msg("a", 3, 2, {"type": 2, "pos1": 0, "pos2": 2, "props": {"k": 1}, "combiningOp": {"name": "incr"}})] + _tick(4),
+     [[".", None], ["abcd", {"k": None}]]),
+    ("empty array head, NaN next: apart", "",
+     [_ins("a", 1, 0, 0, "ab", {"k": []}), _ins("a", 2, 1, 2, "cd", {"k": 5}),
+      msg("a", 3, 2, {"type": 2, "pos1": 2, "pos2": 4, "props": {"k": 1}, "combiningOp": {"name": "incr"}})] + _tick(4),
+     [[".", None], ["ab", {"k": []}], ["cd", {"k": None}]]),
+    ("NaN head, non-empty object next: apart", "",
+     [_ins("a", 1, 0, 0, "ab", {"k": 5}), _ins("a", 2, 1, 2, "cd", {"k": {"x": 1}}),
+      msg("a", 3, 2, {"type": 2, "pos1": 0, "pos2": 2, "props": {"k": 1}, "combiningOp": {"name": "incr"}})] + _tick(4),
+     [[".", None], ["ab", {"k": None}], ["cd", {"k": {"x": 1}}]]),
 ]
 
 # (name, initial text, messages, error substring): the reference mutates a shared object or throws

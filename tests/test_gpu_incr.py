@@ -9,8 +9,8 @@ Bar: bit-exact against the oracle (canonical dump, text, state digest, SnapshotV
 * live-client farms (helpers.run_local_farm(incr=...)) with local incr annotates, acks and reconnects (a
   remote incr also modifies pending local keys, shouldModifyKey);
 * string values (JS string concatenation, string defaultValue / minValue): results from the op's table;
-* an incr over an object value: the engine fails that document loudly (MTB_E_UNSUPPORTED), the other documents
-  of the batch replay.
+* object and array values (String() form + "undefined", object defaultValue / minValue): results from the op's
+  table too; KATs and generated logs.
 """
 import pytest
 
@@ -65,31 +65,69 @@ def test_local_incr_farm(seed):
     assert _replay_record(rec, seed, seed % 2 == 0, 1, "hello world") > 0
 
 
-def test_incr_over_an_object_fails_its_document_only():
+def test_incr_over_string_object_and_array_values():
     """A string value concatenates (tests/test_incr.py::test_incr_string_concatenates_and_min_value on the oracle;
-    the engine reads the result from the op's table), an object value fails its document (DERR_INCR)."""
-    from fluidframework_amd import MergeTreeBatch, MergeTreeError
+    the engine reads the result from the op's table), and so do object and array values through their String()
+    form (tests/test_incr.py::test_incr_object_and_array_values_concatenate_their_string_form), object minValue
+    included."""
+    from fluidframework_amd import MergeTreeBatch
     from pyoracle import OracleDoc
     B = MergeTreeBatch(2)
-    msgs = [msg("a", 1, 0, {"type": 2, "pos1": 0, "pos2": 2, "props": {"s": "abc", "n": 2, "o": {"x": 1}}})]
-    bad = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"o": 1}, "combiningOp": {"name": "incr"}})]
-    good = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"s": 1}, "combiningOp": {"name": "incr"}}),
+    msgs = [msg("a", 1, 0, {"type": 2, "pos1": 0, "pos2": 2, "props": {"s": "abc", "n": 2, "o": {"x": 1}, "a": [1, [2]]}})]
+    objs = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"o": 1, "a": 2},
+                                   "combiningOp": {"name": "incr"}}),
+                   msg("a", 3, 2, {"type": 2, "pos1": 1, "pos2": 3, "props": {"o": 1, "a": 1},
+                                   "combiningOp": {"name": "incr", "defaultValue": [5], "minValue": {"m": 0}}})]
+    strs = msgs + [msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 1, "props": {"s": 1}, "combiningOp": {"name": "incr"}}),
                    msg("a", 3, 2, {"type": 2, "pos1": 1, "pos2": 2, "props": {"s": 1},
                                    "combiningOp": {"name": "incr", "minValue": "zz"}})]
-    for i, ms in enumerate((bad, good)):
+    orc = []
+    for i, ms in enumerate((objs, strs)):
         B[i].insertTextLocal(0, "hello")
         B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc()
+        o.insert_text_local(0, "hello")
+        o.start_collab("obs")
         for m in ms:
             B[i].applyMsg(m)
-    with pytest.raises(MergeTreeError, match="incr"):
-        B.replay()
-    o = OracleDoc()
-    o.insert_text_local(0, "hello")
-    o.start_collab("obs")
-    for m in good:
-        o.apply_msg(m)
-    _same(B, 1, o, "good document")
+            o.apply_msg(m)
+        orc.append(o)
+    assert B.replay()["errors"] == 0
+    for i, o in enumerate(orc):
+        _same(B, i, o, f"document {i}")
+    assert '"o":"[object Object]undefined"' in B.dump_segments(0) and '"a":"1,2undefined"' in B.dump_segments(0)
     assert '"s":"abcundefined"' in B.dump_segments(1) and '"s":"zz"' in B.dump_segments(1)
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_object_incr_logs(new_mode):
+    """Generated logs with object / array values under a key that incr annotates name (object defaultValue and
+    minValue too), two flushes, SnapshotV1 at the end: bit-exact against the oracle."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyoracle import OracleDoc
+    logs = [make_incr_log(850 + s + 20 * int(new_mode), 900, n_clients=3 + s % 3, lag=4 + 5 * s, new_mode=new_mode,
+                          p_incr=0.3, string_incr=True, object_incr=True) for s in range(8)]
+    B = MergeTreeBatch(len(logs), new_length_calc=new_mode)
+    orc = []
+    for i, (init, _) in enumerate(logs):
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc(new_length_calc=new_mode)
+        o.insert_text_local(0, init)
+        o.start_collab("obs")
+        orc.append(o)
+    for part in (slice(0, 450), slice(450, None)):
+        for i, (_, msgs) in enumerate(logs):
+            for m in msgs[part]:
+                B[i].applyMsg(m)
+                orc[i].apply_msg(m)
+        st = B.replay()
+        assert st["errors"] == 0, st
+        for i, o in enumerate(orc):
+            _same(B, i, o, f"log {i} {part}")
+    for i, o in enumerate(orc):
+        gb, gs = B.summarize_v1(i)
+        assert [list(x) for x in gb] == o.summarize_v1()["blobs"], f"log {i}: SnapshotV1 differs"
 
 
 @pytest.mark.parametrize("new_mode", [False, True])

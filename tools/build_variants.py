@@ -5,6 +5,7 @@ they are profiling builds, not part of the package):
   profpack  + MTB_PROFILE_PACK               packParent / zamboni sub-phase counters
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
   ppcrumbs  profpack + MTB_CRUMBS            ticket breadcrumbs in host memory (fault triage, mtb_crumbs lines)
+  ppinline  profpack + MTB_TICK_INLINE       the ticket kernel's hand-over helpers inlined (no calls; fault triage)
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -20,6 +21,7 @@ VARIANTS = {
     "profpack": ["MTB_PROFILE", "MTB_PROFILE_PACK"],
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
     "ppcrumbs": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CRUMBS"],
+    "ppinline": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_TICK_INLINE"],
 }
 
 if __name__ == "__main__":
