@@ -4417,8 +4417,11 @@ __device__ __forceinline__ uint32_t xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
   return x;
 }
-// (MTB_TICK_INLINE: the hand-over helpers inlined, so the kernel makes no calls -- fault-triage builds)
-#ifdef MTB_TICK_INLINE
+// The hand-over helpers are called functions in the product build (inlined, their spin loop and fence made the
+// engine spill).  Builds whose engine spills anyway (MTB_PROFILE) inline them: a kernel that both uses scratch and
+// makes calls faulted deterministically in the MTB_PROFILE_PACK build (DESIGN.md §4 "Round 6": independent of
+// hand-overs, gone with the calls inlined); tests/test_code_object.py keeps the product kernel free of scratch.
+#if defined(MTB_TICK_INLINE) || defined(MTB_PROFILE)
 #define TICK_FN __device__ __forceinline__
 #else
 #define TICK_FN __device__ __attribute__((noinline))
@@ -4880,8 +4883,8 @@ __device__ __forceinline__ bool ex_props_match(uint32_t a, uint32_t b, const uin
                                                const Tables& tab) {
   if ((tab.irr_any ? b : (a | b)) & MTB_PNAN) return false;  // NaN !== NaN (a's NaN: irr_value_match)
   if (a == b && !tab.irr_any) return true;
-  const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + a) : nullptr;
-  const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + b) : nullptr;
+  const uint32_t* pa = a ? ((a & MTB_GPROPS) ? pool + (a & ~MTB_GPROPS) : A + (a & ~MTB_PNAN)) : nullptr;
+  const uint32_t* pb = b ? ((b & MTB_GPROPS) ? pool + (b & ~MTB_GPROPS) : A + (b & ~MTB_PNAN)) : nullptr;
   const uint32_t na = pa ? pa[0] : 0, nb = pb ? pb[0] : 0;
   if (na != nb) return false;
   for (uint32_t i = 0; i < na; i++) {
