@@ -278,3 +278,5 @@ struct Tables {
                           // observer; mtb_host.cpp HostDoc::obsRef), mapped back by the digest
 #define DSF_PHANTOM 8      // a loaded summary left phantom partial lengths (DocState.ph; mtb_replay.hip)
 #define DSF_MKDUP 4        // a marker id is carried by two markers: blockUpdate re-maps ids (mergeTree.ts:296-306)
+#define DSF_VARIANT 32     // the document replays on the marker variant (marker ids, phantom tables, irregular keys);
+                           // the observer kernels skip it and the marker kernel replays only such documents

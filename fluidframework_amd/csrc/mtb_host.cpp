@@ -190,6 +190,11 @@ struct Interner {
   std::vector<uint32_t> valLocal;                          // value -> index in its key's list
   std::vector<hj::Value> valStore;
   uint32_t nIrr = 0;
+  uint32_t nIrrKeys() const {
+    uint32_t n = 0;
+    for (uint8_t x : keyIrr) n += x;
+    return n;
+  }
   // consensus values ({value: undefined, seq}) are matched by nothing as the second argument, and as the first
   // only by a two-key object {value: null | {} | [], seq: <that seq>} ("cv-like"): such values are refused on a
   // key that holds consensus values, so a set holding one matches no set (valFalsy bit 3, like NaN)
@@ -836,7 +841,8 @@ struct mtb_dev {
   double lastKernelMs = 0;
   // rewind support: state right after the first upload of every document's records
   bool haveRewind = false;
-  bool tightCaps = false;  // slices sized by caps_for's tight formula (large batches; capacity retry in replay())
+  bool tightCaps = false;
+  uint32_t variantDocs = 0;  // documents flagged DSF_VARIANT by the last mark_variant_docs  // slices sized by caps_for's tight formula (large batches; capacity retry in replay())
   std::vector<DocState> hPristine;
   DevBuf<DocState> dPristine;
   DevBuf<uint32_t> dPSeg;
@@ -2135,6 +2141,36 @@ void sched_result(mtb_dev* b) {
             w[MTB_SCHED_BAD], w[MTB_SCHED_BAD + 1], w[MTB_SCHED_BAD + 2], w[MTB_SCHED_BAD + 4], w[MTB_SCHED_BAD + 3]);
 }
 
+// Which kernel replays each document (DocState.flags DSF_VARIANT): the marker variant for a document that met a
+// marker id, loaded phantom partial lengths or uses a property key whose matchProperties is no equivalence
+// (irregular in the batch), the observer kernels for every other -- so one such document no longer moves the whole
+// batch onto the marker variant (the observer kernels skip flagged documents, the marker kernel the others).
+// Live batches replay every document on the live kernel (no flags).
+// the marker kernel over the flagged documents (the others return at once), before the observer kernels' launch
+void launch_variant_docs(mtb_dev* b, const Tables& t) {
+  HIPCHK(mtb_launch_replay(b->stream, b->ndocs, b->dDocs.p, b->dOps.p, b->dSegs.p, b->dBlks.p, b->dLists.p, b->dText.p,
+                           b->dHeap.p, b->dAux.p, b->dFree.p, t, 2));
+}
+void mark_variant_docs(mtb_dev* b) {
+  uint32_t nv = 0;
+  for (uint32_t i = 0; i < b->ndocs; i++) {
+    HostDoc& d = b->docs[i];
+    DocState& s = b->hst[i];
+    bool v = false;
+    if (!b->live && !b->matrix) {
+      v = !d.markerAmbig.empty() || d.markerIdAnnot || d.phantom;
+      if (!v && b->in.nIrrKeys()) {
+        b->in.note(d.vals);
+        for (const auto& kv : d.vals.keyVals)
+          if (b->in.keyIrr[kv.first]) { v = true; break; }
+      }
+    }
+    s.flags = v ? (s.flags | DSF_VARIANT) : (s.flags & ~DSF_VARIANT);
+    nv += v;
+  }
+  b->variantDocs = nv;
+}
+
 void launch_main(mtb_dev* b, const Tables& t) {
   if (getenv("MTB_DEBUG_POOLS")) {  // (fault triage: the pools' address ranges, to place a faulting address)
     const struct { const char* name; const void* p; size_t bytes; } pools[] = {
@@ -2156,9 +2192,10 @@ void launch_main(mtb_dev* b, const Tables& t) {
     // the live-client kernel carries the marker code too; otherwise the marker variant runs only for
     // batches where some document met a marker id
     // (the marker variant carries the phantom tables and the irregular-key matchProperties too)
-    bool markers = b->in.nIrr != 0;
-    for (uint32_t i = 0; i < b->ndocs && !markers; i++)
-      markers = !b->docs[i].markerAmbig.empty() || b->docs[i].markerIdAnnot || b->docs[i].phantom;
+    // (mark_variant_docs: every document on the marker variant, some, or none)
+    const bool markers = b->variantDocs != 0 && b->variantDocs == b->ndocs;
+    const bool someMarkers = b->variantDocs != 0 && !markers;
+    if (someMarkers) launch_variant_docs(b, t);
     // more documents than wave slots: tickets, one per workgroup (mtb_replay_tick_kernel, the default;
     // MTB_CHUNKS / MTB_CHUNK_PLAN set the tickets per document) or passes of equal chunks (MTB_SCHED=passes);
     // MTB_SCHED=0 launches one wave per whole document
@@ -2468,6 +2505,7 @@ void replay(mtb_dev* b, mtb_stats* out) {
       *out++ = o;
     }
   });
+  mark_variant_docs(b);
   // catch-up delta slices: a record's delta has at most one entry per unit of its range
   {
     uint64_t tot = 0;

@@ -4156,6 +4156,13 @@ __device__ __forceinline__ uint32_t replay_doc(SCR& sh, uint32_t doc, int32_t* x
   const uint32_t dw1 = lane_id() < (int)(sizeof(DocState) / 4 - 64) ? reinterpret_cast<const uint32_t*>(ds)[64 + lane_id()] : 0u;
 #define DSF(f) ds_word(dw0, dw1, offsetof(DocState, f) / 4)
 #define DSF64(f) (((uint64_t)ds_word(dw0, dw1, offsetof(DocState, f) / 4 + 1) << 32) | ds_word(dw0, dw1, offsetof(DocState, f) / 4))
+  // a document on the marker variant (DSF_VARIANT, mtb_host.cpp mark_variant_docs) is the marker kernel's; every
+  // other document of such a batch the observer kernels'
+  if constexpr (MODE == MODE_REPLAY) {
+    if (DSF(flags) & DSF_VARIANT) return DSF(op_next);
+  } else if constexpr (MODE == MODE_MARKERS) {
+    if (!(DSF(flags) & DSF_VARIANT)) return DSF(op_next);
+  }
 #ifdef MTB_CHECK
   {
     uint32_t* rep = &ds->pad3[0];

@@ -74,3 +74,43 @@ def test_mixed_kinds_in_one_batch(new_mode):
         gb, _ = B.summarize_v1(i)
         assert [list(x) for x in gb] == o.summarize_v1()["blobs"], f"{docs[i][0]} doc {i}: SnapshotV1 differs"
         o.close()
+
+
+def test_marker_documents_beside_a_ticket_scheduled_batch():
+    """The kernel is chosen per document (mtb_host.cpp mark_variant_docs): 4,200 plain generated documents replay on
+    the ticket-scheduled observer kernel while the batch's marker-id documents (and a property log with irregular
+    keys) replay on the marker variant, in one mtb_replay; every document equals the oracle, also after a rewind
+    and resident replay."""
+    from fluidframework_amd import MergeTreeBatch
+    from pyloggen import LogBatch, make_cfg
+    from pyoracle import OracleDoc
+    from helpers import load_logbatch
+    lb = LogBatch(make_cfg(seed=1607, n_ops=150), 0, 4200)
+    extra = [make_marker_log(1600 + s, 400, n_clients=3, lag=8, dup_ids=2 * s) for s in range(2)] + \
+            [make_props_log(1650, 400, n_clients=3, lag=6)]
+    B = MergeTreeBatch(lb.n + len(extra))
+    load_logbatch(B, lb)
+    orc = []
+    for j, (init, msgs) in enumerate(extra):
+        i = lb.n + j
+        B[i].insertTextLocal(0, init)
+        B[i].startOrUpdateCollaboration("obs")
+        o = OracleDoc()
+        o.insert_text_local(0, init)
+        o.start_collab("obs")
+        for m in msgs:
+            B[i].applyMsg(m)
+            o.apply_msg(m)
+        orc.append(o)
+    for rep in range(2):
+        st = B.replay() if rep == 0 else (B.rewind(), B.replay_resident())[1]
+        assert st["errors"] == 0, st
+        assert B.launch_info()["kernel"] == "mtb_replay_tick_kernel"
+        dg = B.digests()
+        bad = [j for j in range(lb.n) if dg[j] != lb.docs[j].digest]
+        assert not bad, f"{len(bad)} plain documents differ (first {bad[:5]})"
+        for j, o in enumerate(orc):
+            i = lb.n + j
+            gd, od = B.dump_segments(i), o.dump_segments()
+            assert gd == od, f"extra doc {j} pass {rep}: segment dump differs: {first_diff(gd, od)}"
+            assert dg[i] == o.digest()
