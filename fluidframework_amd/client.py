@@ -495,6 +495,16 @@ class Client:
               "type": 2}
         return self.applyLocalOp(op if combiningOp is None else {"combiningOp": combiningOp, **op})
 
+    def annotateMarkerNotifyConsensus(self, markerId, props):
+        """Client.annotateMarkerNotifyConsensus (client.ts:155-181): a local consensus annotate of the marker carrying
+        `markerId` -- each key gets {value: undefined, seq: -1} until the op's ack completes it with the ack's seq
+        (updateConsensusProperty, client.ts:1050-1058); returns the op to send.  (The reference's consensus callback,
+        an application notification at a later minimum sequence number, is not part of the replayed state.)"""
+        op = {"combiningOp": {"name": "consensus"}, "props": props, "relativePos1": {"id": markerId, "before": True},
+              "relativePos2": {"id": markerId}, "type": 2}
+        self.applyLocalOp(dict(op, notifyConsensus=True))
+        return op
+
     def annotateRangeLocal(self, start, end, props, combiningOp=None):
         """annotateRangeLocal (client.ts:206): the keys stay pending on the annotated segments until the
         op's ack (a "rewrite" combiningOp: pendingRewriteCount; other combiningOps are rejected by the

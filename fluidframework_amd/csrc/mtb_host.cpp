@@ -29,6 +29,7 @@
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
+#include <set>
 #include <vector>
 
 #include "../../include/mtb.h"
@@ -705,6 +706,7 @@ struct CellStore {
 // ------------------------------------------------------------------ host mirror of a document
 struct HostDoc {
   DocVals vals;  // property values the document can hold (incr result tables)
+  std::set<std::string> pendingConsensus;  // Client.pendingConsensus: marker ids (JSON) of annotateMarkerNotifyConsensus
   std::vector<std::string> longIds;
   std::unordered_map<std::string, uint16_t> shortOf;
   std::string observer;
@@ -1085,11 +1087,26 @@ void pack_delta(mtb_dev* b, HostDoc& d, const hj::Value& op, mtb_op base, std::v
           b->in.nan();
           r.props = b->in.incr_props(r.props, dv, mv, &d.vals);
         } else if (name && name->kind == hj::Value::kStr && name->s == u"consensus") {
-          // a local consensus value is {value: undefined, seq: -1}, completed in place at the ack (client.ts:1050-1058)
-          if ((r.flags & MTB_F_LOCAL) || r.client == (uint16_t)MTB_LOCAL_CLIENT)
-            raise(MTB_E_UNSUPPORTED, "unsupported: local consensus annotate (its value object is completed in place at the ack)");
+          // A live client's own consensus annotate is its value {value: undefined, seq: -1}, completed in place at
+          // the ack through Client.pendingConsensus (client.ts:1050-1058), which only annotateMarkerNotifyConsensus
+          // fills (:155-181; the op createAnnotateMarkerOp makes, flagged "notifyConsensus": true by the caller).
+          // Any other local consensus annotate leaves a minimum-sequence-number listener that dereferences the
+          // missing entry: the reference throws later, refused here.
+          int cseq = (int)r.seq;
+          if (r.client == (uint16_t)MTB_LOCAL_CLIENT)
+            raise(MTB_E_UNSUPPORTED, "unsupported: consensus annotate on a detached client");
+          if (r.flags & MTB_F_LOCAL) {
+            const hj::Value* nc = member(op, u"notifyConsensus");
+            const hj::Value* r1 = member(op, u"relativePos1");
+            const hj::Value* id = r1 && r1->kind == hj::Value::kObj ? member(*r1, u"id") : nullptr;
+            if (!nc || nc->kind != hj::Value::kBool || !nc->b || !id || member(*comb, u"defaultValue"))
+              raise(MTB_E_UNSUPPORTED, "unsupported: local consensus annotate other than annotateMarkerNotifyConsensus "
+                                       "(the reference throws at a later minimum sequence number update)");
+            d.pendingConsensus.insert(hj::dump(*id));
+            cseq = -1;  // UnassignedSequenceNumber
+          }
           r.flags |= MTB_F_CONSENSUS;
-          r.props = b->in.consensus_props(r.props, member(*comb, u"defaultValue"), (int)r.seq);
+          r.props = b->in.consensus_props(r.props, member(*comb, u"defaultValue"), cseq);
           d.vals.propsSeen.push_back(r.props);
         } else {
           raise(MTB_E_UNSUPPORTED, "unsupported: combiningOp other than rewrite / incr / consensus");
@@ -3467,6 +3484,28 @@ void apply_msg(mtb_dev* b, HostDoc& d, const hj::Value& msg) {
           mtb_op r = base;
           r.type = MTB_OP_ACK;
           r.pos2 = t && t->kind == hj::Value::kNum ? (uint32_t)(int)t->n : 0xFFFFFFFFu;
+          // updateConsensusProperty (client.ts:1050-1058): the registered marker's values at the ack's seq
+          const hj::Value* comb = member(op, u"combiningOp");
+          const hj::Value* cname = comb && comb->kind == hj::Value::kObj ? member(*comb, u"name") : nullptr;
+          if (r.pos2 == 2 && cname && cname->kind == hj::Value::kStr && cname->s == u"consensus") {
+            const hj::Value* r1 = member(op, u"relativePos1");
+            const hj::Value* id = r1 && r1->kind == hj::Value::kObj ? member(*r1, u"id") : nullptr;
+            if (!id || !d.pendingConsensus.count(hj::dump(*id)))
+              raise(MTB_E_UNSUPPORTED, "unsupported: consensus ack without annotateMarkerNotifyConsensus (the reference "
+                                       "throws at a later minimum sequence number update)");
+            const hj::Value* props = member(op, u"props");
+            hj::Value empty;
+            empty.kind = hj::Value::kObj;
+            r.props = b->in.consensus_props(b->in.props(props && props->kind == hj::Value::kObj ? *props : empty),
+                                            nullptr, (int)r.seq);
+            d.vals.propsSeen.push_back(r.props);
+            r.flags |= MTB_F_CONSENSUS;
+            // the registered marker (consensusInfo.marker), by its id's ordinal + 1: completed whether or not the
+            // op's range reached it (a removed marker's relative range covers the next segment)
+            auto key = marker_key(id);
+            auto mo = key ? d.markerOrd.find(*key) : d.markerOrd.end();
+            r.payload = mo == d.markerOrd.end() ? 0u : mo->second + 1;
+          }
           recs.push_back(r);
         };
         const hj::Value* t = member(*contents, u"type");

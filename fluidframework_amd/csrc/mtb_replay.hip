@@ -1996,7 +1996,10 @@ struct Eng {
   // ackPendingSegment (mergeTree.ts:1283-1322, BaseSegment.ack mergeTreeNodes.ts:439-480) for the client's
   // own op sequenced at S: the oldest group's segments get seq S (insert) or removedSeq S (remove; already
   // set when a remote remove overtook it), join the LRU in group order, and their paths' lists are rebuilt.
-  __device__ __forceinline__ void ack_group(int S, int opType) {
+  // cprops: the consensus completion of an acked annotateMarkerNotifyConsensus (the op's keys -> {value:
+  // undefined, seq: S}, Interner::consensus_props; 0: none), applied to the registered marker -- `mk` = its id's
+  // ordinal + 1 -- whether or not the op's range reached it (updateConsensusProperty, client.ts:1050-1058)
+  __device__ __forceinline__ void ack_group(int S, int opType, uint32_t cprops = 0, uint32_t mk = 0) {
     if (pend_n == 0) return;
     bool ack_ow = false;
     const auto e = grp_ent(0);
@@ -2034,6 +2037,25 @@ struct Eng {
       n_mod += 1;
       wsync();
       lru_add(sid, b, sc, S);  // addToLRUSet(segment, seq)
+    }
+    if constexpr (hasMk) {
+      if (COLD(cprops != 0 && mk != 0)) {
+        const uint32_t ord = mk - 1;
+        const uint32_t sid = ord < U(ds->mk_n) ? U(aux[U(ds->mk_map) + ord]) : MTB_NONE;
+        const uint32_t b = sid < seg_used ? U(segp[sid]) : MTB_NONE;
+        if (b < blk_used) {
+          const uint32_t id = lane < MTB_MAXCH ? blk[b].f[F_ID][lane] : MTB_NONE;
+          const unsigned long long m = __ballot(id == (MTB_LEAF | sid));
+          if (m) {
+            const int j = first_set(m);
+            const uint32_t np = props_apply_slow(U(blk[b].f[F_PROPS][j]), cprops, 5);
+            if (bad()) return;
+            memo_old = MTB_NONE;
+            if (lane == 0) blk[b].f[F_PROPS][j] = np;
+            wsync();
+          }
+        }
+      }
     }
     // nodesToUpdate (distinct parents in first-appearance order): blockUpdate re-maps marker ids
     // (mergeTree.ts:1316 -> :2392), annotate acks included
@@ -2552,15 +2574,23 @@ struct Eng {
           if (r == MTB_NONE) { fail(DERR_INCR); return 0; }
           v = r;
         }
-      } else if (COLD(comb == 3)) {
+      } else if (COLD(comb >= 3)) {
         // consensus (properties.ts:46-62): a present value stays -- unless it is an object whose seq is -1,
         // completed in place by the reference (shared with split clones): refused; an absent one takes the
-        // host-made value (Interner::consensus_props; MTB_NONE: a null defaultValue, the reference throws)
+        // host-made value (Interner::consensus_props; MTB_NONE: a null defaultValue, the reference throws).
+        // comb 4: a live client's own annotateMarkerNotifyConsensus (seq -1: such an object's seq stays -1);
+        // comb 5: its completion at the ack (client.ts:1050-1058): the marker's own pending value {value:
+        // undefined, seq: -1} (a consensus value with seq -1, val_falsy bits 2 and 3) takes the ack's seq
         if (at >= 0) {
-          if (sh->tab.val_falsy[sh->pv[at]] & 4) { fail(DERR_CONSENSUS); return 0; }
-          continue;
+          const uint32_t f = sh->tab.val_falsy[sh->pv[at]];
+          if (!(comb == 5 && (f & 12) == 12)) {
+            if (comb != 4 && (f & 4)) { fail(DERR_CONSENSUS); return 0; }
+            continue;
+          }
+        } else if (v == MTB_NONE) {
+          fail(DERR_CONSENSUS);
+          return 0;
         }
-        if (v == MTB_NONE) { fail(DERR_CONSENSUS); return 0; }
       }
       if (v == MTB_NONE) {
         if (at >= 0) {
@@ -4074,8 +4104,10 @@ struct Eng {
         t0 = PROF_T();
         const uint32_t dfrom = delta_used;
         if (isLive) sh->memo[2] = 0;
-        node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props,
-                 o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_COMB) >> 2);  // 1 rewrite, 2 incr, 3 consensus
+        // 1 rewrite, 2 incr, 3 consensus, 4 a live client's own consensus (annotateMarkerNotifyConsensus)
+        int comb = o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_COMB) >> 2;
+        if (isLive && comb == 3 && local) comb = 4;
+        node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props, comb);
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);
@@ -4093,7 +4125,7 @@ struct Eng {
         break;
       }
       case MTB_OP_ACK:
-        if (isLive) ack_group(S, (int)o.pos2);
+        if (isLive) ack_group(S, (int)o.pos2, (o.flags & MTB_F_COMB) == MTB_F_CONSENSUS ? o.props : 0u, o.payload);
         zamboni_p();
         break;
       case MTB_OP_REGEN:

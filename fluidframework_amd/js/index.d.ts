@@ -67,6 +67,7 @@ export declare class Client {
   regeneratePendingOp(resetOp: Record<string, unknown> | string, segmentGroup?: unknown): Record<string, unknown>;
   annotateRangeLocal(start: number, end: number, props: Record<string, unknown>, combiningOp?: unknown): Record<string, unknown>;
   annotateMarker(markerId: string, props: Record<string, unknown>, combiningOp?: unknown): Record<string, unknown>;
+  annotateMarkerNotifyConsensus(markerId: string, props: Record<string, unknown>): Record<string, unknown>;
   startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
   load(runtime: { clientId?: string } | undefined,
        storage: { readBlob(path: string): Promise<ArrayBufferLike | Uint8Array | string> }): Promise<{ catchupOpsP: Promise<unknown[]> }>;

@@ -248,6 +248,16 @@ class Client {
     return this.applyLocalOp(combiningOp === undefined ? op : { combiningOp, ...op });
   }
 
+  /** Client.annotateMarkerNotifyConsensus (client.ts:155-181): each key of `props` is {value: undefined, seq: -1}
+   * on the marker until the op's ack completes it with the ack's seq (updateConsensusProperty, :1050-1058);
+   * returns the op to send. */
+  annotateMarkerNotifyConsensus(markerId, props) {
+    const op = { combiningOp: { name: "consensus" }, props, relativePos1: { id: markerId, before: true },
+      relativePos2: { id: markerId }, type: 2 };
+    this.applyLocalOp({ ...op, notifyConsensus: true });
+    return op;
+  }
+
   /** Client.annotateRangeLocal (client.ts:206): the keys stay pending until the op's ack; returns the op. */
   annotateRangeLocal(start, end, props, combiningOp) {
     // createAnnotateRangeOp (opBuilder.ts:52-65): a local "rewrite" is pending (pendingRewriteCount) until its ack

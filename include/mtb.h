@@ -199,7 +199,10 @@ int mtb_apply_msg_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t
  * client.ts:641-662).  A local annotate's keys stay pending on its segments until its ack (remote annotates
  * leave them alone, segmentPropertiesManager.ts:60-157; a local rewrite annotate counts as a pending rewrite).
  * Marker-relative positions resolve in the client's own view.  Matrix and catch-up batches are
- * MTB_E_UNSUPPORTED (a live client's own ops are not tracked as catch-up messages). */
+ * MTB_E_UNSUPPORTED (a live client's own ops are not tracked as catch-up messages).  A consensus annotate is
+ * accepted as Client.annotateMarkerNotifyConsensus makes it (client.ts:155-181: createAnnotateMarkerOp's op,
+ * flagged with the member "notifyConsensus": true, which is not part of the op sent): its values are
+ * {value: undefined, seq: -1} until its ack completes them with the ack's seq (client.ts:1050-1058). */
 int mtb_local_op_json(mtb_batch* b, uint32_t doc, const char* json_utf8, size_t len);
 /* A detached edit before collaboration (TestClient.insertTextLocal / removeRangeLocal / annotateRangeLocal
  * while the collab window is not collaborating, client.ts:196-247 with getLocalSequenceNumber() =

@@ -979,7 +979,9 @@ Comb parse_comb(const JVal* comb) {
 // whose seq is -1 gets seq (in place: the op's defaultValue object is shared by the op's segments alone, so a
 // copy equals it; a previous value may be shared with other segments by split clones -- not restated); any
 // other value stays.  A null defaultValue makes the reference throw reading its seq.
-static JVal combine_consensus(const Comb& c, const JVal* prev, int seq) {
+// `complete`: the ack of this client's own annotateMarkerNotifyConsensus (client.ts:1050-1058), whose marker's
+// value object (its own, made by the local op) is completed in place -- not a shared object
+static JVal combine_consensus(const Comb& c, const JVal* prev, int seq, bool complete = false) {
   const bool fromPrev = prev && prev->t != JVal::Undef;
   JVal cur = fromPrev ? *prev : c.defaultValue;
   if (cur.t == JVal::Undef) {
@@ -992,7 +994,9 @@ static JVal combine_consensus(const Comb& c, const JVal* prev, int seq) {
   if (cur.t == JVal::Null) fail_unsupported("consensus with a null defaultValue (the reference throws reading its seq)");
   const JVal* cs = cur.t == JVal::Obj ? obj_get(cur.obj, u"seq") : nullptr;
   if (cs && cs->t == JVal::Num && cs->num == -1) {
-    if (fromPrev) fail_unsupported("consensus over a property value object whose seq is -1 (mutates a shared object)");
+    if (seq == UnassignedSeq) return cur;  // (a local op sets seq -1 to -1)
+    if (fromPrev && !complete)
+      fail_unsupported("consensus over a property value object whose seq is -1 (mutates a shared object)");
     obj_set(cur.obj, u"seq", JVal::number(seq));
   }
   return cur;
@@ -1052,7 +1056,7 @@ static JVal combine_incr(const Comb& c, const JVal* prev) {
 }
 // deltaKeys (when given) receives the keys of the returned propertyDeltas, in their insertion order
 static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq = UniversalSeq, bool collaborating = false,
-                       std::vector<u16str>* deltaKeys = nullptr) {
+                       std::vector<u16str>* deltaKeys = nullptr, bool complete = false) {
   s->hasPropManager = true;
   if (!s->props) s->props = JObj();
   if (collaborating && s->pendingRewrite > 0 && seq != UnassignedSeq && seq != UniversalSeq) return;
@@ -1086,7 +1090,7 @@ static void applyProps(Seg* s, const JObj& newProps, const Comb& comb, int seq =
       }
     }
     addDelta(kv.first);
-    if (comb.kind == Comb::Consensus) obj_set(old, kv.first, combine_consensus(comb, obj_get(old, kv.first), seq));
+    if (comb.kind == Comb::Consensus) obj_set(old, kv.first, combine_consensus(comb, obj_get(old, kv.first), seq, complete));
     else if (combining) obj_set(old, kv.first, combine_incr(comb, obj_get(old, kv.first)));
     else if (kv.second.t == JVal::Null) obj_del(old, kv.first);
     else obj_set(old, kv.first, kv.second);
@@ -1574,6 +1578,15 @@ void Doc::applyMsgCore(const JVal& msg) {
         const JVal* cname = comb && comb->t == JVal::Obj ? obj_get(comb->obj, u"name") : nullptr;
         const bool rw = cname && cname->t == JVal::Str && cname->str == u"rewrite";
         mt.ackPendingSegment(t && t->t == JVal::Num ? (int)t->num : -1, pr && pr->t == JVal::Obj ? &pr->obj : nullptr, seq, rw);
+        // updateConsensusProperty (client.ts:1050-1058): the registered marker's values at the ack's seq
+        if (t && t->t == JVal::Num && (int)t->num == 2 && cname && cname->t == JVal::Str && cname->str == u"consensus") {
+          const JVal* r1 = obj_get(op.obj, u"relativePos1");
+          auto key = r1 && r1->t == JVal::Obj ? MergeTree::markerIdKey(obj_get(r1->obj, u"id")) : std::nullopt;
+          auto it = key ? pendingConsensus.find(*key) : pendingConsensus.end();
+          if (it == pendingConsensus.end())
+            fail_unsupported("consensus ack without annotateMarkerNotifyConsensus (the reference throws later)");
+          applyProps(it->second, pr && pr->t == JVal::Obj ? pr->obj : JObj(), parse_comb(comb), seq, true, nullptr, true);
+        }
       };
       const JVal* t = obj_get(contents->obj, u"type");
       if (t && t->t == JVal::Num && (int)t->num == 3) {
@@ -1681,11 +1694,16 @@ std::string Doc::removeLocalOp(int start, int end) {
   mt.markRangeRemoved(start, end, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   return "{\"pos1\":" + std::to_string(start) + ",\"pos2\":" + std::to_string(end) + ",\"type\":1}";
 }
-std::string Doc::annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp) {
+std::string Doc::annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp, bool notifyConsensus) {
   if (!mt.window.collaborating) throw OracleError(-1, "not collaborating");
   const Comb comb = parse_comb(combiningOp);  // annotateRangeLocal(start, end, props, combiningOp)
-  // (a local consensus value is {value: undefined, seq: -1}, completed in place at the ack: not restated)
-  if (comb.kind == Comb::Consensus) fail_unsupported("local consensus annotate");
+  // A local consensus value is {value: undefined, seq: -1}, completed in place at the ack -- through
+  // Client.pendingConsensus, which only annotateMarkerNotifyConsensus fills (client.ts:155-181).  Any other local
+  // consensus annotate leaves a minimum-sequence-number listener that dereferences the missing entry (the reference
+  // throws at a later update): not restated.
+  if (comb.kind == Comb::Consensus && !notifyConsensus)
+    fail_unsupported("local consensus annotate other than annotateMarkerNotifyConsensus (the reference throws at a "
+                     "later minimum sequence number update)");
   validLocalRange(start, end, mt.length(), false);
   mt.annotateRange(start, end, props, comb, mt.window.currentSeq, mt.window.clientId, UnassignedSeq);
   JVal pv;
@@ -1719,8 +1737,27 @@ std::string Doc::localOpJson(const JVal& op) {
   } else if (type == 2) {
     const JVal* pr = obj_get(op.obj, u"props");
     const JVal* comb = obj_get(op.obj, u"combiningOp");
+    // annotateMarkerNotifyConsensus (client.ts:155-181): the op createAnnotateMarkerOp makes, flagged by the
+    // caller with "notifyConsensus": true (not part of the op sent)
+    const JVal* nc = obj_get(op.obj, u"notifyConsensus");
+    const bool notify = nc && nc->t == JVal::True;
+    Seg* marker = nullptr;
+    if (notify) {
+      const JVal* r1 = obj_get(op.obj, u"relativePos1");
+      auto key = r1 && r1->t == JVal::Obj ? MergeTree::markerIdKey(obj_get(r1->obj, u"id")) : std::nullopt;
+      auto it = key ? mt.idToSegment.find(*key) : mt.idToSegment.end();
+      if (it == mt.idToSegment.end()) throw OracleError(-1, "annotateMarkerNotifyConsensus: marker without id");
+      marker = it->second;
+      pendingConsensus[*key] = marker;
+    }
     out = annotateLocalOp(pos(u"pos1", u"relativePos1", false), pos(u"pos2", u"relativePos2", false),
-                          pr && pr->t == JVal::Obj ? pr->obj : JObj(), comb && comb->t != JVal::Undef ? comb : nullptr);
+                          pr && pr->t == JVal::Obj ? pr->obj : JObj(), comb && comb->t != JVal::Undef ? comb : nullptr,
+                          notify);
+    if (notify) {
+      JVal sent = op;
+      obj_del(sent.obj, u"notifyConsensus");
+      return json_stringify(sent);
+    }
   } else {
     throw OracleError(-8, "unsupported local op type");
   }

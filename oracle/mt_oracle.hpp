@@ -300,7 +300,11 @@ class Doc {
   // and returned as the IMergeTreeOp JSON to submit; acked by applyMsg of the sequenced message
   std::string insertLocalOp(int pos, const JVal& segSpec);
   std::string removeLocalOp(int start, int end);
-  std::string annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp = nullptr);
+  std::string annotateLocalOp(int start, int end, const JObj& props, const JVal* combiningOp = nullptr,
+                              bool notifyConsensus = false);
+  // Client.pendingConsensus (client.ts:155-181, 1050-1058): marker id -> the marker annotateMarkerNotifyConsensus
+  // annotated; the ack of a consensus annotate naming it completes the marker's values at the ack's seq
+  std::map<std::string, Seg*> pendingConsensus;
   // a live client's local op given as the IMergeTreeOp JSON it sends (pos1 / pos2 or marker-relative
   // relativePos1 / relativePos2, resolved in the local view by getValidOpRange, client.ts:527-547); returns
   // the op to send (the input itself when it names relative positions, as Client.annotateMarker does)

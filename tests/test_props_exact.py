@@ -6,6 +6,7 @@ import json
 import pytest
 
 import props_cases as pc
+from test_reference_kats import msg
 
 
 def _run(init, msgs):
@@ -64,3 +65,44 @@ def test_consensus_beside_cv_like_values_is_refused_at_apply():
         B[0].applyMsg(msg("a", 1, 0, first))
         with pytest.raises(MergeTreeError, match=r"\{value, seq\}"):
             B[0].applyMsg(msg("a", 2, 1, second))
+
+
+def _consensus_marker_log():
+    """A live client "me" inserts a marker with id "m1" (acked), annotates it with annotateMarkerNotifyConsensus
+    (client.ts:155-181) while remote ops arrive, and receives the ack: the value is {value: undefined, seq: -1}
+    (JSON {"seq": -1}) until the ack, then completed in place with the ack's seq (client.ts:1050-1058)."""
+    marker = {"type": 0, "pos1": 1, "seg": {"marker": {"refType": 1}, "props": {"markerId": "m1"}}}
+    notify = {"type": 2, "props": {"k": 1, "j": 2}, "relativePos1": {"id": "m1", "before": True},
+              "relativePos2": {"id": "m1"}, "combiningOp": {"name": "consensus"}, "notifyConsensus": True}
+    return marker, notify
+
+
+def test_local_consensus_through_annotate_marker_notify_consensus():
+    from pyoracle import OracleDoc
+    marker, notify = _consensus_marker_log()
+    o = OracleDoc(verify=True)
+    o.insert_text_local(0, "abcd")
+    o.start_collab("me")
+    sent_marker = o.local_op_json(marker)
+    o.apply_msg(msg("me", 1, 0, sent_marker))
+    o.apply_msg(msg("x", 2, 1, {"type": 2, "pos1": 0, "pos2": 5, "props": {"j": 7}}))
+    sent = o.local_op_json(notify)
+    assert "notifyConsensus" not in sent and sent["relativePos1"] == {"id": "m1", "before": True}
+    rows = [r[7] for r in json.loads("[" + ",".join(o.dump_segments().splitlines()[1:]) + "]") if r[1] == "M"]
+    assert rows == [{"markerId": "m1", "j": 7, "k": {"seq": -1}}], rows  # (j stays: a present value stays)
+    o.apply_msg(msg("x", 3, 2, {"type": 0, "pos1": 0, "seg": "Z"}))
+    o.apply_msg(msg("me", 4, 2, sent, msn=2))
+    rows = [r[7] for r in json.loads("[" + ",".join(o.dump_segments().splitlines()[1:]) + "]") if r[1] == "M"]
+    assert rows == [{"markerId": "m1", "j": 7, "k": {"seq": 4}}], rows
+
+
+def test_plain_local_consensus_is_refused():
+    from pyoracle import OracleDoc
+    marker, notify = _consensus_marker_log()
+    o = OracleDoc()
+    o.insert_text_local(0, "abcd")
+    o.start_collab("me")
+    o.apply_msg(msg("me", 1, 0, o.local_op_json(marker)))
+    del notify["notifyConsensus"]
+    with pytest.raises(Exception, match="annotateMarkerNotifyConsensus"):
+        o.local_op_json(notify)
