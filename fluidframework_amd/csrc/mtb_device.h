@@ -261,7 +261,9 @@ struct Tables {
                              // lengths (partialLengths.ts:543-577 addSeq below newer entries): unsupported
 #define DERR_INCR 24         // an incr annotate over a value its op's result table lacks (engine invariant)
 #define DERR_CONSENSUS 26    // a consensus annotate over an object value whose seq is -1 (completed in place, shared
-                             // with split clones) or, with a null defaultValue, over a segment lacking the key
+                             // with split clones)
+#define DERR_CONS_NULL 27    // a consensus annotate with a null defaultValue over a segment lacking the key: the
+                             // reference throws reading the null's seq (properties.ts:56-57), so does the engine
 // ticket scheduler words (mtb_replay_tick_kernel): queue q's ticket counter at MTB_SCHED_TICK * q (one
 // 128-byte line each, q < 8), the abort flag, then per-document progress from MTB_SCHED_HDR
 #define MTB_SCHED_TICK 32

@@ -2032,8 +2032,9 @@ std::string derr_text(int e) {
     case DERR_RELPOS: return "unsupported: relative position whose marker is not in the document (posFromRelativePos -1) or resolves below 0";
     case DERR_INCR: return "internal: incr annotate over a value missing from its result table (Interner::incr_props)";
     case DERR_CONSENSUS: return "unsupported: consensus annotate over an object value whose seq is -1 (the reference completes "
-                                "it in place, shared with split clones), or with a null defaultValue over a segment lacking the key "
-                                "(the reference throws reading its seq)";
+                                "it in place, shared with split clones)";
+    case DERR_CONS_NULL: return "TypeError: Cannot read properties of null (reading 'seq') (properties.ts:56-57: a consensus "
+                                "annotate with a null defaultValue over a segment lacking the key; the reference throws here)";
     case DERR_STALE: return "unsupported: summary body segment older than entries already in its blocks' partial lengths "
                             "(the reference's addSeq leaves their cumulative lengths stale, partialLengths.ts:543-577)";
     default: return "device error " + std::to_string(e);
@@ -2042,7 +2043,7 @@ std::string derr_text(int e) {
 int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
   if ((e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) || e == DERR_CAP_DELTA || e == DERR_CAP_PEND) return MTB_E_CAPACITY;
-  if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN || e == DERR_ASSERT_MKID) return MTB_E_ASSERT;
+  if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN || e == DERR_ASSERT_MKID || e == DERR_CONS_NULL) return MTB_E_ASSERT;
   if (e == DERR_SCHED) return MTB_E_INTERNAL;
   return MTB_E_UNSUPPORTED;
 }

@@ -2588,7 +2588,7 @@ struct Eng {
             continue;
           }
         } else if (v == MTB_NONE) {
-          fail(DERR_CONSENSUS);
+          fail(DERR_CONS_NULL);
           return 0;
         }
       }

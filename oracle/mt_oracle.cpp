@@ -991,7 +991,9 @@ static JVal combine_consensus(const Comb& c, const JVal* prev, int seq, bool com
     obj_set(cv.obj, u"seq", JVal::number(seq));
     return cv;
   }
-  if (cur.t == JVal::Null) fail_unsupported("consensus with a null defaultValue (the reference throws reading its seq)");
+  if (cur.t == JVal::Null)  // (cv.seq of null: the reference's own failure, as an assert is)
+    throw OracleError(-4, "TypeError: Cannot read properties of null (reading 'seq') (properties.ts:56-57: a "
+                          "consensus annotate with a null defaultValue over a segment lacking the key)");
   const JVal* cs = cur.t == JVal::Obj ? obj_get(cur.obj, u"seq") : nullptr;
   if (cs && cs->t == JVal::Num && cs->num == -1) {
     if (seq == UnassignedSeq) return cur;  // (a local op sets seq -1 to -1)

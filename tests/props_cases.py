@@ -99,10 +99,14 @@ REFUSED = [
      [_ins("a", 1, 0, 0, "xy", {"k": {"seq": -1}}),
       msg("a", 2, 1, {"type": 2, "pos1": 0, "pos2": 3, "props": {"k": 1}, "combiningOp": {"name": "consensus"}})],
      "seq is -1"),
+]
+
+# (name, initial text, messages, error substring): the reference itself throws at the last message (JS TypeError)
+THROWS = [
     ("consensus with a null defaultValue over a segment lacking the key", "abcd",
      [msg("a", 1, 0, {"type": 2, "pos1": 0, "pos2": 3, "props": {"k": 1},
                       "combiningOp": {"name": "consensus", "defaultValue": None}})],
-     "null defaultValue"),
+     "TypeError"),
 ]
 
 

@@ -7,7 +7,8 @@ Bar: bit-exact against the oracle (canonical dump, text, state digest, SnapshotV
 * the hand-derived known answers of tests/props_cases.py (CPU: tests/test_props_exact.py), rows included;
 * generated logs (helpers.make_props_log), both length modes, two flushes, then a SnapshotV1 round trip
   loaded by the engine and continued;
-* the refused cases (an object value whose seq is -1, a null defaultValue): the engine fails that document
+* the refused case (an object value whose seq is -1) and the reference's own failure (a null consensus
+  defaultValue: a TypeError there, MTB_E_ASSERT here): the engine fails that document
   loudly (DERR_CONSENSUS), the other documents of the batch replay."""
 import pytest
 
@@ -53,7 +54,7 @@ def test_refused_cases_fail_their_documents_only():
     from fluidframework_amd import MergeTreeBatch, MergeTreeError
     from pyoracle import OracleDoc
     good = pc.CASES[9]
-    docs = [c[1:3] for c in pc.REFUSED] + [good[1:3]]
+    docs = [c[1:3] for c in pc.REFUSED + pc.THROWS] + [good[1:3]]
     B = MergeTreeBatch(len(docs))
     for i, (init, msgs) in enumerate(docs):
         B[i].insertTextLocal(0, init)
@@ -62,6 +63,15 @@ def test_refused_cases_fail_their_documents_only():
             B[i].applyMsg(m)
     with pytest.raises(MergeTreeError, match="consensus"):
         B.flush()
+    for c in pc.REFUSED + pc.THROWS:  # each alone: its own error (THROWS: the reference's own failure, MTB_E_ASSERT)
+        one = MergeTreeBatch(1)
+        one[0].insertTextLocal(0, c[1])
+        one[0].startOrUpdateCollaboration("obs")
+        for m in c[2]:
+            one[0].applyMsg(m)
+        with pytest.raises(MergeTreeError, match=c[3] if c in pc.THROWS else "unsupported") as ei:
+            one.flush()
+        assert ei.value.code == (-4 if c in pc.THROWS else -6), (c[0], ei.value.code)
     o = OracleDoc()
     o.insert_text_local(0, good[1])
     o.start_collab("obs")

@@ -38,6 +38,13 @@ def test_refused_cases_on_the_oracle(case):
         _run(init, msgs)
 
 
+@pytest.mark.parametrize("case", pc.THROWS, ids=[c[0] for c in pc.THROWS])
+def test_reference_failures_on_the_oracle(case):
+    name, init, msgs, err = case
+    with pytest.raises(Exception, match=err):
+        _run(init, msgs)
+
+
 def test_consensus_values_coalesce_after_a_summary_round_trip():
     """Live, two {value: undefined, seq} values never match (b.value is undefined); loaded from a summary they
     are {"seq": S} objects, which do: the loaded document's own summary coalesces them."""
