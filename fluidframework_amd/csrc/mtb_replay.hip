@@ -1499,11 +1499,15 @@ struct Eng {
   // places the segment, before its own entries are appended.
   // A phantom's removal entries (seq = its rseq) are in the exact list but not in the reference's partials: a
   // removal entry newer than S counts only when the removals of that op under N outweigh N's phantoms of it.
+  // Round 6: only an update that finds an entry AT S is stale -- addSeq then replaces that entry's seglen while
+  // the later entries keep lengths built on the old one (:569-575); a new entry below newer ones goes through
+  // PartialSequenceLengthsSet.addOrUpdate, which raises them (:24-47), so the exact lists agree.  (The oracle
+  // counts the same condition: MergeTree::counters.staleDeficits.)
   __device__ __forceinline__ bool stale_at(int d, int S) {
     uint32_t loff, lcnt, lcap;
     meta_of(d - 1, loff, lcnt, lcap);
     const uint32_t slot = U(sh->slot[d - 1]), N = U(sh->path[d]);
-    bool st = false, rem = false;
+    bool st = false, rem = false, atS = false;
     for (uint32_t base = 0; base < lcnt; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       if (i < lcnt) {
@@ -1512,6 +1516,7 @@ struct Eng {
           if (((uint32_t)e.ck >> 16 & 0xF) == WK_OVERLAP || e.delta < 0) rem = true;  // (a removal's entries)
           else st = true;
         }
+        atS |= e.seq == S && ((uint32_t)e.ck >> 20) == slot && ((uint32_t)e.ck >> 16 & 0xF) == WK_MAIN;
       }
     }
     if constexpr (hasPh) {
@@ -1519,12 +1524,18 @@ struct Eng {
         const uint32_t n = U(aux[ph_off]);
         for (uint32_t base = 0; base < n; base += 64) {
           const uint32_t i = base + (uint32_t)lane;
-          if (i < n) st |= aux[ph_off + 2 + 8 * i] == N && (int)aux[ph_off + 2 + 8 * i + 5] > S;
+          if (i < n) {
+            const bool mine = aux[ph_off + 2 + 8 * i] == N;
+            st |= mine && (int)aux[ph_off + 2 + 8 * i + 5] > S;
+            atS |= mine && (int)aux[ph_off + 2 + 8 * i + 5] == S;
+          }
         }
+        if (__ballot(atS) == 0) return false;
         if (__ballot(st) == 0 && __ballot(rem) != 0) st = COLD(ph_rem_stale(loff, lcnt, slot, N, S));
         return __ballot(st) != 0;
       }
     }
+    if (__ballot(atS) == 0) return false;
     return __ballot(st || rem) != 0;
   }
   // some op newer than S removed under N more than N's phantoms of that op (lane-uniform result)
@@ -1683,7 +1694,9 @@ struct Eng {
       add_len_levels(0, d, d, candLen);
       if constexpr (isLoad) {
         ld_stale = 0;
-        if (C != -2)  // (a collaborating client's segment: update() on the path, see stale_at)
+        // (a collaborating client's segment: update() on the path, see stale_at; one removed at its own seq adds
+        // nothing at S, so it replaces no seglen)
+        if (C != -2 && (int)U(sh->nseg[F_RSEQ]) != S)
           for (int i = 1; i <= d; i++)
             if (stale_at(i, S)) ld_stale |= 1u << i;
         load_entries(d, S, C);

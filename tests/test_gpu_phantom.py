@@ -103,8 +103,9 @@ def _tail_summary(seed, n_noncollab, n_client, chunk_len, msn=10, seq=40):
 
 def _load_and_continue(blobs, tail, new_mode, chunk=0):
     """Load `blobs` on the oracle and on the engine, then apply `tail`.  The reference's outcome decides:
-    * a body insert whose incremental update meets newer entries below the root (the oracle counts these: addSeq
-      leaves stale cumulative lengths) -- the engine refuses the document (DERR_STALE);
+    * a body insert whose incremental update replaces the seglen of an existing entry below newer ones, below the
+      root (the oracle counts these, stale_deficits: addSeq leaves the later cumulative lengths short) -- the engine
+      refuses the document (DERR_STALE); an update that only inserts an entry below newer ones is exact;
     * "MergeTree insert failed" at load or at a later op -- the engine fails the same step;
     * otherwise the engine's state equals the oracle's after the load and after the tail.
     Returns "stale", "failed" or "equal" (plus the number of phantom body segments)."""
@@ -120,7 +121,7 @@ def _load_and_continue(blobs, tail, new_mode, chunk=0):
     except Exception as e:
         assert "MergeTree insert failed" in str(e), str(e)
         ofail = str(e)
-    if o.stale_updates():
+    if o.stale_deficits():
         with pytest.raises(MergeTreeError, match="stale"):
             B.flush()
         return "stale"
