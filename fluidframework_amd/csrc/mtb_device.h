@@ -199,8 +199,8 @@ struct DocState {     // 448 bytes
   uint32_t pend_cap;    // directory entries (a power of two, 0: none yet; doubles when full)
   uint32_t mk_all;      // aux offset of [n, cap, (segment, ordinal)*]: every marker inserted with an id (0: none)
   uint32_t pad3[4];
-  // phantom partial lengths of a loaded summary's removed collaborator-inserted body segments (DSF_PHANTOM):
-  // aux offset of [n, cap, (block, removedSeq, length, removedClientIds[0], removers list, -, -, -) * cap]
+  // phantom partial lengths and partial-length deficits of a loaded summary's collaborator-inserted body segments
+  // (DSF_PHANTOM): aux offset of [n, cap, 8-word entry * cap], entry kinds PH_* below (mtb_replay.hip)
   uint32_t ph;
   uint32_t pad4[15];
 };
@@ -258,7 +258,8 @@ struct Tables {
 #define DERR_SCHED 22      // a document without an error did not run all of its records (engine invariant)
 #define DERR_ASSERT_MKID 23  // 0x5ad "Cannot change the markerId of an existing marker" (mergeTree.ts:1912-1918)
 #define DERR_STALE 25        // a summary body insert whose incremental partial-length update leaves stale cumulative
-                             // lengths (partialLengths.ts:543-577 addSeq below newer entries): unsupported
+                             // lengths (partialLengths.ts:543-577) in a document without a deficit table (engine
+                             // invariant: the host gives every load with collaborating body segments one)
 #define DERR_INCR 24         // an incr annotate over a value its op's result table lacks (engine invariant)
 #define DERR_CONSENSUS 26    // a consensus annotate over an object value whose seq is -1 (completed in place, shared
                              // with split clones)
@@ -278,6 +279,13 @@ struct Tables {
 #define MTB_GRP_REWRITE 0x80000000u  // pending ANNOTATE group / orphan props word: the local op was a rewrite
 #define DSF_OBS_SHIFT 16  // flags >> 16: the reference's short id of the engine's client 0 (a loaded summary's
                           // observer; mtb_host.cpp HostDoc::obsRef), mapped back by the digest
+// DocState.ph table entry kinds (word 6): a phantom insert, a main-set deficit (refSeq >= t), a client-set
+// deficit (client c, refSeq < t), a main-set deficit copied down into minLength (always)
+#define PH_PHANTOM 0u
+#define PH_DEF_MAIN 1u
+#define PH_DEF_CLI 2u
+#define PH_DEF_MIN 3u
+#define PH_NOSEQ 0x7FFFFFFF
 #define DSF_PHANTOM 8      // a loaded summary left phantom partial lengths (DocState.ph; mtb_replay.hip)
 #define DSF_MKDUP 4        // a marker id is carried by two markers: blockUpdate re-maps ids (mergeTree.ts:296-306)
 #define DSF_VARIANT 32     // the document replays on the marker variant (marker ids, phantom tables, irregular keys);

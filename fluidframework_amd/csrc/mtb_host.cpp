@@ -1477,13 +1477,17 @@ void load_one(mtb_dev* b, HostDoc& d, const mtb_blob* blobs, uint32_t nblobs, co
     d.obsRef = so;
   }
   build_load_image(d, hdr);
-  // removed body segments inserted by collaborating clients: their inserts take blockUpdateLength's incremental
-  // path and leave phantom partial lengths (mtb_replay.hip "phantom partial lengths"); the table starts empty
+  // body segments inserted by collaborating clients take blockUpdateLength's incremental path: the removed ones
+  // leave phantom partial lengths, and an update that meets an entry at its own seq below newer ones leaves
+  // deficits (mtb_replay.hip "phantom partial lengths"); the table starts empty and grows on the device
   {
-    size_t nph = 0;
-    for (const LoadSeg& g : body) nph += g.rseq >= 0 && g.client != -2;
-    if (nph && !d.perm) {
-      const uint32_t cap = (uint32_t)std::min<size_t>(8 * nph + 16, 1u << 20);
+    size_t nph = 0, ncol = 0;
+    for (const LoadSeg& g : body) {
+      nph += g.rseq >= 0 && g.client != -2;
+      ncol += g.client != -2;
+    }
+    if (ncol && !d.perm) {
+      const uint32_t cap = (uint32_t)std::min<size_t>(8 * nph + 2 * ncol + 16, 1u << 20);
       d.img.ph = (uint32_t)d.img.aux.size();
       d.img.aux.push_back(0);
       d.img.aux.push_back(cap);
@@ -4928,8 +4932,8 @@ int leaf_length(const HostDoc& d, const Seg& g, int R, int C, bool newMode, int 
 // {"pos", "start", "end", "segment"} per visited leaf (start / end relative to the segment, as the
 // reference's handler receives them), at most `limit` entries (0 = all).
 namespace {
-// The phantom surplus of each block of a loaded document (mtb_replay.hip "phantom partial lengths") in the
-// (R, C) view; empty for the local view and for documents without a table.
+// The phantom surplus less the deficits of each block of a loaded document (mtb_replay.hip "phantom partial
+// lengths") in the (R, C) view; empty for the local view and for documents without a table.
 std::unordered_map<uint32_t, int64_t> phantom_surplus(const HostDoc& d, const DocState& s, int R, int C) {
   std::unordered_map<uint32_t, int64_t> sur;
   if (!s.ph || !(s.flags & DSF_PHANTOM) || C == 0 || (size_t)s.ph + 2 > d.aux.size()) return sur;
@@ -4938,10 +4942,17 @@ std::unordered_map<uint32_t, int64_t> phantom_surplus(const HostDoc& d, const Do
   const int Rl = std::max(R, (int)s.min_seq);
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t* e = d.aux.data() + s.ph + 2 + 8ull * i;
-    bool vis = (int)e[1] <= Rl || (int)(int16_t)e[3] == C;
-    if (!vis && e[4] && e[4] < d.aux.size())
-      for (uint32_t r = 0; r < d.aux[e[4]] && e[4] + 1 + r < d.aux.size() && !vis; r++) vis = (int)d.aux[e[4] + 1 + r] == C;
-    if (vis) sur[e[0]] += e[2];
+    if (e[0] == MTB_NONE) continue;  // (a dead deficit)
+    if (e[6] == PH_PHANTOM) {
+      bool vis = (int)e[1] <= Rl || (int)(int16_t)e[3] == C;
+      if (!vis && e[4] && e[4] < d.aux.size())
+        for (uint32_t r = 0; r < d.aux[e[4]] && e[4] + 1 + r < d.aux.size() && !vis; r++)
+          vis = (int)d.aux[e[4] + 1 + r] == C;
+      if (vis) sur[e[0]] += e[2];
+    } else if (e[6] == PH_DEF_MIN || (e[6] == PH_DEF_MAIN && Rl >= (int)e[1]) ||
+               (e[6] == PH_DEF_CLI && (int)(int16_t)e[3] == C && Rl < (int)e[1])) {
+      sur[e[0]] -= e[2];  // (getPartialLength's shortfall, mtb_replay.hip ph_view)
+    }
   }
   return sur;
 }

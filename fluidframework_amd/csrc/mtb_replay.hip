@@ -1377,13 +1377,19 @@ struct Eng {
   // blockUpdateLength's incremental path (snapshotLoader.ts:242-254 -> mergeTree.ts:2436-2453): every block
   // that update() reaches adds P's cachedLength at P's seq (removedSeq !== seq, partialLengths.ts:636-686) and
   // nothing ever records P's removal there.  The window lists stay exact; the surplus is a per-document table
-  // in the aux arena (DocState.ph): [n, cap, (block, rseq, len, rc0, rcx, -, -, -) * cap].  A block child's
-  // length in a remote view then adds len(P) for each of its entries whose exact-list removal would count:
-  // rseq <= max(refSeq, minSeq), or the viewer is one of P's removers.  Entries follow the reference's
-  // recombinations (PartialSequenceLengths.combine, :256-338): a recombined block of segments has none, a
-  // recombined block of blocks the union of its children's; update() leaves them.
-  __device__ __forceinline__ void ph_add(uint32_t node, uint32_t rseq, uint32_t len, uint32_t rc0, uint32_t rcx,
-                                         uint32_t seq = 0) {
+  // in the aux arena (DocState.ph): [n, cap, entry * cap], 8 words an entry, word 6 its kind:
+  //   PH_PHANTOM  (block, rseq, len, rc0, rcx, seq, 0, inserting client)
+  //   PH_DEF_MAIN (block, t, d, -, -, seq, 1, -)   main-set deficit: lengths at refSeq >= t are short by d
+  //   PH_DEF_CLI  (block, t, d, c, -, seq, 2, -)   client-set deficit: client c's lengths below t are short by d
+  //   PH_DEF_MIN  (block, -, d, -, -, seq, 3, -)   a main-set deficit copied down into minLength: always short
+  // A block child's length in a remote view then adds len(P) for each phantom whose exact-list removal would
+  // count (rseq <= max(refSeq, minSeq), or the viewer is one of P's removers) and takes off each deficit that
+  // applies.  Entries follow the reference's recombinations (PartialSequenceLengths.combine, :256-338): a
+  // recombined block of segments has none (fromLeaves is exact), a recombined block of blocks the union of its
+  // children's phantoms and copied-down deficits (combine sums the children's minLength, :304-308, and rebuilds
+  // the entries from seglen, so every other shortfall is gone); update() leaves them.  Dead entries: block MTB_NONE.
+  __device__ __forceinline__ void ph_add(uint32_t node, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4,
+                                         uint32_t w5 = 0, uint32_t kind = PH_PHANTOM, uint32_t w7 = 0) {
     const uint32_t n = U(aux[ph_off]), cap = U(aux[ph_off + 1]);
     if (n >= cap) {
       const uint32_t ncap = 2 * cap + 8;
@@ -1398,8 +1404,8 @@ struct Eng {
       ph_off = h;
     }
     if (lane < 8) {
-      const uint32_t v = lane == 0 ? node : lane == 1 ? rseq : lane == 2 ? len : lane == 3 ? rc0 : lane == 4 ? rcx
-                         : lane == 5 ? seq : 0u;
+      const uint32_t v = lane == 0 ? node : lane == 1 ? w1 : lane == 2 ? w2 : lane == 3 ? w3 : lane == 4 ? w4
+                         : lane == 5 ? w5 : lane == 6 ? kind : w7;
       aux[ph_off + 2 + 8 * n + lane] = v;
     }
     if (lane == 0) aux[ph_off] = n + 1;
@@ -1411,16 +1417,16 @@ struct Eng {
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       const bool v = i < n;
-      uint32_t e[6];
+      uint32_t e[8];
 #pragma unroll
-      for (int q = 0; q < 6; q++) e[q] = v ? aux[ph_off + 2 + 8 * i + q] : 0u;
+      for (int q = 0; q < 8; q++) e[q] = v ? aux[ph_off + 2 + 8 * i + q] : 0u;
       const bool keep = v && e[0] != node;
       const unsigned long long m = __ballot(keep);
       wsync();  // (the chunk is read before its entries move down: w <= base)
       if (keep) {
         const uint32_t o = w + rank_below(m);
 #pragma unroll
-        for (int q = 0; q < 6; q++) aux[ph_off + 2 + 8 * o + q] = e[q];
+        for (int q = 0; q < 8; q++) aux[ph_off + 2 + 8 * o + q] = e[q];
       }
       w += (uint32_t)__popcll(m);
       wsync();
@@ -1440,14 +1446,17 @@ struct Eng {
     for (uint32_t base = 0; base < n && !err; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       const uint32_t node = i < n ? aux[ph_off + 2 + 8 * i] : MTB_NONE;
+      const uint32_t kind = i < n ? aux[ph_off + 2 + 8 * i + 6] : PH_DEF_MAIN;
       bool match = false;
       for (uint32_t q = 0; q < cnt; q++) match |= node == rlu(kid, (int)q);
+      match &= kind == PH_PHANTOM || kind == PH_DEF_MIN;
       unsigned long long m = __ballot(match);
       while (m && !err) {
         const uint32_t t = base + (uint32_t)first_set(m);
         m &= m - 1;
         const uint32_t o = ph_off + 2 + 8 * t;
-        ph_add(X, U(aux[o + 1]), U(aux[o + 2]), U(aux[o + 3]), U(aux[o + 4]), U(aux[o + 5]));
+        ph_add(X, U(aux[o + 1]), U(aux[o + 2]), U(aux[o + 3]), U(aux[o + 4]), U(aux[o + 5]), U(aux[o + 6]),
+               U(aux[o + 7]));
       }
     }
   }
@@ -1459,6 +1468,31 @@ struct Eng {
       b = U(blk[b].parent);
     }
   }
+  // update() of the blocks `a` and path[lo..hi] (partialLengths.ts:682-684 zamboni): copyDown moves the
+  // main-set deficits whose first short entry is at or below minSeq into minLength
+  __device__ __forceinline__ void ph_touch(uint32_t a, int lo, int hi) {
+    const uint32_t n = U(aux[ph_off]);
+    bool any = false;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      if (i < n && aux[ph_off + 2 + 8 * i + 6] == PH_DEF_MAIN && (int)aux[ph_off + 2 + 8 * i + 1] <= minSeq) {
+        const uint32_t node = aux[ph_off + 2 + 8 * i];
+        bool hit = node == a;
+        for (int q = lo; q <= hi; q++) hit |= node == U(sh->path[q]);
+        if (hit) {
+          aux[ph_off + 2 + 8 * i + 6] = PH_DEF_MIN;
+          any = true;
+        }
+      }
+    }
+    if (__ballot(any)) wsync();
+  }
+  __device__ __forceinline__ void ph_touch_up(uint32_t b) {
+    for (int guard = 0; b != MTB_NONE && guard < MTB_VDEPTH; guard++) {
+      ph_touch(b, 1, 0);
+      b = U(blk[b].parent);
+    }
+  }
   // the surplus of each block child of the record on lanes 0..7 (ids `w`) in the (Rl, C) view, into corr[]
   __device__ __forceinline__ int ph_view(uint32_t w, int count, int Rl, int C) {
     if (lane < MTB_MAXCH) sh->corr[lane] = 0;
@@ -1466,104 +1500,212 @@ struct Eng {
     const uint32_t n = U(aux[ph_off]);
     for (uint32_t base = 0; base < n; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
-      uint32_t node = MTB_NONE, rseq = 0, len = 0, rc0 = 0, rcx = 0;
+      uint32_t node = MTB_NONE, w1 = 0, len = 0, w3 = 0, rcx = 0, kind = 0;
       if (i < n) {
         const uint32_t o = ph_off + 2 + 8 * i;
         node = aux[o];
-        rseq = aux[o + 1];
+        w1 = aux[o + 1];
         len = aux[o + 2];
-        rc0 = aux[o + 3];
+        w3 = aux[o + 3];
         rcx = aux[o + 4];
+        kind = aux[o + 6];
       }
       int j = -1;
       for (int q = 0; q < count; q++)
         if (node == rlu(w, q) && !(node & MTB_LEAF)) j = q;
       if (j >= 0) {
-        bool vis = (int)rseq <= Rl || (int)(int16_t)rc0 == C;
-        if (!vis && rcx) {
-          const uint32_t nr = aux[rcx];
-          for (uint32_t r = 0; r < nr && !vis; r++) vis = (int)aux[rcx + 1 + r] == C;
+        if (kind == PH_PHANTOM) {
+          bool vis = (int)w1 <= Rl || (int)(int16_t)w3 == C;
+          if (!vis && rcx) {
+            const uint32_t nr = aux[rcx];
+            for (uint32_t r = 0; r < nr && !vis; r++) vis = (int)aux[rcx + 1 + r] == C;
+          }
+          if (vis) atomicAdd(&sh->corr[j], (int)len);
+        } else {
+          // getPartialLength (partialLengths.ts:698-716): the main entry latestLeq(refSeq) is short from t on;
+          // the client's cliLatest.len - precedingCli.len is short while precedingCli is below t
+          const bool hit = kind == PH_DEF_MIN || (kind == PH_DEF_MAIN && Rl >= (int)w1) ||
+                           (kind == PH_DEF_CLI && (int)(int16_t)w3 == C && Rl < (int)w1);
+          if (hit) atomicAdd(&sh->corr[j], -(int)len);
         }
-        if (vis) atomicAdd(&sh->corr[j], (int)len);
       }
     }
     wsync();
     return lane < MTB_MAXCH ? sh->corr[lane] : 0;
   }
 
-  // Would PartialSequenceLengths.update(N, S) (partialLengths.ts:636-686) meet an entry newer than S in N's
-  // partials?  addSeq (:543-577) then inserts S below it without raising the later entries' cumulative `len`:
-  // their lengths stay short by S's seglen from then on.  Only a summary body's inserts can be older than what
-  // a block already holds.  N = the block at depth d of the walk (d >= 1); its entries are the list entries of
-  // its parent (depth d - 1) tagged with N's slot, plus the phantom inserts of N's table.  Checked as the walk
-  // places the segment, before its own entries are appended.
-  // A phantom's removal entries (seq = its rseq) are in the exact list but not in the reference's partials: a
-  // removal entry newer than S counts only when the removals of that op under N outweigh N's phantoms of it.
-  // Round 6: only an update that finds an entry AT S is stale -- addSeq then replaces that entry's seglen while
-  // the later entries keep lengths built on the old one (:569-575); a new entry below newer ones goes through
-  // PartialSequenceLengthsSet.addOrUpdate, which raises them (:24-47), so the exact lists agree.  (The oracle
-  // counts the same condition: MergeTree::counters.staleDeficits.)
-  __device__ __forceinline__ bool stale_at(int d, int S) {
-    uint32_t loff, lcnt, lcap;
-    meta_of(d - 1, loff, lcnt, lcap);
-    const uint32_t slot = U(sh->slot[d - 1]), N = U(sh->path[d]);
-    bool st = false, rem = false, atS = false;
+  // PartialSequenceLengths.update(N, S) (partialLengths.ts:636-686) of a summary body insert: does N's main set
+  // hold an entry AT S already, and which entries follow it?  addSeq (:543-577) then replaces that entry's
+  // seglen and recomputes its len from the entry before it, while the later entries keep lengths built on the
+  // old seglen: short by the segment from `t1` (N's first main entry above S) on, and client C's set the same
+  // below `t1c` (C's first entry above S).  A new entry below newer ones is exact (PartialSequenceLengthsSet.
+  // addOrUpdate raises them, :24-47).  N = the block at depth d of the walk (d >= 1); its entries are the list
+  // entries of its parent tagged with N's slot, plus the phantom inserts of N's table.  A phantom's removal
+  // entries (seq = its rseq) are in the exact list but not in the reference's partials: a removal seq counts
+  // only when the removals of that op under N outweigh N's phantoms of it.  Checked as the walk places the
+  // segment, before its own entries are appended; t1 / t1c = PH_NOSEQ when nothing follows.
+  __device__ __forceinline__ static int wave_min(int v) {
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+  }
+  __device__ __noinline__ bool ph_later(int d, int S, int C, int& t1, int& t1c) {
+    // N's entries: for d >= 1 the entries of its parent's list tagged with N's slot; for the root (d = 0) its own
+    // list whole, or, when the root holds segments, those segments' inserts and removals (fromLeaves' view of
+    // them, the segment being placed excluded)
+    const uint32_t N = U(sh->path[d]);
+    const uint32_t Cm = (uint32_t)C & 0xFFFF;
+    const bool leafRoot = d == 0 && (U(sh->v[0].f[F_ID][0]) & MTB_LEAF);
+    uint32_t loff = 0, lcnt = 0, lcap = 0, slot = MTB_NONE;
+    if (leafRoot) {
+      lcnt = (uint32_t)sh->v[0].count;
+    } else if (d >= 1) {
+      meta_of(d - 1, loff, lcnt, lcap);
+      slot = U(sh->slot[d - 1]);
+    } else {
+      meta_of(0, loff, lcnt, lcap);
+    }
+    const int skip = leafRoot ? (int)U(ins_slot) : -1;
+    // entry i of the source on this lane: up to two (insert, removal) for a segment; kind 0 insert, 1 removal
+    // (amount = length removed by its first remover), 2 an overlapping remover (amount 0)
+    auto entry = [&](uint32_t i, int which, int& seq, uint32_t& cl, int& kind, int& amt) -> bool {
+      if (leafRoot) {
+        if ((int)i == skip) return false;
+        const uint32_t sq = sh->v[0].f[F_SEQ][i], rs = sh->v[0].f[F_RSEQ][i], ci = sh->v[0].f[F_CLI][i];
+        if (which == 0) {
+          seq = (int)sq;
+          cl = (uint32_t)cli_client(ci) & 0xFFFF;
+          kind = 0;
+          amt = (int)sh->v[0].f[F_LEN][i];
+          return (int)sq >= 0 && (int)sq < MTB_PEND;
+        }
+        if (!((int)rs >= 0 && (int)rs < MTB_PEND)) return false;
+        seq = (int)rs;
+        cl = (uint32_t)cli_rc0(ci) & 0xFFFF;
+        kind = 1;
+        amt = (int)sh->v[0].f[F_LEN][i];
+        return true;
+      }
+      if (which != 0) return false;
+      const WEnt e = lst[loff + i];
+      const uint32_t ck = (uint32_t)e.ck, k = (ck >> 16) & 0xF;
+      if (slot != MTB_NONE && (ck >> 20) != slot) return false;
+      seq = e.seq;
+      cl = ck & 0xFFFF;
+      kind = k == WK_OVERLAP ? 2 : e.delta < 0 ? 1 : 0;
+      amt = e.delta < 0 ? -e.delta : e.delta;
+      return true;
+    };
+    // a leaf root's overlapping removers: client c removed at the segment's rseq too
+    auto leaf_rc = [&](uint32_t i, uint32_t c) -> bool {
+      const uint32_t rcx = sh->v[0].f[F_RCX][i];
+      if (!rcx) return false;
+      const uint32_t nr = aux[rcx];
+      for (uint32_t r = 0; r < nr; r++)
+        if (((uint32_t)aux[rcx + 1 + r] & 0xFFFF) == c) return true;
+      return false;
+    };
+    bool atS = false;
+    int mi = PH_NOSEQ, mc = PH_NOSEQ;
     for (uint32_t base = 0; base < lcnt; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       if (i < lcnt) {
-        const WEnt e = lst[loff + i];
-        if (e.seq > S && e.seq > minSeq && ((uint32_t)e.ck >> 20) == slot) {
-          if (((uint32_t)e.ck >> 16 & 0xF) == WK_OVERLAP || e.delta < 0) rem = true;  // (a removal's entries)
-          else st = true;
-        }
-        atS |= e.seq == S && ((uint32_t)e.ck >> 20) == slot && ((uint32_t)e.ck >> 16 & 0xF) == WK_MAIN;
-      }
-    }
-    if constexpr (hasPh) {
-      if (phDoc) {
-        const uint32_t n = U(aux[ph_off]);
-        for (uint32_t base = 0; base < n; base += 64) {
-          const uint32_t i = base + (uint32_t)lane;
-          if (i < n) {
-            const bool mine = aux[ph_off + 2 + 8 * i] == N;
-            st |= mine && (int)aux[ph_off + 2 + 8 * i + 5] > S;
-            atS |= mine && (int)aux[ph_off + 2 + 8 * i + 5] == S;
+        int seq, kind, amt;
+        uint32_t cl;
+        if (entry(i, 0, seq, cl, kind, amt) && kind == 0) {
+          atS |= seq == S;
+          if (seq > S && seq > minSeq) {
+            mi = min(mi, seq);
+            if (cl == Cm) mc = min(mc, seq);
           }
         }
-        if (__ballot(atS) == 0) return false;
-        if (__ballot(st) == 0 && __ballot(rem) != 0) st = COLD(ph_rem_stale(loff, lcnt, slot, N, S));
-        return __ballot(st) != 0;
+      }
+    }
+    const uint32_t n = phDoc ? U(aux[ph_off]) : 0u;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      if (i < n && aux[ph_off + 2 + 8 * i] == N && aux[ph_off + 2 + 8 * i + 6] == PH_PHANTOM) {
+        const int q = (int)aux[ph_off + 2 + 8 * i + 5];
+        atS |= q == S;
+        if (q > S) {
+          mi = min(mi, q);
+          if ((aux[ph_off + 2 + 8 * i + 7] & 0xFFFF) == Cm) mc = min(mc, q);
+        }
       }
     }
     if (__ballot(atS) == 0) return false;
-    return __ballot(st || rem) != 0;
-  }
-  // some op newer than S removed under N more than N's phantoms of that op (lane-uniform result)
-  __device__ __noinline__ bool ph_rem_stale(uint32_t loff, uint32_t lcnt, uint32_t slot, uint32_t N, int S) {
-    const uint32_t n = U(aux[ph_off]);
-    for (uint32_t j = 0; j < lcnt; j++) {
-      const WEnt c = lst[loff + j];
-      if (!(c.seq > S && c.seq > minSeq && ((uint32_t)c.ck >> 20) == slot && ((uint32_t)c.ck >> 16 & 0xF) == WK_MAIN &&
-            c.delta < 0))
-        continue;
-      int acc = 0;  // removed under N at c.seq minus N's phantom lengths removed at c.seq
+    // removal entries below the insert bounds, lowest seq first, until one is the reference's
+    int floor = S;
+    for (int guard = 0; guard < (1 << 20); guard++) {
+      mi = wave_min(mi);
+      mc = wave_min(mc);
+      int q = PH_NOSEQ;
+      for (uint32_t base = 0; base < lcnt; base += 64) {
+        const uint32_t i = base + (uint32_t)lane;
+        int seq, kind, amt;
+        uint32_t cl;
+        if (i < lcnt && entry(i, leafRoot ? 1 : 0, seq, cl, kind, amt) && kind != 0 && seq > floor && seq > minSeq &&
+            (seq < mi || (seq < mc && (cl == Cm || (leafRoot && leaf_rc(i, Cm))))))
+          q = min(q, seq);
+      }
+      q = wave_min(q);
+      if (q == PH_NOSEQ) break;
+      // removed under N at q, less N's phantom lengths removed at q; and whether client C removed there
+      int acc = 0;
+      bool byC = false;
       for (uint32_t base = 0; base < lcnt; base += 64) {
         const uint32_t i = base + (uint32_t)lane;
         if (i < lcnt) {
-          const WEnt e = lst[loff + i];
-          if (e.seq == c.seq && ((uint32_t)e.ck >> 20) == slot && ((uint32_t)e.ck >> 16 & 0xF) == WK_MAIN && e.delta < 0)
-            acc -= e.delta;
+          int seq, kind, amt;
+          uint32_t cl;
+          if (entry(i, leafRoot ? 1 : 0, seq, cl, kind, amt) && kind != 0 && seq == q) {
+            if (kind == 1) acc += amt;
+            byC |= cl == Cm || (leafRoot && leaf_rc(i, Cm));
+          }
         }
       }
       for (uint32_t base = 0; base < n; base += 64) {
         const uint32_t i = base + (uint32_t)lane;
-        if (i < n && aux[ph_off + 2 + 8 * i] == N && (int)aux[ph_off + 2 + 8 * i + 1] == c.seq)
+        if (i < n && aux[ph_off + 2 + 8 * i] == N && aux[ph_off + 2 + 8 * i + 6] == PH_PHANTOM &&
+            (int)aux[ph_off + 2 + 8 * i + 1] == q)
           acc -= (int)aux[ph_off + 2 + 8 * i + 2];
       }
       for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-      if (acc > 0) return true;
+      byC = __ballot(byC) != 0;
+      if (acc > 0) {
+        mi = min(mi, q);
+        if (byC) mc = min(mc, q);
+      }
+      floor = q;
     }
-    return false;
+    t1 = wave_min(mi);
+    t1c = wave_min(mc);
+    return true;
+  }
+  // the load's update(N, S) with an entry at S (ph_later): the deficits that began at S's entry (recomputed now
+  // from the entry before it) begin at the next one; the segment's own length, when it counts at S, leaves a
+  // new main deficit from t1 and a client deficit below t1c
+  __device__ __noinline__ void ph_load_update(int d, int S, int C, int len, int t1, int t1c) {
+    const uint32_t N = U(sh->path[d]);
+    const uint32_t Cm = (uint32_t)C & 0xFFFF;
+    const uint32_t n = U(aux[ph_off]);
+    bool any = false;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      if (i < n && aux[ph_off + 2 + 8 * i] == N && (int)aux[ph_off + 2 + 8 * i + 1] == S) {
+        const uint32_t o = ph_off + 2 + 8 * i, kind = aux[o + 6];
+        const bool cli = kind == PH_DEF_CLI && (aux[o + 3] & 0xFFFF) == Cm;
+        if (kind == PH_DEF_MAIN || cli) {
+          const int t = kind == PH_DEF_MAIN ? t1 : t1c;
+          if (t == PH_NOSEQ) aux[o] = MTB_NONE;
+          else aux[o + 1] = (uint32_t)t;
+          any = true;
+        }
+      }
+    }
+    if (__ballot(any)) wsync();
+    if (len > 0 && t1 != PH_NOSEQ) ph_add(N, (uint32_t)t1, (uint32_t)len, 0u, 0u, (uint32_t)S, PH_DEF_MAIN);
+    if (bad()) return;
+    if (len > 0 && t1c != PH_NOSEQ) ph_add(N, (uint32_t)t1c, (uint32_t)len, Cm, 0u, (uint32_t)S, PH_DEF_CLI);
   }
 
   // blockInsert's continuePredicate (mergeTree.ts:1611-1615, forwardExcursion mergeTreeNodeWalk.ts:121-138):
@@ -1694,14 +1836,25 @@ struct Eng {
       add_len_levels(0, d, d, candLen);
       if constexpr (isLoad) {
         ld_stale = 0;
-        // (a collaborating client's segment: update() on the path, see stale_at; one removed at its own seq adds
-        // nothing at S, so it replaces no seglen)
-        if (C != -2 && (int)U(sh->nseg[F_RSEQ]) != S)
-          for (int i = 1; i <= d; i++)
-            if (stale_at(i, S)) ld_stale |= 1u << i;
+        // (a collaborating client's segment: update() on the path, see ph_later; one removed at its own seq adds
+        // nothing at S, so it leaves no deficit, but its entry at S is still recomputed)
+        if (C != -2) {
+          const int own = (int)U(sh->nseg[F_RSEQ]) != S ? (int)U(sh->nseg[F_LEN]) : 0;  // (its cachedLength)
+          for (int i = 0; i <= d && !err; i++) {
+            if (!phDoc && i == 0) continue;  // (the root's partial lengths are never walked)
+            int t1, t1c;
+            if (!ph_later(i, S, C, t1, t1c)) continue;
+            if (phDoc) ph_load_update(i, S, C, own, t1, t1c);
+            else if (own > 0 && t1 != PH_NOSEQ) ld_stale |= 1u << i;
+          }
+          if (bad()) return false;
+        }
         load_entries(d, S, C);
       } else {
         append_levels(0, d, S, C, WK_MAIN, candLen);
+        if constexpr (hasPh) {
+          if (COLD(phDoc) && S < MTB_PEND) ph_touch(MTB_NONE, 1, d);  // (blockInsert's update() of the path)
+        }
       }
       pending_fix = d;
       return true;
@@ -2091,13 +2244,15 @@ struct Eng {
     }
     if constexpr (hasPh) {
       // blockUpdatePathLengths(node, seq, clientId, overwrite): recombined only with overwrite
-      if (COLD(phDoc && ack_ow)) {
-        prev = MTB_NONE;
+      // (and update() otherwise, annotate acks included: copyDown, ph_touch)
+      if (COLD(phDoc)) {
         for (uint32_t i = 0; i < cnt && !err; i++) {
           const uint32_t b = U(segp[U(aux[off + i])]);
           bool seen = false;
           for (uint32_t q = 0; q < i; q++) seen |= U(segp[U(aux[off + q])]) == b;
-          if (!seen) ph_up(b);
+          if (seen) continue;
+          if (ack_ow) ph_up(b);
+          else ph_touch_up(b);
         }
       }
     }
@@ -2932,11 +3087,13 @@ struct Eng {
       const int count = U(V.count);
       const int bpos = U(sh->pp[d]);  // position of the block's start in the (R, C) view
       const int idx = U(sh->sidx[d]);
+      int walked = -1;  // a block of segments: the length of its leaves in the view (nodeMap's pos advance)
       if (!exiting) {
         if (idx == 0 && count > 0 && (U(V.f[F_ID][0]) & MTB_LEAF)) {
           // a block of segments: every touched segment at once
           const int tot = map_leaf_block(d, bpos, start, end, S, C, remove, opId, comb);
           if (bad()) return;
+          walked = tot;
           if (bpos + tot >= end) exiting = true;
         } else {
           int rlj = 0;
@@ -2993,6 +3150,22 @@ struct Eng {
         if (COLD(phDoc && ph_ow)) {
           ph_combine(U(sh->path[d]));
           if (bad()) return;
+        } else if (COLD(phDoc && remove && d > 0 && S < MTB_PEND)) {
+          ph_touch(U(sh->path[d]), 1, 0);
+        }
+        // depthFirstNodeWalk moves nodeMap's pos past a block it descended into by what it counted there (leaf
+        // lengths, and the partial lengths of the blocks it skipped), not by the block's own partial length:
+        // phantoms and deficits make the two differ, so the parent's later siblings start from the former
+        if (COLD(phDoc) && d > 0) {
+          if (walked < 0) {
+            const int r = lane < count ? V.rl[lane] : 0;
+            walked = rl(cscan8(r > 0 ? r : 0), 7);
+          }
+          if (lane == 0) {
+            sh->v[d - 1].rl[U(sh->slot[d - 1])] = walked;
+            sh->v[d - 1].rlv = 0;  // (not the view's lengths any more: a later load_view recomputes them)
+          }
+          wsync();
         }
       }
       if (d == 0) break;
@@ -3955,8 +4128,8 @@ struct Eng {
       settle();
       if (bad()) return;
       // a collaborating client's segment takes update() on every path block that did not split (the split halves
-      // and a new root were recombined): refuse when that leaves stale cumulative lengths below the root (the
-      // root's own partial lengths are never walked)
+      // and a new root were recombined, which clears their deficits again); a document without a deficit table
+      // (the host gives one to every load with collaborating body segments) refuses a stale update instead
       const int top = ph_split_top < dins + 1 ? ph_split_top : dins + 1;
       if (C != -2 && (ld_stale & ((1u << top) - 1u))) { fail(DERR_STALE); return; }
       if constexpr (hasPh) {
@@ -3967,7 +4140,8 @@ struct Eng {
           } else if (rseq >= 0) {
             // a removed segment of a collaborating client: update() records its insert, never its removal
             for (int i = 0; i < top && !err; i++)
-              ph_add(U(sh->path[i]), (uint32_t)rseq, (uint32_t)len, o.msn, o.pos1, (uint32_t)S);
+              ph_add(U(sh->path[i]), (uint32_t)rseq, (uint32_t)len, o.msn, o.pos1, (uint32_t)S, PH_PHANTOM,
+                     (uint32_t)C & 0xFFFF);
           }
           if (bad()) return;
         }

@@ -23,3 +23,25 @@ def test_phantom_kat_on_the_oracle(new_mode):
     assert o.get_text() == pc.KAT_TEXT != pc.EXACT_TEXT
     assert [r[2] for r in (json.loads(x) for x in o.dump_segments().splitlines()[1:])][9:] == \
         ["a", "Z", "b", "Y", "c", "d"]
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_deficit_kat_on_the_oracle(new_mode):
+    from pyoracle import OracleDoc
+    o = OracleDoc(new_length_calc=new_mode)
+    o.load_v1(pc.def_summary(), "L")
+    assert o.get_text() == "h1234567ABCDEF"
+    assert o.stale_deficits() == 1
+    rows = [json.loads(r) for r in o.dump_segments().splitlines()[1:]]
+    # root [ L1 [h 1 2 3], L2 [4 5 6 7 AB CD EF], L3 [a b c d] ]
+    assert [(r[0], r[2]) for r in rows] == [([0, 0], "h"), ([0, 1], "1"), ([0, 2], "2"), ([0, 3], "3"),
+                                           ([1, 0], "4"), ([1, 1], "5"), ([1, 2], "6"), ([1, 3], "7"),
+                                           ([1, 4], "AB"), ([1, 5], "CD"), ([1, 6], "EF"),
+                                           ([2, 0], "a"), ([2, 1], "b"), ([2, 2], "c"), ([2, 3], "d")]
+    msgs = pc.def_msgs()
+    o.apply_msg(msgs[0])
+    assert o.get_text() == "h1234567ABCDEFY"  # the client term: Y passes L2
+    o.apply_msg(msgs[1])
+    assert o.get_text() == pc.DEF_TEXT != pc.DEF_EXACT_TEXT
+    assert [r[2] for r in (json.loads(x) for x in o.dump_segments().splitlines()[1:])][11:] == \
+        ["a", "Z", "Y", "b", "c", "d"]
