@@ -2039,8 +2039,8 @@ std::string derr_text(int e) {
                                 "it in place, shared with split clones)";
     case DERR_CONS_NULL: return "TypeError: Cannot read properties of null (reading 'seq') (properties.ts:56-57: a consensus "
                                 "annotate with a null defaultValue over a segment lacking the key; the reference throws here)";
-    case DERR_STALE: return "unsupported: summary body segment older than entries already in its blocks' partial lengths "
-                            "(the reference's addSeq leaves their cumulative lengths stale, partialLengths.ts:543-577)";
+    case DERR_STALE: return "internal: stale cumulative partial lengths in a loaded document without a deficit table "
+                            "(partialLengths.ts:543-577; the host gives every load with collaborating body segments one)";
     default: return "device error " + std::to_string(e);
   }
 }
@@ -2048,7 +2048,7 @@ int derr_code(int e) {
   if (e == DERR_INSERT) return MTB_E_INSERT;
   if ((e >= DERR_CAP_SEG && e <= DERR_CAP_AUX) || e == DERR_CAP_DELTA || e == DERR_CAP_PEND) return MTB_E_CAPACITY;
   if (e == DERR_ASSERT_SEQ || e == DERR_ASSERT_MSN || e == DERR_ASSERT_MKID || e == DERR_CONS_NULL) return MTB_E_ASSERT;
-  if (e == DERR_SCHED) return MTB_E_INTERNAL;
+  if (e == DERR_SCHED || e == DERR_STALE || e == DERR_INCR) return MTB_E_INTERNAL;
   return MTB_E_UNSUPPORTED;
 }
 
