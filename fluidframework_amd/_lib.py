@@ -23,7 +23,7 @@ EXPORTS = ["mtb_batch_create", "mtb_batch_destroy", "mtb_last_error", "mtb_free"
            "mtb_apply_msg_json", "mtb_append_ops", "mtb_add_client", "mtb_intern_props", "mtb_replay",
            "mtb_get_text", "mtb_get_length", "mtb_get_seq", "mtb_dump_segments", "mtb_doc_checksum",
            "mtb_summarize_v1", "mtb_blob_list_free", "mtb_summarize_legacy", "mtb_rewind", "mtb_replay_resident", "mtb_replay_resident_ex", "mtb_refresh_digests",
-           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_doc_digests",
+           "mtb_export_pending", "mtb_props_json", "mtb_client_long_id", "mtb_map_range", "mtb_debug_blocks", "mtb_doc_digests",
            "mtb_summarize_v1_many", "mtb_blob_list_fnv", "mtb_local_op_json", "mtb_regenerate_pending_op",
            "mtb_get_launch_info", "mtb_detached_op_json", "mtb_maintenance"]
 
@@ -124,6 +124,7 @@ def lib():
     L.mtb_rewind.argtypes = [vp]
     L.mtb_map_range.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, u32,
                                 ctypes.POINTER(vp), ctypes.POINTER(sz)]
+    L.mtb_debug_blocks.argtypes = [vp, u32, ctypes.c_int64, ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(sz)]
     L.mtb_replay_resident.argtypes = [vp, ctypes.POINTER(MtbStats)]
     L.mtb_replay_resident_ex.argtypes = [vp, ctypes.POINTER(MtbStats), u32]
     L.mtb_refresh_digests.argtypes = [vp, ctypes.POINTER(MtbStats)]

@@ -305,6 +305,19 @@ class MergeTreeBatch:
         finally:
             self._L.mtb_free(p)
 
+    def debug_blocks(self, doc, ref_seq=-1, long_client_id=None):
+        """Diagnostic: per block (tree order) its path, each child block's [length the engine walks, leaf sum] in
+        the (ref_seq, client) view and the document's phantom / deficit entries for it (mtb_debug_blocks)."""
+        self._ensure_flushed()
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.mtb_debug_blocks(self._h, doc, ref_seq, None if long_client_id is None else long_client_id.encode(),
+                                           ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return [json.loads(x) for x in ctypes.string_at(p, n.value).decode("utf-8").splitlines()]
+        finally:
+            self._L.mtb_free(p)
+
     def summarize_legacy(self, doc, msn=-1, seq=-1, catchup=None):
         """SnapshotLegacy summary (snapshotlegacy.ts): (blobs, ISummaryTreeWithStats); `catchup` is the list of
         messages above the MSN (SharedSegmentSequence.messagesSinceMSNChange)."""

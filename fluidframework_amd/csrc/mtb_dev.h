@@ -43,6 +43,8 @@ int mtbx_dump_segments(mtb_dev* b, uint32_t doc, char** out, size_t* out_len);
 int mtbx_doc_checksum(mtb_dev* b, uint32_t doc, uint64_t* out);
 int mtbx_doc_digests(mtb_dev* b, uint32_t first, uint32_t n, uint64_t* out);
 int mtbx_get_launch_info(mtb_dev* b, mtb_launch_info* out);
+int mtbx_debug_blocks(mtb_dev* b, uint32_t doc, int64_t ref_seq, const char* long_client_id, char** out,
+                      size_t* out_len);
 int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq,
                   const char* long_client_id, uint32_t limit, char** out, size_t* out_len);
 int mtbx_summarize_v1(mtb_dev* b, uint32_t doc, int64_t msn, int64_t seq,

@@ -8,6 +8,7 @@
 //  * Read-outs (text, canonical segment dump, SnapshotV1 summary) download a document's slices and
 //    walk its tree on the host.  There is no CPU replay path: without a GPU every compute entry point
 //    fails with MTB_E_NODEV.
+#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -4957,6 +4958,71 @@ std::unordered_map<uint32_t, int64_t> phantom_surplus(const HostDoc& d, const Do
   return sur;
 }
 }  // namespace
+
+int mtbx_debug_blocks(mtb_dev* b, uint32_t doc, int64_t ref_seq, const char* long_client_id, char** out,
+                      size_t* out_len) {
+  return guarded(b, [&] {
+    HostDoc& d = docref(b, doc);
+    if (!out) raise(MTB_E_ARG, "null output");
+    if (!d.onDevice || !b->devInit) raise(MTB_E_ARG, "document has not been replayed");
+    if (b->hst[doc].err) raise(derr_code(b->hst[doc].err), derr_text(b->hst[doc].err));
+    download_doc(b, doc);
+    const DocState& s = b->hst[doc];
+    const bool newMode = b->opts.new_length_calc != 0;
+    const int R = ref_seq < 0 ? (int)s.cur_seq : (int)ref_seq;
+    int C = 0;
+    if (long_client_id) {
+      auto it = d.shortOf.find(long_client_id);
+      C = it == d.shortOf.end() ? -3 : it->second;
+    }
+    std::unordered_map<uint32_t, int64_t> sur = phantom_surplus(d, s, R, C);
+    std::vector<int> rc;
+    std::function<int64_t(uint32_t)> leafsum = [&](uint32_t c) -> int64_t {
+      if (c & MTB_LEAF) {
+        const int l = leaf_length(d, d.segs[c & ~MTB_LEAF], R, C, newMode, (int)s.min_seq, rc);
+        return l > 0 ? l : 0;
+      }
+      const Blk& B = d.blks.at(c);
+      int64_t t = 0;
+      for (int i = 0; i < B.count; i++) t += leafsum(B.child[i]);
+      return t;
+    };
+    std::string o;
+    std::function<void(uint32_t, const std::string&)> visit = [&](uint32_t bi, const std::string& path) {
+      const Blk& B = d.blks.at(bi);
+      o += "{\"path\":[" + path + "],\"kids\":[";
+      for (int i = 0; i < B.count; i++) {
+        const uint32_t c = B.child[i];
+        if (i) o += ",";
+        if (c & MTB_LEAF) {
+          o += "null";
+        } else {
+          const int64_t ls = leafsum(c);
+          auto it = sur.find(c);
+          o += "[" + std::to_string(ls + (it == sur.end() ? 0 : it->second)) + "," + std::to_string(ls) + "]";
+        }
+      }
+      o += "],\"table\":[";
+      bool first = true;
+      if (s.ph && (size_t)s.ph + 2 <= d.aux.size()) {
+        const uint32_t n = d.aux[s.ph];
+        for (uint32_t i = 0; i < n && (size_t)s.ph + 2 + 8ull * (i + 1) <= d.aux.size(); i++) {
+          const uint32_t* e = d.aux.data() + s.ph + 2 + 8ull * i;
+          if (e[0] != bi) continue;
+          o += std::string(first ? "" : ",") + "[" + std::to_string(e[6]) + "," + std::to_string((int)e[1]) + "," +
+               std::to_string((int)e[2]) + "," + std::to_string((int)(int16_t)e[3]) + "]";
+          first = false;
+        }
+      }
+      o += "]}\n";
+      for (int i = 0; i < B.count; i++)
+        if (!(B.child[i] & MTB_LEAF)) visit(B.child[i], path + (path.empty() ? "" : ",") + std::to_string(i));
+    };
+    visit(s.root, "");
+    *out = dup(o);
+    if (out_len) *out_len = o.size();
+  });
+}
 
 int mtbx_map_range(mtb_dev* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq, const char* long_client_id,
                   uint32_t limit, char** out, size_t* out_len) {

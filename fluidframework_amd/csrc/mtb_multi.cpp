@@ -433,6 +433,11 @@ int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_
   DOC_CALL(doc, mtbx_map_range(d_, l_, start, end, ref_seq, long_client_id, limit, out, out_len));
 }
 
+int mtb_debug_blocks(mtb_batch* b, uint32_t doc, int64_t ref_seq, const char* long_client_id, char** out,
+                     size_t* out_len) {
+  DOC_CALL(doc, mtbx_debug_blocks(d_, l_, ref_seq, long_client_id, out, out_len));
+}
+
 int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq, mtb_blob_list* out) {
   DOC_CALL(doc, mtbx_summarize_v1(d_, l_, msn, seq, out));
 }

@@ -281,6 +281,13 @@ int mtb_get_launch_info(mtb_batch* b, mtb_launch_info* out);
  * "properties"?}} (short client ids), at most `limit` entries (0 = all); free with mtb_free. */
 int mtb_map_range(mtb_batch* b, uint32_t doc, int64_t start, int64_t end, int64_t ref_seq,
                   const char* long_client_id, uint32_t limit, char** out, size_t* out_len);
+/* Diagnostic (no reference counterpart): the partial lengths the engine walks in the (ref_seq, long_client_id)
+ * view.  *out = one JSON line per block in tree order: {"path": [child indices from the root], "kids": [null for
+ * a segment | [length in the view, leaf sum in the view]], "table": [[kind, t or removedSeq, length, client],
+ * ...]} -- the length is the leaf sum plus the block's phantom surplus less its partial-length deficits
+ * (DESIGN.md section 7), "table" the document's entries for that block.  Free with mtb_free. */
+int mtb_debug_blocks(mtb_batch* b, uint32_t doc, int64_t ref_seq, const char* long_client_id, char** out,
+                     size_t* out_len);
 /* Client.summarize with newMergeTreeSnapshotFormat: if `msn`/`seq` >= 0 first runs
  * updateSeqNumbers(msn, seq) (client.ts:979).  long_client_ids may be NULL (use registered ids). */
 int mtb_summarize_v1(mtb_batch* b, uint32_t doc, int64_t msn, int64_t seq,

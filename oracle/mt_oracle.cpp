@@ -102,10 +102,60 @@ int PartialLengths::getPartialLength(int refSeq, int clientId) {
   }
   return pLen;
 }
+static bool defcheck() {
+  static const bool on = getenv("MTO_DEFCHECK") != nullptr;
+  return on;
+}
 void PartialLengths::zamboni(const CollabWindow& w) {
+  if (defcheck()) {
+    // copyDown: the main-set deficits that began at or below the copied entry move into minLength; a client
+    // set's are dropped with its minLength
+    PSL* m = partialLengths.latestLeq(w.minSeq);
+    if (m) {
+      int h = 0;
+      for (auto& e : partialLengths.items) {
+        h += e.seglen;
+        if (&e == m) break;
+      }
+      hmin += h;
+      for (auto& d : defs)
+        if (d.kind == 1 && d.t <= m->seq) d.kind = 3;
+    }
+    for (size_t k = 0; k < clientSeqNumbers.size(); k++) {
+      PSL* mc = clientSeqNumbers[k].latestLeq(w.minSeq);
+      if (!mc) continue;
+      const int c = (int)k - 2, tm = mc->seq;
+      defs.erase(std::remove_if(defs.begin(), defs.end(), [&](const Def& d) { return d.kind == 2 && d.c == c && d.t <= tm; }),
+                 defs.end());
+    }
+  }
   minLength += partialLengths.copyDown(w.minSeq);
   minSeq = w.minSeq;
   for (auto& cs : clientSeqNumbers) cs.copyDown(w.minSeq);
+  if (defcheck()) checkDefs("zamboni");
+}
+void PartialLengths::checkDefs(const char* where) const {
+  auto check = [&](const PSLSet& st, int kind, int c) {
+    int h = 0;
+    for (auto& e : st.items) {
+      h += e.seglen;
+      int want = 0;
+      for (auto& d : defs)
+        if (d.kind == kind && (kind == 1 || d.c == c) && d.t <= e.seq) want += d.d;
+      if (h - e.len != want)
+        throw OracleError(-9, std::string("deficit model: ") + where + ": set " + (kind == 1 ? "main" : "client " + std::to_string(c)) +
+                                  " entry " + std::to_string(e.seq) + " short by " + std::to_string(h - e.len) +
+                                  ", model " + std::to_string(want));
+    }
+  };
+  check(partialLengths, 1, 0);
+  for (size_t k = 0; k < clientSeqNumbers.size(); k++) check(clientSeqNumbers[k], 2, (int)k - 2);
+  int m = 0;
+  for (auto& d : defs)
+    if (d.kind == 3) m += d.d;
+  if (hmin - minLength != m)
+    throw OracleError(-9, std::string("deficit model: ") + where + ": minLength short by " + std::to_string(hmin - minLength) +
+                              ", model " + std::to_string(m));
 }
 void PartialLengths::addClientSeqNumber(int clientId, int seq, int seglen) {
   PSL p;
@@ -163,6 +213,7 @@ MergeTree::MergeTree(const Options& o) : options(o) {
 Block* MergeTree::makeBlock(int childCount) {
   blockPool.emplace_back();
   Block* b = &blockPool.back();
+  b->id = (int)blockPool.size() - 1;
   b->childCount = childCount;
   return b;
 }
@@ -777,6 +828,7 @@ std::unique_ptr<PartialLengths> MergeTree::fromLeaves(Block* b) {  // partialLen
     prevLen = p.len;
     pl->addClientSeqNumberFromPartial(p);
   }
+  pl->hmin = pl->minLength;
   return pl;
 }
 
@@ -803,6 +855,11 @@ std::unique_ptr<PartialLengths> MergeTree::combine(Block* b, bool recur) {  // p
       combined->segmentCount += cp->segmentCount;
       combined->minLength += cp->minLength;
       lists.push_back(&cp->partialLengths.items);
+      if (defcheck()) {  // (only the children's minLength shortfalls survive the rebuild)
+        combined->hmin += cp->hmin;
+        for (auto& d : cp->defs)
+          if (d.kind == 3) combined->defs.push_back(d);
+      }
     }
     // mergePartialLengths + mergeSortedListsBySeq (partialLengths.ts:1013-1060)
     std::vector<size_t> next(lists.size(), 0);
@@ -823,6 +880,7 @@ std::unique_ptr<PartialLengths> MergeTree::combine(Block* b, bool recur) {  // p
     combined = std::move(leafPL);
   }
   combined->zamboni(window);
+  if (defcheck()) combined->checkDefs("combine");
   return combined;
 }
 
@@ -848,9 +906,30 @@ void MergeTree::plUpdate(PartialLengths& pl, Block* node, int seq, int clientId)
     }
   }
   pl.segmentCount = segCount;
+  if (defcheck()) {
+    // addSeq over an entry at seq: the deficits that began there begin at the next entry; the later entries are
+    // short by the seglen change
+    auto model = [&](PSLSet& st, int kind, int c) {
+      auto [exists, idx] = st.find(seq);
+      if (!exists) return;
+      const int t1 = idx + 1 < st.items.size() ? st.items[idx + 1].seq : INT32_MAX;
+      for (auto& d : pl.defs)
+        if (d.kind == kind && (kind == 1 || d.c == c) && d.t == seq) d.t = t1;
+      pl.defs.erase(std::remove_if(pl.defs.begin(), pl.defs.end(), [](const PartialLengths::Def& d) { return d.t == INT32_MAX; }),
+                    pl.defs.end());
+      const int dd = seqSeglen - st.items[idx].seglen;
+      if (t1 != INT32_MAX && dd) pl.defs.push_back({kind, t1, dd, c});
+      if (getenv("MTO_DEFTRACE"))
+        fprintf(stderr, "update block %d seq %d client %d kind %d: t1 %d d %d (defs %zu)\n", node->id, seq, clientId, kind,
+                t1 == INT32_MAX ? -1 : t1, dd, pl.defs.size());
+    };
+    model(pl.partialLengths, 1, 0);
+    model(pl.cli(clientId), 2, clientId);
+  }
   const int d1 = addSeq(pl.partialLengths, seq, seqSeglen, clientId);
   const int d2 = addSeq(pl.cli(clientId), seq, seqSeglen, 0);
   if (node != root && (d1 || d2)) counters.staleDeficits++;
+  if (defcheck()) pl.checkDefs("update");
   pl.zamboni(window);
 }
 

@@ -126,11 +126,19 @@ struct PartialLengths {
   }
   int getPartialLength(int refSeq, int clientId);
   void zamboni(const CollabWindow& w);
+  // Shadow of the engine's deficit model (test infrastructure, checked when MTO_DEFCHECK is set; DESIGN.md §7
+  // "Deficits"): kind 1 = main-set entries from t on short by d, 2 = client c's set from t on, 3 = in minLength;
+  // hmin = minLength without the kind-3 shortfalls.
+  struct Def { int kind, t, d, c; };
+  std::vector<Def> defs;
+  int hmin = 0;
+  void checkDefs(const char* where) const;
   void addClientSeqNumber(int clientId, int seq, int seglen);
   void addClientSeqNumberFromPartial(const PSL& p);
 };
 
 struct Block : Node {
+  int id = 0;  // creation order (diagnostics)
   int childCount = 0;
   std::vector<Node*> children;
   int needsScour = -1;  // -1 undefined, 0 false, 1 true  (IMergeBlock.needsScour)

@@ -1,3 +1,4 @@
+#include <functional>
 // ORACLE / TEST INFRASTRUCTURE ONLY.  C entry points over the CPU restatement, loaded by tests/
 // through ctypes (tests/oracle.py) and by bench.py's cpu_baseline leg.  Never linked by the product.
 #include <cstring>
@@ -74,6 +75,69 @@ int orc_matrix_apply_msg_json(orc_matrix* m, const char* json, size_t len) {
 
 // Client.walkSegments / getContainingSegment / getPropertiesAtPosition through mapRange (same JSON as the
 // engine's mtb_map_range): [{"pos","start","end","segment":{...}}...]
+// Debug view (test infrastructure): one JSON line per block in tree order -- its path, the partial length of each
+// child in the (ref_seq, long_id) view next to the child's leaf sum in that view, and the block's main and
+// client partial-length sets ([seq, len, seglen]).
+int orc_debug_blocks(orc_doc* d, int ref_seq, const char* long_id, char** out, size_t* len) {
+  return guard(d, [&] {
+    Doc& doc = d->doc;
+    MergeTree& t = doc.mt;
+    const int R = ref_seq < 0 ? t.window.currentSeq : ref_seq;
+    int C = t.window.clientId;
+    if (long_id) {
+      auto it = doc.longToShort.find(long_id);
+      C = it == doc.longToShort.end() ? -3 : it->second;
+    }
+    std::string o;
+    std::function<int(Node*)> leafsum = [&](Node* n) -> int {
+      if (n->leaf) {
+        const int l = t.nodeLength(n, R, C);
+        return l > 0 ? l : 0;
+      }
+      Block* b = static_cast<Block*>(n);
+      int s = 0;
+      for (int i = 0; i < b->childCount; i++) s += leafsum(b->children[i]);
+      return s;
+    };
+    auto set_json = [](const PSLSet& st) {
+      std::string j = "[";
+      for (size_t i = 0; i < st.items.size(); i++) {
+        if (i) j += ",";
+        j += "[" + std::to_string(st.items[i].seq) + "," + std::to_string(st.items[i].len) + "," +
+             std::to_string(st.items[i].seglen) + "]";
+      }
+      return j + "]";
+    };
+    std::function<void(Block*, std::string)> visit = [&](Block* b, std::string path) {
+      o += "{\"path\":[" + path + "],\"kids\":[";
+      for (int i = 0; i < b->childCount; i++) {
+        Node* c = b->children[i];
+        if (i) o += ",";
+        if (c->leaf) o += "null";
+        else o += "[" + std::to_string(t.nodeLength(c, R, C)) + "," + std::to_string(leafsum(c)) + "]";
+      }
+      o += "]";
+      if (b->partial) {
+        PartialLengths& pl = *b->partial;
+        o += ",\"minLength\":" + std::to_string(pl.minLength) + ",\"main\":" + set_json(pl.partialLengths);
+        const size_t k = (size_t)(C + 2);
+        o += ",\"cli\":" + (k < pl.clientSeqNumbers.size() ? set_json(pl.clientSeqNumbers[k]) : std::string("[]"));
+        o += ",\"id\":" + std::to_string(b->id) + ",\"defs\":[";  // (the MTO_DEFCHECK shadow model)
+        for (size_t q = 0; q < pl.defs.size(); q++)
+          o += std::string(q ? "," : "") + "[" + std::to_string(pl.defs[q].kind) + "," + std::to_string(pl.defs[q].t) + "," +
+               std::to_string(pl.defs[q].d) + "," + std::to_string(pl.defs[q].c) + "]";
+        o += "]";
+      }
+      o += "}\n";
+      for (int i = 0; i < b->childCount; i++)
+        if (!b->children[i]->leaf)
+          visit(static_cast<Block*>(b->children[i]), path + (path.empty() ? "" : ",") + std::to_string(i));
+    };
+    visit(t.root, "");
+    *out = dupstr(o, len);
+  });
+}
+
 int orc_map_range(orc_doc* d, int start, int end, int ref_seq, const char* long_id, unsigned limit, char** out, size_t* len) {
   return guard(d, [&] {
     Doc& doc = d->doc;

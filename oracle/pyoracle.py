@@ -86,6 +86,7 @@ def lib():
         L.orc_regenerate.argtypes = [vp, cp, pp, ctypes.POINTER(sz)]
         L.orc_local_op_json.argtypes = [vp, cp, pp, ctypes.POINTER(sz)]
         L.orc_map_range.argtypes = [vp, i, i, i, cp, ctypes.c_uint, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.orc_debug_blocks.argtypes = [vp, i, cp, ctypes.POINTER(vp), ctypes.POINTER(sz)]
         L.orc_sa2d_create.restype = vp
         L.orc_sa2d_destroy.argtypes = [vp]
         L.orc_sa2d_set.argtypes = [vp, u32, u32, cp]
@@ -247,6 +248,18 @@ class OracleDoc:
                                         ctypes.byref(p), ctypes.byref(n)))
         try:
             return json.loads(ctypes.string_at(p, n.value).decode("utf-8"))
+        finally:
+            self._L.orc_free(p)
+
+    def debug_blocks(self, ref_seq=-1, long_client_id=None):
+        """Debug view: per block (tree order) its path, each block child's [partial length, leaf sum] in the
+        (ref_seq, client) view, minLength and the main / client partial-length sets ([seq, len, seglen])."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._chk(self._L.orc_debug_blocks(self._h, ref_seq, None if long_client_id is None else long_client_id.encode(),
+                                           ctypes.byref(p), ctypes.byref(n)))
+        try:
+            return [json.loads(x) for x in ctypes.string_at(p, n.value).decode("utf-8").splitlines()]
         finally:
             self._L.orc_free(p)
 

@@ -197,13 +197,13 @@ def test_constructed_summaries_with_removed_client_segments_in_the_body(new_mode
     assert set(out) <= {"deficit", "failed", "equal"} and "deficit" in out
 
 
-def _rising_tail(o, seed, n_ops, start_seq, msn_lag=3):
+def _rising_tail(o, seed, n_ops, start_seq, msn_lag=3, out=None):
     """Remote ops after a load whose MSN trails the seq by `msn_lag` (each author has seen everything): blocks the
     ops update copy their deficits down into minLength (partialLengths.ts:809-819), and recombinations then carry
     them up (:304-308) -- or drop the ones not copied down yet."""
     import random
     rng = random.Random(seed)
-    msgs = []
+    msgs = [] if out is None else out
     seq = start_seq
     for _ in range(n_ops):
         seq += 1
@@ -219,8 +219,8 @@ def _rising_tail(o, seed, n_ops, start_seq, msn_lag=3):
         m = {"clientId": rng.choice(["client-0", "client-1", "client-7"]), "sequenceNumber": seq,
              "referenceSequenceNumber": seq - 1, "minimumSequenceNumber": max(10, seq - msn_lag), "type": "op",
              "contents": contents}
-        o.apply_msg(m)
         msgs.append(m)
+        o.apply_msg(m)  # (raises at an op the reference fails: msgs ends with it)
     return msgs
 
 
@@ -228,11 +228,12 @@ def _rising_tail(o, seed, n_ops, start_seq, msn_lag=3):
 def test_small_summaries_with_deficits(new_mode):
     """Small constructed summaries (4-16 NonCollab, 3-19 client segments, chunks of 6-12 chars) whose loads leave
     deficits in the reference, in one batch: the engine equals the oracle after the load and after 60 remote ops
-    with a rising MSN (and, separately, 30 with the MSN held at 10)."""
-    from fluidframework_amd import MergeTreeBatch
+    with a rising MSN (or 30 with the MSN held at 10); where the reference fails one of the 60 ("MergeTree insert
+    failed": the deficits put its position past the blocks' lengths), the engine fails that op too."""
+    from fluidframework_amd import MergeTreeBatch, MergeTreeError
     from pyoracle import OracleDoc
     from test_gpu_load import _remote_tail
-    cases = []
+    cases, fails = [], []
     for k in range(300):
         blobs = _tail_summary(7000 + k, 4 + k % 13, 3 + (k // 13) % 17, 6 + k % 7)
         o = OracleDoc(new_length_calc=new_mode)
@@ -244,7 +245,19 @@ def test_small_summaries_with_deficits(new_mode):
             continue
         g = OracleDoc(new_length_calc=new_mode)
         g.load_v1(blobs, "obs")
-        tail = _rising_tail(g, k, 60, 40) if k % 2 == 0 else _remote_tail(g, k, 30, 40, 10, ["client-0", "client-1", "client-7"])
+        if k % 2:
+            try:
+                tail = _remote_tail(g, k, 30, 40, 10, ["client-0", "client-1", "client-7"])
+            except Exception:
+                continue
+        else:
+            tail = []
+            try:
+                tail = _rising_tail(g, k, 60, 40, out=tail)
+            except Exception as e:  # the reference fails a later insert: the engine must fail the same op
+                assert "MergeTree insert failed" in str(e)
+                fails.append((blobs, tail))
+                continue
         cases.append((blobs, o, tail))
     assert len(cases) >= 100
     B = MergeTreeBatch(len(cases), new_length_calc=new_mode)
@@ -259,6 +272,26 @@ def test_small_summaries_with_deficits(new_mode):
     B.flush()
     for j, (blobs, o, tail) in enumerate(cases):
         _same(B, j, o, f"case {j} after load + tail")
+    # the tails the reference fails: equal before the failing op, "MergeTree insert failed" at it
+    assert fails
+    F = MergeTreeBatch(2 * len(fails), new_length_calc=new_mode)
+    for j, (blobs, tail) in enumerate(fails):
+        for q, n in ((2 * j, len(tail) - 1), (2 * j + 1, len(tail))):
+            F[q].load(blobs, "loader")
+            for m in tail[:n]:
+                F[q].applyMsg(m)
+    try:
+        F.flush()
+    except MergeTreeError:
+        pass
+    for j, (blobs, tail) in enumerate(fails):
+        o = OracleDoc(new_length_calc=new_mode)
+        o.load_v1(blobs, "loader")
+        for m in tail[:-1]:
+            o.apply_msg(m)
+        _same(F, 2 * j, o, f"failing case {j} before its failing op")
+        with pytest.raises(MergeTreeError, match="MergeTree insert failed"):  # (reads raise a document's error)
+            F.map_range(2 * j + 1, 0, 1)
 
 
 @pytest.mark.parametrize("new_mode", [False, True])
