@@ -188,7 +188,7 @@ def make_matrix_log(seed, n_msgs, n_clients=4, lag=16, p_set=0.45, max_count=8, 
 
 
 def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True, initial="hello world", verify=False,
-                   record=None, reconnect=0.0, rewrite=0.0, marker_ids=0, incr=0.0):
+                   record=None, reconnect=0.0, rewrite=0.0, marker_ids=0, incr=0.0, summary=None):
     """A conflict farm in the style of the reference's (client.conflictFarm.spec.ts with TestClientLogger):
     `n_clients` live clients make local ops against their own view, a sequencer orders them (refSeq = the
     client's currentSeq at submission, MSN = the lowest refSeq any client can still send), and every client
@@ -203,20 +203,31 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     marker-relative inserts and annotateMarker ops (relativePos1 {id, before}, relativePos2 {id}) for ids
     their own view resolves.  With `incr` > 0 that fraction of the local annotates are combiningOp "incr"
     annotates (their numeric keys become NaN; a remote incr modifies pending keys too, shouldModifyKey).
+    With `summary` (SnapshotV1 blobs) every client and the observer start by loading it (Client.load with their
+    own ids) instead of from `initial`, and the sequence numbers continue from the summary's.
     Returns (clients, observer, sequenced messages)."""
     import random
     from pyoracle import OracleDoc, OracleError
     rng = random.Random(seed)
     ids = [f"c{k}" for k in range(n_clients)]
     clients = []
+    seq0 = 0
+    if summary is not None:
+        import json as _json
+        seq0 = _json.loads(summary[0][1])["headerMetadata"]["sequenceNumber"]
+
+    def start(o, cid):
+        if summary is not None:
+            o.load_v1(summary, cid)
+        else:
+            o.insert_text_local(0, initial)
+            o.start_collab(cid)
     for cid in ids:
         o = OracleDoc(new_length_calc=new_mode, verify=verify)
-        o.insert_text_local(0, initial)
-        o.start_collab(cid)
+        start(o, cid)
         clients.append(o)
     obs = OracleDoc(new_length_calc=new_mode, verify=verify)
-    obs.insert_text_local(0, initial)
-    obs.start_collab("obs")
+    start(obs, "obs")
     queue, log, seen = [], [], [0] * n_clients
     words = ["a", "bc", "def", "\n", "xyz" * 3, "\U0001F600"]
 
@@ -254,7 +265,7 @@ def run_local_farm(seed, n_clients=4, n_rounds=60, new_mode=False, annotate=True
     def sequence(m):
         cid, ref, op = queue.pop(0)
         msn = min([c.current_seq for c in clients] + [q[1] for q in queue] + [ref])
-        msg = {"clientId": cid, "sequenceNumber": len(log) + 1, "referenceSequenceNumber": ref,
+        msg = {"clientId": cid, "sequenceNumber": seq0 + len(log) + 1, "referenceSequenceNumber": ref,
                "minimumSequenceNumber": msn, "type": "op", "contents": op}
         log.append(msg)
 

@@ -22,22 +22,29 @@ def _replay_farm(seed, n_clients, n_rounds, new_mode, rounds_per_replay=1, annot
     return _replay_record(rec, seed, new_mode, rounds_per_replay, "hello world")
 
 
-def _replay_record(rec, seed, new_mode, rounds_per_replay, initial, observer=None):
+def _replay_record(rec, seed, new_mode, rounds_per_replay, initial, observer=None, summary=None):
     """observer: an OracleDoc that applied rec["obs_log"]; it becomes one more document of the (live) batch,
-    fed its messages in four parts across the replays, and is compared at the end."""
+    fed its messages in four parts across the replays, and is compared at the end.  summary: SnapshotV1 blobs
+    every client (and the observer) loads first, as in run_local_farm(summary=...)."""
     import json
     from fluidframework_amd import MergeTreeBatch
     ids = rec["ids"]
     n_clients = len(ids)
     B = MergeTreeBatch(n_clients + (observer is not None), new_length_calc=new_mode)
     for k, cid in enumerate(ids):
+        if summary is not None:
+            B[k].load(summary, cid)
+            continue
         if initial:
             B[k].insertTextLocal(0, initial)
         B[k].startOrUpdateCollaboration(cid)
     if observer is not None:
-        if initial:
-            B[n_clients].insertTextLocal(0, initial)
-        B[n_clients].startOrUpdateCollaboration("obs")
+        if summary is not None:
+            B[n_clients].load(summary, "obs")
+        else:
+            if initial:
+                B[n_clients].insertTextLocal(0, initial)
+            B[n_clients].startOrUpdateCollaboration("obs")
         obs_log = rec["obs_log"]
         obs_parts = [obs_log[len(obs_log) * q // 4: len(obs_log) * (q + 1) // 4] for q in range(4)]
     checked = 0
@@ -291,3 +298,36 @@ def test_live_client_summaries_match_oracle(seed, reconnect):
             assert [list(b) for b in gb] == osum["blobs"], f"seed {seed} round {r} client {k}: summary blobs"
             assert gs == osum["summary"], f"seed {seed} round {r} client {k}: summary tree"
     assert pending_seen > 0
+
+
+@pytest.mark.parametrize("new_mode", [False, True])
+def test_live_farm_on_summaries_with_deficits(new_mode):
+    """Live clients that each load a constructed summary whose body leaves the reference with partial-length
+    deficits (tests/test_gpu_phantom._tail_summary; DESIGN.md section 7 "Deficits"), then run a conflict farm:
+    local ops in their own views, acks (update() of the acked segments' blocks: copyDown of deficits), remote ops
+    in deficit-shortened views, zamboni.  Every client's digest and text equal its oracle client's after every
+    round, and the observer's dump at the end."""
+    from pyoracle import OracleDoc, OracleError
+    from test_gpu_phantom import _tail_summary
+    done = 0
+    for k in range(0, 400, 7):
+        blobs = _tail_summary(7000 + k, 4 + k % 13, 3 + (k // 13) % 17, 6 + k % 7)
+        o = OracleDoc(new_length_calc=new_mode)
+        try:
+            o.load_v1(blobs, "c0")
+        except OracleError:
+            continue
+        if not o.stale_deficits():
+            continue
+        rec = {}
+        try:
+            _, obs, _ = run_local_farm(k, n_clients=3, n_rounds=25, new_mode=new_mode, annotate=True, record=rec,
+                                       summary=blobs)
+        except OracleError as e:  # (a deficit put a local op's position past a block: the reference throws)
+            assert "MergeTree insert failed" in str(e)
+            continue
+        assert _replay_record(rec, k, new_mode, 1, None, observer=obs, summary=blobs) > 0
+        done += 1
+        if done >= 8:
+            break
+    assert done >= 4
