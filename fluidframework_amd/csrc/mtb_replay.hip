@@ -1548,7 +1548,7 @@ struct Eng {
     for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
     return v;
   }
-  __device__ __noinline__ bool ph_later(int d, int S, int C, int& t1, int& t1c) {
+  __device__ __forceinline__ bool ph_later(int d, int S, int C, int& t1, int& t1c) {
     // N's entries: for d >= 1 the entries of its parent's list tagged with N's slot; for the root (d = 0) its own
     // list whole, or, when the root holds segments, those segments' inserts and removals (fromLeaves' view of
     // them, the segment being placed excluded)
@@ -1684,7 +1684,7 @@ struct Eng {
   // the load's update(N, S) with an entry at S (ph_later): the deficits that began at S's entry (recomputed now
   // from the entry before it) begin at the next one; the segment's own length, when it counts at S, leaves a
   // new main deficit from t1 and a client deficit below t1c
-  __device__ __noinline__ void ph_load_update(int d, int S, int C, int len, int t1, int t1c) {
+  __device__ __forceinline__ void ph_load_update(int d, int S, int C, int len, int t1, int t1c) {
     const uint32_t N = U(sh->path[d]);
     const uint32_t Cm = (uint32_t)C & 0xFFFF;
     const uint32_t n = U(aux[ph_off]);
