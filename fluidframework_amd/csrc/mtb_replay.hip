@@ -942,45 +942,66 @@ struct Eng {
   // each block child k, the entries of k's own list plus entries derived from k's segment children
   // (the combine semantics of partialLengths.ts:256).  Returns the new metadata; the caller stores it
   // where P's metadata lives.
+  // hold_nh >= 0 (packParent, every new child a block of segments): P's children are the hold_cc blocks packParent
+  // just filled from sh->hold[.][0..hold_nh) in its order (the first hold_nh % hold_cc get one more), so their
+  // segments are read from LDS instead of from the records written a moment before (two dependent round trips
+  // fewer); such children have no lists of their own.
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out, int hold_nh = -1, int hold_cc = 0) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
-    const uint32_t* src = bw(P);
-    const uint32_t w = src[lane];
-    const int count = U((int)src[FB_HDR]);
-    (&Z.f[0][0])[lane] = w;
-    wsync();
+    const bool fromHold = hold_nh >= 0;
+    int count = hold_cc;
+    if (!fromHold) {
+      const uint32_t* src = bw(P);
+      const uint32_t w = src[lane];
+      count = U((int)src[FB_HDR]);
+      (&Z.f[0][0])[lane] = w;
+      wsync();
+    }
     // lane (k, s): segment child s of block child k
     const int k = lane >> 3, s = lane & 7;
     uint32_t ck = MTB_NONE;
-    if (k < count) ck = Z.f[F_ID][k];
-    const bool kblk = k < count && !(ck & MTB_LEAF);
+    if (!fromHold && k < count) ck = Z.f[F_ID][k];
+    const bool kblk = k < count && (fromHold || !(ck & MTB_LEAF));
     int ne = 0, nov = 0;
     int slen = 0, sseq = 0, srseq = -1;
     uint32_t scli = 0, srcx = 0;
     if (kblk) {
-      const uint32_t* c = bw(ck);
-      const int ccount = (int)c[FB_HDR];
-      if (s < ccount) {
-        const uint32_t sid = c[F_ID * 8 + s];
-        if (sid & MTB_LEAF) {
-          slen = (int)c[F_LEN * 8 + s];
-          sseq = (int)c[F_SEQ * 8 + s];
-          srseq = (int)c[F_RSEQ * 8 + s];
-          scli = c[F_CLI * 8 + s];
-          srcx = c[F_RCX * 8 + s];
-          if (sseq > minSeq) ne++;
-          if (srseq >= 0 && srseq > minSeq) {
-            ne++;
-            if (srcx) nov = (int)aux[srcx];
+      if (fromHold) {
+        const int base = hold_nh / hold_cc, rem = hold_nh % hold_cc;
+        const int nk = base + (k < rem ? 1 : 0), start = k * base + (k < rem ? k : rem);
+        if (s < nk) {
+          const int i = start + s;
+          slen = (int)sh->hold[F_LEN][i];
+          sseq = (int)sh->hold[F_SEQ][i];
+          srseq = (int)sh->hold[F_RSEQ][i];
+          scli = sh->hold[F_CLI][i];
+          srcx = sh->hold[F_RCX][i];
+        }
+      } else {
+        const uint32_t* c = bw(ck);
+        const int ccount = (int)c[FB_HDR];
+        if (s < ccount) {
+          const uint32_t sid = c[F_ID * 8 + s];
+          if (sid & MTB_LEAF) {
+            slen = (int)c[F_LEN * 8 + s];
+            sseq = (int)c[F_SEQ * 8 + s];
+            srseq = (int)c[F_RSEQ * 8 + s];
+            scli = c[F_CLI * 8 + s];
+            srcx = c[F_RCX * 8 + s];
           }
         }
+      }
+      if (sseq > minSeq) ne++;
+      if (srseq >= 0 && srseq > minSeq) {
+        ne++;
+        if (srcx) nov = (int)aux[srcx];
       }
     }
     // the block children's own lists (metadata in P's slots), concatenated
     uint32_t lc = 0, lo = 0;
-    if (lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
+    if (!fromHold && lane < count && !(Z.f[F_ID][lane] & MTB_LEAF)) {
       lo = Z.f[F_SEQ][lane];
       lc = Z.f[F_RSEQ][lane];
     }
@@ -3630,12 +3651,14 @@ struct Eng {
       // ... then the lists: of the new blocks whose children are blocks, and last of P itself (one rebuild
       // site; rebuild uses the union as scratch)
       uint32_t a = 0, c2 = 0, e = 0;
+      // (every new child a block of segments: P's list is rebuilt from the scour output still in LDS)
+      const bool leafKids = cc > 0 && __ballot(lane < cc && kbs != 0) == 0;
       for (int q = 0; q <= cc; q++) {
         const bool isP = q == cc;
         const uint32_t nb = isP ? parent : rlu(nbs, q);
         a = c2 = e = 0;
         if (isP || rl(kbs, q)) {
-          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e);
+          rebuild(nb, isP ? ploff : 0u, isP ? pcap : 0u, a, c2, e, isP && leafKids ? nh : -1, cc);
           if (bad()) return;
         }
         if (isP) break;
