@@ -946,16 +946,24 @@ struct Eng {
   // just filled from sh->hold[.][0..hold_nh) in its order (the first hold_nh % hold_cc get one more), so their
   // segments are read from LDS instead of from the records written a moment before (two dependent round trips
   // fewer); such children have no lists of their own.
+  // pv (a split's parent): P's record as the walk's LDS view of it holds it, instead of a read of the record.
   __device__ __forceinline__ void rebuild(uint32_t P, uint32_t old_loff, uint32_t old_lcap, uint32_t& loff_out,
-                                         uint32_t& lcnt_out, uint32_t& lcap_out, int hold_nh = -1, int hold_cc = 0) {
+                                         uint32_t& lcnt_out, uint32_t& lcap_out, int hold_nh = -1, int hold_cc = 0,
+                                         const View* pv = nullptr) {
     PROF_CNT(CN_REBUILD, 1);
     Rec& Z = sh->zr;
     const bool fromHold = hold_nh >= 0;
     int count = hold_cc;
     if (!fromHold) {
-      const uint32_t* src = bw(P);
-      const uint32_t w = src[lane];
-      count = U((int)src[FB_HDR]);
+      uint32_t w;
+      if (pv) {
+        w = (&pv->f[0][0])[lane];
+        count = U(pv->count);
+      } else {
+        const uint32_t* src = bw(P);
+        w = src[lane];
+        count = U((int)src[FB_HDR]);
+      }
       (&Z.f[0][0])[lane] = w;
       wsync();
     }
@@ -1285,6 +1293,7 @@ struct Eng {
       }
       uint32_t X, ooff = 0, ocnt = 0, ocap = 0;
       const int L = level - 1;
+      const View* xv = nullptr;  // (the parent: its view is current)
       if (phase == 1) {
         X = b;
         meta_of(level, ooff, ocnt, ocap);
@@ -1337,10 +1346,11 @@ struct Eng {
         insert_slot(L, k + 1);
         X = U(P.b);
         meta_of(L, ooff, ocnt, ocap);
+        xv = &P;
         phase = 4;
       }
       uint32_t a, c2, e;
-      rebuild(X, ooff, ocap, a, c2, e);
+      rebuild(X, ooff, ocap, a, c2, e, -1, 0, xv);
       if (err) break;
       if (phase == 2) {
         sp_loffL = a;
