@@ -4539,6 +4539,24 @@ __device__ __forceinline__ uint32_t replay_doc(SCR& sh, uint32_t doc, int32_t* x
       }
       e.cur_k = k;
       CRUMB(ndocs + doc, k);
+#ifdef MTB_TABCHECK  // (fault triage, DESIGN.md section 4: is the LDS copy of the batch tables intact at each op?)
+      {
+        const bool ok = sh.tab.pool == tables.pool && sh.tab.pidx == tables.pidx && sh.tab.val_class == tables.val_class &&
+                        sh.tab.val_falsy == tables.val_falsy && sh.tab.key_rank == tables.key_rank &&
+                        sh.tab.key_irr == tables.key_irr && sh.tab.val_local == tables.val_local &&
+                        sh.tab.irr == tables.irr && sh.gheap == gheap && sh.gtext == text + DSF64(text_base);
+        if (__ballot(!ok)) {
+          if (e.lane == 0) {
+            ds->pad3[0] = 1;
+            ds->pad3[1] = k;
+            ds->pad3[2] = (uint32_t)(uintptr_t)sh.tab.val_falsy;
+            ds->pad3[3] = 0;
+          }
+          e.fail(DERR_SHAPE);
+          break;
+        }
+      }
+#endif
       if constexpr (MODE == MODE_MATRIX) {
         if (cur.type == MTB_OP_SETCELL) {
           e.setcell(cur, par);

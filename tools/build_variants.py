@@ -6,6 +6,8 @@ they are profiling builds, not part of the package):
   check     + MTB_CHECK                      bounds-checked slices (mtb_check lines on stderr)
   ppcrumbs  profpack + MTB_CRUMBS            ticket breadcrumbs in host memory (fault triage, mtb_crumbs lines)
   ppinline  profpack + MTB_TICK_INLINE       the ticket kernel's hand-over helpers inlined (no calls; fault triage)
+  tabcheck  profpack + MTB_TABCHECK          the LDS copy of the batch tables checked against the kernel argument
+                                             before every op (fault triage; a mismatch fails the document)
 
 usage: python3 tools/build_variants.py [name ...]   (default: all)
 """
@@ -22,6 +24,7 @@ VARIANTS = {
     "check": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CHECK"],
     "ppcrumbs": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_CRUMBS"],
     "ppinline": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_TICK_INLINE"],
+    "tabcheck": ["MTB_PROFILE", "MTB_PROFILE_PACK", "MTB_TABCHECK"],
 }
 
 if __name__ == "__main__":
