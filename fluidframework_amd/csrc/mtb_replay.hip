@@ -343,6 +343,29 @@ struct Eng {
   uint32_t ld_stale;            // MODE_LOAD: bit d = the walk's depth-d block holds entries newer than the segment
   uint64_t prof[NPH];
   uint32_t evc[NCN];
+#ifdef MTB_TABCHECK  // fault triage (tools/build_variants.py tabcheck): the pointers the engine dereferences, as set up
+  const void* x_sh;
+  const void* x_ptr[4];
+  const Tables* x_tab;
+  __device__ __forceinline__ void tchk(uint32_t site) {
+    const bool ok = (const void*)sh == x_sh && (const void*)RAW(segp) == x_ptr[0] && (const void*)RAW(blk) == x_ptr[1] &&
+                    (const void*)RAW(lst) == x_ptr[2] && (const void*)RAW(aux) == x_ptr[3] && sh->tab.pool == x_tab->pool &&
+                    sh->tab.pidx == x_tab->pidx && sh->tab.val_class == x_tab->val_class &&
+                    sh->tab.val_falsy == x_tab->val_falsy && sh->tab.key_irr == x_tab->key_irr;
+    if (__ballot(!ok) && !err) {
+      if (lane == 0) {
+        ds->pad3[0] = 1;
+        ds->pad3[1] = site;
+        ds->pad3[2] = cur_k;
+        ds->pad3[3] = 0;
+      }
+      fail(DERR_SHAPE);
+    }
+  }
+#define TCHK(site) tchk(site)
+#else
+#define TCHK(site) ((void)0)
+#endif
 
   // ------------------------------------------------------------------ errors / allocation
   __device__ __forceinline__ void fail(int code) {
@@ -3586,10 +3609,12 @@ struct Eng {
       const uint32_t* pm = pparent == MTB_NONE ? &blk[parent].loff : &blk[pparent].f[F_SEQ][pindex];
       const uint32_t ploff_v = pm[0], pcap_v = pparent == MTB_NONE ? pm[2] : pm[2 * MTB_MAXCH];
       stage_recs(pc, kids);
+      TCHK(12);
       const uint32_t ploff = U(ploff_v), pcap = U(pcap_v);
       PROF_PADD(PH_HEAP, tp);
       tp = PROF_T();
       const int nh = scour(pc, 0);
+      TCHK(13);
       if (bad()) return;
       PROF_PADD(PH_STAGE, tp);
       tp = PROF_T();
@@ -3686,6 +3711,7 @@ struct Eng {
         }
         wsync();
       }
+      TCHK(14);
       store_meta_of(parent, pparent, pindex, a, c2, e);
       if (cc < MTB_MAXCH / 2 && pparent != MTB_NONE) {
         parent = pparent;
@@ -3867,14 +3893,17 @@ struct Eng {
       PROF_ZADD(PH_HEAP, tz);
       tz = PROF_T();
       const uint32_t b = U(bp);
+      TCHK(7);
       if (b == MTB_NONE) { PROF_CNT(CN_PSKIP, 1); PROF_ZADD(PH_STAGE, tz); continue; }
       stage_recs(1, b);
+      TCHK(8);
       const int sc = U(sh->pr[0].scour);
       PROF_ZADD(PH_STAGE, tz);
       if (sc == 0) { PROF_CNT(CN_PSKIP, 1); continue; }
       const int count = U(sh->pr[0].count);
       const uint32_t parent = U(sh->pr[0].parent);
       const int nh = scour(1, 0);
+      TCHK(9);
       if (bad()) return;
       tz = PROF_T();
       if (lane == 0) blk[b].scour = 0;
@@ -3884,8 +3913,10 @@ struct Eng {
         place_children(b, 0, nh);
         PROF_ZADD(PH_PLACE, tz);
         tz = PROF_T();
+        TCHK(10);
         if (COLD(nh < MTB_MAXCH / 2 && parent != MTB_NONE)) {
           pack_parent(parent);
+          TCHK(11);
         } else {
           mk_remap_hold(0, nh);  // blockUpdatePathLengths(block, .., true) (zamboni.ts:55)
           if constexpr (hasPh) {
@@ -4242,6 +4273,7 @@ struct Eng {
     switch (o.type) {
       case MTB_OP_INSERT: {
         ops_applied++;
+        TCHK(1);
         view_clear();
         uint64_t t0 = PROF_T();
         int p1 = (int)o.pos1;
@@ -4253,6 +4285,7 @@ struct Eng {
         walk(p1, R, C, -2, false, 0);  // ensureIntervalBoundary
         settle();
         PROF_ADD(PH_BOUNDARY, t0);
+        TCHK(2);
         if (bad()) return;
         const bool marker = (o.flags & MTB_F_MARKER) != 0;
         const int len = marker ? 1 : (int)o.pos2;
@@ -4287,7 +4320,9 @@ struct Eng {
             fail(DERR_INSERT);
             return;
           }
+          TCHK(3);
           settle();
+          TCHK(4);
           if (local) grp_add(sid, MTB_OP_INSERT, 0);  // saveIfLocal (mergeTree.ts:1617-1637)
           else if (S > minSeq) lru_add(sid, U(ins_blk), U(ins_scour), S);
           if (COLD(delta_on)) {
@@ -4327,7 +4362,9 @@ struct Eng {
         // 1 rewrite, 2 incr, 3 consensus, 4 a live client's own consensus (annotateMarkerNotifyConsensus)
         int comb = o.type != MTB_OP_ANNOTATE ? 0 : (o.flags & MTB_F_COMB) >> 2;
         if (isLive && comb == 3 && local) comb = 4;
+        TCHK(5);
         node_map(p1, p2, R, C, S, o.type == MTB_OP_REMOVE, o.props, comb);
+        TCHK(6);
         if (COLD(delta_on)) {
           if (bad()) return;
           delta_positions(dfrom);
@@ -4436,6 +4473,14 @@ __device__ __forceinline__ uint32_t replay_doc(SCR& sh, uint32_t doc, int32_t* x
   sh.gfree = freel + DSF64(free_base);
   sh.gtext = text + DSF64(text_base);
   e.sh = &sh;
+#ifdef MTB_TABCHECK
+  e.x_sh = &sh;
+  e.x_ptr[0] = RAW(e.segp);
+  e.x_ptr[1] = RAW(e.blk);
+  e.x_ptr[2] = RAW(e.lst);
+  e.x_ptr[3] = RAW(e.aux);
+  e.x_tab = &tables;
+#endif
   e.lane = lane_id();
   e.minSeq = (int)DSF(min_seq);
   e.curSeq = (int)DSF(cur_seq);
